@@ -1,0 +1,181 @@
+/*
+ * libsat_hip -- C ABI of the MI355X-native Self-attention Tacotron hot path.
+ *
+ * The reference (rhoposit/self-attention-tacotron) is Python/TF1 with no FFI of its own; its
+ * plugin surface for this path is Python:
+ *   attention_mechanism_factory(AttentionOptions) -> mechanism(query, state)
+ *       modules/attentions.py:25-62, modules/forward_attention.py:88-136
+ *   ZoneoutLSTMCell / DecoderRNNV2 / DualSourceAttentionRNN step
+ *       modules/module.py:1017-1048, 1522-1540 (ext tacotron2)
+ *   RNNTransformer training branch (dynamic_decode + causal self-attention + projections)
+ *       modules/module.py:726-765, modules/self_attention.py:13-144
+ *   ZoneoutCBHG / SelfAttentionCBHGEncoder  modules/module.py:30-113, 374-441
+ * Each entry point below replaces the TF ops of one of those functions; the Python host side
+ * (package sat_amd) binds this header with ctypes and mirrors the Python surface.
+ *
+ * Conventions
+ *  - fp32 row-major contiguous tensors unless a stride argument says otherwise; batch-major.
+ *  - Every pointer is caller-owned DEVICE memory.  Nothing here allocates or synchronises, so
+ *    every call can be captured into a hipGraph.  `stream` is a hipStream_t passed as void*.
+ *  - Return 0 on success, a negative SAT_ERR_* code otherwise; sat_last_error_string() gives
+ *    the message (thread-local).  No global mutable state: calls are re-entrant across
+ *    streams and devices.
+ */
+#ifndef SAT_ABI_H
+#define SAT_ABI_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SAT_OK 0
+#define SAT_ERR_ARGUMENT -1
+#define SAT_ERR_HIP -2
+#define SAT_ERR_UNSUPPORTED -3
+
+/* ---------------------------------------------------------------- library */
+int sat_version(void);                         /* 100*major + minor */
+const char* sat_last_error_string(void);
+int sat_device_arch(char* buf, int len);       /* gcnArchName of the current device */
+
+/* ---------------------------------------------------------------- GEMM (fp32 MFMA 32x32x2)
+ * C[b] = act(alpha * opA[b] @ opB[b] + beta * C[b] + bias[b])      (M x N, reduction K)
+ * Replaces tf.layers.Dense / tf.tensordot (Projection, modules/module.py:626-643), the
+ * Conv1D(SAME) of ext tacotron2 Conv1d (module.py:46-68) and their gradients.
+ * A modes: 0 dense  A(m,k) = A[m*a_sm + k*a_sk]
+ *          1 im2col A(m,k): m = s*L + n, k = tap*a_C + c, row = n + tap - a_shift,
+ *                   A = A[(s*L+row)*a_sm + c*a_sk] if 0 <= row < L else 0   (Conv1D SAME)
+ *          2 im2col-transposed A(i,k) = im2col(m=k, kk=i) with the mode-1 addressing
+ *                   (conv dW = im2col(x)^T @ dY in one product)
+ * B modes: 0 dense  B(k,n) = B[k*b_sk + n*b_sn]
+ *          1 flipped conv kernel W[taps][N][b_C]: k = tap*b_C + o,
+ *                   B = W[((taps-1-tap)*N + n)*b_C + o]                     (conv dX)
+ * act: 0 none, 1 relu, 2 tanh, 3 sigmoid.  bias may be NULL.
+ * mul (optional, [M][N] row stride mul_sm): C = act(...) * mul  (fused dropout masks).
+ */
+typedef struct SatGemmDesc {
+  int32_t M, N, K, batch;
+  int32_t a_mode, a_L, a_C, a_shift;
+  const float* A;
+  int64_t a_sm, a_sk, a_sbatch;
+  int32_t b_mode, b_taps, b_C, act;
+  const float* B;
+  int64_t b_sk, b_sn, b_sbatch;
+  float* C;
+  int64_t c_sm, c_sbatch;
+  const float* bias;
+  int64_t bias_sbatch;
+  float alpha, beta;
+  const float* mul;
+  int64_t mul_sm, mul_sbatch;
+} SatGemmDesc;
+
+int sat_gemm(const SatGemmDesc* desc, void* stream);
+
+/* ---------------------------------------------------------------- RNG masks
+ * Counter-based (Philox-4x32-10) Bernoulli masks: out[i] = (u_i < keep) ? on_value : 0.
+ * The per-step seed is read from DEVICE memory (seed_ptr[0]) so a captured graph draws fresh
+ * masks on every replay.  Replaces the dropout draws of tf.layers.dropout / tf.nn.dropout
+ * (PreNet, ZoneoutLSTMCell, modules/self_attention.py:60). */
+int sat_rng_fill(float* out, int64_t n, const uint64_t* seed_ptr, uint64_t stream_id,
+                 float keep, float on_value, void* stream);
+int sat_counter_add(uint64_t* counter, uint64_t inc, void* stream);
+
+/* ---------------------------------------------------------------- (Zoneout)LSTM step
+ * One time step of TF LSTMCell wrapped in ext tacotron2 ZoneoutLSTMCell,
+ * as used by ZoneoutCBHG's BiLSTM (modules/module.py:93-108) and DecoderRNNV2 /
+ * DualSourceAttentionRNN (module.py:1522-1540).  The input projection x@W_x+b is hoisted
+ * (xproj, one GEMM over all steps); the kernel computes the recurrent product rin@W_r, the
+ * gates (i, j, f, o; forget_bias 1), zoneout and the sequence-length copy-through of
+ * bidirectional_dynamic_rnn.  Weights and gates are gate-interleaved: [K][U][4].
+ * Output h_raw = h' (the cell output); state (c_out, h_out) = zoned state.
+ * Training: mask_c/mask_h (1 = take new) ; eval: NULL masks -> (1-z)*new + z*old. */
+typedef struct SatLstmFwd {
+  int32_t B, U, K, t;
+  const float* xproj; int64_t xproj_sb;   /* [B][U][4] row stride xproj_sb (includes bias) */
+  const float* bias;                      /* [U][4], used when xproj == NULL */
+  const float* rin; int64_t rin_sb;       /* recurrent input [B][K] */
+  const float* W;                         /* [K][U][4] */
+  const float* c_prev;                    /* [B][U] (NULL = zeros) */
+  const float* h_prev; int64_t h_prev_sb; /* [B][U] (NULL = zeros) */
+  const float* mask_c; const float* mask_h;
+  float zc, zh;
+  const int64_t* lengths;                 /* optional: step t valid iff t < lengths[b] */
+  float* h_raw; int64_t h_raw_sb;
+  float* c_out;
+  float* h_out; int64_t h_out_sb;
+  float* gates;                           /* [B][U][4] activated gates for the backward */
+} SatLstmFwd;
+
+/* Backward of one step (reverse time).  dL/dh_t = dh_carry + dgates_{t+1} . W[hoff+u, :]
+ * (the recurrent product is done here), dL/dh'_t = dy + sum(dq_i . wq_i[u]) + m_h dL/dh_t. */
+typedef struct SatLstmBwd {
+  int32_t B, U, K, hoff, t;
+  const float* W;
+  const float* dgates_next;
+  const float* gates;
+  const float* c_prev;
+  const float* dy; int64_t dy_sb;
+  const float* dq0; const float* wq0; int32_t dq0_n;
+  const float* dq1; const float* wq1; int32_t dq1_n;
+  const float* dh_carry;
+  const float* dc_carry;
+  const float* mask_c; const float* mask_h;
+  float zc, zh;
+  const int64_t* lengths;
+  float* dgates;
+  float* dh_carry_out;
+  float* dc_carry_out;
+} SatLstmBwd;
+
+int sat_lstm_step_fwd(const SatLstmFwd* args, void* stream);
+int sat_lstm_step_bwd(const SatLstmBwd* args, void* stream);
+
+/* ---------------------------------------------------------------- dual-source attention step
+ * Replaces, for one decoder step, the two attention mechanisms of DualSourceAttentionRNN
+ * (modules/module.py:1520-1530) inside TF AttentionWrapper:
+ *   mechanism 1: ForwardAttention.__call__ (modules/forward_attention.py:88-122) when
+ *                att1_forward = 1, else BahdanauAttention (modules/attentions.py:53-57);
+ *   mechanism 2: BahdanauAttention (additive, normalize=False);
+ *   contexts   : AttentionWrapper._compute_attention (alignments @ values).
+ * Keys/values are the masked memories precomputed once per utterance (memory_layer GEMM).
+ * Launches the tile kernel (grid ntiles x B) and the per-utterance combine kernel.
+ * Outputs: s_out (softmax alignments = next location-conv input), a_out (alpha = returned
+ * alignments), s2_out, contexts [c1 | c2] into ctx (row stride ctx_sb), stats [B][4] for the
+ * backward.  e1/e2/part are scratch. */
+typedef struct SatAttnStep {
+  int32_t B, N, D1, M1, D2, M2, F, KW, NT, ntiles, att1_forward;
+  float u;                                  /* forward-attention transition factor (0.5) */
+  const float* q; int64_t q_sb;             /* [B][D1 + D2] processed queries */
+  const float* K1; const float* V1;         /* [B][N][D1], [B][N][M1] */
+  const float* K2; const float* V2;         /* [B][N][D2], [B][N][M2] */
+  const int64_t* lengths;                   /* [B] memory lengths */
+  const float* s_prev; const float* a_prev; /* [B][N] previous state (att1) */
+  const float* v1; const float* b1;         /* attention_variable, attention_bias [D1] */
+  const float* convW; const float* convb;   /* location conv [KW][1][F], [F] */
+  const float* locW;                        /* location layer [F][D1] */
+  const float* v2;                          /* attention_v of mechanism 2 [D2] */
+  float* e1; float* e2;                     /* scratch [B][N] */
+  float* part; int64_t part_stride;         /* scratch [B][ntiles][part_stride] */
+  float* s_out; float* a_out; float* s2_out;/* [B][N] */
+  float* ctx; int64_t ctx_sb;               /* [B][M1 + M2] */
+  float* stats;                             /* [B][4] or NULL */
+} SatAttnStep;
+
+int sat_attn_part_stride(int32_t M1, int32_t M2);
+/* q = x @ [W1 | W2] (query_layer of both mechanisms), x [B][K] row stride x_sb */
+int sat_attn_query(int32_t B, int32_t K, int32_t N1, int32_t N2, const float* x, int64_t x_sb,
+                   const float* W1, const float* W2, float* q, int64_t q_sb, void* stream);
+int sat_attn_step_fwd(const SatAttnStep* args, void* stream);
+
+/* ---------------------------------------------------------------- elementwise
+ * out[b,n,:] = x[b,n,:] * (n < lengths[b])  -- TF _prepare_memory (memory_sequence_length). */
+int sat_seq_mask(const float* x, float* out, int32_t B, int32_t N, int32_t C,
+                 const int64_t* lengths, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SAT_ABI_H */

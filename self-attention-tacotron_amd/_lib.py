@@ -1,0 +1,116 @@
+"""ctypes binding of ``libsat_hip.so`` (declared in ``include/sat_abi.h``).
+
+Torch tensors are plumbing: only their device pointers, sizes and the current HIP stream cross
+the boundary.  There is no fallback -- if the library is missing or was not built for this GPU,
+every op raises ``SatLibraryError``.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "libsat_hip.so")
+
+
+class SatLibraryError(RuntimeError):
+    pass
+
+
+class SatGemmDesc(ctypes.Structure):
+    _fields_ = [
+        ("M", ctypes.c_int32), ("N", ctypes.c_int32), ("K", ctypes.c_int32),
+        ("batch", ctypes.c_int32),
+        ("a_mode", ctypes.c_int32), ("a_L", ctypes.c_int32), ("a_C", ctypes.c_int32),
+        ("a_shift", ctypes.c_int32),
+        ("A", ctypes.c_void_p),
+        ("a_sm", ctypes.c_int64), ("a_sk", ctypes.c_int64), ("a_sbatch", ctypes.c_int64),
+        ("b_mode", ctypes.c_int32), ("b_taps", ctypes.c_int32), ("b_C", ctypes.c_int32),
+        ("act", ctypes.c_int32),
+        ("B", ctypes.c_void_p),
+        ("b_sk", ctypes.c_int64), ("b_sn", ctypes.c_int64), ("b_sbatch", ctypes.c_int64),
+        ("C", ctypes.c_void_p),
+        ("c_sm", ctypes.c_int64), ("c_sbatch", ctypes.c_int64),
+        ("bias", ctypes.c_void_p), ("bias_sbatch", ctypes.c_int64),
+        ("alpha", ctypes.c_float), ("beta", ctypes.c_float),
+        ("mul", ctypes.c_void_p), ("mul_sm", ctypes.c_int64), ("mul_sbatch", ctypes.c_int64),
+    ]
+
+
+_P = ctypes.c_void_p
+_I32, _I64, _U64, _F = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_float
+
+
+def _struct(name, spec):
+    """spec: 'type:field ...' with types i32 i64 f32 ptr."""
+    tmap = {"i32": _I32, "i64": _I64, "f32": _F, "ptr": _P}
+    fields = [(f, tmap[t]) for t, f in (item.split(":") for item in spec.split())]
+    return type(name, (ctypes.Structure,), {"_fields_": fields})
+
+
+SatLstmFwd = _struct("SatLstmFwd", """
+    i32:B i32:U i32:K i32:t ptr:xproj i64:xproj_sb ptr:bias ptr:rin i64:rin_sb ptr:W
+    ptr:c_prev ptr:h_prev i64:h_prev_sb ptr:mask_c ptr:mask_h f32:zc f32:zh ptr:lengths
+    ptr:h_raw i64:h_raw_sb ptr:c_out ptr:h_out i64:h_out_sb ptr:gates""")
+
+SatLstmBwd = _struct("SatLstmBwd", """
+    i32:B i32:U i32:K i32:hoff i32:t ptr:W ptr:dgates_next ptr:gates ptr:c_prev
+    ptr:dy i64:dy_sb ptr:dq0 ptr:wq0 i32:dq0_n ptr:dq1 ptr:wq1 i32:dq1_n
+    ptr:dh_carry ptr:dc_carry ptr:mask_c ptr:mask_h f32:zc f32:zh ptr:lengths
+    ptr:dgates ptr:dh_carry_out ptr:dc_carry_out""")
+
+SatAttnStep = _struct("SatAttnStep", """
+    i32:B i32:N i32:D1 i32:M1 i32:D2 i32:M2 i32:F i32:KW i32:NT i32:ntiles i32:att1_forward
+    f32:u ptr:q i64:q_sb ptr:K1 ptr:V1 ptr:K2 ptr:V2 ptr:lengths ptr:s_prev ptr:a_prev
+    ptr:v1 ptr:b1 ptr:convW ptr:convb ptr:locW ptr:v2 ptr:e1 ptr:e2 ptr:part i64:part_stride
+    ptr:s_out ptr:a_out ptr:s2_out ptr:ctx i64:ctx_sb ptr:stats""")
+
+# name -> argtypes (restype is int for all but sat_last_error_string)
+SIGNATURES = {
+    "sat_version": [],
+    "sat_device_arch": [ctypes.c_char_p, _I32],
+    "sat_gemm": [ctypes.POINTER(SatGemmDesc), _P],
+    "sat_rng_fill": [_P, _I64, _P, _U64, _F, _F, _P],
+    "sat_counter_add": [_P, _U64, _P],
+    "sat_lstm_step_fwd": [ctypes.POINTER(SatLstmFwd), _P],
+    "sat_lstm_step_bwd": [ctypes.POINTER(SatLstmBwd), _P],
+    "sat_attn_part_stride": [_I32, _I32],
+    "sat_attn_query": [_I32, _I32, _I32, _I32, _P, _I64, _P, _P, _P, _I64, _P],
+    "sat_attn_step_fwd": [ctypes.POINTER(SatAttnStep), _P],
+    "sat_seq_mask": [_P, _P, _I32, _I32, _I32, _P, _P],
+}
+
+_lib: Optional[ctypes.CDLL] = None
+
+
+def load(path: str = LIB_PATH) -> ctypes.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise SatLibraryError(f"{path} not found: run __graft_entry__.build() (make -C csrc)")
+    lib = ctypes.CDLL(path)
+    for name, argtypes in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.argtypes = argtypes
+        fn.restype = ctypes.c_int
+    lib.sat_last_error_string.argtypes = []
+    lib.sat_last_error_string.restype = ctypes.c_char_p
+    _lib = lib
+    return lib
+
+
+def exported_symbols():
+    return list(SIGNATURES) + ["sat_last_error_string"]
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = load().sat_last_error_string().decode(errors="replace")
+        raise SatLibraryError(f"{what} failed (rc={rc}): {msg}")
+
+
+def call(name: str, *args) -> None:
+    check(getattr(load(), name)(*args), name)

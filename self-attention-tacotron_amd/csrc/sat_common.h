@@ -1,0 +1,79 @@
+// Internal helpers shared by the libsat_hip kernels (gfx950 / CDNA4 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <cmath>
+
+#include "sat_abi.h"
+
+namespace sat {
+
+constexpr int kWave = 64;
+
+// thread-local last error (sat_last_error_string)
+void set_error(const char* fmt, ...);
+
+#define SAT_CHECK_ARG(cond, ...)                                                            \
+  do {                                                                                      \
+    if (!(cond)) {                                                                          \
+      ::sat::set_error(__VA_ARGS__);                                                        \
+      return SAT_ERR_ARGUMENT;                                                              \
+    }                                                                                       \
+  } while (0)
+
+#define SAT_LAUNCH_CHECK(name)                                                              \
+  do {                                                                                      \
+    hipError_t e_ = hipGetLastError();                                                      \
+    if (e_ != hipSuccess) {                                                                 \
+      ::sat::set_error("%s: launch failed: %s", name, hipGetErrorString(e_));               \
+      return SAT_ERR_HIP;                                                                   \
+    }                                                                                       \
+  } while (0)
+
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
+
+// accurate tanh (the parity bar is 1e-4 mean-L1 over 500 recurrent steps: no fast approximations)
+__device__ __forceinline__ float tanhf_(float x) { return tanhf(x); }
+__device__ __forceinline__ float sigmf(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// block-wide reductions; `scratch` needs blockDim.x/64 floats; result broadcast to all threads
+__device__ __forceinline__ float block_sum(float v, float* scratch) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  v = wave_sum(v);
+  __syncthreads();
+  if (lane == 0) scratch[w] = v;
+  __syncthreads();
+  float r = 0.f;
+  for (int i = 0; i < nw; ++i) r += scratch[i];
+  return r;
+}
+__device__ __forceinline__ float block_max(float v, float* scratch) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  v = wave_max(v);
+  __syncthreads();
+  if (lane == 0) scratch[w] = v;
+  __syncthreads();
+  float r = -INFINITY;
+  for (int i = 0; i < nw; ++i) r = fmaxf(r, scratch[i]);
+  return r;
+}
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+inline int ceil_div(int64_t a, int64_t b) { return static_cast<int>((a + b - 1) / b); }
+
+}  // namespace sat

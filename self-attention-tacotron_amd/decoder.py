@@ -1,0 +1,165 @@
+"""DualSourceTransformerDecoder teacher-forced loop on libsat_hip (forward).
+
+Mirrors ``DualSourceTransformerDecoder.call`` (modules/module.py:1499-1562) with
+``RNNTransformer``'s training branch (:743-747): ``dynamic_decode`` over T' = T/r steps of
+``DecoderRNNV2 = MultiRNNCell([DualSourceAttentionRNN, ZoneoutLSTM, ZoneoutLSTM])``.
+
+MI355X restructuring (same arithmetic, different schedule):
+* teacher forcing makes every decoder input known up front, so the prenets and every LSTM's
+  input projection (x @ W_x + b) are hoisted out of the recurrence into large MFMA GEMMs;
+* the recurrence of the attention RNN (ZoneoutLSTM 256 -> query -> dual-source attention) runs
+  first over all steps: 3 launches per step (LSTM step, query GEMV, attention tile+combine);
+* the two decoder LSTMs depend only on the attention RNN's outputs, so they run afterwards as
+  their own recurrences with hoisted input GEMMs (1 launch per step each).
+
+All state histories are kept (step-major ``[T'+1, B, .]``) for the hand-written BPTT.
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Dict, Optional
+
+import torch
+
+from . import kernels as K
+from .params import Dims
+
+
+@dataclass
+class DecoderSaved:
+    B: int
+    N: int
+    Tp: int
+    tensors: Dict[str, torch.Tensor] = field(default_factory=dict)
+
+    def __getattr__(self, k):
+        t = self.__dict__.get("tensors", {})
+        if k in t:
+            return t[k]
+        raise AttributeError(k)
+
+
+def teacher_inputs(targets: torch.Tensor, r: int, n_feed: int) -> torch.Tensor:
+    """TransformerTrainingHelper (modules/helpers.py:44-58): step 0 = go frame (zeros),
+    step t = targets.reshape(B, T/r, M*r)[:, t-1, -M*n_feed:].  Pure data movement."""
+    B, T, M = targets.shape
+    Tp = T // r
+    x = torch.zeros(B, Tp, M * n_feed, device=targets.device, dtype=targets.dtype)
+    g = targets.view(B, Tp, M * r)
+    x[:, 1:].copy_(g[:, :-1, M * (r - n_feed):])
+    return x
+
+
+def decoder_forward(P: Dict[str, torch.Tensor], hp, d: Dims, m1: torch.Tensor, m2: torch.Tensor,
+                    lengths: torch.Tensor, targets: torch.Tensor,
+                    masks: Optional[Dict[str, torch.Tensor]], attn_tile: int = 16,
+                    spk: Optional[torch.Tensor] = None):
+    dev = m1.device
+    B, N, _ = m1.shape
+    r, nf = d.r, hp.n_feed_frame
+    Tp = targets.shape[1] // r
+    A, Dd = d.att_rnn, d.dec
+    M1, M2, D1, D2 = d.m1, d.m2, d.d1, d.d2
+    zc, zh = hp.zoneout_factor_cell, hp.zoneout_factor_output
+    f32 = dict(device=dev, dtype=torch.float32)
+    mk = (lambda name: masks[name]) if masks is not None else (lambda name: None)
+
+    S = {}
+    # ---- memories (TF _prepare_memory + memory_layer), once per utterance
+    V1 = K.seq_mask(m1, lengths)
+    V2 = K.seq_mask(m2, lengths)
+    K1 = K.linear(V1, P["decoder/attention1/memory_layer/kernel"])
+    K2 = K.linear(V2, P["decoder/attention2/memory_layer/kernel"])
+    S.update(V1=V1, V2=V2, K1=K1, K2=K2)
+
+    # ---- prenets over all frames (teacher forcing), dropout fused as a multiplicative epilogue
+    xin = teacher_inputs(targets, r, nf)
+    if spk is not None:
+        raise NotImplementedError("multi-speaker prenet: see decoder_forward_ms (next row)")
+    pre = xin
+    pres = [xin]
+    for i in range(len(d.dec_prenet)):
+        pre = K.linear(pre, P[f"decoder/prenet{i}/kernel"], P[f"decoder/prenet{i}/bias"],
+                       act="relu", mul=mk(f"dec/prenet{i}"))
+        pres.append(pre)
+    S["prenet"] = pres
+    p_w = pre.shape[-1]
+
+    # ---- attention RNN (ZoneoutLSTM A) input projection of the prenet part
+    W0 = P["decoder/attention_lstm/kernel"]          # [p + M1 + M2 + A, 4A] (gate-interleaved)
+    X0 = K.linear(pre, W0[:p_w], P["decoder/attention_lstm/bias"])     # [B, T', 4A]
+    R0 = M1 + M2 + A                                 # recurrent input [c1 | c2 | h0]
+    REC0 = torch.zeros(Tp + 1, B, R0, **f32)
+    C0 = torch.zeros(Tp + 1, B, A, **f32)
+    H0RAW = torch.empty(Tp, B, A, **f32)
+    G0 = torch.empty(Tp, B, 4 * A, **f32)
+    Q = torch.empty(Tp, B, D1 + D2, **f32)
+    S1 = torch.zeros(Tp + 1, B, N, **f32)
+    AL1 = torch.zeros(Tp + 1, B, N, **f32)
+    AL1[0, :, 0] = 1.0                               # forward_attention.py:131-133
+    S2 = torch.empty(Tp, B, N, **f32)
+    ST = torch.empty(Tp, B, 4, **f32)
+    ntiles = (N + attn_tile - 1) // attn_tile
+    pst = K.part_stride(M1, M2)
+    E1 = torch.empty(B, N, **f32)
+    E2 = torch.empty(B, N, **f32)
+    PART = torch.empty(B, ntiles, pst, **f32)
+    att1_fwd = 1 if d.att1 == "forward" else 0
+    if d.att2 != "additive":
+        raise NotImplementedError("attention2 must be 'additive' (hparams.py:98)")
+    a1 = "decoder/attention1"
+    Wr0 = W0[p_w:]
+    zc0, zh0 = mk("dec/lstm0/zc"), mk("dec/lstm0/zh")
+    for t in range(Tp):
+        K.lstm_step_fwd(B=B, U=A, K=R0, t=t, xproj=X0[:, t], rin=REC0[t], W=Wr0,
+                        c_prev=C0[t], h_prev=REC0[t, :, M1 + M2:],
+                        mask_c=None if zc0 is None else zc0[t],
+                        mask_h=None if zh0 is None else zh0[t], zc=zc, zh=zh,
+                        h_raw=H0RAW[t], c_out=C0[t + 1], h_out=REC0[t + 1, :, M1 + M2:],
+                        gates=G0[t])
+        K.attn_query(H0RAW[t], P[f"{a1}/query_layer/kernel"],
+                     P["decoder/attention2/query_layer/kernel"], Q[t])
+        K.attn_step_fwd(
+            B=B, N=N, D1=D1, M1=M1, D2=D2, M2=M2, F=d.loc_f, KW=d.loc_k, NT=attn_tile,
+            ntiles=ntiles, att1_forward=att1_fwd, u=0.5, q=Q[t], q_sb=D1 + D2,
+            K1=K1, V1=V1, K2=K2, V2=V2, lengths=lengths, s_prev=S1[t], a_prev=AL1[t],
+            v1=P[f"{a1}/attention_variable"] if att1_fwd else P[f"{a1}/attention_v"],
+            b1=P[f"{a1}/attention_bias"] if att1_fwd else None,
+            convW=P[f"{a1}/location_conv/kernel"] if att1_fwd else None,
+            convb=P[f"{a1}/location_conv/bias"] if att1_fwd else None,
+            locW=P[f"{a1}/location_layer/kernel"] if att1_fwd else None,
+            v2=P["decoder/attention2/attention_v"], e1=E1, e2=E2, part=PART, part_stride=pst,
+            s_out=S1[t + 1], a_out=AL1[t + 1], s2_out=S2[t], ctx=REC0[t + 1], ctx_sb=R0,
+            stats=ST[t])
+    S.update(X0=X0, REC0=REC0, C0=C0, H0RAW=H0RAW, G0=G0, Q=Q, S1=S1, AL1=AL1, S2=S2, ST=ST)
+
+    # ---- decoder LSTM 1: input o_t = [h0'_t | c1_t | c2_t]  (ConcatOutputAndAttentionWrapper)
+    W1 = P["decoder/lstm1/kernel"]                   # [A + M1 + M2 + D, 4D]
+    X1 = K.linear(H0RAW.view(Tp * B, A), W1[:A], P["decoder/lstm1/bias"])
+    ctx_all = REC0[1:].reshape(Tp * B, R0)[:, :M1 + M2]
+    K.gemm(ctx_all, W1[A:A + M1 + M2], X1, beta=1.0)
+    X1 = X1.view(Tp, B, 4 * Dd)
+    H1RAW, C1S, H1S, G1 = _run_lstm(X1, W1[A + M1 + M2:], Tp, B, Dd, zc, zh,
+                                     mk("dec/lstm1/zc"), mk("dec/lstm1/zh"), f32)
+    # ---- decoder LSTM 2: input h1'_t
+    W2 = P["decoder/lstm2/kernel"]
+    X2 = K.linear(H1RAW.view(Tp * B, Dd), W2[:Dd], P["decoder/lstm2/bias"]).view(Tp, B, 4 * Dd)
+    H2RAW, C2S, H2S, G2 = _run_lstm(X2, W2[Dd:], Tp, B, Dd, zc, zh,
+                                     mk("dec/lstm2/zc"), mk("dec/lstm2/zh"), f32)
+    S.update(X1=X1, H1RAW=H1RAW, C1S=C1S, H1S=H1S, G1=G1, X2=X2, H2RAW=H2RAW, C2S=C2S,
+             H2S=H2S, G2=G2)
+    return H2RAW, DecoderSaved(B, N, Tp, S)
+
+
+def _run_lstm(X, Wr, Tp, B, U, zc, zh, mc, mh, f32):
+    HRAW = torch.empty(Tp, B, U, **f32)
+    CS = torch.zeros(Tp + 1, B, U, **f32)
+    HS = torch.zeros(Tp + 1, B, U, **f32)
+    G = torch.empty(Tp, B, 4 * U, **f32)
+    for t in range(Tp):
+        K.lstm_step_fwd(B=B, U=U, K=U, t=t, xproj=X[t], rin=HS[t], W=Wr, c_prev=CS[t],
+                        h_prev=HS[t], mask_c=None if mc is None else mc[t],
+                        mask_h=None if mh is None else mh[t], zc=zc, zh=zh, h_raw=HRAW[t],
+                        c_out=CS[t + 1], h_out=HS[t + 1], gates=G[t])
+    return HRAW, CS, HS, G

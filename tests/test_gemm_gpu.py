@@ -1,0 +1,80 @@
+"""fp32 MFMA GEMM (sat_gemm) against torch fp64 CPU products, every operand mode."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    return float((a.double().cpu() - b.double()).abs().max() / (b.double().abs().max() + 1e-12))
+
+
+@pytest.mark.parametrize("M,N,K", [(1, 1, 1), (33, 17, 5), (64, 64, 64), (200, 300, 129),
+                                   (1000, 1024, 544), (6400, 128, 2048)])
+@pytest.mark.parametrize("ta,tb", [(False, False), (True, False), (False, True)])
+def test_gemm_dense(cuda, M, N, K, ta, tb):
+    from sat_amd import kernels
+    g = torch.Generator().manual_seed(M * 7 + N)
+    A = torch.randn(K, M, generator=g) if ta else torch.randn(M, K, generator=g)
+    B = torch.randn(N, K, generator=g) if tb else torch.randn(K, N, generator=g)
+    bias = torch.randn(N, generator=g)
+    Ad, Bd = A.to(cuda), B.to(cuda)
+    C = kernels.gemm(Ad.t() if ta else Ad, Bd.t() if tb else Bd, bias=bias.to(cuda), act="tanh")
+    Al, Bl = (A.t() if ta else A).double(), (B.t() if tb else B).double()
+    ref = torch.tanh(Al @ Bl + bias.double())
+    # fp32 accumulation bound (tanh is 1-Lipschitz): |err| <= c * eps32 * (|A| @ |B| + |bias|)
+    bound = 4e-7 * (Al.abs() @ Bl.abs() + bias.double().abs()) + 1e-7
+    assert bool(((C.double().cpu() - ref).abs() <= bound).all())
+
+
+def test_gemm_batched_beta(cuda):
+    from sat_amd import kernels
+    g = torch.Generator().manual_seed(0)
+    A, B, C0 = torch.randn(4, 50, 70, generator=g), torch.randn(4, 70, 30, generator=g), \
+        torch.randn(4, 50, 30, generator=g)
+    C = C0.to(cuda)
+    kernels.gemm(A.to(cuda), B.to(cuda), C, alpha=0.5, beta=2.0)
+    ref = 0.5 * A.double() @ B.double() + 2.0 * C0.double()
+    assert _rel(C, ref) < 1e-5
+
+
+def _conv_ref(x, W, b=None):
+    from oracle.sat_oracle import conv1d_same
+    return conv1d_same(x.double(), W.double(), None if b is None else b.double())
+
+
+@pytest.mark.parametrize("taps", [1, 2, 3, 10, 16])
+def test_conv1d_fwd_dx_dw(cuda, taps):
+    from sat_amd import kernels
+    g = torch.Generator().manual_seed(taps)
+    S, L, Ci, Co = 3, 37, 24, 20
+    x = torch.randn(S, L, Ci, generator=g, dtype=torch.float64, requires_grad=True)
+    W = torch.randn(taps, Ci, Co, generator=g, dtype=torch.float64, requires_grad=True)
+    b = torch.randn(Co, generator=g, dtype=torch.float64)
+    y = _conv_ref(x, W, b)
+    dy = torch.randn(S, L, Co, generator=g, dtype=torch.float64)
+    y.backward(dy)
+    xd, Wd = x.detach().float().to(cuda), W.detach().float().to(cuda)
+    yd = kernels.conv1d(xd, Wd, b.float().to(cuda))
+    assert _rel(yd, y.detach()) < 1e-5
+    dxd = kernels.conv1d_dx(dy.float().to(cuda), Wd)
+    assert _rel(dxd, x.grad) < 1e-5
+    dWd = torch.empty_like(Wd)
+    kernels.conv1d_dw(xd, dy.float().to(cuda), dWd)
+    assert _rel(dWd, W.grad) < 1e-5
+
+
+def test_rng_fill(cuda):
+    from sat_amd import kernels
+    seed = torch.tensor([1234], dtype=torch.int64, device=cuda)
+    out = torch.empty(1_000_003, device=cuda)
+    kernels.rng_fill(out, seed, 7, 0.9, 1.0 / 0.9)
+    vals = out.cpu()
+    keep = float((vals != 0).double().mean())
+    assert abs(keep - 0.9) < 3e-3
+    assert torch.allclose(vals[vals != 0], torch.tensor(1.0 / 0.9))
+    out2 = torch.empty_like(out)
+    kernels.rng_fill(out2, seed, 7, 0.9, 1.0 / 0.9)
+    assert torch.equal(out, out2)
+    kernels.rng_fill(out2, seed, 8, 0.9, 1.0 / 0.9)
+    assert not torch.equal(out, out2)

@@ -1,0 +1,177 @@
+"""CPU tests of the oracle restatement (no GPU).
+
+The reference's only behavioural test, ``modules/transformer_test.py:44-90``, asserts that the
+RNNTransformer training branch (loop, then post-hoc causal self-attention) equals the
+teacher-forced incremental branch (self-attention re-run over the growing history) -- ported
+here as a hypothesis property on the oracle, plus unit checks of the TF semantics the oracle
+restates.
+"""
+import numpy as np
+import pytest
+import torch
+from hypothesis import given, settings, strategies as st
+
+from oracle import sat_oracle as O
+
+
+def _sa_params(dim, heads, seed):
+    g = torch.Generator().manual_seed(seed)
+    p = {}
+    for name in ("query", "key", "value", "output"):
+        p[f"decoder/self_attention0/mha/{name}_projection/kernel"] = \
+            torch.randn(dim, dim, generator=g, dtype=torch.float64) / dim ** 0.5
+        p[f"decoder/self_attention0/mha/{name}_projection/bias"] = \
+            torch.randn(dim, generator=g, dtype=torch.float64) * 0.1
+    p["decoder/self_attention0/transform/kernel"] = torch.randn(dim, dim, generator=g,
+                                                                dtype=torch.float64) / dim ** 0.5
+    p["decoder/self_attention0/transform/bias"] = torch.zeros(dim, dtype=torch.float64)
+    return p
+
+
+@settings(max_examples=25, deadline=None)
+@given(batch=st.integers(1, 3), dim=st.integers(1, 10).map(lambda x: 2 * x),
+       t_factor=st.integers(2, 8), r=st.integers(1, 2), seed=st.integers(0, 2 ** 16))
+def test_equality_between_training_and_inference(batch, dim, t_factor, r, seed):
+    """modules/transformer_test.py:44-90: one-hot targets, plain LSTMCell(dim*r) decoder cell,
+    RNNTransformer with 2 heads and dropout 0; training branch == incremental branch."""
+    from sat_amd import hparams
+    rng = np.random.default_rng(seed)
+    T = t_factor * r
+    ids = rng.integers(0, dim, size=(batch, T))
+    tgt = torch.zeros(batch, T, dim, dtype=torch.float64)
+    tgt.scatter_(2, torch.tensor(ids).unsqueeze(-1), 1.0)
+    units = dim * r
+    hp = hparams.ljspeech_hparams(num_mels=dim, outputs_per_step=r, n_feed_frame=r,
+                                  decoder_self_attention_num_heads=2,
+                                  decoder_self_attention_out_units=units, decoder_out_units=units)
+    p = _sa_params(units, 2, seed)
+    g = torch.Generator().manual_seed(seed + 1)
+    p["decoder/out_projection/kernel"] = torch.randn(units, dim * r, generator=g, dtype=torch.float64)
+    p["decoder/out_projection/bias"] = torch.zeros(dim * r, dtype=torch.float64)
+    p["decoder/stop_token_projection/kernel"] = torch.randn(units, 1, generator=g, dtype=torch.float64)
+    p["decoder/stop_token_projection/bias"] = torch.zeros(1, dtype=torch.float64)
+    W = torch.randn(dim * r + units, 4 * units, generator=g, dtype=torch.float64) * 0.3
+    bvec = torch.zeros(4 * units, dtype=torch.float64)
+    x = O.teacher_inputs(tgt, r, r)
+    c = h = torch.zeros(batch, units, dtype=torch.float64)
+    outs = []
+    for t in range(x.shape[1]):
+        h, c = O.lstm_cell(x[:, t], c, h, W, bvec)
+        outs.append(h)
+    dout = torch.stack(outs, 1)
+    mel_t, stop_t, _ = O.decoder_head(dout, p, hp, None)
+    mel_i, stop_i = O.decoder_head_incremental(dout, p, hp)
+    np.testing.assert_allclose(mel_t.numpy(), mel_i.numpy(), rtol=1e-6, atol=1e-6)
+    np.testing.assert_allclose(stop_t.numpy(), stop_i.numpy(), rtol=1e-6, atol=1e-6)
+    # argmax samples (modules/module.py:760-763)
+    s_t = mel_t.view(batch, -1, r, dim).argmax(-1)
+    s_i = mel_i.view(batch, -1, r, dim).argmax(-1)
+    assert torch.equal(s_t, s_i)
+
+
+def test_full_model_training_equals_incremental_head():
+    from sat_amd import hparams, params, data
+    hp = hparams.ljspeech_hparams()
+    p = O.to_torch(params.init_params(hp, seed=3))
+    bufs = O.to_torch(params.init_bn_buffers(hp))
+    b = O.to_torch(data.synthetic_batch(hp, 2, N=9, T=12, shape="ljs", seed=1))
+    out = O.model_forward(p, bufs, hp, b, None, training=False)
+    mel_i, stop_i = O.decoder_head_incremental(out["dout"], p, hp)
+    np.testing.assert_allclose(out["mel"].reshape(mel_i.shape).numpy(), mel_i.numpy(),
+                               rtol=1e-9, atol=1e-9)
+    np.testing.assert_allclose(out["stop"].numpy(), stop_i.numpy(), rtol=1e-9, atol=1e-9)
+
+
+def test_conv1d_same_padding_even_kernel():
+    # TF SAME for k=10: pad_left = 4, pad_right = 5 (cross-correlation)
+    x = torch.zeros(1, 12, 1, dtype=torch.float64)
+    x[0, 6, 0] = 1.0
+    w = torch.arange(10, dtype=torch.float64).view(10, 1, 1)
+    y = O.conv1d_same(x, w, None)[0, :, 0]
+    # y[n] = sum_j x[n + j - 4] w[j]  ->  nonzero where n + j - 4 == 6  ->  y[n] = w[10 - n]
+    expect = torch.tensor([0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0], dtype=torch.float64)
+    for n in range(12):
+        j = 6 + 4 - n
+        if 0 <= j < 10:
+            expect[n] = j
+    assert torch.equal(y, expect)
+
+
+def test_maxpool_same():
+    x = torch.tensor([[[1.0], [3.0], [2.0], [0.0]]], dtype=torch.float64)
+    assert O.maxpool2_same(x)[0, :, 0].tolist() == [3.0, 3.0, 2.0, 0.0]
+
+
+def test_zoneout_eval_blend_and_masks():
+    g = torch.Generator().manual_seed(0)
+    x, c, h = (torch.randn(2, 3, generator=g, dtype=torch.float64) for _ in range(3))
+    W = torch.randn(6, 12, generator=g, dtype=torch.float64)
+    b = torch.zeros(12, dtype=torch.float64)
+    hr, cr = O.lstm_cell(x, c, h, W, b)
+    out, c2, h2 = O.zoneout_lstm_step(x, c, h, W, b, 0.1, 0.1, None, None)
+    assert torch.allclose(out, hr)
+    assert torch.allclose(c2, 0.9 * cr + 0.1 * c) and torch.allclose(h2, 0.9 * hr + 0.1 * h)
+    m = torch.tensor([[1.0, 0.0, 1.0], [0.0, 1.0, 0.0]], dtype=torch.float64)
+    _, c3, h3 = O.zoneout_lstm_step(x, c, h, W, b, 0.1, 0.1, m, m)
+    assert torch.allclose(c3, m * cr + (1 - m) * c) and torch.allclose(h3, m * hr + (1 - m) * h)
+
+
+def test_forward_attention_properties():
+    """alpha sums to 1, is exactly 0 past the memory length, and starts monotonic at n=0."""
+    from sat_amd import hparams, params
+    hp = hparams.ljspeech_hparams()
+    p = O.to_torch(params.init_params(hp, seed=1))
+    g = torch.Generator().manual_seed(0)
+    mem = torch.randn(2, 11, 256, generator=g, dtype=torch.float64)
+    lens = torch.tensor([11, 6])
+    att = O.ForwardAttentionOracle(p, "decoder/attention1", mem, lens)
+    st_ = att.initial_state(2, 11, torch.float64)
+    for _ in range(5):
+        q = torch.randn(2, 256, generator=g, dtype=torch.float64)
+        a, st_ = att(q, st_)
+        assert torch.allclose(a.sum(1), torch.ones(2, dtype=torch.float64))
+        assert float(a[1, 6:].abs().max()) == 0.0
+    # after one step from alpha_0 = onehot(0), mass can only be at n in {0, 1} up to the 1e-7 floor
+    st0 = att.initial_state(2, 11, torch.float64)
+    a1, _ = att(torch.zeros(2, 256, dtype=torch.float64), st0)
+    assert float(a1[:, 2:].sum()) < 1e-4
+
+
+def test_losses_sum_by_nonzero_weights():
+    mel = torch.zeros(1, 4, 2, dtype=torch.float64)
+    tgt = torch.ones(1, 4, 2, dtype=torch.float64)
+    mask = torch.tensor([[1.0, 1.0, 0.0, 0.0]], dtype=torch.float64)
+    stop = torch.zeros(1, 2, 1, dtype=torch.float64)
+    done = torch.tensor([[0.0, 1.0]], dtype=torch.float64)
+    dmask = torch.tensor([[1.0, 0.0]], dtype=torch.float64)
+    loss, l1, bce = O.losses(mel, stop, tgt, mask, done, dmask)
+    assert float(l1) == pytest.approx(1.0)
+    assert float(bce) == pytest.approx(np.log(2.0))
+    assert float(loss) == pytest.approx(0.1 + np.log(2.0))
+
+
+def test_learning_rate_and_adam():
+    assert O.learning_rate(5e-4, 0) == pytest.approx(5e-4 * 4000 ** 0.5 * 4000 ** -1.5)
+    assert O.learning_rate(5e-4, 3999) == pytest.approx(5e-4 * 4000 ** 0.5 * 4000 ** -0.5)
+    assert O.learning_rate(5e-4, 15999) < O.learning_rate(5e-4, 3999)
+    p = torch.ones(3, dtype=torch.float64)
+    g = torch.tensor([1.0, -2.0, 0.0], dtype=torch.float64)
+    p2, m, v = O.adam_tf(p, g, torch.zeros(3, dtype=torch.float64),
+                         torch.zeros(3, dtype=torch.float64), 0.1, 1)
+    # first step of TF Adam moves every non-zero-gradient coordinate by ~lr against the sign
+    assert torch.allclose(p2[:2], torch.tensor([0.9, 1.1], dtype=torch.float64), atol=1e-6)
+    clipped, norm = O.clip_by_global_norm([torch.tensor([3.0, 4.0])], 1.0)
+    assert norm == pytest.approx(5.0) and torch.allclose(clipped[0], torch.tensor([0.6, 0.8]))
+
+
+def test_oracle_gradients_flow_everywhere():
+    from sat_amd import hparams, params, data
+    hp = hparams.ljspeech_hparams()
+    p = {k: v.requires_grad_(True) for k, v in O.to_torch(params.init_params(hp)).items()}
+    bufs = O.to_torch(params.init_bn_buffers(hp))
+    b = O.to_torch(data.synthetic_batch(hp, 2, N=8, T=8, shape="max", seed=2))
+    m = O.to_torch(data.synthetic_masks(hp, 2, 8, 4, seed=3))
+    out = O.model_forward(p, bufs, hp, b, m, training=True)
+    out["loss"].backward()
+    missing = [k for k, v in p.items() if v.grad is None]
+    assert missing == []

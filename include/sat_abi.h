@@ -54,6 +54,10 @@ int sat_device_arch(char* buf, int len);       /* gcnArchName of the current dev
  *                   B = W[((taps-1-tap)*N + n)*b_C + o]                     (conv dX)
  * act: 0 none, 1 relu, 2 tanh, 3 sigmoid.  bias may be NULL.
  * mul (optional, [M][N] row stride mul_sm): C = act(...) * mul  (fused dropout masks).
+ * add (optional, row stride add_sm, 0 = broadcast one row): C = act(...) * mul + add
+ *     (fused residual connections, e.g. SelfAttentionTransformer x + tanh(Dense(.))).
+ * Batching: blockIdx.z = z1 * batch2 + z2 (batch = z1 count, batch2 >= 1 inner count); every
+ * operand is offset by z1 * s?batch + z2 * s?batch2 (e.g. z1 = utterance, z2 = head).
  */
 typedef struct SatGemmDesc {
   int32_t M, N, K, batch;
@@ -70,6 +74,10 @@ typedef struct SatGemmDesc {
   float alpha, beta;
   const float* mul;
   int64_t mul_sm, mul_sbatch;
+  int32_t batch2, pad0;
+  int64_t a_sbatch2, b_sbatch2, c_sbatch2, mul_sbatch2;
+  const float* add;
+  int64_t add_sm, add_sbatch;
 } SatGemmDesc;
 
 int sat_gemm(const SatGemmDesc* desc, void* stream);
@@ -174,6 +182,69 @@ int sat_attn_step_fwd(const SatAttnStep* args, void* stream);
  * out[b,n,:] = x[b,n,:] * (n < lengths[b])  -- TF _prepare_memory (memory_sequence_length). */
 int sat_seq_mask(const float* x, float* out, int32_t B, int32_t N, int32_t C,
                  const int64_t* lengths, void* stream);
+
+/* Embedding lookup (ext tacotron2 Embedding, models/models.py:28,54): out[r] = table[ids[r]-offset];
+ * an id outside [offset, offset+V) writes zeros and sets *err = 1 (the reference's
+ * tf.assert_* raises InvalidArgumentError).  Backward: fp32 atomic scatter-add. */
+int sat_embedding_fwd(const float* table, const int64_t* ids, float* out, int64_t R, int32_t D,
+                      int32_t V, int64_t offset, int32_t* err, void* stream);
+int sat_embedding_bwd(const float* dout, const int64_t* ids, float* dtable, int64_t R, int32_t D,
+                      int32_t V, int64_t offset, void* stream);
+
+/* Column reductions over x [M][C] (row stride ld*): workspace of sat_workspace_colreduce bytes. */
+int64_t sat_workspace_colreduce(int32_t M, int32_t C);
+/* tf.layers.BatchNormalization (inside ext tacotron2 Conv1d, modules/module.py:46-68):
+ * training statistics over every row (biased var), moving averages with `momentum`
+ * (mov_* may be NULL); apply y = gamma (x-mean)/sqrt(var+eps) + beta [relu] [+ res];
+ * backward: dgamma/dbeta ACCUMULATE, dx = beta_out*dx + BN'(gate(dy)) where gate = the
+ * post-ReLU output (NULL if no ReLU); training=0 differentiates the moving-stat (eval) form. */
+int sat_bn_stats(const float* x, int64_t ldx, int32_t M, int32_t C, float* mean, float* var,
+                 float* mov_mean, float* mov_var, float momentum, void* workspace, void* stream);
+int sat_bn_apply(const float* x, int64_t ldx, float* y, int64_t ldy, int32_t M, int32_t C,
+                 const float* mean, const float* var, float eps, const float* gamma,
+                 const float* beta, int32_t relu, const float* res, int64_t ldr, void* stream);
+int sat_bn_bwd(const float* dy, int64_t lddy, const float* x, int64_t ldx, const float* gate,
+               int64_t ldg, float* dx, int64_t lddx, int32_t M, int32_t C, const float* mean,
+               const float* var, float eps, const float* gamma, float* dgamma, float* dbeta,
+               int32_t training, float beta_out, void* workspace, void* stream);
+/* out[c] = beta*out[c] + sum_m x[m][c]   (bias gradients) */
+int sat_colsum(const float* x, int64_t ldx, int32_t M, int32_t C, float* out, float beta,
+               void* workspace, void* stream);
+
+/* MaxPooling1D(pool 2, stride 1, SAME) over [B][N][C] (modules/module.py:54,80) and its
+ * gradient (first index wins ties, as TF MaxPoolGrad). */
+int sat_maxpool2(const float* x, float* y, int32_t B, int32_t N, int32_t C, void* stream);
+int sat_maxpool2_bwd(const float* x, const float* dy, float* dx, int32_t B, int32_t N, int32_t C,
+                     void* stream);
+
+/* ext tacotron2 HighwayNet combine y = h*t + x*(1-t) (h = ReLU dense, t = sigmoid dense) and
+ * its backward to the pre-activations (dh_pre, dt_pre) and the carry path dx. */
+int sat_highway_fwd(const float* h, const float* t, const float* x, float* y, int64_t n,
+                    void* stream);
+int sat_highway_bwd(const float* h, const float* t, const float* x, const float* dy,
+                    float* dh_pre, float* dt_pre, float* dx, int64_t n, void* stream);
+
+/* dx = beta*dx + dy * act'(y) [* mask]; act 0 identity, 1 relu, 2 tanh, 3 sigmoid. */
+int sat_act_bwd(const float* dy, const float* y, const float* mask, float* dx, int64_t n,
+                int32_t act, float beta, void* stream);
+/* y = a*x + b*y */
+int sat_axpby(const float* x, float* y, int64_t n, float a, float b, void* stream);
+
+/* ScaledDotProductAttentionMechanism softmax (modules/self_attention.py:45-65):
+ * P = softmax(scale*S) per row of length L, causal (use_subsequent_mask) masks col > row%Lq,
+ * Pd = P * mask (tf.layers.dropout on the probabilities).  Backward gives dS. */
+int sat_softmax_fwd(const float* S, float* P, float* Pd, const float* mask, int64_t R, int32_t L,
+                    int32_t Lq, int32_t causal, float scale, void* stream);
+int sat_softmax_bwd(const float* P, const float* dPd, const float* mask, float* dS, int64_t R,
+                    int32_t L, float scale, void* stream);
+
+/* Loss of models/models.py:159-173: l1_weight * L1(mel, tgt; tmask) + sigmoid xent(stop, done;
+ * dmask), tf.losses SUM_BY_NONZERO_WEIGHTS.  out[0..4] = loss, L1, BCE, counts; if dmel/dstop
+ * are given, also writes the gradients of out[0]. */
+int sat_loss_fwd_bwd(const float* mel, const float* tgt, const float* tmask, const float* stop,
+                     const float* done, const float* dmask, int32_t B, int32_t T, int32_t M,
+                     int32_t Tp, float l1_weight, float* out, float* dmel, float* dstop,
+                     void* stream);
 
 #ifdef __cplusplus
 }

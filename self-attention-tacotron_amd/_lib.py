@@ -36,6 +36,10 @@ class SatGemmDesc(ctypes.Structure):
         ("bias", ctypes.c_void_p), ("bias_sbatch", ctypes.c_int64),
         ("alpha", ctypes.c_float), ("beta", ctypes.c_float),
         ("mul", ctypes.c_void_p), ("mul_sm", ctypes.c_int64), ("mul_sbatch", ctypes.c_int64),
+        ("batch2", ctypes.c_int32), ("pad0", ctypes.c_int32),
+        ("a_sbatch2", ctypes.c_int64), ("b_sbatch2", ctypes.c_int64),
+        ("c_sbatch2", ctypes.c_int64), ("mul_sbatch2", ctypes.c_int64),
+        ("add", ctypes.c_void_p), ("add_sm", ctypes.c_int64), ("add_sbatch", ctypes.c_int64),
     ]
 
 
@@ -80,7 +84,25 @@ SIGNATURES = {
     "sat_attn_query": [_I32, _I32, _I32, _I32, _P, _I64, _P, _P, _P, _I64, _P],
     "sat_attn_step_fwd": [ctypes.POINTER(SatAttnStep), _P],
     "sat_seq_mask": [_P, _P, _I32, _I32, _I32, _P, _P],
+    "sat_embedding_fwd": [_P, _P, _P, _I64, _I32, _I32, _I64, _P, _P],
+    "sat_embedding_bwd": [_P, _P, _P, _I64, _I32, _I32, _I64, _P],
+    "sat_bn_stats": [_P, _I64, _I32, _I32, _P, _P, _P, _P, _F, _P, _P],
+    "sat_bn_apply": [_P, _I64, _P, _I64, _I32, _I32, _P, _P, _F, _P, _P, _I32, _P, _I64, _P],
+    "sat_bn_bwd": [_P, _I64, _P, _I64, _P, _I64, _P, _I64, _I32, _I32, _P, _P, _F, _P, _P, _P,
+                   _I32, _F, _P, _P],
+    "sat_colsum": [_P, _I64, _I32, _I32, _P, _F, _P, _P],
+    "sat_maxpool2": [_P, _P, _I32, _I32, _I32, _P],
+    "sat_maxpool2_bwd": [_P, _P, _P, _I32, _I32, _I32, _P],
+    "sat_highway_fwd": [_P, _P, _P, _P, _I64, _P],
+    "sat_highway_bwd": [_P, _P, _P, _P, _P, _P, _P, _I64, _P],
+    "sat_act_bwd": [_P, _P, _P, _P, _I64, _I32, _F, _P],
+    "sat_axpby": [_P, _P, _I64, _F, _F, _P],
+    "sat_softmax_fwd": [_P, _P, _P, _P, _I64, _I32, _I32, _I32, _F, _P],
+    "sat_softmax_bwd": [_P, _P, _P, _P, _I64, _I32, _F, _P],
+    "sat_loss_fwd_bwd": [_P, _P, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _F, _P, _P, _P, _P],
 }
+
+RESTYPES = {"sat_workspace_colreduce": (ctypes.c_int64, [_I32, _I32])}
 
 _lib: Optional[ctypes.CDLL] = None
 
@@ -98,12 +120,16 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         fn.restype = ctypes.c_int
     lib.sat_last_error_string.argtypes = []
     lib.sat_last_error_string.restype = ctypes.c_char_p
+    for name, (res, argtypes) in RESTYPES.items():
+        fn = getattr(lib, name)
+        fn.argtypes = argtypes
+        fn.restype = res
     _lib = lib
     return lib
 
 
 def exported_symbols():
-    return list(SIGNATURES) + ["sat_last_error_string"]
+    return list(SIGNATURES) + list(RESTYPES) + ["sat_last_error_string"]
 
 
 def check(rc: int, what: str) -> None:

@@ -1,18 +1,349 @@
-// Small bandwidth-bound kernels of the path (vectorised where the shapes allow).
+// Bandwidth-bound kernels of the path: memory masking, embedding, BatchNormalization, max-pool,
+// highway combine, row softmax (self-attention), activation backward, the fused loss.
+// All reductions are deterministic (fixed per-thread order + fixed-shape tree), except the
+// embedding backward scatter-add (fp32 atomics, ~1.6 M adds per step).
 #include "sat_common.h"
 
 namespace sat {
 namespace {
 
-// out[b, n, :] = x[b, n, :] * (n < len[b])      (TF _prepare_memory / sequence_mask)
+inline int grid_for(int64_t n, int block = 256, int cap = 4096) {
+  return (int)std::max<int64_t>(1, std::min<int64_t>((n + block - 1) / block, cap));
+}
+
+#define GRID_STRIDE(i, n) \
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < (n); i += (int64_t)gridDim.x * blockDim.x)
+
+// ---------------------------------------------------------------- memory masking
 __global__ void seq_mask_kernel(const float* __restrict__ x, float* __restrict__ out, int B, int N,
                                 int C, const int64_t* __restrict__ lengths) {
   const int64_t total = (int64_t)B * N * C;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
-       i += (int64_t)gridDim.x * blockDim.x) {
+  GRID_STRIDE(i, total) {
     const int64_t row = i / C;
     const int b = (int)(row / N), n = (int)(row - (int64_t)b * N);
     out[i] = n < lengths[b] ? x[i] : 0.f;
+  }
+}
+
+// ---------------------------------------------------------------- embedding (ext tacotron2)
+__global__ void embed_fwd_kernel(const float* __restrict__ table, const int64_t* __restrict__ ids,
+                                 float* __restrict__ out, int64_t R, int D, int V, int64_t offset,
+                                 int* err) {
+  GRID_STRIDE(i, R * D) {
+    const int64_t r = i / D;
+    const int c = (int)(i - r * D);
+    const int64_t id = ids[r] - offset;
+    if (id < 0 || id >= V) {
+      out[i] = 0.f;
+      if (err) *err = 1;
+    } else {
+      out[i] = table[id * D + c];
+    }
+  }
+}
+
+__global__ void embed_bwd_kernel(const float* __restrict__ dout, const int64_t* __restrict__ ids,
+                                 float* __restrict__ dtable, int64_t R, int D, int V, int64_t offset) {
+  GRID_STRIDE(i, R * D) {
+    const int64_t r = i / D;
+    const int c = (int)(i - r * D);
+    const int64_t id = ids[r] - offset;
+    if (id >= 0 && id < V) atomicAdd(&dtable[id * D + c], dout[i]);
+  }
+}
+
+// ---------------------------------------------------------------- column reductions
+// out1[c] = sum_m x[m, c]  (and out2[c] = sum_m x[m,c]*y[m,c] when y != null), fp64 accumulation.
+// Block = 256 threads = 64 columns x 4 row groups; grid = ceil(C/64) x RB row blocks (partials
+// combined by a second pass in colreduce_finish).
+__global__ void colreduce_kernel(const float* __restrict__ x, int64_t ldx, const float* __restrict__ y,
+                                 int64_t ldy, int M, int C, double* __restrict__ part1,
+                                 double* __restrict__ part2, int mode, const float* __restrict__ mean,
+                                 const float* __restrict__ var, float eps, const float* __restrict__ gate,
+                                 int64_t ldg) {
+  // mode 0: sum(x), sum(x*x)         (BN statistics; part2 = sum of squares)
+  // mode 1: sum(dy), sum(dy * xhat)  (BN backward; x = dy, y = pre-BN input, mean/var given,
+  //                                   gate = post-BN ReLU output or null)
+  // mode 2: sum(x), sum(x * y)       (bias grads / generic)
+  __shared__ double s1[4][64], s2[4][64];
+  const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  const int rows_per = (M + gridDim.y - 1) / gridDim.y;
+  const int r0 = blockIdx.y * rows_per, r1 = min(M, r0 + rows_per);
+  double a1 = 0.0, a2 = 0.0;
+  if (c < C) {
+    float mu = 0.f, rs = 0.f;
+    if (mode == 1) { mu = mean[c]; rs = rsqrtf(var[c] + eps); }
+    for (int m = r0 + grp; m < r1; m += 4) {
+      float v = x[(int64_t)m * ldx + c];
+      if (mode == 0) { a1 += v; a2 += (double)v * v; }
+      else if (mode == 1) {
+        if (gate && gate[(int64_t)m * ldg + c] <= 0.f) v = 0.f;
+        const float xh = (y[(int64_t)m * ldy + c] - mu) * rs;
+        a1 += v; a2 += (double)v * xh;
+      } else {
+        a1 += v;
+        if (y) a2 += (double)v * y[(int64_t)m * ldy + c];
+      }
+    }
+  }
+  s1[grp][lane] = a1;
+  s2[grp][lane] = a2;
+  __syncthreads();
+  if (grp == 0 && c < C) {
+    part1[(int64_t)blockIdx.y * C + c] = s1[0][lane] + s1[1][lane] + s1[2][lane] + s1[3][lane];
+    part2[(int64_t)blockIdx.y * C + c] = s2[0][lane] + s2[1][lane] + s2[2][lane] + s2[3][lane];
+  }
+}
+
+// BN statistics finish: mean, biased var; moving averages (momentum, Bessel-corrected var).
+__global__ void bn_stats_finish_kernel(const double* part1, const double* part2, int RB, int M, int C,
+                                       float* mean, float* var, float* mov_mean, float* mov_var,
+                                       float momentum) {
+  GRID_STRIDE(c, (int64_t)C) {
+    double s = 0.0, q = 0.0;
+    for (int r = 0; r < RB; ++r) { s += part1[(int64_t)r * C + c]; q += part2[(int64_t)r * C + c]; }
+    const double mu = s / M;
+    const double v = fmax(q / M - mu * mu, 0.0);
+    mean[c] = (float)mu;
+    var[c] = (float)v;
+    if (mov_mean) {
+      const double unb = M > 1 ? v * M / (M - 1) : v;
+      mov_mean[c] = (float)(momentum * mov_mean[c] + (1.0 - momentum) * mu);
+      mov_var[c] = (float)(momentum * mov_var[c] + (1.0 - momentum) * unb);
+    }
+  }
+}
+
+// generic finish: out1[c] = beta*out1[c] + sum1 ; out2 likewise (either may be null)
+// and, when given, acc1[c] += sum1, acc2[c] += sum2 (gradient accumulation)
+__global__ void colreduce_finish_kernel(const double* part1, const double* part2, int RB, int C,
+                                        float* out1, float* out2, float beta, float* acc1,
+                                        float* acc2) {
+  GRID_STRIDE(c, (int64_t)C) {
+    double s = 0.0, q = 0.0;
+    for (int r = 0; r < RB; ++r) { s += part1[(int64_t)r * C + c]; q += part2[(int64_t)r * C + c]; }
+    if (out1) out1[c] = (float)(beta * out1[c] + s);
+    if (out2) out2[c] = (float)(beta * out2[c] + q);
+    if (acc1) acc1[c] += (float)s;
+    if (acc2) acc2[c] += (float)q;
+  }
+}
+
+// ---------------------------------------------------------------- BatchNormalization apply / bwd
+__global__ void bn_apply_kernel(const float* __restrict__ x, int64_t ldx, float* __restrict__ y,
+                                int64_t ldy, int M, int C, const float* __restrict__ mean,
+                                const float* __restrict__ var, float eps, const float* __restrict__ gamma,
+                                const float* __restrict__ beta, int relu, const float* __restrict__ res,
+                                int64_t ldr) {
+  GRID_STRIDE(i, (int64_t)M * C) {
+    const int64_t m = i / C;
+    const int c = (int)(i - m * C);
+    float v = gamma[c] * (x[m * ldx + c] - mean[c]) * rsqrtf(var[c] + eps) + beta[c];
+    if (relu) v = fmaxf(v, 0.f);
+    if (res) v += res[m * ldr + c];
+    y[m * ldy + c] = v;
+  }
+}
+
+// dx = gamma*rstd*(g - s1/M - xhat*s2/M)   (training) ; gamma*rstd*g (eval), g = gated dy
+__global__ void bn_bwd_apply_kernel(const float* __restrict__ dy, int64_t lddy, const float* __restrict__ x,
+                                    int64_t ldx, const float* __restrict__ gate, int64_t ldg,
+                                    float* __restrict__ dx, int64_t lddx, int M, int C,
+                                    const float* __restrict__ mean, const float* __restrict__ var,
+                                    float eps, const float* __restrict__ gamma,
+                                    const float* __restrict__ sum_dy, const float* __restrict__ sum_dyx,
+                                    int training, float beta_out) {
+  GRID_STRIDE(i, (int64_t)M * C) {
+    const int64_t m = i / C;
+    const int c = (int)(i - m * C);
+    float g = dy[m * lddy + c];
+    if (gate && gate[m * ldg + c] <= 0.f) g = 0.f;
+    const float rs = rsqrtf(var[c] + eps);
+    float v;
+    if (training) {
+      const float xh = (x[m * ldx + c] - mean[c]) * rs;
+      v = gamma[c] * rs * (g - sum_dy[c] / M - xh * sum_dyx[c] / M);
+    } else {
+      v = gamma[c] * rs * g;
+    }
+    float* o = dx + m * lddx + c;
+    *o = beta_out != 0.f ? beta_out * (*o) + v : v;
+  }
+}
+
+// ---------------------------------------------------------------- MaxPooling1D(2, 1, SAME)
+__global__ void maxpool_fwd_kernel(const float* __restrict__ x, float* __restrict__ y, int B, int N,
+                                   int C) {
+  GRID_STRIDE(i, (int64_t)B * N * C) {
+    const int64_t row = i / C;
+    const int n = (int)(row % N);
+    const float a = x[i];
+    y[i] = (n + 1 < N) ? fmaxf(a, x[i + C]) : a;
+  }
+}
+
+// routes dy[n] to argmax of window {n, n+1} (first index on ties, as TF MaxPoolGrad)
+__global__ void maxpool_bwd_kernel(const float* __restrict__ x, const float* __restrict__ dy,
+                                   float* __restrict__ dx, int B, int N, int C) {
+  GRID_STRIDE(i, (int64_t)B * N * C) {
+    const int64_t row = i / C;
+    const int n = (int)(row % N);
+    float g = 0.f;
+    // own window n: goes to n if x[n] >= x[n+1] (or n is last)
+    if (n + 1 >= N || x[i] >= x[i + C]) g += dy[i];
+    // window n-1 picks n when x[n-1] < x[n]
+    if (n > 0 && x[i - C] < x[i]) g += dy[i - C];
+    dx[i] = g;
+  }
+}
+
+// ---------------------------------------------------------------- HighwayNet (ext tacotron2)
+__global__ void highway_fwd_kernel(const float* __restrict__ h, const float* __restrict__ t,
+                                   const float* __restrict__ x, float* __restrict__ y, int64_t n) {
+  GRID_STRIDE(i, n) { y[i] = h[i] * t[i] + x[i] * (1.f - t[i]); }
+}
+
+__global__ void highway_bwd_kernel(const float* __restrict__ h, const float* __restrict__ t,
+                                   const float* __restrict__ x, const float* __restrict__ dy,
+                                   float* __restrict__ dh_pre, float* __restrict__ dt_pre,
+                                   float* __restrict__ dx, int64_t n) {
+  GRID_STRIDE(i, n) {
+    const float g = dy[i], tv = t[i], hv = h[i];
+    dh_pre[i] = hv > 0.f ? g * tv : 0.f;
+    dt_pre[i] = g * (hv - x[i]) * tv * (1.f - tv);
+    dx[i] = g * (1.f - tv);
+  }
+}
+
+// ---------------------------------------------------------------- activation backward
+// dx = dy * act'(y) [* mask], act: 1 relu (y>0), 2 tanh (1-y^2), 3 sigmoid y(1-y), 0 identity
+__global__ void act_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ y,
+                               const float* __restrict__ mask, float* __restrict__ dx, int64_t n,
+                               int act, float beta) {
+  GRID_STRIDE(i, n) {
+    float g = dy[i];
+    if (mask) g *= mask[i];
+    const float yv = y ? y[i] : 0.f;
+    if (act == 1) g = yv > 0.f ? g : 0.f;
+    else if (act == 2) g *= 1.f - yv * yv;
+    else if (act == 3) g *= yv * (1.f - yv);
+    dx[i] = beta != 0.f ? beta * dx[i] + g : g;
+  }
+}
+
+__global__ void axpby_kernel(const float* __restrict__ x, float* __restrict__ y, int64_t n, float a,
+                             float b) {
+  GRID_STRIDE(i, n) { y[i] = a * x[i] + (b != 0.f ? b * y[i] : 0.f); }
+}
+
+// ---------------------------------------------------------------- row softmax (self-attention)
+// P = softmax(scale * S) over the last dim, optional causal mask (col > row-in-sequence -> -inf),
+// Pd = P * mask (dropout on probabilities).  One wave per row.
+__global__ void softmax_fwd_kernel(const float* __restrict__ S, float* __restrict__ P,
+                                   float* __restrict__ Pd, const float* __restrict__ mask, int64_t R,
+                                   int L, int Lq, int causal, float scale) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = blockIdx.x * (int64_t)(blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (r >= R) return;
+  const int qi = (int)(r % Lq);
+  const int lim = causal ? min(L, qi + 1) : L;
+  const float* s = S + r * L;
+  float mx = -INFINITY;
+  for (int j = lane; j < lim; j += 64) mx = fmaxf(mx, s[j] * scale);
+  mx = wave_max(mx);
+  float z = 0.f;
+  for (int j = lane; j < lim; j += 64) z += expf(s[j] * scale - mx);
+  z = wave_sum(z);
+  const float inv = 1.f / z;
+  for (int j = lane; j < L; j += 64) {
+    const float pv = j < lim ? expf(s[j] * scale - mx) * inv : 0.f;
+    P[r * L + j] = pv;
+    if (Pd) Pd[r * L + j] = mask ? pv * mask[r * L + j] : pv;
+  }
+}
+
+// dS = scale * P * (dP - sum_j dP_j P_j), dP = dPd * mask
+__global__ void softmax_bwd_kernel(const float* __restrict__ P, const float* __restrict__ dPd,
+                                   const float* __restrict__ mask, float* __restrict__ dS, int64_t R,
+                                   int L, float scale) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = blockIdx.x * (int64_t)(blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (r >= R) return;
+  const float* p = P + r * L;
+  const float* g = dPd + r * L;
+  const float* m = mask ? mask + r * L : nullptr;
+  float acc = 0.f;
+  for (int j = lane; j < L; j += 64) acc += (m ? g[j] * m[j] : g[j]) * p[j];
+  acc = wave_sum(acc);
+  for (int j = lane; j < L; j += 64) {
+    const float dp = m ? g[j] * m[j] : g[j];
+    dS[r * L + j] = scale * p[j] * (dp - acc);
+  }
+}
+
+// ---------------------------------------------------------------- loss (models/models.py:159-173)
+// pass 1 (one workgroup): sums and non-zero-weight counts
+__global__ void __launch_bounds__(1024) loss_reduce_kernel(
+    const float* __restrict__ mel, const float* __restrict__ tgt, const float* __restrict__ tmask,
+    const float* __restrict__ stop, const float* __restrict__ done, const float* __restrict__ dmask,
+    int B, int T, int M, int Tp, float l1w, float* __restrict__ out) {
+  __shared__ double sh[4][16];
+  double l1 = 0.0, c1 = 0.0, bce = 0.0, c2 = 0.0;
+  const int64_t n1 = (int64_t)B * T * M;
+  for (int64_t i = threadIdx.x; i < n1; i += blockDim.x) {
+    const float w = tmask[i / M];
+    if (w != 0.f) { l1 += (double)w * fabsf(mel[i] - tgt[i]); c1 += 1.0; }
+  }
+  const int64_t n2 = (int64_t)B * Tp;
+  for (int64_t i = threadIdx.x; i < n2; i += blockDim.x) {
+    const float w = dmask[i];
+    if (w != 0.f) {
+      const float x = stop[i], z = done[i];
+      bce += (double)w * (fmaxf(x, 0.f) - x * z + log1pf(expf(-fabsf(x))));
+      c2 += 1.0;
+    }
+  }
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int o = 32; o > 0; o >>= 1) {
+    l1 += __shfl_xor(l1, o, 64); c1 += __shfl_xor(c1, o, 64);
+    bce += __shfl_xor(bce, o, 64); c2 += __shfl_xor(c2, o, 64);
+  }
+  if (lane == 0) { sh[0][wv] = l1; sh[1][wv] = c1; sh[2][wv] = bce; sh[3][wv] = c2; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double a[4] = {0, 0, 0, 0};
+    for (int k = 0; k < 4; ++k)
+      for (int w = 0; w < (int)(blockDim.x >> 6); ++w) a[k] += sh[k][w];
+    const double cl1 = fmax(a[1], 1.0), cb = fmax(a[3], 1.0);
+    const double L1 = a[0] / cl1, BCE = a[2] / cb;
+    out[0] = (float)(l1w * L1 + BCE);   // loss
+    out[1] = (float)L1;
+    out[2] = (float)BCE;
+    out[3] = (float)cl1;                // counts, used by the gradient pass
+    out[4] = (float)cb;
+  }
+}
+
+// pass 2: dmel = l1w * sign(mel - tgt) * w / count ; dstop = (sigmoid(x) - z) * w / count
+__global__ void loss_grad_kernel(const float* __restrict__ mel, const float* __restrict__ tgt,
+                                 const float* __restrict__ tmask, const float* __restrict__ stop,
+                                 const float* __restrict__ done, const float* __restrict__ dmask,
+                                 int B, int T, int M, int Tp, const float* __restrict__ red,
+                                 float l1w, float* __restrict__ dmel, float* __restrict__ dstop) {
+  const int64_t n1 = (int64_t)B * T * M, n2 = (int64_t)B * Tp;
+  const float s1 = l1w / red[3], s2 = 1.f / red[4];
+  GRID_STRIDE(i, n1 + n2) {
+    if (i < n1) {
+      const float w = tmask[i / M];
+      const float dlt = mel[i] - tgt[i];
+      const float sg = dlt > 0.f ? 1.f : (dlt < 0.f ? -1.f : 0.f);
+      dmel[i] = w * sg * s1;
+    } else {
+      const int64_t j = i - n1;
+      const float w = dmask[j];
+      dstop[j] = w * (1.f / (1.f + expf(-stop[j])) - done[j]) * s2;
+    }
   }
 }
 
@@ -25,9 +356,195 @@ extern "C" int sat_seq_mask(const float* x, float* out, int32_t B, int32_t N, in
                             const int64_t* lengths, void* stream) {
   SAT_CHECK_ARG(x && out && lengths && B > 0 && N > 0 && C > 0, "sat_seq_mask: bad args");
   const int64_t total = (int64_t)B * N * C;
-  const int blocks = (int)std::min<int64_t>((total + 255) / 256, 2048);
-  hipLaunchKernelGGL(seq_mask_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), x, out, B, N,
-                     C, lengths);
+  hipLaunchKernelGGL(seq_mask_kernel, dim3(grid_for(total)), dim3(256), 0, as_stream(stream), x,
+                     out, B, N, C, lengths);
   SAT_LAUNCH_CHECK("sat_seq_mask");
+  return SAT_OK;
+}
+
+extern "C" int sat_embedding_fwd(const float* table, const int64_t* ids, float* out, int64_t R,
+                                 int32_t D, int32_t V, int64_t offset, int32_t* err, void* stream) {
+  SAT_CHECK_ARG(table && ids && out && R >= 0 && D > 0 && V > 0, "sat_embedding_fwd: bad args");
+  if (R == 0) return SAT_OK;
+  hipLaunchKernelGGL(embed_fwd_kernel, dim3(grid_for(R * D)), dim3(256), 0, as_stream(stream),
+                     table, ids, out, R, D, V, offset, err);
+  SAT_LAUNCH_CHECK("sat_embedding_fwd");
+  return SAT_OK;
+}
+
+extern "C" int sat_embedding_bwd(const float* dout, const int64_t* ids, float* dtable, int64_t R,
+                                 int32_t D, int32_t V, int64_t offset, void* stream) {
+  SAT_CHECK_ARG(dout && ids && dtable && R >= 0 && D > 0 && V > 0, "sat_embedding_bwd: bad args");
+  if (R == 0) return SAT_OK;
+  hipLaunchKernelGGL(embed_bwd_kernel, dim3(grid_for(R * D)), dim3(256), 0, as_stream(stream),
+                     dout, ids, dtable, R, D, V, offset);
+  SAT_LAUNCH_CHECK("sat_embedding_bwd");
+  return SAT_OK;
+}
+
+static int row_blocks(int M) { return std::max(1, std::min(64, (M + 127) / 128)); }
+
+extern "C" int64_t sat_workspace_colreduce(int32_t M, int32_t C) {
+  // bytes: fp64 partials [2][RB][C] + two fp32 sums [C] used by the column reductions below
+  return (int64_t)2 * row_blocks(M) * C * (int64_t)sizeof(double) + (int64_t)2 * C * 4;
+}
+
+extern "C" int sat_bn_stats(const float* x, int64_t ldx, int32_t M, int32_t C, float* mean,
+                            float* var, float* mov_mean, float* mov_var, float momentum,
+                            void* workspace, void* stream) {
+  SAT_CHECK_ARG(x && mean && var && workspace && M > 0 && C > 0, "sat_bn_stats: bad args");
+  const int RB = row_blocks(M);
+  double* p1 = reinterpret_cast<double*>(workspace);
+  double* p2 = p1 + (int64_t)RB * C;
+  hipStream_t s = as_stream(stream);
+  hipLaunchKernelGGL(colreduce_kernel, dim3(ceil_div(C, 64), RB), dim3(256), 0, s, x, ldx,
+                     (const float*)nullptr, (int64_t)0, M, C, p1, p2, 0, (const float*)nullptr,
+                     (const float*)nullptr, 0.f, (const float*)nullptr, (int64_t)0);
+  hipLaunchKernelGGL(bn_stats_finish_kernel, dim3(grid_for(C)), dim3(256), 0, s, p1, p2, RB, M, C,
+                     mean, var, mov_mean, mov_var, momentum);
+  SAT_LAUNCH_CHECK("sat_bn_stats");
+  return SAT_OK;
+}
+
+extern "C" int sat_bn_apply(const float* x, int64_t ldx, float* y, int64_t ldy, int32_t M,
+                            int32_t C, const float* mean, const float* var, float eps,
+                            const float* gamma, const float* beta, int32_t relu, const float* res,
+                            int64_t ldr, void* stream) {
+  SAT_CHECK_ARG(x && y && mean && var && gamma && beta && M > 0 && C > 0, "sat_bn_apply: bad args");
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(grid_for((int64_t)M * C)), dim3(256), 0,
+                     as_stream(stream), x, ldx, y, ldy, M, C, mean, var, eps, gamma, beta, relu,
+                     res, ldr);
+  SAT_LAUNCH_CHECK("sat_bn_apply");
+  return SAT_OK;
+}
+
+extern "C" int sat_bn_bwd(const float* dy, int64_t lddy, const float* x, int64_t ldx,
+                          const float* gate, int64_t ldg, float* dx, int64_t lddx, int32_t M,
+                          int32_t C, const float* mean, const float* var, float eps,
+                          const float* gamma, float* dgamma, float* dbeta, int32_t training,
+                          float beta_out, void* workspace, void* stream) {
+  SAT_CHECK_ARG(dy && x && dx && mean && var && gamma && dgamma && dbeta && workspace,
+                "sat_bn_bwd: bad args");
+  const int RB = row_blocks(M);
+  double* p1 = reinterpret_cast<double*>(workspace);
+  double* p2 = p1 + (int64_t)RB * C;
+  hipStream_t s = as_stream(stream);
+  float* sum1 = reinterpret_cast<float*>(p2 + (int64_t)RB * C);
+  float* sum2 = sum1 + C;
+  hipLaunchKernelGGL(colreduce_kernel, dim3(ceil_div(C, 64), RB), dim3(256), 0, s, dy, lddy, x,
+                     ldx, M, C, p1, p2, 1, mean, var, eps, gate, ldg);
+  // dbeta += sum(g), dgamma += sum(g * xhat)  (gradients accumulate into the grad arena)
+  hipLaunchKernelGGL(colreduce_finish_kernel, dim3(grid_for(C)), dim3(256), 0, s, p1, p2, RB, C,
+                     sum1, sum2, 0.f, dbeta, dgamma);
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_for((int64_t)M * C)), dim3(256), 0, s, dy,
+                     lddy, x, ldx, gate, ldg, dx, lddx, M, C, mean, var, eps, gamma, sum1, sum2,
+                     training, beta_out);
+  SAT_LAUNCH_CHECK("sat_bn_bwd");
+  return SAT_OK;
+}
+
+extern "C" int sat_colsum(const float* x, int64_t ldx, int32_t M, int32_t C, float* out,
+                          float beta, void* workspace, void* stream) {
+  SAT_CHECK_ARG(x && out && workspace && M >= 0 && C > 0, "sat_colsum: bad args");
+  if (M == 0) return SAT_OK;
+  const int RB = row_blocks(M);
+  double* p1 = reinterpret_cast<double*>(workspace);
+  double* p2 = p1 + (int64_t)RB * C;
+  hipStream_t s = as_stream(stream);
+  hipLaunchKernelGGL(colreduce_kernel, dim3(ceil_div(C, 64), RB), dim3(256), 0, s, x, ldx,
+                     (const float*)nullptr, (int64_t)0, M, C, p1, p2, 2, (const float*)nullptr,
+                     (const float*)nullptr, 0.f, (const float*)nullptr, (int64_t)0);
+  hipLaunchKernelGGL(colreduce_finish_kernel, dim3(grid_for(C)), dim3(256), 0, s, p1, p2, RB, C,
+                     out, (float*)nullptr, beta, (float*)nullptr, (float*)nullptr);
+  SAT_LAUNCH_CHECK("sat_colsum");
+  return SAT_OK;
+}
+
+extern "C" int sat_maxpool2(const float* x, float* y, int32_t B, int32_t N, int32_t C,
+                            void* stream) {
+  SAT_CHECK_ARG(x && y && B > 0 && N > 0 && C > 0, "sat_maxpool2: bad args");
+  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_for((int64_t)B * N * C)), dim3(256), 0,
+                     as_stream(stream), x, y, B, N, C);
+  SAT_LAUNCH_CHECK("sat_maxpool2");
+  return SAT_OK;
+}
+
+extern "C" int sat_maxpool2_bwd(const float* x, const float* dy, float* dx, int32_t B, int32_t N,
+                                int32_t C, void* stream) {
+  SAT_CHECK_ARG(x && dy && dx && B > 0 && N > 0 && C > 0, "sat_maxpool2_bwd: bad args");
+  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_for((int64_t)B * N * C)), dim3(256), 0,
+                     as_stream(stream), x, dy, dx, B, N, C);
+  SAT_LAUNCH_CHECK("sat_maxpool2_bwd");
+  return SAT_OK;
+}
+
+extern "C" int sat_highway_fwd(const float* h, const float* t, const float* x, float* y, int64_t n,
+                               void* stream) {
+  SAT_CHECK_ARG(h && t && x && y && n >= 0, "sat_highway_fwd: bad args");
+  hipLaunchKernelGGL(highway_fwd_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), h, t,
+                     x, y, n);
+  SAT_LAUNCH_CHECK("sat_highway_fwd");
+  return SAT_OK;
+}
+
+extern "C" int sat_highway_bwd(const float* h, const float* t, const float* x, const float* dy,
+                               float* dh_pre, float* dt_pre, float* dx, int64_t n, void* stream) {
+  SAT_CHECK_ARG(h && t && x && dy && dh_pre && dt_pre && dx, "sat_highway_bwd: bad args");
+  hipLaunchKernelGGL(highway_bwd_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), h, t,
+                     x, dy, dh_pre, dt_pre, dx, n);
+  SAT_LAUNCH_CHECK("sat_highway_bwd");
+  return SAT_OK;
+}
+
+extern "C" int sat_act_bwd(const float* dy, const float* y, const float* mask, float* dx, int64_t n,
+                           int32_t act, float beta, void* stream) {
+  SAT_CHECK_ARG(dy && dx && n >= 0 && act >= 0 && act <= 3, "sat_act_bwd: bad args");
+  SAT_CHECK_ARG(act == 0 || y, "sat_act_bwd: activation output needed");
+  hipLaunchKernelGGL(act_bwd_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), dy, y,
+                     mask, dx, n, act, beta);
+  SAT_LAUNCH_CHECK("sat_act_bwd");
+  return SAT_OK;
+}
+
+extern "C" int sat_axpby(const float* x, float* y, int64_t n, float a, float b, void* stream) {
+  SAT_CHECK_ARG(x && y && n >= 0, "sat_axpby: bad args");
+  hipLaunchKernelGGL(axpby_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), x, y, n, a,
+                     b);
+  SAT_LAUNCH_CHECK("sat_axpby");
+  return SAT_OK;
+}
+
+extern "C" int sat_softmax_fwd(const float* S, float* P, float* Pd, const float* mask, int64_t R,
+                               int32_t L, int32_t Lq, int32_t causal, float scale, void* stream) {
+  SAT_CHECK_ARG(S && P && R >= 0 && L > 0 && Lq > 0, "sat_softmax_fwd: bad args");
+  hipLaunchKernelGGL(softmax_fwd_kernel, dim3(ceil_div(R, 4)), dim3(256), 0, as_stream(stream), S,
+                     P, Pd, mask, R, L, Lq, causal, scale);
+  SAT_LAUNCH_CHECK("sat_softmax_fwd");
+  return SAT_OK;
+}
+
+extern "C" int sat_softmax_bwd(const float* P, const float* dPd, const float* mask, float* dS,
+                               int64_t R, int32_t L, float scale, void* stream) {
+  SAT_CHECK_ARG(P && dPd && dS && R >= 0 && L > 0, "sat_softmax_bwd: bad args");
+  hipLaunchKernelGGL(softmax_bwd_kernel, dim3(ceil_div(R, 4)), dim3(256), 0, as_stream(stream), P,
+                     dPd, mask, dS, R, L, scale);
+  SAT_LAUNCH_CHECK("sat_softmax_bwd");
+  return SAT_OK;
+}
+
+extern "C" int sat_loss_fwd_bwd(const float* mel, const float* tgt, const float* tmask,
+                                const float* stop, const float* done, const float* dmask,
+                                int32_t B, int32_t T, int32_t M, int32_t Tp, float l1_weight,
+                                float* out, float* dmel, float* dstop, void* stream) {
+  SAT_CHECK_ARG(mel && tgt && tmask && stop && done && dmask && out, "sat_loss_fwd_bwd: bad args");
+  hipStream_t s = as_stream(stream);
+  hipLaunchKernelGGL(loss_reduce_kernel, dim3(1), dim3(1024), 0, s, mel, tgt, tmask, stop, done,
+                     dmask, B, T, M, Tp, l1_weight, out);
+  if (dmel && dstop) {
+    const int64_t n = (int64_t)B * T * M + (int64_t)B * Tp;
+    hipLaunchKernelGGL(loss_grad_kernel, dim3(grid_for(n)), dim3(256), 0, s, mel, tgt, tmask, stop,
+                       done, dmask, B, T, M, Tp, out, l1_weight, dmel, dstop);
+  }
+  SAT_LAUNCH_CHECK("sat_loss_fwd_bwd");
   return SAT_OK;
 }

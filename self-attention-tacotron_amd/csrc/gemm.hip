@@ -32,6 +32,10 @@ struct GemmP {
   float alpha, beta;
   const float* mul;
   int64_t mul_sm, mul_sbatch;
+  int batch2;
+  int64_t a_sbatch2, b_sbatch2, c_sbatch2, mul_sbatch2;
+  const float* add;
+  int64_t add_sm, add_sbatch;
   int a_kcontig, b_ncontig;
 };
 
@@ -79,10 +83,10 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmP p) {
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = (wave >> 1) * WM, wn = (wave & 1) * WN;
-  const int bz = blockIdx.z;
+  const int bz = blockIdx.z / p.batch2, bz2 = blockIdx.z - bz * p.batch2;
   const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
-  const float* A = p.A + bz * p.a_sbatch;
-  const float* B = p.B + bz * p.b_sbatch;
+  const float* A = p.A + bz * p.a_sbatch + bz2 * p.a_sbatch2;
+  const float* B = p.B + bz * p.b_sbatch + bz2 * p.b_sbatch2;
 
   float ra[EA], rb[EB];
   auto fetch = [&](int k0) {
@@ -154,9 +158,10 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmP p) {
   }
 
   // epilogue: C/D map of 32x32 f32 MFMA: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
-  float* C = p.C + bz * p.c_sbatch;
+  float* C = p.C + bz * p.c_sbatch + bz2 * p.c_sbatch2;
   const float* bias = p.bias ? p.bias + bz * p.bias_sbatch : nullptr;
-  const float* mul = p.mul ? p.mul + bz * p.mul_sbatch : nullptr;
+  const float* mul = p.mul ? p.mul + bz * p.mul_sbatch + bz2 * p.mul_sbatch2 : nullptr;
+  const float* add = p.add ? p.add + bz * p.add_sbatch : nullptr;
 #pragma unroll
   for (int i = 0; i < SM; ++i)
 #pragma unroll
@@ -173,6 +178,7 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmP p) {
         if (p.beta != 0.f) v += p.beta * (*dst);
         v = apply_act(v + bv, p.act);
         if (mul) v *= mul[(int64_t)row * p.mul_sm + col];
+        if (add) v += add[(int64_t)row * p.add_sm + col];
         *dst = v;
       }
     }
@@ -203,16 +209,20 @@ extern "C" int sat_gemm(const SatGemmDesc* d, void* stream) {
   p.bias = d->bias; p.bias_sbatch = d->bias_sbatch;
   p.alpha = d->alpha; p.beta = d->beta;
   p.mul = d->mul; p.mul_sm = d->mul_sm; p.mul_sbatch = d->mul_sbatch;
+  p.batch2 = d->batch2 > 0 ? d->batch2 : 1;
+  p.a_sbatch2 = d->a_sbatch2; p.b_sbatch2 = d->b_sbatch2; p.c_sbatch2 = d->c_sbatch2;
+  p.mul_sbatch2 = d->mul_sbatch2;
+  p.add = d->add; p.add_sm = d->add_sm; p.add_sbatch = d->add_sbatch;
   // coalescing order of the tile loaders
   p.a_kcontig = (d->a_mode == 1) ? 1 : (d->a_mode == 2 ? 0 : (d->a_sk == 1 ? 1 : 0));
   p.b_ncontig = (d->b_mode == 1) ? 0 : (d->b_sn == 1 ? 1 : 0);
   hipStream_t s = as_stream(stream);
   const bool big = (int64_t)d->M * d->N >= (int64_t)256 * 128 * 128 && d->N >= 96 && d->M >= 96;
   if (big) {
-    dim3 grid(ceil_div(d->N, 128), ceil_div(d->M, 128), d->batch);
+    dim3 grid(ceil_div(d->N, 128), ceil_div(d->M, 128), d->batch * p.batch2);
     hipLaunchKernelGGL((gemm_kernel<128, 128>), grid, dim3(256), 0, s, p);
   } else {
-    dim3 grid(ceil_div(d->N, 64), ceil_div(d->M, 64), d->batch);
+    dim3 grid(ceil_div(d->N, 64), ceil_div(d->M, 64), d->batch * p.batch2);
     hipLaunchKernelGGL((gemm_kernel<64, 64>), grid, dim3(256), 0, s, p);
   }
   SAT_LAUNCH_CHECK("sat_gemm");

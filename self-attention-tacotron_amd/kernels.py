@@ -28,57 +28,78 @@ def _f32(t, name):
         raise TypeError(f"{name}: expected a float32 device tensor, got {t.dtype} on {t.device}")
 
 
+def _bstrides(t, nd):
+    """batch strides (s1, s2) of a tensor with nd leading batch dims (0 = broadcast)."""
+    if t is None:
+        return 0, 0
+    lead = t.dim() - 2
+    if lead == 2:
+        return t.stride(0), t.stride(1)
+    if lead == 1:
+        return (t.stride(0), 0) if nd >= 1 else (0, 0)
+    return 0, 0
+
+
 def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor = None, *, alpha=1.0, beta=0.0,
-         bias=None, act=None, mul=None) -> torch.Tensor:
-    """C = act(alpha * A @ B + beta * C + bias).  A [.., M, K], B [.., K, N] (any strides: pass
-    ``x.t()`` / ``x.transpose(-1,-2)`` views for transposed operands), optional batch dim 0."""
+         bias=None, act=None, mul=None, add=None) -> torch.Tensor:
+    """C = act(alpha * A @ B + beta * C + bias) * mul + add.
+
+    A [.., M, K], B [.., K, N] with up to two leading batch dims (any strides: pass ``x.t()`` /
+    ``x.transpose(-1, -2)`` views for transposed operands); C gets the broadcast batch shape.
+    """
     _f32(A, "A"); _f32(B, "B")
-    batched = A.dim() == 3 or B.dim() == 3
     M, K = A.shape[-2], A.shape[-1]
     K2, N = B.shape[-2], B.shape[-1]
     if K != K2:
-        raise ValueError(f"gemm: inner dims differ {A.shape} @ {B.shape}")
-    nb = A.shape[0] if A.dim() == 3 else (B.shape[0] if B.dim() == 3 else 1)
+        raise ValueError(f"gemm: inner dims differ {tuple(A.shape)} @ {tuple(B.shape)}")
+    lead = A.shape[:-2] if A.dim() >= B.dim() else B.shape[:-2]
+    if len(lead) > 2:
+        raise ValueError("gemm: at most two batch dims")
     if C is None:
-        C = torch.empty((nb, M, N) if batched else (M, N), device=A.device, dtype=torch.float32)
         if beta != 0.0:
             raise ValueError("beta != 0 needs an output tensor")
+        C = torch.empty((*lead, M, N), device=A.device, dtype=torch.float32)
     _f32(C, "C")
     if C.stride(-1) != 1:
         raise ValueError("gemm: C must have unit column stride")
+    nd = len(lead)
+    nb = lead[0] if nd >= 1 else 1
+    nb2 = lead[1] if nd == 2 else 1
     d = _lib.SatGemmDesc()
-    d.M, d.N, d.K, d.batch = M, N, K, nb
-    d.a_mode = 0
-    d.A = _p(A)
+    d.M, d.N, d.K, d.batch, d.batch2 = M, N, K, nb, nb2
+    d.a_mode, d.A = 0, _p(A)
     d.a_sm, d.a_sk = A.stride(-2), A.stride(-1)
-    d.a_sbatch = A.stride(0) if A.dim() == 3 else 0
-    d.b_mode = 0
-    d.B = _p(B)
+    d.a_sbatch, d.a_sbatch2 = _bstrides(A, nd)
+    d.b_mode, d.B = 0, _p(B)
     d.b_sk, d.b_sn = B.stride(-2), B.stride(-1)
-    d.b_sbatch = B.stride(0) if B.dim() == 3 else 0
-    d.C = _p(C)
-    d.c_sm = C.stride(-2)
-    d.c_sbatch = C.stride(0) if C.dim() == 3 else 0
-    d.bias = _p(bias)
-    d.bias_sbatch = 0
+    d.b_sbatch, d.b_sbatch2 = _bstrides(B, nd)
+    d.C, d.c_sm = _p(C), C.stride(-2)
+    d.c_sbatch, d.c_sbatch2 = _bstrides(C, nd)
+    d.bias, d.bias_sbatch = _p(bias), 0
     d.act = ACT[act]
     d.alpha, d.beta = alpha, beta
     if mul is not None:
         d.mul, d.mul_sm = _p(mul), mul.stride(-2)
-        d.mul_sbatch = mul.stride(0) if mul.dim() == 3 else 0
+        d.mul_sbatch, d.mul_sbatch2 = _bstrides(mul, nd)
+    if add is not None:
+        d.add = _p(add)
+        d.add_sm = add.stride(-2) if add.dim() >= 2 else 0
+        d.add_sbatch = add.stride(0) if add.dim() == 3 else 0
     _lib.check(_lib.load().sat_gemm(ctypes.byref(d), _stream()), "sat_gemm")
     return C
 
 
 def linear(x: torch.Tensor, W: torch.Tensor, bias=None, act=None, out=None, beta=0.0,
-           mul=None):
+           mul=None, add=None):
     """tf.layers.Dense over the last dim of x (any leading shape; x must be row-contiguous);
-    ``mul`` (same shape as the output) is multiplied in after the activation (dropout)."""
+    ``mul`` (same shape as the output) is multiplied in after the activation (dropout), ``add``
+    added last (residual)."""
     lead = x.shape[:-1]
     x2 = x.reshape(-1, x.shape[-1])
     o2 = None if out is None else out.view(-1, W.shape[1])
     m2 = None if mul is None else mul.reshape(-1, W.shape[1])
-    y = gemm(x2, W, o2, bias=bias, act=act, beta=beta, mul=m2)
+    a2 = None if add is None else add.reshape(-1, W.shape[1])
+    y = gemm(x2, W, o2, bias=bias, act=act, beta=beta, mul=m2, add=a2)
     return y.view(*lead, W.shape[1])
 
 
@@ -204,3 +225,111 @@ def attn_step_fwd(**kw):
     for k, v in kw.items():
         setattr(a, k, _p(v) if isinstance(v, torch.Tensor) else v)
     _lib.check(_lib.load().sat_attn_step_fwd(ctypes.byref(a), _stream()), "sat_attn_step_fwd")
+
+
+# ---------------------------------------------------------------- elementwise / reductions
+
+class Workspace:
+    """Grow-only fp64 scratch for column reductions (one per stream/model)."""
+
+    def __init__(self, device):
+        self.device = device
+        self.buf = torch.empty(0, dtype=torch.uint8, device=device)
+
+    def get(self, M, C) -> int:
+        need = int(_lib.load().sat_workspace_colreduce(M, C))
+        if self.buf.numel() < need:
+            self.buf = torch.empty(max(need, 2 * self.buf.numel()), dtype=torch.uint8,
+                                   device=self.device)
+        return self.buf.data_ptr()
+
+
+def embedding_fwd(table, ids, out, offset=0, err=None):
+    R = ids.numel()
+    _lib.call("sat_embedding_fwd", _p(table), _p(ids), _p(out), R, table.shape[1],
+              table.shape[0], offset, _p(err), _stream())
+    return out
+
+
+def embedding_bwd(dout, ids, dtable, offset=0):
+    _lib.call("sat_embedding_bwd", _p(dout), _p(ids), _p(dtable), ids.numel(), dtable.shape[1],
+              dtable.shape[0], offset, _stream())
+
+
+def bn_stats(x2, mean, var, ws, mov_mean=None, mov_var=None, momentum=0.99):
+    M, C = x2.shape
+    _lib.call("sat_bn_stats", _p(x2), x2.stride(0), M, C, _p(mean), _p(var), _p(mov_mean),
+              _p(mov_var), momentum, ws.get(M, C), _stream())
+
+
+def bn_apply(x2, y2, mean, var, gamma, beta, relu=False, res=None, eps=1e-3):
+    M, C = x2.shape
+    _lib.call("sat_bn_apply", _p(x2), x2.stride(0), _p(y2), y2.stride(0), M, C, _p(mean),
+              _p(var), eps, _p(gamma), _p(beta), int(relu), _p(res), _rs(res), _stream())
+
+
+def bn_bwd(dy2, x2, gate2, dx2, mean, var, gamma, dgamma, dbeta, ws, training=True,
+           beta_out=0.0, eps=1e-3):
+    M, C = x2.shape
+    _lib.call("sat_bn_bwd", _p(dy2), dy2.stride(0), _p(x2), x2.stride(0), _p(gate2),
+              _rs(gate2), _p(dx2), dx2.stride(0), M, C, _p(mean), _p(var), eps, _p(gamma),
+              _p(dgamma), _p(dbeta), int(training), beta_out, ws.get(M, C), _stream())
+
+
+def colsum(x2, out, ws, beta=1.0):
+    M, C = x2.shape
+    _lib.call("sat_colsum", _p(x2), x2.stride(0), M, C, _p(out), beta, ws.get(M, C), _stream())
+
+
+def maxpool2(x, y):
+    B, N, C = x.shape
+    _lib.call("sat_maxpool2", _p(x), _p(y), B, N, C, _stream())
+    return y
+
+
+def maxpool2_bwd(x, dy, dx):
+    B, N, C = x.shape
+    _lib.call("sat_maxpool2_bwd", _p(x), _p(dy), _p(dx), B, N, C, _stream())
+    return dx
+
+
+def highway_fwd(h, t, x, y):
+    _lib.call("sat_highway_fwd", _p(h), _p(t), _p(x), _p(y), y.numel(), _stream())
+    return y
+
+
+def highway_bwd(h, t, x, dy, dh_pre, dt_pre, dx):
+    _lib.call("sat_highway_bwd", _p(h), _p(t), _p(x), _p(dy), _p(dh_pre), _p(dt_pre), _p(dx),
+              dy.numel(), _stream())
+
+
+def act_bwd(dy, y, dx, act, mask=None, beta=0.0):
+    _lib.call("sat_act_bwd", _p(dy), _p(y), _p(mask), _p(dx), dy.numel(), ACT[act], beta,
+              _stream())
+    return dx
+
+
+def axpby(x, y, a, b):
+    _lib.call("sat_axpby", _p(x), _p(y), x.numel(), a, b, _stream())
+    return y
+
+
+def softmax_fwd(S, P, Pd=None, mask=None, causal=False, scale=1.0):
+    L = S.shape[-1]
+    Lq = S.shape[-2]
+    R = S.numel() // L
+    _lib.call("sat_softmax_fwd", _p(S), _p(P), _p(Pd), _p(mask), R, L, Lq, int(causal), scale,
+              _stream())
+
+
+def softmax_bwd(P, dPd, dS, mask=None, scale=1.0):
+    L = P.shape[-1]
+    _lib.call("sat_softmax_bwd", _p(P), _p(dPd), _p(mask), _p(dS), P.numel() // L, L, scale,
+              _stream())
+
+
+def loss_fwd_bwd(mel, tgt, tmask, stop, done, dmask, out, dmel=None, dstop=None, l1_weight=0.1):
+    B, T, M = mel.shape
+    Tp = stop.shape[1]
+    _lib.call("sat_loss_fwd_bwd", _p(mel), _p(tgt), _p(tmask), _p(stop), _p(done), _p(dmask),
+              B, T, M, Tp, l1_weight, _p(out), _p(dmel), _p(dstop), _stream())

@@ -1,0 +1,244 @@
+"""Self-attention Tacotron teacher-forced step on libsat_hip: encoder, self-attention heads, loss.
+
+Forward mirrors ``model_fn`` TRAIN / EVAL-with-teacher (models/models.py:23-173):
+  Embedding -> SelfAttentionCBHGEncoder (modules/module.py:425-438)
+            -> DualSourceTransformerDecoder (decoder.py) -> RNNTransformer head (module.py:754-764)
+            -> 0.1 * L1 + BCE loss.
+Every arithmetic op is a libsat_hip kernel; torch only allocates, views and copies.
+Activations that the backward needs are kept in ``Saved`` (HBM is 288 GB: store, don't recompute,
+except the attention energies which the backward recomputes to avoid a [T', B, N, 224] tensor).
+"""
+
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional, Tuple
+
+import numpy as np
+import torch
+
+from . import kernels as K
+from . import params as PR
+from .decoder import decoder_forward
+
+
+class BNState:
+    """Moving statistics of every BatchNormalization, two flat buffers (means, variances) laid
+    out in ``params.bn_buffer_names`` order, so the 16 conv-bank BNs are one contiguous span."""
+
+    def __init__(self, hp, device):
+        self.names = PR.bn_buffer_names(hp)
+        self.offsets = {}
+        off = 0
+        for scope, ch in self.names:
+            self.offsets[scope] = (off, ch)
+            off += ch
+        self.mean = torch.zeros(off, device=device)
+        self.var = torch.ones(off, device=device)
+
+    def span(self, first_scope: str, count_ch: int):
+        o, _ = self.offsets[first_scope]
+        return self.mean[o:o + count_ch], self.var[o:o + count_ch]
+
+
+def _contig_span(P: Dict[str, torch.Tensor], names: List[str]) -> torch.Tensor:
+    """A view covering consecutive arena tensors (asserts adjacency)."""
+    first = P[names[0]]
+    n = sum(P[x].numel() for x in names)
+    base = first.data_ptr()
+    off = 0
+    for x in names:
+        if P[x].data_ptr() != base + 4 * off:
+            raise RuntimeError(f"parameter {x} is not adjacent in the arena")
+        off += P[x].numel()
+    return first.view(-1).as_strided((n,), (1,))
+
+
+def mha_fwd(x: torch.Tensor, P, scope: str, heads: int, causal: bool,
+            probs_mask: Optional[torch.Tensor], sv: dict, key: str):
+    """MultiHeadAttention (modules/self_attention.py:108-128) over x [B, L, W]."""
+    B, L, W = x.shape
+    q = K.linear(x, P[f"{scope}/query_projection/kernel"], P[f"{scope}/query_projection/bias"])
+    k = K.linear(x, P[f"{scope}/key_projection/kernel"], P[f"{scope}/key_projection/bias"])
+    v = K.linear(x, P[f"{scope}/value_projection/kernel"], P[f"{scope}/value_projection/bias"])
+    model = q.shape[-1]
+    dh = model // heads
+
+    def hv(t):  # [B, L, model] -> [B, H, L, dh] view
+        return t.view(B, L, heads, dh).permute(0, 2, 1, 3)
+
+    S = K.gemm(hv(q), hv(k).transpose(-1, -2))                 # [B, H, L, L]
+    Pm = torch.empty_like(S)
+    Pd = torch.empty_like(S) if probs_mask is not None else Pm
+    K.softmax_fwd(S, Pm, Pd if probs_mask is not None else None, probs_mask, causal=causal,
+                  scale=1.0 / math.sqrt(dh))
+    o = torch.empty(B, L, model, device=x.device)
+    K.gemm(Pd, hv(v), hv(o))                                   # heads written in place
+    y = K.linear(o, P[f"{scope}/output_projection/kernel"], P[f"{scope}/output_projection/bias"])
+    sv[key] = dict(x=x, q=q, k=k, v=v, P=Pm, Pd=Pd, o=o, y=y, mask=probs_mask, heads=heads,
+                   dh=dh)
+    return y
+
+
+def sa_transformer_fwd(x, P, scope, heads, causal, probs_mask, sv, key):
+    """SelfAttentionTransformer.call (modules/module.py:363-371): x + tanh(Dense(MHA(x)))."""
+    y = mha_fwd(x, P, f"{scope}/mha", heads, causal, probs_mask, sv, key)
+    z = K.linear(y, P[f"{scope}/transform/kernel"], P[f"{scope}/transform/bias"], act="tanh",
+                 add=x)
+    sv[key]["z"] = z
+    return z
+
+
+def encoder_fwd(P, bn: BNState, hp, d: PR.Dims, ids, lengths, masks, training, ws, sv):
+    """SelfAttentionCBHGEncoder.call (modules/module.py:425-438) -> (M1, M2)."""
+    dev = ids.device
+    B, N = ids.shape
+    mk = (lambda n: masks[n]) if masks is not None else (lambda n: None)
+    emb = torch.empty(B, N, d.embed, device=dev)
+    err = torch.zeros(1, dtype=torch.int32, device=dev)
+    K.embedding_fwd(P["embedding"], ids, emb, 0, err)
+    sv["emb_err"] = err
+    x = emb
+    pre = [emb]
+    for i in range(len(d.enc_prenet)):                                # ext PreNet x2
+        x = K.linear(x, P[f"encoder/prenet{i}/kernel"], P[f"encoder/prenet{i}/bias"], act="relu",
+                     mul=mk(f"enc/prenet{i}"))
+        pre.append(x)
+    sv["enc_pre"] = pre
+    inp = x
+    C = d.conv_ch
+    KC = d.max_k * C
+    bank_pre = torch.empty(B, N, KC, device=dev)
+    for k in range(1, d.max_k + 1):                                   # module.py:78
+        sc = f"encoder/cbhg/conv_bank/K{k}"
+        K.conv1d(inp, P[f"{sc}/kernel"], P[f"{sc}/bias"], out=bank_pre[:, :, (k - 1) * C:k * C])
+    bank = torch.empty_like(bank_pre)
+    names = [f"encoder/cbhg/conv_bank/K{k}" for k in range(1, d.max_k + 1)]
+    gam = _contig_span(P, [f"{n}/bn/gamma" for n in names])
+    bet = _contig_span(P, [f"{n}/bn/beta" for n in names])
+    st_bank = _bn(bank_pre.view(-1, KC), bank.view(-1, KC), gam, bet, bn, f"{names[0]}/bn", KC, True,
+                  training, ws)
+    mp = torch.empty_like(bank)
+    K.maxpool2(bank, mp)                                              # module.py:80
+    p1_pre = K.conv1d(mp, P["encoder/cbhg/proj1/kernel"], P["encoder/cbhg/proj1/bias"])
+    p1 = torch.empty_like(p1_pre)
+    st_p1 = _bn(p1_pre.view(-1, d.proj1), p1.view(-1, d.proj1), P["encoder/cbhg/proj1/bn/gamma"],
+                P["encoder/cbhg/proj1/bn/beta"], bn, "encoder/cbhg/proj1/bn", d.proj1, True,
+                training, ws)
+    p2_pre = K.conv1d(p1, P["encoder/cbhg/proj2/kernel"], P["encoder/cbhg/proj2/bias"])
+    hw = torch.empty_like(p2_pre)                                     # BN(proj2) + residual
+    st_p2 = _bn(p2_pre.view(-1, d.proj2), hw.view(-1, d.proj2), P["encoder/cbhg/proj2/bn/gamma"],
+                P["encoder/cbhg/proj2/bn/beta"], bn, "encoder/cbhg/proj2/bn", d.proj2, False,
+                training, ws, res=inp.view(-1, d.proj2))
+    sv.update(bank_pre=bank_pre, bank=bank, mp=mp, p1_pre=p1_pre, p1=p1, p2_pre=p2_pre,
+              st_bank=st_bank, st_p1=st_p1, st_p2=st_p2)
+    if d.needs_adjust:                                                # module.py:88-89
+        sv["hw_in_adjust"] = hw
+        hw = K.linear(hw, P["encoder/cbhg/adjustment/kernel"], P["encoder/cbhg/adjustment/bias"])
+    hws = [hw]
+    for i in range(d.num_highway):                                    # ext HighwayNet
+        h = K.linear(hw, P[f"encoder/cbhg/highway{i}/H/kernel"],
+                     P[f"encoder/cbhg/highway{i}/H/bias"], act="relu")
+        t = K.linear(hw, P[f"encoder/cbhg/highway{i}/T/kernel"],
+                     P[f"encoder/cbhg/highway{i}/T/bias"], act="sigmoid")
+        y = torch.empty_like(hw)
+        K.highway_fwd(h, t, hw, y)
+        hws.append((h, t, y))
+        hw = y
+    sv["hws"] = hws
+    # bidirectional ZoneoutLSTM (module.py:93-110): outputs written straight into M1 halves
+    U = d.cbhg_half
+    m1 = torch.empty(B, N, 2 * U, device=dev)
+    zc, zh = hp.zoneout_factor_cell, hp.zoneout_factor_output
+    lstm = {}
+    for dr, rev in (("fw", False), ("bw", True)):
+        Wk = P[f"encoder/cbhg/lstm_{dr}/kernel"]
+        X = K.linear(hw, Wk[:hw.shape[-1]], P[f"encoder/cbhg/lstm_{dr}/bias"])   # [B, N, 4U]
+        CS = torch.zeros(N + 1, B, U, device=dev)
+        HS = torch.zeros(N + 1, B, U, device=dev)
+        G = torch.empty(N, B, 4 * U, device=dev)
+        mc, mh = mk(f"enc/lstm_{dr}/zc"), mk(f"enc/lstm_{dr}/zh")
+        out = m1[:, :, U:] if rev else m1[:, :, :U]
+        order = range(N - 1, -1, -1) if rev else range(N)
+        for n in order:
+            prev, nxt = (n + 1, n) if rev else (n, n + 1)
+            K.lstm_step_fwd(B=B, U=U, K=U, t=n, xproj=X[:, n], rin=HS[prev], W=Wk[hw.shape[-1]:],
+                            c_prev=CS[prev], h_prev=HS[prev],
+                            mask_c=None if mc is None else mc[n],
+                            mask_h=None if mh is None else mh[n], zc=zc, zh=zh,
+                            h_raw=out[:, n], c_out=CS[nxt], h_out=HS[nxt], gates=G[n],
+                            lengths=lengths)
+        lstm[dr] = dict(X=X, CS=CS, HS=HS, G=G)
+    sv["enc_lstm"] = lstm
+    sv["m1"] = m1
+    s0 = K.linear(m1, P["encoder/self_attention_projection/kernel"],
+                  P["encoder/self_attention_projection/bias"])          # module.py:429
+    x = s0
+    sv["s0"] = s0
+    for h in range(d.enc_hops):
+        x = sa_transformer_fwd(x, P, f"encoder/self_attention{h}", d.enc_heads, False,
+                               mk(f"enc/sa{h}/probs"), sv, f"enc_sa{h}")
+    return m1, x
+
+
+def _bn(x2, y2, gamma, beta, bn: BNState, scope, C, relu, training, ws, res=None):
+    dev = x2.device
+    if training:
+        mean = torch.empty(C, device=dev)
+        var = torch.empty(C, device=dev)
+        mm, mv = bn.span(scope, C)
+        K.bn_stats(x2, mean, var, ws, mm, mv, momentum=0.99)
+    else:
+        mean, var = bn.span(scope, C)
+    K.bn_apply(x2, y2, mean, var, gamma, beta, relu=relu, res=res)
+    return dict(mean=mean, var=var, gamma=gamma, beta=beta)
+
+
+def head_fwd(P, hp, d: PR.Dims, dout_sm: torch.Tensor, masks, sv):
+    """RNNTransformer training-branch tail (modules/module.py:754-764)."""
+    Tp, B, Dd = dout_sm.shape
+    mk = (lambda n: masks[n]) if masks is not None else (lambda n: None)
+    D = dout_sm.transpose(0, 1).contiguous()                          # [B, T', D] (data movement)
+    z = D
+    for h in range(d.dec_hops):
+        z = sa_transformer_fwd(z, P, f"decoder/self_attention{h}", d.dec_heads, True,
+                               mk(f"dec/sa{h}/probs"), sv, f"dec_sa{h}")
+    mel = K.linear(z, P["decoder/out_projection/kernel"], P["decoder/out_projection/bias"])
+    stop = K.linear(z, P["decoder/stop_token_projection/kernel"],
+                    P["decoder/stop_token_projection/bias"])
+    sv.update(D=D, Z=z)
+    return mel, stop
+
+
+class Saved(dict):
+    pass
+
+
+def model_forward(P, bn: BNState, hp, d: PR.Dims, batch: Dict[str, torch.Tensor],
+                  masks: Optional[Dict[str, torch.Tensor]], training: bool, ws: K.Workspace,
+                  compute_grad_seeds: bool = True, attn_tile: int = 16):
+    """model_fn forward + loss.  Returns (outputs dict, Saved)."""
+    sv = Saved()
+    ids, lengths = batch["source"], batch["source_length"]
+    m1, m2 = encoder_fwd(P, bn, hp, d, ids, lengths, masks, training, ws, sv)
+    spk = None
+    if d.multi_speaker:
+        raise NotImplementedError("VCTK multi-speaker prenet is the next row (SURVEY 8(f) #3)")
+    dout, dsv = decoder_forward(P, hp, d, m1, m2, lengths, batch["mel"], masks,
+                                attn_tile=attn_tile, spk=spk)
+    sv["dec"] = dsv
+    mel_r, stop = head_fwd(P, hp, d, dout, masks, sv)
+    B, Tp, _ = mel_r.shape
+    mel = mel_r.view(B, Tp * d.r, d.num_mels)                         # module.py:1561
+    loss = torch.zeros(8, device=m1.device)
+    dmel = dstop = None
+    if compute_grad_seeds:
+        dmel = torch.empty_like(mel)
+        dstop = torch.empty(B, Tp, device=m1.device)
+    K.loss_fwd_bwd(mel, batch["mel"], batch["mel_mask"], stop.view(B, Tp), batch["done"],
+                   batch["done_mask"], loss, dmel, dstop)
+    sv.update(mel=mel, stop=stop, dmel=dmel, dstop=dstop, m2=m2, batch=batch, masks=masks,
+              training=training)
+    out = {"mel": mel, "stop": stop, "loss": loss[0:1], "l1": loss[1:2], "bce": loss[2:3],
+           "m1": m1, "m2": m2, "dout": dout, "alignment1": dsv.AL1[1:], "alignment2": dsv.S2}
+    return out, sv

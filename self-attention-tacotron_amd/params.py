@@ -153,11 +153,17 @@ def param_specs(hp) -> List[ParamSpec]:
     for i, u in enumerate(d.enc_prenet):
         _dense(s, f"encoder/prenet{i}", w, u)
         w = u
-    for k in range(1, d.max_k + 1):                                 # module.py:46-52
-        sc = f"encoder/cbhg/conv_bank/K{k}"
+    # conv bank K=1..max_k (module.py:46-52).  Grouped by kind so the 16 BatchNorm gammas /
+    # betas / biases are each ONE contiguous [max_k * C] vector: the bank's BN runs as a single
+    # launch over the concatenated 2048 channels.
+    bank = [f"encoder/cbhg/conv_bank/K{k}" for k in range(1, d.max_k + 1)]
+    for k, sc in enumerate(bank, start=1):
         s.append(ParamSpec(f"{sc}/kernel", (k, w, d.conv_ch)))
+    for sc in bank:
         s.append(ParamSpec(f"{sc}/bias", (d.conv_ch,), "zeros"))
+    for sc in bank:
         s.append(ParamSpec(f"{sc}/bn/gamma", (d.conv_ch,), "ones"))
+    for sc in bank:
         s.append(ParamSpec(f"{sc}/bn/beta", (d.conv_ch,), "zeros"))
     for name, cin, cout in (("proj1", d.max_k * d.conv_ch, d.proj1), ("proj2", d.proj1, d.proj2)):
         sc = f"encoder/cbhg/{name}"                                   # module.py:56-68

@@ -128,6 +128,7 @@ typedef struct SatLstmBwd {
   const float* dy; int64_t dy_sb;
   const float* dq0; const float* wq0; int32_t dq0_n;
   const float* dq1; const float* wq1; int32_t dq1_n;
+  int32_t dq_parts; int64_t dq_pstride, dq_bstride;   /* dq rows: sum over dq_parts partials */
   const float* dh_carry;
   const float* dc_carry;
   const float* mask_c; const float* mask_h;
@@ -177,6 +178,39 @@ int sat_attn_part_stride(int32_t M1, int32_t M2);
 int sat_attn_query(int32_t B, int32_t K, int32_t N1, int32_t N2, const float* x, int64_t x_sb,
                    const float* W1, const float* W2, float* q, int64_t q_sb, void* stream);
 int sat_attn_step_fwd(const SatAttnStep* args, void* stream);
+
+/* Backward of one attention step (reverse time t).  Inputs: dctx = dL/d[c1|c2] at t (all
+ * sources), dalpha_next / df_next = the gradients the step t+1 backward sent to alpha_t and to
+ * the location features (NULL at the last step); the forward state of step t (s_t = s_out,
+ * a_t = a_out, a_prev, s_prev, s2_t, stats, q).  Outputs: dalpha_prev, df_out (for step t-1),
+ * dqp [B][ntiles][D1+D2] per-tile query-gradient partials (overwritten), and ACCUMULATED
+ * dK1 [B][N][D1], dK2 [B][N][D2], pg [B*ntiles][pg_stride] = per-tile partial parameter grads
+ * [dv1 D1 | dW_loc F*D1 | dconvW KW*F | dconvb F | dv2 D2].  DA, DS2 are [B][N] scratch.
+ * The value gradients dV = alignments^T dctx are left to one batched GEMM after the loop. */
+typedef struct SatAttnStepBwd {
+  int32_t B, N, D1, M1, D2, M2, F, KW, NT, ntiles, att1_forward;
+  float u;
+  const float* dctx; int64_t dctx_sb;
+  const float* dalpha_next;
+  const float* V1; const float* V2;
+  float* DA; float* DS2;
+  const float* s_t; const float* a_t; const float* a_prev; const float* s_prev; const float* s2_t;
+  const float* stats;
+  const float* df_next;
+  const int64_t* lengths;
+  const float* q; int64_t q_sb;
+  const float* K1; const float* K2;
+  const float* v1; const float* b1; const float* convW; const float* convb; const float* locW;
+  const float* v2;
+  float* dalpha_prev;
+  float* df_out;
+  float* dK1; float* dK2;
+  float* dqp;
+  float* pg; int64_t pg_stride;
+} SatAttnStepBwd;
+
+int sat_attn_pg_stride(int32_t D1, int32_t D2, int32_t F, int32_t KW);
+int sat_attn_step_bwd(const SatAttnStepBwd* args, void* stream);
 
 /* ---------------------------------------------------------------- elementwise
  * out[b,n,:] = x[b,n,:] * (n < lengths[b])  -- TF _prepare_memory (memory_sequence_length). */

@@ -288,7 +288,8 @@ def teacher_inputs(targets, r, n_feed):
 
 
 def decoder_prenets(x, p, hp, masks, spk):
-    g = (lambda k: masks[k]) if masks is not None else (lambda k: None)
+    # decoder prenet masks are stored step-major [T', B, u]; x is [B, T', .]
+    g = (lambda k: masks[k].transpose(0, 1)) if masks is not None else (lambda k: None)
     n = len(hp.decoder_prenet_out_units)
     if spk is not None:                                               # multi_speaker_modules.py:27-32
         d0 = dense(x, p, "decoder/prenet0/dense0", torch.relu)

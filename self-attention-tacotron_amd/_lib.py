@@ -62,8 +62,15 @@ SatLstmFwd = _struct("SatLstmFwd", """
 SatLstmBwd = _struct("SatLstmBwd", """
     i32:B i32:U i32:K i32:hoff i32:t ptr:W ptr:dgates_next ptr:gates ptr:c_prev
     ptr:dy i64:dy_sb ptr:dq0 ptr:wq0 i32:dq0_n ptr:dq1 ptr:wq1 i32:dq1_n
-    ptr:dh_carry ptr:dc_carry ptr:mask_c ptr:mask_h f32:zc f32:zh ptr:lengths
+    i32:dq_parts i64:dq_pstride i64:dq_bstride ptr:dh_carry ptr:dc_carry ptr:mask_c ptr:mask_h f32:zc f32:zh ptr:lengths
     ptr:dgates ptr:dh_carry_out ptr:dc_carry_out""")
+
+SatAttnStepBwd = _struct("SatAttnStepBwd", """
+    i32:B i32:N i32:D1 i32:M1 i32:D2 i32:M2 i32:F i32:KW i32:NT i32:ntiles i32:att1_forward
+    f32:u ptr:dctx i64:dctx_sb ptr:dalpha_next ptr:V1 ptr:V2 ptr:DA ptr:DS2 ptr:s_t ptr:a_t
+    ptr:a_prev ptr:s_prev ptr:s2_t ptr:stats ptr:df_next ptr:lengths ptr:q i64:q_sb ptr:K1 ptr:K2
+    ptr:v1 ptr:b1 ptr:convW ptr:convb ptr:locW ptr:v2 ptr:dalpha_prev ptr:df_out ptr:dK1 ptr:dK2
+    ptr:dqp ptr:pg i64:pg_stride""")
 
 SatAttnStep = _struct("SatAttnStep", """
     i32:B i32:N i32:D1 i32:M1 i32:D2 i32:M2 i32:F i32:KW i32:NT i32:ntiles i32:att1_forward
@@ -83,6 +90,8 @@ SIGNATURES = {
     "sat_attn_part_stride": [_I32, _I32],
     "sat_attn_query": [_I32, _I32, _I32, _I32, _P, _I64, _P, _P, _P, _I64, _P],
     "sat_attn_step_fwd": [ctypes.POINTER(SatAttnStep), _P],
+    "sat_attn_pg_stride": [_I32, _I32, _I32, _I32],
+    "sat_attn_step_bwd": [ctypes.POINTER(SatAttnStepBwd), _P],
     "sat_seq_mask": [_P, _P, _I32, _I32, _I32, _P, _P],
     "sat_embedding_fwd": [_P, _P, _P, _I64, _I32, _I32, _I64, _P, _P],
     "sat_embedding_bwd": [_P, _P, _P, _I64, _I32, _I32, _I64, _P],

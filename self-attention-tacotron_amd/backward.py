@@ -1,0 +1,381 @@
+"""Hand-written backward (BPTT) of the teacher-forced step, on libsat_hip.
+
+Reverse of ``model.model_forward``: loss seeds -> RNNTransformer head -> decoder LSTM2, LSTM1
+recurrences -> attention RNN + dual-source attention recurrence -> memories -> encoder
+(self-attention, BiLSTM, highway, CBHG convolutions + BatchNorm, prenets) -> embedding.
+Weight gradients ACCUMULATE into the flat gradient arena (``G`` views, zeroed by the caller);
+every per-step weight product is deferred to one big MFMA GEMM over all steps after each
+recurrence (dW = sum_t x_t^T dgates_t).
+"""
+
+from __future__ import annotations
+
+import math
+from typing import Dict
+
+import torch
+
+from . import kernels as K
+from .model import _contig_span
+
+
+def lin_bwd(x, dy, W, dW, db, ws, dx=None, beta_dx=0.0, need_dx=True):
+    """Dense backward: dW += x^T dy, db += colsum(dy), dx (=|+=) dy W^T.  x [.., in], dy [.., out]."""
+    x2 = x.reshape(-1, x.shape[-1])
+    dy2 = dy.reshape(-1, dy.shape[-1])
+    K.gemm(x2.t(), dy2, dW, beta=1.0)
+    if db is not None:
+        K.colsum(dy2, db, ws, beta=1.0)
+    if not need_dx:
+        return None
+    if dx is None:
+        dx = torch.empty(*dy.shape[:-1], W.shape[0], device=dy.device)
+    K.gemm(dy2, W.t(), dx.reshape(-1, W.shape[0]), beta=beta_dx)
+    return dx
+
+
+def mha_bwd(P, G, scope, s, dy, ws):
+    """Backward of model.mha_fwd.  Returns dx [B, L, W]."""
+    x, q, k, v, o = s["x"], s["q"], s["k"], s["v"], s["o"]
+    B, L, W = x.shape
+    H, dh = s["heads"], s["dh"]
+    model = q.shape[-1]
+
+    def hv(t):
+        return t.view(B, L, H, dh).permute(0, 2, 1, 3)
+
+    do = lin_bwd(o, dy, P[f"{scope}/output_projection/kernel"],
+                 G[f"{scope}/output_projection/kernel"], G[f"{scope}/output_projection/bias"], ws)
+    dPd = K.gemm(hv(do), hv(v).transpose(-1, -2))                   # [B, H, L, L]
+    dv = torch.empty(B, L, model, device=x.device)
+    K.gemm(s["Pd"].transpose(-1, -2), hv(do), hv(dv))
+    dS = torch.empty_like(dPd)
+    K.softmax_bwd(s["P"], dPd, dS, mask=s["mask"], scale=1.0 / math.sqrt(dh))
+    dq = torch.empty(B, L, model, device=x.device)
+    K.gemm(dS, hv(k), hv(dq))
+    dk = torch.empty(B, L, model, device=x.device)
+    K.gemm(dS.transpose(-1, -2), hv(q), hv(dk))
+    dx = lin_bwd(x, dq, P[f"{scope}/query_projection/kernel"], G[f"{scope}/query_projection/kernel"],
+                 G[f"{scope}/query_projection/bias"], ws)
+    lin_bwd(x, dk, P[f"{scope}/key_projection/kernel"], G[f"{scope}/key_projection/kernel"],
+            G[f"{scope}/key_projection/bias"], ws, dx=dx, beta_dx=1.0)
+    lin_bwd(x, dv, P[f"{scope}/value_projection/kernel"], G[f"{scope}/value_projection/kernel"],
+            G[f"{scope}/value_projection/bias"], ws, dx=dx, beta_dx=1.0)
+    return dx
+
+
+def sa_transformer_bwd(P, G, scope, s, dz, ws):
+    """z = x + tanh(Dense(MHA(x)))  ->  dx."""
+    du = torch.empty_like(dz)
+    K.act_bwd(dz, s["u"], du, "tanh")
+    dy = lin_bwd(s["y"], du, P[f"{scope}/transform/kernel"], G[f"{scope}/transform/kernel"],
+                 G[f"{scope}/transform/bias"], ws)
+    dx = mha_bwd(P, G, f"{scope}/mha", s, dy, ws)
+    K.axpby(dz, dx, 1.0, 1.0)                                        # residual
+    return dx
+
+
+def head_bwd(P, G, hp, d, sv, ws):
+    """RNNTransformer head backward -> dL/dD step-major [T', B, dec]."""
+    Z = sv["Z"]
+    B, Tp, _ = Z.shape
+    dmel_r = sv["dmel"].view(B, Tp, d.num_mels * d.r)
+    dstop = sv["dstop"].view(B, Tp, 1)
+    dZ = lin_bwd(Z, dmel_r, P["decoder/out_projection/kernel"], G["decoder/out_projection/kernel"],
+                 G["decoder/out_projection/bias"], ws)
+    lin_bwd(Z, dstop, P["decoder/stop_token_projection/kernel"],
+            G["decoder/stop_token_projection/kernel"], G["decoder/stop_token_projection/bias"], ws,
+            dx=dZ, beta_dx=1.0)
+    dz = dZ
+    for h in reversed(range(d.dec_hops)):
+        dz = sa_transformer_bwd(P, G, f"decoder/self_attention{h}", sv[f"dec_sa{h}"], dz, ws)
+    return dz.transpose(0, 1).contiguous()                           # [T', B, D] (data movement)
+
+
+def _lstm_loop_bwd(*, B, U, Kr, hoff, Tp, Wr, G_, CS, dY, mc, mh, zc, zh, order, nxt_of,
+                   cprev_of, lengths=None, extra=None):
+    """Reverse recurrence of one LSTM layer; returns DG (same layout as the forward gates)."""
+    dev = G_.device
+    DG = torch.empty_like(G_)
+    hc = [torch.zeros(B, U, device=dev), torch.zeros(B, U, device=dev)]
+    cc = [torch.zeros(B, U, device=dev), torch.zeros(B, U, device=dev)]
+    first = True
+    cur = 0
+    for t in order:
+        nt = nxt_of(t)
+        kw = dict(extra(t)) if extra is not None else {}
+        K.lstm_step_bwd(B=B, U=U, K=Kr, hoff=hoff, t=t, W=Wr,
+                        dgates_next=None if nt is None else DG[nt], gates=G_[t],
+                        c_prev=cprev_of(t), dy=None if dY is None else dY(t),
+                        dh_carry=None if first else hc[cur], dc_carry=None if first else cc[cur],
+                        mask_c=None if mc is None else mc[t], mask_h=None if mh is None else mh[t],
+                        zc=zc, zh=zh, dgates=DG[t], dh_carry_out=hc[1 - cur],
+                        dc_carry_out=cc[1 - cur], lengths=lengths, **kw)
+        first = False
+        cur = 1 - cur
+    return DG
+
+
+def decoder_bwd(P, G, hp, d, dsv, dH2, masks, ws, attn_tile=16):
+    """Backward of decoder.decoder_forward.  Returns (dm1, dm2) batch-major."""
+    S = dsv.tensors
+    B, N, Tp = dsv.B, dsv.N, dsv.Tp
+    dev = dH2.device
+    A, Dd, M1, M2, D1, D2 = d.att_rnn, d.dec, d.m1, d.m2, d.d1, d.d2
+    zc, zh = hp.zoneout_factor_cell, hp.zoneout_factor_output
+    mk = (lambda n: masks[n]) if masks is not None else (lambda n: None)
+    rev = list(range(Tp - 1, -1, -1))
+    nxt = lambda t: t + 1 if t + 1 < Tp else None
+
+    # ---- LSTM 2
+    W2 = P["decoder/lstm2/kernel"]
+    dW2 = G["decoder/lstm2/kernel"]
+    DG2 = _lstm_loop_bwd(B=B, U=Dd, Kr=Dd, hoff=0, Tp=Tp, Wr=W2[Dd:], G_=S["G2"], CS=S["C2S"],
+                         dY=lambda t: dH2[t], mc=mk("dec/lstm2/zc"), mh=mk("dec/lstm2/zh"),
+                         zc=zc, zh=zh, order=rev, nxt_of=nxt, cprev_of=lambda t: S["C2S"][t])
+    DG2f = DG2.view(Tp * B, 4 * Dd)
+    K.gemm(S["H2S"][:Tp].reshape(Tp * B, Dd).t(), DG2f, dW2[Dd:], beta=1.0)
+    dH1 = lin_bwd(S["H1RAW"], DG2, W2[:Dd], dW2[:Dd], G["decoder/lstm2/bias"], ws)
+
+    # ---- LSTM 1
+    W1 = P["decoder/lstm1/kernel"]
+    dW1 = G["decoder/lstm1/kernel"]
+    R0 = M1 + M2 + A
+    DG1 = _lstm_loop_bwd(B=B, U=Dd, Kr=Dd, hoff=0, Tp=Tp, Wr=W1[A + M1 + M2:], G_=S["G1"],
+                         CS=S["C1S"], dY=lambda t: dH1[t], mc=mk("dec/lstm1/zc"),
+                         mh=mk("dec/lstm1/zh"), zc=zc, zh=zh, order=rev, nxt_of=nxt,
+                         cprev_of=lambda t: S["C1S"][t])
+    DG1f = DG1.view(Tp * B, 4 * Dd)
+    K.gemm(S["H1S"][:Tp].reshape(Tp * B, Dd).t(), DG1f, dW1[A + M1 + M2:], beta=1.0)
+    K.colsum(DG1f, G["decoder/lstm1/bias"], ws)
+    ctx_all = S["REC0"][1:].reshape(Tp * B, R0)[:, :M1 + M2]
+    K.gemm(S["H0RAW"].view(Tp * B, A).t(), DG1f, dW1[:A], beta=1.0)
+    K.gemm(ctx_all.t(), DG1f, dW1[A:A + M1 + M2], beta=1.0)
+    dH0 = K.gemm(DG1f, W1[:A].t()).view(Tp, B, A)
+    DCTX = K.gemm(DG1f, W1[A:A + M1 + M2].t()).view(Tp, B, M1 + M2)
+
+    # ---- attention RNN + dual-source attention recurrence
+    W0 = P["decoder/attention_lstm/kernel"]
+    dW0 = G["decoder/attention_lstm/kernel"]
+    p_w = S["prenet"][-1].shape[-1]
+    W0r = W0[p_w:]
+    a1, a2 = "decoder/attention1", "decoder/attention2"
+    fwd = d.att1 == "forward"
+    ntiles = (N + attn_tile - 1) // attn_tile
+    pgs = K.pg_stride(D1, D2, d.loc_f, d.loc_k)
+    f32 = dict(device=dev, dtype=torch.float32)
+    DG0 = torch.empty(Tp, B, 4 * A, **f32)
+    DA = torch.empty(B, N, **f32)
+    DS2 = torch.empty(B, N, **f32)
+    DAP = [torch.zeros(B, N, **f32), torch.zeros(B, N, **f32)]
+    DF = [torch.zeros(B, N, max(d.loc_f, 1), **f32), torch.zeros(B, N, max(d.loc_f, 1), **f32)]
+    DQP = torch.empty(Tp, B, ntiles, D1 + D2, **f32)
+    dK1 = torch.zeros(B, N, D1, **f32)
+    dK2 = torch.zeros(B, N, D2, **f32)
+    PG = torch.zeros(B * ntiles, pgs, **f32)
+    hc = [torch.zeros(B, A, **f32), torch.zeros(B, A, **f32)]
+    cc = [torch.zeros(B, A, **f32), torch.zeros(B, A, **f32)]
+    mc0, mh0 = mk("dec/lstm0/zc"), mk("dec/lstm0/zh")
+    cur = 0
+    for i, t in enumerate(rev):
+        last = i == 0
+        if not last:   # gradient of c_t through the attention RNN's input at step t+1
+            K.gemm(DG0[t + 1], W0r[:M1 + M2].t(), DCTX[t], beta=1.0)
+        K.attn_step_bwd(
+            B=B, N=N, D1=D1, M1=M1, D2=D2, M2=M2, F=d.loc_f, KW=d.loc_k, NT=attn_tile,
+            ntiles=ntiles, att1_forward=1 if fwd else 0, u=0.5, dctx=DCTX[t],
+            dctx_sb=M1 + M2, dalpha_next=None if last else DAP[cur], V1=S["V1"], V2=S["V2"],
+            DA=DA, DS2=DS2, s_t=S["S1"][t + 1], a_t=S["AL1"][t + 1], a_prev=S["AL1"][t],
+            s_prev=S["S1"][t], s2_t=S["S2"][t], stats=S["ST"][t],
+            df_next=None if last else DF[cur], lengths=None, q=S["Q"][t], q_sb=D1 + D2,
+            K1=S["K1"], K2=S["K2"],
+            v1=P[f"{a1}/attention_variable"] if fwd else P[f"{a1}/attention_v"],
+            b1=P[f"{a1}/attention_bias"] if fwd else None,
+            convW=P[f"{a1}/location_conv/kernel"] if fwd else None,
+            convb=P[f"{a1}/location_conv/bias"] if fwd else None,
+            locW=P[f"{a1}/location_layer/kernel"] if fwd else None,
+            v2=P[f"{a2}/attention_v"], dalpha_prev=DAP[1 - cur], df_out=DF[1 - cur],
+            dK1=dK1, dK2=dK2, dqp=DQP[t], pg=PG, pg_stride=pgs)
+        K.lstm_step_bwd(B=B, U=A, K=R0, hoff=M1 + M2, t=t, W=W0r,
+                        dgates_next=None if last else DG0[t + 1], gates=S["G0"][t],
+                        c_prev=S["C0"][t], dy=dH0[t], dh_carry=None if last else hc[cur],
+                        dc_carry=None if last else cc[cur],
+                        mask_c=None if mc0 is None else mc0[t],
+                        mask_h=None if mh0 is None else mh0[t], zc=zc, zh=zh, dgates=DG0[t],
+                        dh_carry_out=hc[1 - cur], dc_carry_out=cc[1 - cur],
+                        dq0=DQP[t][:, :, :D1], wq0=P[f"{a1}/query_layer/kernel"],
+                        dq1=DQP[t][:, :, D1:], wq1=P[f"{a2}/query_layer/kernel"],
+                        dq_parts=ntiles, dq_pstride=D1 + D2, dq_bstride=ntiles * (D1 + D2))
+        cur = 1 - cur
+
+    DG0f = DG0.view(Tp * B, 4 * A)
+    K.gemm(S["REC0"][:Tp].reshape(Tp * B, R0).t(), DG0f, dW0[p_w:], beta=1.0)
+    dP = lin_bwd(S["prenet"][-1], DG0, W0[:p_w], dW0[:p_w], G["decoder/attention_lstm/bias"], ws)
+    # decoder prenets (inputs are teacher frames: no input gradient needed for the first one)
+    pres = S["prenet"]
+    for i in reversed(range(len(d.dec_prenet))):
+        y = pres[i + 1]
+        dpre = torch.empty_like(y)
+        K.act_bwd(dP, y, dpre, "relu", mask=mk(f"dec/prenet{i}"))
+        dP = lin_bwd(pres[i], dpre, P[f"decoder/prenet{i}/kernel"], G[f"decoder/prenet{i}/kernel"],
+                     G[f"decoder/prenet{i}/bias"], ws, need_dx=i > 0)
+
+    # ---- attention parameters from the per-tile partials
+    pg_sum = torch.zeros(pgs, **f32)
+    K.colsum(PG, pg_sum, ws, beta=0.0)
+    o = 0
+    if fwd:
+        F, KW = d.loc_f, d.loc_k
+        K.axpby(pg_sum[o:o + D1], G[f"{a1}/attention_variable"], 1.0, 1.0); o += D1
+        K.axpby(pg_sum[o:o + F * D1], G[f"{a1}/location_layer/kernel"].view(-1), 1.0, 1.0)
+        o += F * D1
+        K.axpby(pg_sum[o:o + KW * F], G[f"{a1}/location_conv/kernel"].view(-1), 1.0, 1.0)
+        o += KW * F
+        K.axpby(pg_sum[o:o + F], G[f"{a1}/location_conv/bias"], 1.0, 1.0); o += F
+    else:
+        K.axpby(pg_sum[o:o + D1], G[f"{a1}/attention_v"], 1.0, 1.0)
+        o += D1 + 0
+        o = (1 + d.loc_f) * D1 + d.loc_k * d.loc_f + d.loc_f
+    K.axpby(pg_sum[o:o + D2], G[f"{a2}/attention_v"], 1.0, 1.0)
+    DQf = DQP.view(Tp * B * ntiles, D1 + D2)
+    if fwd:
+        qsum = torch.zeros(D1 + D2, **f32)
+        K.colsum(DQf, qsum, ws, beta=0.0)
+        K.axpby(qsum[:D1], G[f"{a1}/attention_bias"], 1.0, 1.0)
+    H0f = S["H0RAW"].view(Tp * B, A)
+    DQt = DQP.view(Tp * B, ntiles, D1 + D2)
+    for tile in range(ntiles):
+        K.gemm(H0f.t(), DQt[:, tile, :D1], G[f"{a1}/query_layer/kernel"], beta=1.0)
+        K.gemm(H0f.t(), DQt[:, tile, D1:], G[f"{a2}/query_layer/kernel"], beta=1.0)
+    # ---- memories: values via the alignment histories, keys via memory_layer
+    dV1 = K.gemm(S["AL1"][1:].permute(1, 2, 0), DCTX[:, :, :M1].permute(1, 0, 2))   # [B, N, M1]
+    dV2 = K.gemm(S["S2"].permute(1, 2, 0), DCTX[:, :, M1:].permute(1, 0, 2))        # [B, N, M2]
+    lin_bwd(S["V1"], dK1, P[f"{a1}/memory_layer/kernel"], G[f"{a1}/memory_layer/kernel"], None,
+            ws, dx=dV1, beta_dx=1.0)
+    lin_bwd(S["V2"], dK2, P[f"{a2}/memory_layer/kernel"], G[f"{a2}/memory_layer/kernel"], None,
+            ws, dx=dV2, beta_dx=1.0)
+    return dV1, dV2          # caller applies the sequence mask (values were masked memories)
+
+
+def encoder_bwd(P, G, hp, d, sv, dm1, dm2, lengths, masks, ws):
+    dev = dm1.device
+    mk = (lambda n: masks[n]) if masks is not None else (lambda n: None)
+    B, N, _ = dm1.shape
+    training = sv["training"]
+    # encoder self-attention hops
+    dz = dm2
+    for h in reversed(range(d.enc_hops)):
+        dz = sa_transformer_bwd(P, G, f"encoder/self_attention{h}", sv[f"enc_sa{h}"], dz, ws)
+    lin_bwd(sv["m1"], dz, P["encoder/self_attention_projection/kernel"],
+            G["encoder/self_attention_projection/kernel"],
+            G["encoder/self_attention_projection/bias"], ws, dx=dm1, beta_dx=1.0)
+    # BiLSTM
+    U = d.cbhg_half
+    hws = sv["hws"]
+    hw = hws[-1][2] if len(hws) > 1 else hws[0]
+    Win = hw.shape[-1]
+    hw_sm = hw.transpose(0, 1).contiguous()                          # [N, B, Win] (data movement)
+    dhw = torch.empty(B, N, Win, device=dev)
+    zc, zh = hp.zoneout_factor_cell, hp.zoneout_factor_output
+    for i, (dr, rev) in enumerate((("fw", False), ("bw", True))):
+        st = sv["enc_lstm"][dr]
+        Wk = P[f"encoder/cbhg/lstm_{dr}/kernel"]
+        dWk = G[f"encoder/cbhg/lstm_{dr}/kernel"]
+        half = slice(U, 2 * U) if rev else slice(0, U)
+        dmh = dm1[:, :, half]
+        if rev:
+            order, nxt_of = list(range(N)), (lambda n: n - 1 if n > 0 else None)
+            cprev_of = lambda n, CS=st["CS"]: CS[n + 1]
+        else:
+            order, nxt_of = list(range(N - 1, -1, -1)), (lambda n: n + 1 if n + 1 < N else None)
+            cprev_of = lambda n, CS=st["CS"]: CS[n]
+        DG = _lstm_loop_bwd(B=B, U=U, Kr=U, hoff=0, Tp=N, Wr=Wk[Win:], G_=st["G"], CS=st["CS"],
+                            dY=lambda n, dmh=dmh: dmh[:, n], mc=mk(f"enc/lstm_{dr}/zc"),
+                            mh=mk(f"enc/lstm_{dr}/zh"), zc=zc, zh=zh, order=order,
+                            nxt_of=nxt_of, cprev_of=cprev_of, lengths=lengths)
+        DGf = DG.view(N * B, 4 * U)
+        hprev = st["HS"][1:N + 1] if rev else st["HS"][:N]
+        K.gemm(hprev.reshape(N * B, U).t(), DGf, dWk[Win:], beta=1.0)
+        K.gemm(hw_sm.view(N * B, Win).t(), DGf, dWk[:Win], beta=1.0)
+        K.colsum(DGf, G[f"encoder/cbhg/lstm_{dr}/bias"], ws)
+        # dhw[b, n, :] (+)= DG[n, b, :] @ Wx^T  -- batched over n, written transposed
+        K.gemm(DG, Wk[:Win].t(), dhw.transpose(0, 1), beta=1.0 if i else 0.0)
+    # highway stack
+    dy = dhw
+    for i in reversed(range(d.num_highway)):
+        h, t, y = hws[i + 1]
+        x = hws[i] if i == 0 else hws[i][2]
+        dh_pre = torch.empty_like(h)
+        dt_pre = torch.empty_like(t)
+        dx = torch.empty_like(x)
+        K.highway_bwd(h, t, x, dy, dh_pre, dt_pre, dx)
+        lin_bwd(x, dh_pre, P[f"encoder/cbhg/highway{i}/H/kernel"],
+                G[f"encoder/cbhg/highway{i}/H/kernel"], G[f"encoder/cbhg/highway{i}/H/bias"], ws,
+                dx=dx, beta_dx=1.0)
+        lin_bwd(x, dt_pre, P[f"encoder/cbhg/highway{i}/T/kernel"],
+                G[f"encoder/cbhg/highway{i}/T/kernel"], G[f"encoder/cbhg/highway{i}/T/bias"], ws,
+                dx=dx, beta_dx=1.0)
+        dy = dx
+    if d.needs_adjust:
+        dy = lin_bwd(sv["hw_in_adjust"], dy, P["encoder/cbhg/adjustment/kernel"],
+                     G["encoder/cbhg/adjustment/kernel"], G["encoder/cbhg/adjustment/bias"], ws)
+    # proj2: hw0 = BN(p2_pre) + inp
+    inp = sv["enc_pre"][-1]
+    C2 = d.proj2
+    dinp = dy.clone()                                                # residual branch
+    dp2 = torch.empty_like(sv["p2_pre"])
+    s2 = sv["st_p2"]
+    K.bn_bwd(dy.view(-1, C2), sv["p2_pre"].view(-1, C2), None, dp2.view(-1, C2), s2["mean"],
+             s2["var"], s2["gamma"], G["encoder/cbhg/proj2/bn/gamma"],
+             G["encoder/cbhg/proj2/bn/beta"], ws, training=training)
+    K.conv1d_dw(sv["p1"], dp2, G["encoder/cbhg/proj2/kernel"], beta=1.0)
+    K.colsum(dp2.view(-1, C2), G["encoder/cbhg/proj2/bias"], ws)
+    dp1 = K.conv1d_dx(dp2, P["encoder/cbhg/proj2/kernel"])
+    # proj1: p1 = relu(BN(p1_pre))
+    C1 = d.proj1
+    dp1_pre = torch.empty_like(dp1)
+    s1 = sv["st_p1"]
+    K.bn_bwd(dp1.view(-1, C1), sv["p1_pre"].view(-1, C1), sv["p1"].view(-1, C1),
+             dp1_pre.view(-1, C1), s1["mean"], s1["var"], s1["gamma"],
+             G["encoder/cbhg/proj1/bn/gamma"], G["encoder/cbhg/proj1/bn/beta"], ws,
+             training=training)
+    K.conv1d_dw(sv["mp"], dp1_pre, G["encoder/cbhg/proj1/kernel"], beta=1.0)
+    K.colsum(dp1_pre.view(-1, C1), G["encoder/cbhg/proj1/bias"], ws)
+    dmp = K.conv1d_dx(dp1_pre, P["encoder/cbhg/proj1/kernel"])
+    # max-pool, conv bank BN (one launch over the concatenated channels), conv bank
+    dbank = torch.empty_like(dmp)
+    K.maxpool2_bwd(sv["bank"], dmp, dbank)
+    C, KC = d.conv_ch, d.max_k * d.conv_ch
+    names = [f"encoder/cbhg/conv_bank/K{k}" for k in range(1, d.max_k + 1)]
+    sb = sv["st_bank"]
+    dbank_pre = torch.empty_like(dbank)
+    K.bn_bwd(dbank.view(-1, KC), sv["bank_pre"].view(-1, KC), sv["bank"].view(-1, KC),
+             dbank_pre.view(-1, KC), sb["mean"], sb["var"], sb["gamma"],
+             _contig_span(G, [f"{n}/bn/gamma" for n in names]),
+             _contig_span(G, [f"{n}/bn/beta" for n in names]), ws, training=training)
+    K.colsum(dbank_pre.view(-1, KC), _contig_span(G, [f"{n}/bias" for n in names]), ws)
+    for k in range(1, d.max_k + 1):
+        sl = dbank_pre[:, :, (k - 1) * C:k * C]
+        K.conv1d_dw(inp, sl, G[f"{names[k - 1]}/kernel"], beta=1.0)
+        K.conv1d_dx(sl, P[f"{names[k - 1]}/kernel"], out=dinp, beta=1.0)
+    # prenets + embedding
+    pre = sv["enc_pre"]
+    dx = dinp
+    for i in reversed(range(len(d.enc_prenet))):
+        y = pre[i + 1]
+        dpre = torch.empty_like(y)
+        K.act_bwd(dx, y, dpre, "relu", mask=mk(f"enc/prenet{i}"))
+        dx = lin_bwd(pre[i], dpre, P[f"encoder/prenet{i}/kernel"], G[f"encoder/prenet{i}/kernel"],
+                     G[f"encoder/prenet{i}/bias"], ws)
+    K.embedding_bwd(dx, sv["batch"]["source"], G["embedding"])
+
+
+def model_backward(P, G, hp, d, sv, ws, attn_tile=16):
+    """Accumulate dL/dparams of model_forward's loss into G (caller zeroes G)."""
+    masks = sv["masks"]
+    dH2 = head_bwd(P, G, hp, d, sv, ws)
+    dV1, dV2 = decoder_bwd(P, G, hp, d, sv["dec"], dH2, masks, ws, attn_tile=attn_tile)
+    lengths = sv["batch"]["source_length"]
+    dm1 = K.seq_mask(dV1, lengths)
+    dm2 = K.seq_mask(dV2, lengths)
+    encoder_bwd(P, G, hp, d, sv, dm1, dm2, lengths, masks, ws)

@@ -123,8 +123,8 @@ __global__ void colreduce_finish_kernel(const double* part1, const double* part2
   GRID_STRIDE(c, (int64_t)C) {
     double s = 0.0, q = 0.0;
     for (int r = 0; r < RB; ++r) { s += part1[(int64_t)r * C + c]; q += part2[(int64_t)r * C + c]; }
-    if (out1) out1[c] = (float)(beta * out1[c] + s);
-    if (out2) out2[c] = (float)(beta * out2[c] + q);
+    if (out1) out1[c] = beta != 0.f ? (float)(beta * out1[c] + s) : (float)s;
+    if (out2) out2[c] = beta != 0.f ? (float)(beta * out2[c] + q) : (float)q;
     if (acc1) acc1[c] += (float)s;
     if (acc2) acc2[c] += (float)q;
   }

@@ -112,6 +112,7 @@ struct LstmBwdP {
   const float* dy; int64_t dy_sb;       // dL/dh'_t (raw output), nullable
   const float* dq0; const float* wq0; int dq0_n;   // optional extra dy += dq0[b] . wq0[u]
   const float* dq1; const float* wq1; int dq1_n;
+  int dq_parts; int64_t dq_pstride, dq_bstride;     // dq0/dq1 rows are sums of dq_parts partials
   const float* dh_carry;                // [B][U] (1-m_h(t+1)) dh_{t+1}, or full dh_t if t+1 invalid
   const float* dc_carry;                // [B][U] dL/dc_t
   const float* mask_c; const float* mask_h;
@@ -139,12 +140,20 @@ __global__ void __launch_bounds__(256) lstm_bwd_kernel(LstmBwdP p) {
     }
   }
   if (active && p.dq0) {
-    for (int d = ks; d < p.dq0_n; d += KS)
-      extra += p.dq0[(int64_t)b * p.dq0_n + d] * p.wq0[(int64_t)u * p.dq0_n + d];
+    for (int d = ks; d < p.dq0_n; d += KS) {
+      float g = 0.f;
+      for (int part = 0; part < p.dq_parts; ++part)
+        g += p.dq0[(int64_t)b * p.dq_bstride + part * p.dq_pstride + d];
+      extra += g * p.wq0[(int64_t)u * p.dq0_n + d];
+    }
   }
   if (active && p.dq1) {
-    for (int d = ks; d < p.dq1_n; d += KS)
-      extra += p.dq1[(int64_t)b * p.dq1_n + d] * p.wq1[(int64_t)u * p.dq1_n + d];
+    for (int d = ks; d < p.dq1_n; d += KS) {
+      float g = 0.f;
+      for (int part = 0; part < p.dq_parts; ++part)
+        g += p.dq1[(int64_t)b * p.dq_bstride + part * p.dq_pstride + d];
+      extra += g * p.wq1[(int64_t)u * p.dq1_n + d];
+    }
   }
 #pragma unroll
   for (int o = 1; o < KS; o <<= 1) {
@@ -218,6 +227,9 @@ extern "C" int sat_lstm_step_bwd(const SatLstmBwd* a, void* stream) {
   p.dy = a->dy; p.dy_sb = a->dy_sb;
   p.dq0 = a->dq0; p.wq0 = a->wq0; p.dq0_n = a->dq0_n;
   p.dq1 = a->dq1; p.wq1 = a->wq1; p.dq1_n = a->dq1_n;
+  p.dq_parts = a->dq_parts > 0 ? a->dq_parts : 1;
+  p.dq_pstride = a->dq_pstride;
+  p.dq_bstride = a->dq_bstride > 0 ? a->dq_bstride : a->dq0_n;
   p.dh_carry = a->dh_carry; p.dc_carry = a->dc_carry;
   p.mask_c = a->mask_c; p.mask_h = a->mask_h; p.zc = a->zc; p.zh = a->zh;
   p.lengths = a->lengths; p.t = a->t;

@@ -42,12 +42,13 @@ class DecoderSaved:
 
 def teacher_inputs(targets: torch.Tensor, r: int, n_feed: int) -> torch.Tensor:
     """TransformerTrainingHelper (modules/helpers.py:44-58): step 0 = go frame (zeros),
-    step t = targets.reshape(B, T/r, M*r)[:, t-1, -M*n_feed:].  Pure data movement."""
+    step t = targets.reshape(B, T/r, M*r)[:, t-1, -M*n_feed:].  Step-major [T', B, M*n_feed];
+    pure data movement."""
     B, T, M = targets.shape
     Tp = T // r
-    x = torch.zeros(B, Tp, M * n_feed, device=targets.device, dtype=targets.dtype)
+    x = torch.zeros(Tp, B, M * n_feed, device=targets.device, dtype=targets.dtype)
     g = targets.view(B, Tp, M * r)
-    x[:, 1:].copy_(g[:, :-1, M * (r - n_feed):])
+    x[1:].copy_(g[:, :-1, M * (r - n_feed):].transpose(0, 1))
     return x
 
 
@@ -88,7 +89,7 @@ def decoder_forward(P: Dict[str, torch.Tensor], hp, d: Dims, m1: torch.Tensor, m
 
     # ---- attention RNN (ZoneoutLSTM A) input projection of the prenet part
     W0 = P["decoder/attention_lstm/kernel"]          # [p + M1 + M2 + A, 4A] (gate-interleaved)
-    X0 = K.linear(pre, W0[:p_w], P["decoder/attention_lstm/bias"])     # [B, T', 4A]
+    X0 = K.linear(pre, W0[:p_w], P["decoder/attention_lstm/bias"])     # [T', B, 4A]
     R0 = M1 + M2 + A                                 # recurrent input [c1 | c2 | h0]
     REC0 = torch.zeros(Tp + 1, B, R0, **f32)
     C0 = torch.zeros(Tp + 1, B, A, **f32)
@@ -112,7 +113,7 @@ def decoder_forward(P: Dict[str, torch.Tensor], hp, d: Dims, m1: torch.Tensor, m
     Wr0 = W0[p_w:]
     zc0, zh0 = mk("dec/lstm0/zc"), mk("dec/lstm0/zh")
     for t in range(Tp):
-        K.lstm_step_fwd(B=B, U=A, K=R0, t=t, xproj=X0[:, t], rin=REC0[t], W=Wr0,
+        K.lstm_step_fwd(B=B, U=A, K=R0, t=t, xproj=X0[t], rin=REC0[t], W=Wr0,
                         c_prev=C0[t], h_prev=REC0[t, :, M1 + M2:],
                         mask_c=None if zc0 is None else zc0[t],
                         mask_h=None if zh0 is None else zh0[t], zc=zc, zh=zh,

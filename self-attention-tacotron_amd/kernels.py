@@ -107,13 +107,14 @@ def conv1d(x: torch.Tensor, W: torch.Tensor, bias=None, out=None, act=None, beta
     """Conv1D(SAME, stride 1), x [S, L, Cin] contiguous, W [taps, Cin, Cout] -> [S, L, Cout]."""
     S, L, Cin = x.shape
     taps, Cin2, Cout = W.shape
-    assert Cin == Cin2 and x.is_contiguous() and W.is_contiguous()
+    assert Cin == Cin2 and x.stride(2) == 1 and x.stride(0) == L * x.stride(1)
+    assert W.is_contiguous()
     if out is None:
         out = torch.empty(S, L, Cout, device=x.device, dtype=torch.float32)
     d = _lib.SatGemmDesc()
     d.M, d.N, d.K, d.batch = S * L, Cout, taps * Cin, 1
     d.a_mode, d.a_L, d.a_C, d.a_shift = 1, L, Cin, (taps - 1) // 2
-    d.A, d.a_sm, d.a_sk = _p(x), Cin, 1
+    d.A, d.a_sm, d.a_sk = _p(x), x.stride(1), 1
     d.b_mode, d.B, d.b_sk, d.b_sn = 0, _p(W), Cout, 1
     d.C, d.c_sm = _p(out), out.stride(1)
     d.bias, d.act, d.alpha, d.beta = _p(bias), ACT[act], 1.0, beta
@@ -130,7 +131,7 @@ def conv1d_dx(dy: torch.Tensor, W: torch.Tensor, out=None, beta=0.0):
     d = _lib.SatGemmDesc()
     d.M, d.N, d.K, d.batch = S * L, Cin, taps * Cout, 1
     d.a_mode, d.a_L, d.a_C, d.a_shift = 1, L, Cout, taps - 1 - (taps - 1) // 2
-    d.A, d.a_sm, d.a_sk = _p(dy), Cout, 1
+    d.A, d.a_sm, d.a_sk = _p(dy), dy.stride(1), 1
     d.b_mode, d.b_taps, d.b_C, d.B = 1, taps, Cout, _p(W)
     d.C, d.c_sm = _p(out), out.stride(1)
     d.alpha, d.beta = 1.0, beta
@@ -145,8 +146,8 @@ def conv1d_dw(x: torch.Tensor, dy: torch.Tensor, dW: torch.Tensor, beta=0.0):
     d = _lib.SatGemmDesc()
     d.M, d.N, d.K, d.batch = taps * Cin, Cout, S * L, 1
     d.a_mode, d.a_L, d.a_C, d.a_shift = 2, L, Cin, (taps - 1) // 2
-    d.A, d.a_sm, d.a_sk = _p(x), Cin, 1
-    d.b_mode, d.B, d.b_sk, d.b_sn = 0, _p(dy), Cout, 1
+    d.A, d.a_sm, d.a_sk = _p(x), x.stride(1), 1
+    d.b_mode, d.B, d.b_sk, d.b_sn = 0, _p(dy), dy.stride(1), 1
     d.C, d.c_sm = _p(dW), Cout
     d.alpha, d.beta = 1.0, beta
     _lib.check(_lib.load().sat_gemm(ctypes.byref(d), _stream()), "sat_gemm(conv1d_dw)")
@@ -195,13 +196,15 @@ def lstm_step_fwd(*, B, U, K, t, xproj, rin, W, c_prev, h_prev, mask_c, mask_h, 
 
 def lstm_step_bwd(*, B, U, K, hoff, t, W, dgates_next, gates, c_prev, dy, dh_carry, dc_carry,
                   mask_c, mask_h, zc, zh, dgates, dh_carry_out, dc_carry_out, lengths=None,
-                  dq0=None, wq0=None, dq1=None, wq1=None):
+                  dq0=None, wq0=None, dq1=None, wq1=None, dq_parts=1, dq_pstride=0,
+                  dq_bstride=0):
     a = _lib.SatLstmBwd()
     a.B, a.U, a.K, a.hoff, a.t = B, U, K, hoff, t
     a.W, a.dgates_next, a.gates, a.c_prev = _p(W), _p(dgates_next), _p(gates), _p(c_prev)
     a.dy, a.dy_sb = _p(dy), _rs(dy)
     a.dq0, a.wq0, a.dq0_n = _p(dq0), _p(wq0), 0 if dq0 is None else dq0.shape[-1]
     a.dq1, a.wq1, a.dq1_n = _p(dq1), _p(wq1), 0 if dq1 is None else dq1.shape[-1]
+    a.dq_parts, a.dq_pstride, a.dq_bstride = dq_parts, dq_pstride, dq_bstride
     a.dh_carry, a.dc_carry = _p(dh_carry), _p(dc_carry)
     a.mask_c, a.mask_h = _p(mask_c), _p(mask_h)
     a.zc, a.zh = zc, zh
@@ -218,6 +221,17 @@ def attn_query(x, W1, W2, q):
 
 def part_stride(M1, M2) -> int:
     return _lib.load().sat_attn_part_stride(M1, M2)
+
+
+def attn_step_bwd(**kw):
+    a = _lib.SatAttnStepBwd()
+    for k, v in kw.items():
+        setattr(a, k, _p(v) if isinstance(v, torch.Tensor) else v)
+    _lib.check(_lib.load().sat_attn_step_bwd(ctypes.byref(a), _stream()), "sat_attn_step_bwd")
+
+
+def pg_stride(D1, D2, F, KW) -> int:
+    return _lib.load().sat_attn_pg_stride(D1, D2, F, KW)
 
 
 def attn_step_fwd(**kw):

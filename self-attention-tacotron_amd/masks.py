@@ -42,8 +42,8 @@ def mask_specs(hp, B: int, N: int, Tp: int) -> List[MaskSpec]:
     for h in range(d.enc_hops):
         out.append(MaskSpec(f"enc/sa{h}/probs", (B, d.enc_heads, N, N), "dropout",
                             hp.self_attention_drop_rate))
-    for i, u in enumerate(d.dec_prenet):
-        out.append(MaskSpec(f"dec/prenet{i}", (B, Tp, u), "dropout", hp.decoder_prenet_drop_rate))
+    for i, u in enumerate(d.dec_prenet):   # step-major like every decoder-loop tensor
+        out.append(MaskSpec(f"dec/prenet{i}", (Tp, B, u), "dropout", hp.decoder_prenet_drop_rate))
     for name, units in (("lstm0", d.att_rnn), ("lstm1", d.dec), ("lstm2", d.dec)):
         out.append(MaskSpec(f"dec/{name}/zc", (Tp, B, units), "zoneout", zc))
         out.append(MaskSpec(f"dec/{name}/zh", (Tp, B, units), "zoneout", zh))

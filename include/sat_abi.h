@@ -171,6 +171,8 @@ typedef struct SatAttnStep {
   float* s_out; float* a_out; float* s2_out;/* [B][N] */
   float* ctx; int64_t ctx_sb;               /* [B][M1 + M2] */
   float* stats;                             /* [B][4] or NULL */
+  int32_t phases;                           /* 0 or 3: both kernels; 1: tile kernel only;
+                                               2: combine only (profiling / split launches) */
 } SatAttnStep;
 
 int sat_attn_part_stride(int32_t M1, int32_t M2);
@@ -279,6 +281,22 @@ int sat_loss_fwd_bwd(const float* mel, const float* tgt, const float* tmask, con
                      const float* done, const float* dmask, int32_t B, int32_t T, int32_t M,
                      int32_t Tp, float l1_weight, float* out, float* dmel, float* dstop,
                      void* stream);
+
+/* ---------------------------------------------------------------- optimiser
+ * models/models.py:175-189 + :283-287 over the whole flat arena in three launches:
+ * global norm (fp64 partials), scalar prepare (Noam lr, clip scale, Adam bias correction, reads
+ * and increments *global_step on the device), elementwise Adam (TF epsilon-hat form).
+ * scalars[4] receives {norm, clip scale, lr, lr_t}.  workspace: sat_workspace_adam() bytes. */
+typedef struct SatAdamConfig {
+  float lr0, beta1, beta2, eps, clip_norm;   /* clip_norm <= 0 disables clipping */
+  int32_t decay, step_factor;
+} SatAdamConfig;
+
+int64_t sat_workspace_adam(void);
+int sat_global_norm_sq(const float* g, int64_t n, double* partials, void* stream);
+int sat_adam_step(float* params, const float* grads, float* m, float* v, int64_t n,
+                  int64_t* global_step, float* scalars, void* workspace,
+                  const SatAdamConfig* cfg, void* stream);
 
 #ifdef __cplusplus
 }

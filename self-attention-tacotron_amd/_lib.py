@@ -65,6 +65,9 @@ SatLstmBwd = _struct("SatLstmBwd", """
     i32:dq_parts i64:dq_pstride i64:dq_bstride ptr:dh_carry ptr:dc_carry ptr:mask_c ptr:mask_h f32:zc f32:zh ptr:lengths
     ptr:dgates ptr:dh_carry_out ptr:dc_carry_out""")
 
+SatAdamConfig = _struct("SatAdamConfig", """
+    f32:lr0 f32:beta1 f32:beta2 f32:eps f32:clip_norm i32:decay i32:step_factor""")
+
 SatAttnStepBwd = _struct("SatAttnStepBwd", """
     i32:B i32:N i32:D1 i32:M1 i32:D2 i32:M2 i32:F i32:KW i32:NT i32:ntiles i32:att1_forward
     f32:u ptr:dctx i64:dctx_sb ptr:dalpha_next ptr:V1 ptr:V2 ptr:DA ptr:DS2 ptr:s_t ptr:a_t
@@ -76,7 +79,7 @@ SatAttnStep = _struct("SatAttnStep", """
     i32:B i32:N i32:D1 i32:M1 i32:D2 i32:M2 i32:F i32:KW i32:NT i32:ntiles i32:att1_forward
     f32:u ptr:q i64:q_sb ptr:K1 ptr:V1 ptr:K2 ptr:V2 ptr:lengths ptr:s_prev ptr:a_prev
     ptr:v1 ptr:b1 ptr:convW ptr:convb ptr:locW ptr:v2 ptr:e1 ptr:e2 ptr:part i64:part_stride
-    ptr:s_out ptr:a_out ptr:s2_out ptr:ctx i64:ctx_sb ptr:stats""")
+    ptr:s_out ptr:a_out ptr:s2_out ptr:ctx i64:ctx_sb ptr:stats i32:phases""")
 
 # name -> argtypes (restype is int for all but sat_last_error_string)
 SIGNATURES = {
@@ -111,7 +114,13 @@ SIGNATURES = {
     "sat_loss_fwd_bwd": [_P, _P, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _F, _P, _P, _P, _P],
 }
 
-RESTYPES = {"sat_workspace_colreduce": (ctypes.c_int64, [_I32, _I32])}
+SIGNATURES.update({
+    "sat_global_norm_sq": [_P, _I64, _P, _P],
+    "sat_adam_step": [_P, _P, _P, _P, _I64, _P, _P, _P, ctypes.POINTER(SatAdamConfig), _P],
+})
+
+RESTYPES = {"sat_workspace_colreduce": (ctypes.c_int64, [_I32, _I32]),
+            "sat_workspace_adam": (ctypes.c_int64, [])}
 
 _lib: Optional[ctypes.CDLL] = None
 

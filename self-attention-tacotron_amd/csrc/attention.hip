@@ -295,8 +295,12 @@ extern "C" int sat_attn_step_fwd(const SatAttnStep* a, void* stream) {
   p.v2 = a->v2; p.u = a->u; p.e1 = a->e1; p.e2 = a->e2; p.part = a->part;
   p.part_stride = a->part_stride;
   hipStream_t s = as_stream(stream);
-  hipLaunchKernelGGL(attn_energy_kernel, dim3(a->ntiles, a->B), dim3(256), 0, s, p);
-  SAT_LAUNCH_CHECK("sat_attn_step_fwd(energy)");
+  const int phases = a->phases == 0 ? 3 : a->phases;
+  if (phases & 1) {
+    hipLaunchKernelGGL(attn_energy_kernel, dim3(a->ntiles, a->B), dim3(256), 0, s, p);
+    SAT_LAUNCH_CHECK("sat_attn_step_fwd(energy)");
+  }
+  if (!(phases & 2)) return SAT_OK;
   AttnCombineP c;
   c.B = a->B; c.N = a->N; c.M1 = a->M1; c.M2 = a->M2; c.ntiles = a->ntiles;
   c.att1_forward = a->att1_forward; c.u = a->u;

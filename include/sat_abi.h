@@ -58,6 +58,8 @@ int sat_device_arch(char* buf, int len);       /* gcnArchName of the current dev
  *     (fused residual connections, e.g. SelfAttentionTransformer x + tanh(Dense(.))).
  * Batching: blockIdx.z = z1 * batch2 + z2 (batch = z1 count, batch2 >= 1 inner count); every
  * operand is offset by z1 * s?batch + z2 * s?batch2 (e.g. z1 = utterance, z2 = head).
+ * ws/ws_bytes (optional caller scratch): enables deterministic split-K for products with few
+ * output tiles and a long reduction (weight gradients); NULL disables it.
  */
 typedef struct SatGemmDesc {
   int32_t M, N, K, batch;
@@ -78,9 +80,16 @@ typedef struct SatGemmDesc {
   int64_t a_sbatch2, b_sbatch2, c_sbatch2, mul_sbatch2;
   const float* add;
   int64_t add_sm, add_sbatch;
+  void* ws;
+  int64_t ws_bytes;
 } SatGemmDesc;
 
 int sat_gemm(const SatGemmDesc* desc, void* stream);
+/* Skinny product C = alpha * A . Bt^T + beta * C, A [M][K], Bt [N][K] rows contiguous in K
+ * (16-B aligned, K % 4 == 0): the per-step gradient of the attention contexts through the
+ * attention RNN's input weights (M = batch). */
+int sat_gemm_rowdot(int32_t M, int32_t N, int32_t K, const float* A, int64_t lda, const float* Bt,
+                    int64_t ldb, float* C, int64_t ldc, float alpha, float beta, void* stream);
 
 /* ---------------------------------------------------------------- RNG masks
  * Counter-based (Philox-4x32-10) Bernoulli masks: out[i] = (u_i < keep) ? on_value : 0.

@@ -40,6 +40,7 @@ class SatGemmDesc(ctypes.Structure):
         ("a_sbatch2", ctypes.c_int64), ("b_sbatch2", ctypes.c_int64),
         ("c_sbatch2", ctypes.c_int64), ("mul_sbatch2", ctypes.c_int64),
         ("add", ctypes.c_void_p), ("add_sm", ctypes.c_int64), ("add_sbatch", ctypes.c_int64),
+        ("ws", ctypes.c_void_p), ("ws_bytes", ctypes.c_int64),
     ]
 
 
@@ -115,6 +116,7 @@ SIGNATURES = {
 }
 
 SIGNATURES.update({
+    "sat_gemm_rowdot": [_I32, _I32, _I32, _P, _I64, _P, _I64, _P, _I64, _F, _F, _P],
     "sat_global_norm_sq": [_P, _I64, _P, _P],
     "sat_adam_step": [_P, _P, _P, _P, _I64, _P, _P, _P, ctypes.POINTER(SatAdamConfig), _P],
 })

@@ -180,7 +180,7 @@ def decoder_bwd(P, G, hp, d, dsv, dH2, masks, ws, attn_tile=16):
     for i, t in enumerate(rev):
         last = i == 0
         if not last:   # gradient of c_t through the attention RNN's input at step t+1
-            K.gemm(DG0[t + 1], W0r[:M1 + M2].t(), DCTX[t], beta=1.0)
+            K.rowdot(DG0[t + 1], W0r[:M1 + M2], DCTX[t], beta=1.0)
         K.attn_step_bwd(
             B=B, N=N, D1=D1, M1=M1, D2=D2, M2=M2, F=d.loc_f, KW=d.loc_k, NT=attn_tile,
             ntiles=ntiles, att1_forward=1 if fwd else 0, u=0.5, dctx=DCTX[t],

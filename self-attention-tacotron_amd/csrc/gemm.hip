@@ -4,10 +4,13 @@
 // products, the Conv1D(SAME) of the CBHG (implicit im2col in the A loader -- no im2col buffer
 // in HBM) and all their gradients (transposes are strides; conv dX / dW are A/B modes).
 //
-// Tile: BM x BN x 16, 256 threads = 4 waves in a 2x2 grid, each wave (BM/2)x(BN/2) made of
-// 32x32 MFMA sub-tiles.  Global -> registers (next tile prefetched while the current one is
-// multiplied) -> LDS ([k][m] / [k][n] images, +1 padding so the transposing stores are
-// conflict-free) -> one f32 per lane per MFMA operand (ds_read_b32, contiguous per 32 lanes).
+// Tile: BM x BN x 32, 256 threads = 4 waves in a 2x2 grid, each wave (BM/2)x(BN/2) made of
+// 32x32 MFMA sub-tiles.  Global -> registers (tile k+1 prefetched while tile k is multiplied,
+// 16-byte loads whenever the contiguous dimension allows) -> double-buffered LDS ([k][m] /
+// [k][n] images) -> one f32 per lane per MFMA operand; one barrier per K-tile.
+// Weight-gradient products (K = T' * B = 16,000 rows, M x N <= 1024 x 1024) have too few output
+// tiles to fill 256 CUs: they run split-K into an fp32 workspace slab [S][M][N] and a second
+// launch sums the slabs in a fixed order and applies the epilogue (deterministic, no atomics).
 #include "sat_common.h"
 
 namespace sat {
@@ -15,7 +18,7 @@ namespace {
 
 using f32x16 = __attribute__((ext_vector_type(16))) float;
 
-constexpr int BK = 16;
+constexpr int BK = 32;
 
 struct GemmP {
   int M, N, K;
@@ -36,7 +39,9 @@ struct GemmP {
   int64_t a_sbatch2, b_sbatch2, c_sbatch2, mul_sbatch2;
   const float* add;
   int64_t add_sm, add_sbatch;
-  int a_kcontig, b_ncontig;
+  int a_kcontig, b_ncontig, a_vec, b_vec;
+  int splits, kchunk;          // split-K: grid.z = splits (batch == 1), partial slabs in ws
+  float* ws;
 };
 
 __device__ __forceinline__ float load_a(const GemmP& p, const float* A, int m, int k) {
@@ -75,50 +80,99 @@ __device__ __forceinline__ float apply_act(float v, int act) {
 
 template <int BM, int BN>
 __global__ void __launch_bounds__(256) gemm_kernel(GemmP p) {
-  constexpr int WM = BM / 2, WN = BN / 2;         // per-wave tile
-  constexpr int SM = WM / 32, SN = WN / 32;       // 32x32 sub-tiles per wave
-  constexpr int EA = BM * BK / 256, EB = BN * BK / 256;
-  __shared__ float As[BK][BM + 1];
-  __shared__ float Bs[BK][BN + 1];
+  constexpr int WM = BM / 2, WN = BN / 2;
+  constexpr int SM = WM / 32, SN = WN / 32;
+  constexpr int EA = BM * BK / 256, EB = BN * BK / 256;   // scalars per thread per tile
+  constexpr int PA = 1, PB = 4;                            // LDS row padding (floats)
+  __shared__ float As[2][BK][BM + PA];
+  __shared__ __attribute__((aligned(16))) float Bs[2][BK][BN + PB];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = (wave >> 1) * WM, wn = (wave & 1) * WN;
-  const int bz = blockIdx.z / p.batch2, bz2 = blockIdx.z - bz * p.batch2;
+  int bz, bz2, split;
+  if (p.splits > 1) { bz = 0; bz2 = 0; split = blockIdx.z; }
+  else { bz = blockIdx.z / p.batch2; bz2 = blockIdx.z - bz * p.batch2; split = 0; }
   const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
   const float* A = p.A + bz * p.a_sbatch + bz2 * p.a_sbatch2;
   const float* B = p.B + bz * p.b_sbatch + bz2 * p.b_sbatch2;
+  const int kbeg = split * p.kchunk;
+  const int kend = min(p.K, kbeg + p.kchunk);
 
   float ra[EA], rb[EB];
   auto fetch = [&](int k0) {
+    if (p.a_vec) {   // k-contiguous, 16-B aligned rows: float4 along k
 #pragma unroll
-    for (int i = 0; i < EA; ++i) {
-      const int e = tid + i * 256;
-      int m, k;
-      if (p.a_kcontig) { m = e / BK; k = e % BK; } else { k = e / BM; m = e % BM; }
-      ra[i] = load_a(p, A, m0 + m, k0 + k);
+      for (int i = 0; i < EA / 4; ++i) {
+        const int e = tid + i * 256;            // float4 index within the tile
+        const int m = e / (BK / 4), kq = (e % (BK / 4)) * 4;
+        const int gm = m0 + m, gk = k0 + kq;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (gm < p.M && gk < kend) v = *reinterpret_cast<const float4*>(A + gm * p.a_sm + gk);
+        ra[4 * i + 0] = v.x; ra[4 * i + 1] = v.y; ra[4 * i + 2] = v.z; ra[4 * i + 3] = v.w;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < EA; ++i) {
+        const int e = tid + i * 256;
+        int m, k;
+        if (p.a_kcontig) { m = e / BK; k = e % BK; } else { k = e / BM; m = e % BM; }
+        ra[i] = (k0 + k < kend) ? load_a(p, A, m0 + m, k0 + k) : 0.f;
+      }
     }
+    if (p.b_vec) {   // n-contiguous, 16-B aligned rows: float4 along n
 #pragma unroll
-    for (int i = 0; i < EB; ++i) {
-      const int e = tid + i * 256;
-      int k, n;
-      if (p.b_ncontig) { k = e / BN; n = e % BN; } else { n = e / BK; k = e % BK; }
-      rb[i] = load_b(p, B, k0 + k, n0 + n);
+      for (int i = 0; i < EB / 4; ++i) {
+        const int e = tid + i * 256;
+        const int k = e / (BN / 4), nq = (e % (BN / 4)) * 4;
+        const int gk = k0 + k, gn = n0 + nq;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (gk < kend && gn < p.N) v = *reinterpret_cast<const float4*>(B + gk * p.b_sk + gn);
+        rb[4 * i + 0] = v.x; rb[4 * i + 1] = v.y; rb[4 * i + 2] = v.z; rb[4 * i + 3] = v.w;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < EB; ++i) {
+        const int e = tid + i * 256;
+        int k, n;
+        if (p.b_ncontig) { k = e / BN; n = e % BN; } else { n = e / BK; k = e % BK; }
+        rb[i] = (k0 + k < kend) ? load_b(p, B, k0 + k, n0 + n) : 0.f;
+      }
     }
   };
-  auto stash = [&]() {
+  auto stash = [&](int buf) {
+    if (p.a_vec) {
 #pragma unroll
-    for (int i = 0; i < EA; ++i) {
-      const int e = tid + i * 256;
-      int m, k;
-      if (p.a_kcontig) { m = e / BK; k = e % BK; } else { k = e / BM; m = e % BM; }
-      As[k][m] = ra[i];
+      for (int i = 0; i < EA / 4; ++i) {
+        const int e = tid + i * 256;
+        const int m = e / (BK / 4), kq = (e % (BK / 4)) * 4;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) As[buf][kq + j][m] = ra[4 * i + j];
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < EA; ++i) {
+        const int e = tid + i * 256;
+        int m, k;
+        if (p.a_kcontig) { m = e / BK; k = e % BK; } else { k = e / BM; m = e % BM; }
+        As[buf][k][m] = ra[i];
+      }
     }
+    if (p.b_vec) {
 #pragma unroll
-    for (int i = 0; i < EB; ++i) {
-      const int e = tid + i * 256;
-      int k, n;
-      if (p.b_ncontig) { k = e / BN; n = e % BN; } else { n = e / BK; k = e % BK; }
-      Bs[k][n] = rb[i];
+      for (int i = 0; i < EB / 4; ++i) {
+        const int e = tid + i * 256;
+        const int k = e / (BN / 4), nq = (e % (BN / 4)) * 4;
+        *reinterpret_cast<float4*>(&Bs[buf][k][nq]) =
+            make_float4(rb[4 * i], rb[4 * i + 1], rb[4 * i + 2], rb[4 * i + 3]);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < EB; ++i) {
+        const int e = tid + i * 256;
+        int k, n;
+        if (p.b_ncontig) { k = e / BN; n = e % BN; } else { n = e / BK; k = e % BK; }
+        Bs[buf][k][n] = rb[i];
+      }
     }
   };
 
@@ -130,34 +184,52 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmP p) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  const int nk = (p.K + BK - 1) / BK;
-  fetch(0);
-  stash();
-  __syncthreads();
+  const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
   const int li = lane & 31, lk = lane >> 5;
+  if (nk > 0) {
+    fetch(kbeg);
+    stash(0);
+    __syncthreads();
+  }
+  int cur = 0;
   for (int kt = 0; kt < nk; ++kt) {
-    if (kt + 1 < nk) fetch((kt + 1) * BK);
+    const bool more = kt + 1 < nk;
+    if (more) fetch(kbeg + (kt + 1) * BK);
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 2) {
       float a[SM], b[SN];
 #pragma unroll
-      for (int i = 0; i < SM; ++i) a[i] = As[kk + lk][wm + i * 32 + li];
+      for (int i = 0; i < SM; ++i) a[i] = As[cur][kk + lk][wm + i * 32 + li];
 #pragma unroll
-      for (int j = 0; j < SN; ++j) b[j] = Bs[kk + lk][wn + j * 32 + li];
+      for (int j = 0; j < SN; ++j) b[j] = Bs[cur][kk + lk][wn + j * 32 + li];
 #pragma unroll
       for (int i = 0; i < SM; ++i)
 #pragma unroll
         for (int j = 0; j < SN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
     }
+    if (more) stash(cur ^ 1);
     __syncthreads();
-    if (kt + 1 < nk) {
-      stash();
-      __syncthreads();
-    }
+    cur ^= 1;
   }
 
   // epilogue: C/D map of 32x32 f32 MFMA: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
+  if (p.splits > 1) {
+    float* slab = p.ws + (int64_t)split * p.M * p.N;
+#pragma unroll
+    for (int i = 0; i < SM; ++i)
+#pragma unroll
+      for (int j = 0; j < SN; ++j) {
+        const int col = n0 + wn + j * 32 + li;
+        if (col >= p.N) continue;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = m0 + wm + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk;
+          if (row < p.M) slab[(int64_t)row * p.N + col] = acc[i][j][r];
+        }
+      }
+    return;
+  }
   float* C = p.C + bz * p.c_sbatch + bz2 * p.c_sbatch2;
   const float* bias = p.bias ? p.bias + bz * p.bias_sbatch : nullptr;
   const float* mul = p.mul ? p.mul + bz * p.mul_sbatch + bz2 * p.mul_sbatch2 : nullptr;
@@ -184,8 +256,72 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmP p) {
     }
 }
 
+// split-K finish: sum S slabs in order, then the same epilogue as gemm_kernel (batch == 1)
+__global__ void __launch_bounds__(256) gemm_splitk_reduce(GemmP p) {
+  const int64_t total = (int64_t)p.M * p.N;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int row = (int)(i / p.N), col = (int)(i - (int64_t)row * p.N);
+    float s = 0.f;
+    for (int k = 0; k < p.splits; ++k) s += p.ws[(int64_t)k * total + i];
+    float* dst = p.C + (int64_t)row * p.c_sm + col;
+    float v = p.alpha * s;
+    if (p.beta != 0.f) v += p.beta * (*dst);
+    v = apply_act(v + (p.bias ? p.bias[col] : 0.f), p.act);
+    if (p.mul) v *= p.mul[(int64_t)row * p.mul_sm + col];
+    if (p.add) v += p.add[(int64_t)row * p.add_sm + col];
+    *dst = v;
+  }
+}
+
+inline bool aligned16(const void* ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 15) == 0; }
+
+// Skinny product C[M][N] = alpha * A[M][K] . Bt[N][K]^T + beta * C with both operands' rows
+// contiguous in K (a per-decoder-step [B=32] x [4U=1024] x [288] gradient product): 8 lanes
+// per output element, 16-byte loads, 3 xor-shuffles -- no LDS, no barrier, 288 workgroups.
+__global__ void __launch_bounds__(256) rowdot_kernel(int M, int N, int K, const float* __restrict__ A,
+                                                     int64_t lda, const float* __restrict__ Bt,
+                                                     int64_t ldb, float* __restrict__ C, int64_t ldc,
+                                                     float alpha, float beta) {
+  const int ks = threadIdx.x & 7;
+  const int64_t pairg = (int64_t)blockIdx.x * 32 + (threadIdx.x >> 3);
+  const int m = (int)(pairg / N), n = (int)(pairg - (int64_t)(pairg / N) * N);
+  float acc = 0.f;
+  if (m < M) {
+    const float4* a = reinterpret_cast<const float4*>(A + m * lda);
+    const float4* bt = reinterpret_cast<const float4*>(Bt + n * ldb);
+#pragma unroll 8
+    for (int c = ks; c < (K >> 2); c += 8) {
+      const float4 x = a[c], w = bt[c];
+      acc += x.x * w.x + x.y * w.y + x.z * w.z + x.w * w.w;
+    }
+  }
+  acc += __shfl_xor(acc, 1, 64);
+  acc += __shfl_xor(acc, 2, 64);
+  acc += __shfl_xor(acc, 4, 64);
+  if (m < M && ks == 0) {
+    float* dst = C + m * ldc + n;
+    *dst = beta != 0.f ? alpha * acc + beta * (*dst) : alpha * acc;
+  }
+}
+
 }  // namespace
 }  // namespace sat
+
+extern "C" int sat_gemm_rowdot(int32_t M, int32_t N, int32_t K, const float* A, int64_t lda,
+                               const float* Bt, int64_t ldb, float* C, int64_t ldc, float alpha,
+                               float beta, void* stream) {
+  using namespace sat;
+  SAT_CHECK_ARG(M >= 0 && N > 0 && K >= 0 && A && Bt && C, "sat_gemm_rowdot: bad args");
+  SAT_CHECK_ARG(K % 4 == 0 && lda % 4 == 0 && ldb % 4 == 0 && aligned16(A) && aligned16(Bt),
+                "sat_gemm_rowdot: rows must be 16-byte aligned with K % 4 == 0");
+  if (M == 0) return SAT_OK;
+  const int64_t pairs = (int64_t)M * N;
+  hipLaunchKernelGGL(rowdot_kernel, dim3((unsigned)((pairs + 31) / 32)), dim3(256), 0,
+                     as_stream(stream), M, N, K, A, lda, Bt, ldb, C, ldc, alpha, beta);
+  SAT_LAUNCH_CHECK("sat_gemm_rowdot");
+  return SAT_OK;
+}
 
 extern "C" int sat_gemm(const SatGemmDesc* d, void* stream) {
   using namespace sat;
@@ -213,18 +349,47 @@ extern "C" int sat_gemm(const SatGemmDesc* d, void* stream) {
   p.a_sbatch2 = d->a_sbatch2; p.b_sbatch2 = d->b_sbatch2; p.c_sbatch2 = d->c_sbatch2;
   p.mul_sbatch2 = d->mul_sbatch2;
   p.add = d->add; p.add_sm = d->add_sm; p.add_sbatch = d->add_sbatch;
-  // coalescing order of the tile loaders
+  // coalescing order / vector width of the tile loaders
   p.a_kcontig = (d->a_mode == 1) ? 1 : (d->a_mode == 2 ? 0 : (d->a_sk == 1 ? 1 : 0));
   p.b_ncontig = (d->b_mode == 1) ? 0 : (d->b_sn == 1 ? 1 : 0);
+  const bool bstr_ok = (p.a_sbatch % 4 == 0) && (p.a_sbatch2 % 4 == 0);
+  p.a_vec = (d->a_mode == 0 && d->a_sk == 1 && d->a_sm % 4 == 0 && d->K % 4 == 0 &&
+             aligned16(d->A) && bstr_ok) ? 1 : 0;
+  p.b_vec = (d->b_mode == 0 && d->b_sn == 1 && d->b_sk % 4 == 0 && d->N % 4 == 0 &&
+             aligned16(d->B) && p.b_sbatch % 4 == 0 && p.b_sbatch2 % 4 == 0) ? 1 : 0;
   hipStream_t s = as_stream(stream);
-  const bool big = (int64_t)d->M * d->N >= (int64_t)256 * 128 * 128 && d->N >= 96 && d->M >= 96;
+  const int nb = d->batch * p.batch2;
+  const bool big = (int64_t)d->M * d->N * nb >= (int64_t)256 * 128 * 128 && d->N >= 96 && d->M >= 96;
+  const int BMs = big ? 128 : 64;
+  const int tiles = ceil_div(d->M, BMs) * ceil_div(d->N, BMs) * nb;
+  // split-K for weight-gradient-shaped products (few output tiles, long reduction)
+  p.splits = 1;
+  p.kchunk = d->K;
+  p.ws = reinterpret_cast<float*>(d->ws);
+  if (nb == 1 && tiles < 160 && d->K >= 512 && d->ws != nullptr) {
+    int S = std::min<int>(std::max(1, 384 / tiles), std::max(1, d->K / 256));
+    S = std::min(S, 64);
+    while (S > 1 && (int64_t)S * d->M * d->N * 4 > d->ws_bytes) --S;
+    if (S > 1) {
+      p.kchunk = (ceil_div(d->K, S) + BK - 1) / BK * BK;
+      S = ceil_div(d->K, p.kchunk);
+      p.splits = S;
+    }
+  }
+  const int gz = p.splits > 1 ? p.splits : nb;
   if (big) {
-    dim3 grid(ceil_div(d->N, 128), ceil_div(d->M, 128), d->batch * p.batch2);
+    dim3 grid(ceil_div(d->N, 128), ceil_div(d->M, 128), gz);
     hipLaunchKernelGGL((gemm_kernel<128, 128>), grid, dim3(256), 0, s, p);
   } else {
-    dim3 grid(ceil_div(d->N, 64), ceil_div(d->M, 64), d->batch * p.batch2);
+    dim3 grid(ceil_div(d->N, 64), ceil_div(d->M, 64), gz);
     hipLaunchKernelGGL((gemm_kernel<64, 64>), grid, dim3(256), 0, s, p);
   }
   SAT_LAUNCH_CHECK("sat_gemm");
+  if (p.splits > 1) {
+    const int64_t total = (int64_t)d->M * d->N;
+    const int blocks = (int)std::min<int64_t>((total + 255) / 256, 2048);
+    hipLaunchKernelGGL(gemm_splitk_reduce, dim3(blocks), dim3(256), 0, s, p);
+    SAT_LAUNCH_CHECK("sat_gemm(split-k reduce)");
+  }
   return SAT_OK;
 }

@@ -124,36 +124,51 @@ struct LstmBwdP {
 };
 
 // dL/dh_t = dh_carry + sum_g dgates_{t+1}[b, g] * W[hoff + u, g]  (the recurrent product)
+// The optional query-gradient term sum_d dq[b, d] wq[u, d] reads dq as `dq_parts` per-tile
+// partials: the workgroup first sums them for its 8 batch rows into LDS (all 256 threads, loads
+// independent), then every (b, u) group dots the LDS row with wq's row.
+constexpr int kMaxDq = 320;
+
 __global__ void __launch_bounds__(256) lstm_bwd_kernel(LstmBwdP p) {
+  __shared__ float dqs[BT][kMaxDq];
   const int tid = threadIdx.x;
   const int ks = tid & (KS - 1), pair = tid >> 3;
   const int u = blockIdx.x * UT + (pair & (UT - 1));
-  const int b = blockIdx.y * BT + (pair >> 2);
+  const int bl = pair >> 2;
+  const int b = blockIdx.y * BT + bl;
   const bool active = (u < p.U) && (b < p.B);
+  const int D0 = p.dq0 ? p.dq0_n : 0, D1 = p.dq1 ? p.dq1_n : 0;
+  if (D0 + D1 > 0) {
+    for (int i = tid; i < BT * (D0 + D1); i += 256) {
+      const int r = i / (D0 + D1), d = i - r * (D0 + D1);
+      const int bb = blockIdx.y * BT + r;
+      float g = 0.f;
+      if (bb < p.B) {
+        const float* src = d < D0 ? p.dq0 + d : p.dq1 + (d - D0);
+        for (int part = 0; part < p.dq_parts; ++part)
+          g += src[(int64_t)bb * p.dq_bstride + part * p.dq_pstride];
+      }
+      dqs[r][d] = g;
+    }
+    __syncthreads();
+  }
   float rec = 0.f, extra = 0.f;
   if (active && p.dgates_next) {
     const float4* dg = reinterpret_cast<const float4*>(p.dgates_next + (int64_t)b * p.U * 4);
     const float4* wr = reinterpret_cast<const float4*>(p.W + (int64_t)(p.hoff + u) * p.U * 4);
+#pragma unroll 8
     for (int v = ks; v < p.U; v += KS) {
       const float4 g = dg[v], w = wr[v];
       rec += g.x * w.x + g.y * w.y + g.z * w.z + g.w * w.w;
     }
   }
-  if (active && p.dq0) {
-    for (int d = ks; d < p.dq0_n; d += KS) {
-      float g = 0.f;
-      for (int part = 0; part < p.dq_parts; ++part)
-        g += p.dq0[(int64_t)b * p.dq_bstride + part * p.dq_pstride + d];
-      extra += g * p.wq0[(int64_t)u * p.dq0_n + d];
-    }
+  if (active && D0 > 0) {
+    const float* w0 = p.wq0 + (int64_t)u * D0;
+    for (int d = ks; d < D0; d += KS) extra = fmaf(dqs[bl][d], w0[d], extra);
   }
-  if (active && p.dq1) {
-    for (int d = ks; d < p.dq1_n; d += KS) {
-      float g = 0.f;
-      for (int part = 0; part < p.dq_parts; ++part)
-        g += p.dq1[(int64_t)b * p.dq_bstride + part * p.dq_pstride + d];
-      extra += g * p.wq1[(int64_t)u * p.dq1_n + d];
-    }
+  if (active && D1 > 0) {
+    const float* w1 = p.wq1 + (int64_t)u * D1;
+    for (int d = ks; d < D1; d += KS) extra = fmaf(dqs[bl][D0 + d], w1[d], extra);
   }
 #pragma unroll
   for (int o = 1; o < KS; o <<= 1) {
@@ -221,6 +236,8 @@ extern "C" int sat_lstm_step_bwd(const SatLstmBwd* a, void* stream) {
   SAT_CHECK_ARG(a->W && a->gates && a->dgates && a->dh_carry_out && a->dc_carry_out,
                 "sat_lstm_step_bwd: null pointer");
   SAT_CHECK_ARG(a->hoff >= 0 && a->hoff + a->U <= a->K, "sat_lstm_step_bwd: hoff out of range");
+  SAT_CHECK_ARG((a->dq0 ? a->dq0_n : 0) + (a->dq1 ? a->dq1_n : 0) <= kMaxDq,
+                "sat_lstm_step_bwd: query width > 320");
   LstmBwdP p;
   p.B = a->B; p.U = a->U; p.K = a->K; p.hoff = a->hoff;
   p.W = a->W; p.dgates_next = a->dgates_next; p.gates = a->gates; p.c_prev = a->c_prev;

@@ -23,6 +23,25 @@ def _p(t) -> int:
     return 0 if t is None else t.data_ptr()
 
 
+_GEMM_WS = {}
+GEMM_WS_BYTES = 32 << 20
+
+
+def _gemm_ws(device):
+    """Per-device split-K scratch (allocated once, before any graph capture)."""
+    key = (device.type, device.index)
+    buf = _GEMM_WS.get(key)
+    if buf is None:
+        buf = torch.empty(GEMM_WS_BYTES, dtype=torch.uint8, device=device)
+        _GEMM_WS[key] = buf
+    return buf
+
+
+def _with_ws(d, device):
+    buf = _gemm_ws(device)
+    d.ws, d.ws_bytes = buf.data_ptr(), buf.numel()
+
+
 def _f32(t, name):
     if t is not None and (t.dtype != torch.float32 or not t.is_cuda):
         raise TypeError(f"{name}: expected a float32 device tensor, got {t.dtype} on {t.device}")
@@ -85,7 +104,17 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor = None, *, alpha=1.0,
         d.add = _p(add)
         d.add_sm = add.stride(-2) if add.dim() >= 2 else 0
         d.add_sbatch = add.stride(0) if add.dim() == 3 else 0
+    _with_ws(d, C.device)
     _lib.check(_lib.load().sat_gemm(ctypes.byref(d), _stream()), "sat_gemm")
+    return C
+
+
+def rowdot(A: torch.Tensor, Bt: torch.Tensor, C: torch.Tensor, alpha=1.0, beta=0.0):
+    """C = alpha * A @ Bt^T + beta * C  (A [M, K], Bt [N, K] row-contiguous)."""
+    M, Kd = A.shape
+    N = Bt.shape[0]
+    _lib.call("sat_gemm_rowdot", M, N, Kd, _p(A), A.stride(0), _p(Bt), Bt.stride(0), _p(C),
+              C.stride(0), alpha, beta, _stream())
     return C
 
 
@@ -150,6 +179,7 @@ def conv1d_dw(x: torch.Tensor, dy: torch.Tensor, dW: torch.Tensor, beta=0.0):
     d.b_mode, d.B, d.b_sk, d.b_sn = 0, _p(dy), dy.stride(1), 1
     d.C, d.c_sm = _p(dW), Cout
     d.alpha, d.beta = 1.0, beta
+    _with_ws(d, dW.device)
     _lib.check(_lib.load().sat_gemm(ctypes.byref(d), _stream()), "sat_gemm(conv1d_dw)")
     return dW
 

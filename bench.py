@@ -49,7 +49,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-baseline-batch", type=int, default=2)
     ap.add_argument("--cpu-baseline-steps", type=int, default=4)
-    ap.add_argument("--attn-tile", type=int, default=16)
+    ap.add_argument("--attn-tile", type=int, default=32)
     return ap.parse_args()
 
 

@@ -196,7 +196,7 @@ int sat_attn_step_fwd(const SatAttnStep* args, void* stream);
  * a_t = a_out, a_prev, s_prev, s2_t, stats, q).  Outputs: dalpha_prev, df_out (for step t-1),
  * dqp [B][ntiles][D1+D2] per-tile query-gradient partials (overwritten), and ACCUMULATED
  * dK1 [B][N][D1], dK2 [B][N][D2], pg [B*ntiles][pg_stride] = per-tile partial parameter grads
- * [dv1 D1 | dW_loc F*D1 | dconvW KW*F | dconvb F | dv2 D2].  DA, DS2 are [B][N] scratch.
+ * [dv1 D1 | dW_loc F*D1 | dconvW KW*F | dconvb F | dv2 D2].  DA, DS2, DSN are [B][N] scratch.
  * The value gradients dV = alignments^T dctx are left to one batched GEMM after the loop. */
 typedef struct SatAttnStepBwd {
   int32_t B, N, D1, M1, D2, M2, F, KW, NT, ntiles, att1_forward;
@@ -204,7 +204,7 @@ typedef struct SatAttnStepBwd {
   const float* dctx; int64_t dctx_sb;
   const float* dalpha_next;
   const float* V1; const float* V2;
-  float* DA; float* DS2;
+  float* DA; float* DS2; float* DSN;
   const float* s_t; const float* a_t; const float* a_prev; const float* s_prev; const float* s2_t;
   const float* stats;
   const float* df_next;
@@ -272,6 +272,9 @@ int sat_highway_bwd(const float* h, const float* t, const float* x, const float*
 /* dx = beta*dx + dy * act'(y) [* mask]; act 0 identity, 1 relu, 2 tanh, 3 sigmoid. */
 int sat_act_bwd(const float* dy, const float* y, const float* mask, float* dx, int64_t n,
                 int32_t act, float beta, void* stream);
+/* out[c][r] = in[r][c]  (weight re-layouts, e.g. query-layer kernels for the per-step rowdot) */
+int sat_transpose(const float* in, int64_t ldi, float* out, int64_t ldo, int32_t R, int32_t C,
+                  void* stream);
 /* y = a*x + b*y */
 int sat_axpby(const float* x, float* y, int64_t n, float a, float b, void* stream);
 

@@ -71,7 +71,7 @@ SatAdamConfig = _struct("SatAdamConfig", """
 
 SatAttnStepBwd = _struct("SatAttnStepBwd", """
     i32:B i32:N i32:D1 i32:M1 i32:D2 i32:M2 i32:F i32:KW i32:NT i32:ntiles i32:att1_forward
-    f32:u ptr:dctx i64:dctx_sb ptr:dalpha_next ptr:V1 ptr:V2 ptr:DA ptr:DS2 ptr:s_t ptr:a_t
+    f32:u ptr:dctx i64:dctx_sb ptr:dalpha_next ptr:V1 ptr:V2 ptr:DA ptr:DS2 ptr:DSN ptr:s_t ptr:a_t
     ptr:a_prev ptr:s_prev ptr:s2_t ptr:stats ptr:df_next ptr:lengths ptr:q i64:q_sb ptr:K1 ptr:K2
     ptr:v1 ptr:b1 ptr:convW ptr:convb ptr:locW ptr:v2 ptr:dalpha_prev ptr:df_out ptr:dK1 ptr:dK2
     ptr:dqp ptr:pg i64:pg_stride""")
@@ -116,6 +116,7 @@ SIGNATURES = {
 }
 
 SIGNATURES.update({
+    "sat_transpose": [_P, _I64, _P, _I64, _I32, _I32, _P],
     "sat_gemm_rowdot": [_I32, _I32, _I32, _P, _I64, _P, _I64, _P, _I64, _F, _F, _P],
     "sat_global_norm_sq": [_P, _I64, _P, _P],
     "sat_adam_step": [_P, _P, _P, _P, _I64, _P, _P, _P, ctypes.POINTER(SatAdamConfig), _P],

@@ -116,7 +116,7 @@ def _lstm_loop_bwd(*, B, U, Kr, hoff, Tp, Wr, G_, CS, dY, mc, mh, zc, zh, order,
     return DG
 
 
-def decoder_bwd(P, G, hp, d, dsv, dH2, masks, ws, attn_tile=16):
+def decoder_bwd(P, G, hp, d, dsv, dH2, masks, ws, attn_tile=32):
     """Backward of decoder.decoder_forward.  Returns (dm1, dm2) batch-major."""
     S = dsv.tensors
     B, N, Tp = dsv.B, dsv.N, dsv.Tp
@@ -167,6 +167,7 @@ def decoder_bwd(P, G, hp, d, dsv, dH2, masks, ws, attn_tile=16):
     DG0 = torch.empty(Tp, B, 4 * A, **f32)
     DA = torch.empty(B, N, **f32)
     DS2 = torch.empty(B, N, **f32)
+    DSN = torch.empty(B, N, **f32)
     DAP = [torch.zeros(B, N, **f32), torch.zeros(B, N, **f32)]
     DF = [torch.zeros(B, N, max(d.loc_f, 1), **f32), torch.zeros(B, N, max(d.loc_f, 1), **f32)]
     DQP = torch.empty(Tp, B, ntiles, D1 + D2, **f32)
@@ -185,7 +186,7 @@ def decoder_bwd(P, G, hp, d, dsv, dH2, masks, ws, attn_tile=16):
             B=B, N=N, D1=D1, M1=M1, D2=D2, M2=M2, F=d.loc_f, KW=d.loc_k, NT=attn_tile,
             ntiles=ntiles, att1_forward=1 if fwd else 0, u=0.5, dctx=DCTX[t],
             dctx_sb=M1 + M2, dalpha_next=None if last else DAP[cur], V1=S["V1"], V2=S["V2"],
-            DA=DA, DS2=DS2, s_t=S["S1"][t + 1], a_t=S["AL1"][t + 1], a_prev=S["AL1"][t],
+            DA=DA, DS2=DS2, DSN=DSN, s_t=S["S1"][t + 1], a_t=S["AL1"][t + 1], a_prev=S["AL1"][t],
             s_prev=S["S1"][t], s2_t=S["S2"][t], stats=S["ST"][t],
             df_next=None if last else DF[cur], lengths=None, q=S["Q"][t], q_sb=D1 + D2,
             K1=S["K1"], K2=S["K2"],
@@ -370,7 +371,7 @@ def encoder_bwd(P, G, hp, d, sv, dm1, dm2, lengths, masks, ws):
     K.embedding_bwd(dx, sv["batch"]["source"], G["embedding"])
 
 
-def model_backward(P, G, hp, d, sv, ws, attn_tile=16):
+def model_backward(P, G, hp, d, sv, ws, attn_tile=32):
     """Accumulate dL/dparams of model_forward's loss into G (caller zeroes G)."""
     masks = sv["masks"]
     dH2 = head_bwd(P, G, hp, d, sv, ws)

@@ -18,7 +18,7 @@
 namespace sat {
 namespace {
 
-constexpr int kMaxD = 256, kMaxF = 16, kMaxKW = 32, kMaxNT = 64;
+constexpr int kMaxD = 256, kMaxF = 16, kMaxKW = 32;
 
 struct AttnFwdP {
   int B, N, D1, M1, D2, M2, F, KW, NT, ntiles, att1_forward;
@@ -39,119 +39,201 @@ struct AttnFwdP {
 // partial record: [0]=m1 [1]=Z1 [2]=A1 [3]=m2 [4]=Z2 [5..7]=pad [8..8+M1) C1 [8+M1..) C2
 constexpr int kPartHdr = 8;
 
+// Tile kernel (NT = 32 memory positions per workgroup, 256 threads = 32 positions x 8 lanes).
+// Each lane owns 4*DW4 consecutive energy dims of one position: its K1 slice arrives as DW4
+// 16-byte loads issued at entry (indices clamped so no load sits behind a branch), the energy
+// is reduced over the 8 lanes with DPP, and the value rows are read as float4 columns (64 lanes
+// x 16 B = one 1 KiB row per wave-instruction) for the unnormalised partial contexts.
+// Shapes are compile-time: <F=5, DW4=7, D2W4=1> is LJSpeech/VCTK (D1=224, D2=32); <8, 8, 2> is
+// the zero-padded generic form (padding lanes carry zero weights, so no guard in the loop).
+// Block -> (b, tile): b = blockIdx % B keeps all tiles of an utterance on one XCD.
+constexpr int kNT = 32;
+
+template <int F, int DW4, int D2W4, bool FWD>
 __global__ void __launch_bounds__(256) attn_energy_kernel(AttnFwdP p) {
-  __shared__ float qb[kMaxD], vv[kMaxD], q2s[kMaxD], v2s[kMaxD];
-  __shared__ float locw[kMaxF * kMaxD];
-  __shared__ float fs[kMaxNT][kMaxF];
-  __shared__ float sp[kMaxNT + kMaxKW];
-  __shared__ float e1s[kMaxNT], e2s[kMaxNT], w1s[kMaxNT], w2s[kMaxNT];
+  constexpr int NT = kNT;
+  constexpr int LD = DW4 * 32;                    // padded energy width
+  constexpr int LD2 = D2W4 * 32;
+  __shared__ __attribute__((aligned(16))) float qb[LD];
+  __shared__ __attribute__((aligned(16))) float vv[LD];
+  __shared__ __attribute__((aligned(16))) float locw[(F > 0 ? F : 1) * LD];
+  __shared__ __attribute__((aligned(16))) float q2s[LD2];
+  __shared__ __attribute__((aligned(16))) float v2s[LD2];
+  __shared__ float cw[kMaxKW * kMaxF + kMaxF];
+  __shared__ float fs[NT][F > 0 ? F : 1];
+  __shared__ float sp[NT + kMaxKW], ap[NT + 1];
+  __shared__ float e1s[NT], e2s[NT], w1s[NT], w2s[NT];
+  __shared__ __attribute__((aligned(16))) float4 cred[4][64];
+  __shared__ __attribute__((aligned(16))) float4 c2red[NT][16];
   __shared__ float red[8];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int b = blockIdx.y, tile = blockIdx.x;
-  const int n0 = tile * p.NT;
-  const int nt = min(p.NT, p.N - n0);
-  const int len = (int)p.lengths[b];
-  const float* q = p.q + (int64_t)b * p.q_sb;
-
-  for (int d = tid; d < p.D1; d += 256) {
-    qb[d] = q[d] + (p.b1 ? p.b1[d] : 0.f);
-    vv[d] = p.v1[d];
-  }
-  for (int d = tid; d < p.D2; d += 256) {
-    q2s[d] = q[p.D1 + d];
-    v2s[d] = p.v2[d];
-  }
+  const int b = blockIdx.x % p.B, tile = blockIdx.x / p.B;
+  const int n0 = tile * NT;
+  const int nt = min(NT, p.N - n0);
+  const int64_t rb = (int64_t)b * p.N;
   const int padl = (p.KW - 1) / 2;
-  if (p.att1_forward) {
-    for (int i = tid; i < p.F * p.D1; i += 256) locw[i] = p.locW[i];
-    // s_{t-1} over [n0 - padl, n0 + nt + (KW-1-padl)) (zero outside [0, N))
+  const int D1 = p.D1;
+  const int nl = tid >> 3, part = tid & 7;
+  const int nc = min(n0 + nl, p.N - 1);       // clamped position for this lane's loads
+
+  // ---- burst: K1 / K2 slices of this lane's position (registers)
+  float4 k1r[DW4];
+  {
+    const int d1q = D1 / 4;
+    const float4* k1p = reinterpret_cast<const float4*>(p.K1 + (rb + nc) * D1);
+#pragma unroll
+    for (int j = 0; j < DW4; ++j) k1r[j] = k1p[min(part * DW4 + j, d1q - 1)];
+  }
+  float4 k2r[D2W4];
+  {
+    const int d2q = p.D2 / 4;
+    const float4* k2p = reinterpret_cast<const float4*>(p.K2 + (rb + nc) * p.D2);
+#pragma unroll
+    for (int j = 0; j < D2W4; ++j) k2r[j] = k2p[min(part * D2W4 + j, d2q - 1)];
+  }
+  const int c4 = tid & 63, g = tid >> 6;
+  const int M1q = p.M1 / 4, M2q = p.M2 / 4;
+  float4 v1r[NT / 4];
+#pragma unroll
+  for (int i = 0; i < NT / 4; ++i) {
+    const int n = min(n0 + g * (NT / 4) + i, p.N - 1);
+    v1r[i] = reinterpret_cast<const float4*>(p.V1 + (rb + n) * p.M1)[min(c4, M1q - 1)];
+  }
+  const float4 v2r = reinterpret_cast<const float4*>(p.V2 + (rb + nc) * p.M2)[min(part, M2q - 1)];
+  // ---- burst: small per-step vectors and weights (LDS, zero padded)
+  const float* q = p.q + (int64_t)b * p.q_sb;
+  for (int d = tid; d < LD; d += 256) {
+    const bool ok = d < D1;
+    qb[d] = ok ? q[d] + (p.b1 ? p.b1[d] : 0.f) : 0.f;
+    vv[d] = ok ? p.v1[d] : 0.f;
+  }
+  for (int d = tid; d < LD2; d += 256) {
+    const bool ok = d < p.D2;
+    q2s[d] = ok ? q[D1 + d] : 0.f;
+    v2s[d] = ok ? p.v2[d] : 0.f;
+  }
+  if (FWD) {
+    for (int i = tid; i < F * LD; i += 256) {
+      const int f = i / LD, d = i - f * LD;
+      locw[i] = (f < p.F && d < D1) ? p.locW[f * D1 + d] : 0.f;
+    }
+    for (int i = tid; i < p.KW * p.F; i += 256) cw[i] = p.convW[i];
+    if (tid < p.F) cw[p.KW * p.F + tid] = p.convb[tid];
     const int span = nt + p.KW - 1;
     for (int i = tid; i < span; i += 256) {
       const int n = n0 - padl + i;
-      sp[i] = (n >= 0 && n < p.N) ? p.s_prev[(int64_t)b * p.N + n] : 0.f;
+      sp[i] = (n >= 0 && n < p.N) ? p.s_prev[rb + n] : 0.f;
     }
+    if (tid <= nt) ap[tid] = (n0 - 1 + tid >= 0) ? p.a_prev[rb + n0 - 1 + tid] : 0.f;
   }
+  const int len = (int)p.lengths[b];
   __syncthreads();
-  if (p.att1_forward) {
-    for (int i = tid; i < nt * p.F; i += 256) {
-      const int nl = i / p.F, f = i - nl * p.F;
-      float acc = p.convb[f];
-      for (int j = 0; j < p.KW; ++j) acc = fmaf(sp[nl + j], p.convW[j * p.F + f], acc);
-      fs[nl][f] = acc;
+  if (FWD) {  // location features f = Conv1D_SAME(s_{t-1}) + bias (padded filters = 0)
+    if (tid < NT * F) {
+      const int i = tid / F, f = tid - i * F;
+      float acc = 0.f;
+      if (f < p.F) {
+        acc = cw[p.KW * p.F + f];
+        for (int j = 0; j < p.KW; ++j) acc = fmaf(sp[i + j], cw[j * p.F + f], acc);
+      }
+      fs[i][f] = acc;
     }
     __syncthreads();
   }
-
-  // energies: one wave per position, lanes over d
-  for (int nl = wave; nl < nt; nl += 4) {
-    const int n = n0 + nl;
-    const float* k1 = p.K1 + ((int64_t)b * p.N + n) * p.D1;
-    float acc = 0.f;
-    for (int d = lane; d < p.D1; d += 64) {
-      float pre = k1[d] + qb[d];
-      if (p.att1_forward) {
-        for (int f = 0; f < p.F; ++f) pre = fmaf(fs[nl][f], locw[f * p.D1 + d], pre);
+  // ---- energies: 4*DW4 dims per lane, 8-lane DPP reduction
+  float fl[F > 0 ? F : 1];
+#pragma unroll
+  for (int f = 0; f < F; ++f) fl[f] = fs[nl][f];
+  float acc = 0.f;
+  const int d0 = part * DW4 * 4;
+#pragma unroll
+  for (int j = 0; j < DW4; ++j) {
+    const int d = d0 + 4 * j;
+    const float4 qv = *reinterpret_cast<const float4*>(&qb[d]);
+    const float4 vw = *reinterpret_cast<const float4*>(&vv[d]);
+    float4 pre = make_float4(k1r[j].x + qv.x, k1r[j].y + qv.y, k1r[j].z + qv.z, k1r[j].w + qv.w);
+    if (FWD) {
+#pragma unroll
+      for (int f = 0; f < F; ++f) {
+        const float4 lw = *reinterpret_cast<const float4*>(&locw[f * LD + d]);
+        pre.x = fmaf(fl[f], lw.x, pre.x); pre.y = fmaf(fl[f], lw.y, pre.y);
+        pre.z = fmaf(fl[f], lw.z, pre.z); pre.w = fmaf(fl[f], lw.w, pre.w);
       }
-      acc = fmaf(vv[d], tanhf(pre), acc);
     }
-    const float* k2 = p.K2 + ((int64_t)b * p.N + n) * p.D2;
-    float acc2 = 0.f;
-    for (int d = lane; d < p.D2; d += 64) acc2 = fmaf(v2s[d], tanhf(k2[d] + q2s[d]), acc2);
-    acc = wave_sum(acc);
-    acc2 = wave_sum(acc2);
-    if (lane == 0) {
-      const bool valid = n < len;
-      e1s[nl] = valid ? acc : -INFINITY;
-      e2s[nl] = valid ? acc2 : -INFINITY;
-    }
+    acc = fmaf(vw.x, tanh_fast(pre.x), acc);
+    acc = fmaf(vw.y, tanh_fast(pre.y), acc);
+    acc = fmaf(vw.z, tanh_fast(pre.z), acc);
+    acc = fmaf(vw.w, tanh_fast(pre.w), acc);
+  }
+  float acc2 = 0.f;
+#pragma unroll
+  for (int j = 0; j < D2W4; ++j) {
+    const int d = (part * D2W4 + j) * 4;
+    const float4 qv = *reinterpret_cast<const float4*>(&q2s[d]);
+    const float4 vw = *reinterpret_cast<const float4*>(&v2s[d]);
+    acc2 = fmaf(vw.x, tanh_fast(k2r[j].x + qv.x), acc2);
+    acc2 = fmaf(vw.y, tanh_fast(k2r[j].y + qv.y), acc2);
+    acc2 = fmaf(vw.z, tanh_fast(k2r[j].z + qv.z), acc2);
+    acc2 = fmaf(vw.w, tanh_fast(k2r[j].w + qv.w), acc2);
+  }
+  acc = group8_sum(acc);
+  acc2 = group8_sum(acc2);
+  if (part == 0 && nl < nt) {
+    const bool valid = n0 + nl < len;
+    e1s[nl] = valid ? acc : -INFINITY;
+    e2s[nl] = valid ? acc2 : -INFINITY;
   }
   __syncthreads();
-
-  // tile statistics (wave 0)
+  // ---- tile statistics (wave 0)
   if (wave == 0) {
-    float m1 = -INFINITY, m2 = -INFINITY;
-    for (int i = lane; i < nt; i += 64) { m1 = fmaxf(m1, e1s[i]); m2 = fmaxf(m2, e2s[i]); }
-    m1 = wave_max(m1);
-    m2 = wave_max(m2);
-    float z1 = 0.f, a1 = 0.f, z2 = 0.f;
-    for (int i = lane; i < nt; i += 64) {
-      const int n = n0 + i;
-      const float pe = (e1s[i] == -INFINITY) ? 0.f : expf(e1s[i] - m1);
-      float w = pe;
-      if (p.att1_forward) {
-        const float ap = p.a_prev[(int64_t)b * p.N + n];
-        const float am = n > 0 ? p.a_prev[(int64_t)b * p.N + n - 1] : 0.f;
-        w = ((1.f - p.u) * ap + p.u * am + 1e-7f) * pe;
-      }
-      const float pe2 = (e2s[i] == -INFINITY) ? 0.f : expf(e2s[i] - m2);
-      w1s[i] = w;
-      w2s[i] = pe2;
-      z1 += pe; a1 += w; z2 += pe2;
-    }
-    z1 = wave_sum(z1); a1 = wave_sum(a1); z2 = wave_sum(z2);
+    const float e1v = lane < nt ? e1s[lane] : -INFINITY;
+    const float e2v = lane < nt ? e2s[lane] : -INFINITY;
+    const float m1 = wave_max(e1v), m2 = wave_max(e2v);
+    const float pe = (e1v == -INFINITY) ? 0.f : expf(e1v - m1);
+    const float pe2 = (e2v == -INFINITY) ? 0.f : expf(e2v - m2);
+    float w = pe;
+    if (FWD && lane < nt) w = ((1.f - p.u) * ap[lane + 1] + p.u * ap[lane] + 1e-7f) * pe;
+    if (lane < NT) { w1s[lane] = lane < nt ? w : 0.f; w2s[lane] = lane < nt ? pe2 : 0.f; }
+    const float z1 = wave_sum_dpp(pe), a1 = wave_sum_dpp(lane < nt ? w : 0.f),
+                z2 = wave_sum_dpp(pe2);
     if (lane == 0) { red[0] = m1; red[1] = z1; red[2] = a1; red[3] = m2; red[4] = z2; }
   }
   __syncthreads();
-
-  float* part = p.part + ((int64_t)b * p.ntiles + tile) * p.part_stride;
-  if (tid < kPartHdr) part[tid] = tid < 5 ? red[tid] : 0.f;
-  for (int i = tid; i < nt; i += 256) {
-    p.e1[(int64_t)b * p.N + n0 + i] = e1s[i];
-    p.e2[(int64_t)b * p.N + n0 + i] = e2s[i];
+  float* part_out = p.part + ((int64_t)b * p.ntiles + tile) * p.part_stride;
+  if (tid < kPartHdr) part_out[tid] = tid < 5 ? red[tid] : 0.f;
+  if (tid < nt) {
+    p.e1[rb + n0 + tid] = e1s[tid];
+    p.e2[rb + n0 + tid] = e2s[tid];
   }
-  // unnormalised partial contexts; threads over the value width (coalesced rows)
-  for (int d = tid; d < p.M1 + p.M2; d += 256) {
-    float acc = 0.f;
-    if (d < p.M1) {
-      const float* v1 = p.V1 + ((int64_t)b * p.N + n0) * p.M1 + d;
-      for (int i = 0; i < nt; ++i) acc = fmaf(w1s[i], v1[(int64_t)i * p.M1], acc);
-    } else {
-      const int d2 = d - p.M1;
-      const float* v2 = p.V2 + ((int64_t)b * p.N + n0) * p.M2 + d2;
-      for (int i = 0; i < nt; ++i) acc = fmaf(w2s[i], v2[(int64_t)i * p.M2], acc);
+  // ---- unnormalised partial contexts
+  float4 c = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int i = 0; i < NT / 4; ++i) {
+    const float w = w1s[g * (NT / 4) + i];
+    c.x = fmaf(w, v1r[i].x, c.x); c.y = fmaf(w, v1r[i].y, c.y);
+    c.z = fmaf(w, v1r[i].z, c.z); c.w = fmaf(w, v1r[i].w, c.w);
+  }
+  cred[g][c4] = c;
+  {
+    const float w = w2s[nl];
+    c2red[nl][part] = make_float4(w * v2r.x, w * v2r.y, w * v2r.z, w * v2r.w);
+  }
+  __syncthreads();
+  if (tid < M1q) {
+    const float4 a0 = cred[0][tid], a1 = cred[1][tid], a2 = cred[2][tid], a3 = cred[3][tid];
+    reinterpret_cast<float4*>(part_out + kPartHdr)[tid] =
+        make_float4((a0.x + a1.x) + (a2.x + a3.x), (a0.y + a1.y) + (a2.y + a3.y),
+                    (a0.z + a1.z) + (a2.z + a3.z), (a0.w + a1.w) + (a2.w + a3.w));
+  } else if (tid >= 64 && tid < 64 + M2q) {
+    const int j = tid - 64;
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 8
+    for (int i = 0; i < NT; ++i) {
+      const float4 v = c2red[i][j];
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
     }
-    part[kPartHdr + d] = acc;
+    reinterpret_cast<float4*>(part_out + kPartHdr + p.M1)[j] = s;
   }
 }
 
@@ -162,34 +244,54 @@ struct AttnCombineP {
   const float* a_prev;
   float* s_out; float* a_out; float* s2_out;   // [B][N]
   float* ctx; int64_t ctx_sb;                  // [B][M1 + M2] (row stride ctx_sb)
-  float* stats;                                // [B][4]: M1, Z1, A1/Z1 (= sum g s), Z2 ... for bwd
+  float* stats;                                // [B][4]: M1, Z1, A1/Z1 (= sum g s), Z2 for the bwd
 };
 
+// Per-utterance combine: all loads issued at entry, tile headers reduced by one wave.
 __global__ void __launch_bounds__(256) attn_combine_kernel(AttnCombineP p) {
-  __shared__ float sc1[256], sc2[256];
+  __shared__ float sc1[64], sc2[64];
   __shared__ float hdr[6];
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int b = blockIdx.x;
+  const int64_t rb = (int64_t)b * p.N;
   const float* part = p.part + (int64_t)b * p.ntiles * p.part_stride;
-  if (tid == 0) {
-    float M1 = -INFINITY, M2 = -INFINITY;
-    for (int j = 0; j < p.ntiles; ++j) {
-      M1 = fmaxf(M1, part[j * p.part_stride + 0]);
-      M2 = fmaxf(M2, part[j * p.part_stride + 3]);
+  const int W = p.M1 + p.M2;
+  constexpr int kMaxPos = 4;
+  float ev[kMaxPos], e2v[kMaxPos], apv[kMaxPos], amv[kMaxPos];
+#pragma unroll
+  for (int i = 0; i < kMaxPos; ++i) {
+    const int n = tid + 256 * i;
+    const bool ok = n < p.N;
+    ev[i] = ok ? p.e1[rb + n] : -INFINITY;
+    e2v[i] = ok ? p.e2[rb + n] : -INFINITY;
+    apv[i] = (ok && p.att1_forward) ? p.a_prev[rb + n] : 0.f;
+    amv[i] = (ok && p.att1_forward && n > 0) ? p.a_prev[rb + n - 1] : 0.f;
+  }
+  float cpart[2][16];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int d = tid + 256 * h;
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      cpart[h][j] = (d < W && j < p.ntiles) ? part[j * p.part_stride + kPartHdr + d] : 0.f;
+  }
+  if (wave == 0) {
+    float hm1 = -INFINITY, hz1 = 0.f, ha1 = 0.f, hm2 = -INFINITY, hz2 = 0.f;
+    if (lane < p.ntiles) {
+      const float* r = part + lane * p.part_stride;
+      hm1 = r[0]; hz1 = r[1]; ha1 = r[2]; hm2 = r[3]; hz2 = r[4];
     }
-    float Z1 = 0.f, A1 = 0.f, Z2 = 0.f;
-    for (int j = 0; j < p.ntiles; ++j) {
-      const float* r = part + j * p.part_stride;
-      const float s1 = (r[0] == -INFINITY) ? 0.f : expf(r[0] - M1);
-      const float s2 = (r[3] == -INFINITY) ? 0.f : expf(r[3] - M2);
-      sc1[j] = s1;
-      sc2[j] = s2;
-      Z1 += r[1] * s1; A1 += r[2] * s1; Z2 += r[4] * s2;
-    }
-    hdr[0] = M1; hdr[1] = Z1; hdr[2] = A1; hdr[3] = Z2; hdr[4] = M2;
-    if (p.stats) {  // sum_n g[n] s[n] = A1 / Z1 (the forward-attention normaliser) for the bwd
-      p.stats[b * 4 + 0] = M1; p.stats[b * 4 + 1] = Z1; p.stats[b * 4 + 2] = A1 / Z1;
-      p.stats[b * 4 + 3] = Z2;
+    const float M1 = wave_max(hm1), M2 = wave_max(hm2);
+    const float s1 = (hm1 == -INFINITY) ? 0.f : expf(hm1 - M1);
+    const float s2 = (hm2 == -INFINITY) ? 0.f : expf(hm2 - M2);
+    if (lane < p.ntiles) { sc1[lane] = s1; sc2[lane] = s2; }
+    const float Z1 = wave_sum(hz1 * s1), A1 = wave_sum(ha1 * s1), Z2 = wave_sum(hz2 * s2);
+    if (lane == 0) {
+      hdr[0] = M1; hdr[1] = Z1; hdr[2] = A1; hdr[3] = Z2; hdr[4] = M2;
+      if (p.stats) {  // sum_n g[n] s[n] = A1 / Z1 (the forward-attention normaliser) for the bwd
+        p.stats[b * 4 + 0] = M1; p.stats[b * 4 + 1] = Z1; p.stats[b * 4 + 2] = A1 / Z1;
+        p.stats[b * 4 + 3] = Z2;
+      }
     }
   }
   __syncthreads();
@@ -197,28 +299,28 @@ __global__ void __launch_bounds__(256) attn_combine_kernel(AttnCombineP p) {
   const float inv1 = 1.f / (p.att1_forward ? A1 : Z1);
   const float invz1 = 1.f / Z1, invz2 = 1.f / Z2;
   float* ctx = p.ctx + (int64_t)b * p.ctx_sb;
-  for (int d = tid; d < p.M1 + p.M2; d += 256) {
-    float acc = 0.f;
-    const bool first = d < p.M1;
-    for (int j = 0; j < p.ntiles; ++j)
-      acc = fmaf(part[j * p.part_stride + kPartHdr + d], first ? sc1[j] : sc2[j], acc);
-    ctx[d] = acc * (first ? inv1 : invz2);
-  }
-  for (int n = tid; n < p.N; n += 256) {
-    const int64_t i = (int64_t)b * p.N + n;
-    const float e = p.e1[i], e2 = p.e2[i];
-    const float pe = (e == -INFINITY) ? 0.f : expf(e - M1);
-    const float pe2 = (e2 == -INFINITY) ? 0.f : expf(e2 - M2);
-    const float s = pe * invz1;
-    p.s_out[i] = s;
-    p.s2_out[i] = pe2 * invz2;
-    if (p.att1_forward) {
-      const float ap = p.a_prev[i];
-      const float am = n > 0 ? p.a_prev[i - 1] : 0.f;
-      p.a_out[i] = ((1.f - p.u) * ap + p.u * am + 1e-7f) * pe * inv1;
-    } else {
-      p.a_out[i] = s;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int d = tid + 256 * h;
+    if (d < W) {
+      const bool first = d < p.M1;
+      float acc = 0.f;
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+        if (j < p.ntiles) acc = fmaf(cpart[h][j], first ? sc1[j] : sc2[j], acc);
+      ctx[d] = acc * (first ? inv1 : invz2);
     }
+  }
+#pragma unroll
+  for (int i = 0; i < kMaxPos; ++i) {
+    const int n = tid + 256 * i;
+    if (n >= p.N) break;
+    const float pe = (ev[i] == -INFINITY) ? 0.f : expf(ev[i] - M1);
+    const float pe2 = (e2v[i] == -INFINITY) ? 0.f : expf(e2v[i] - M2);
+    const float s = pe * invz1;
+    p.s_out[rb + n] = s;
+    p.s2_out[rb + n] = pe2 * invz2;
+    p.a_out[rb + n] = p.att1_forward ? ((1.f - p.u) * apv[i] + p.u * amv[i] + 1e-7f) * pe * inv1 : s;
   }
 }
 
@@ -276,11 +378,17 @@ extern "C" int sat_attn_query(int32_t B, int32_t K, int32_t N1, int32_t N2, cons
 extern "C" int sat_attn_step_fwd(const SatAttnStep* a, void* stream) {
   SAT_CHECK_ARG(a && a->B > 0 && a->N > 0, "sat_attn_step_fwd: bad sizes");
   SAT_CHECK_ARG(a->D1 <= kMaxD && a->D2 <= kMaxD && a->M2 >= 0, "sat_attn_step_fwd: D > 256");
-  SAT_CHECK_ARG(a->NT > 0 && a->NT <= kMaxNT, "sat_attn_step_fwd: tile size must be in [1, 64]");
+  SAT_CHECK_ARG(a->NT == kNT, "sat_attn_step_fwd: tile size must be 32");
+  SAT_CHECK_ARG(a->N <= 1024 && a->M1 <= 256 && a->M1 % 4 == 0 && a->M2 <= 32 && a->M2 % 4 == 0,
+                "sat_attn_step_fwd: N <= 1024, M1 <= 256, M2 <= 32 (multiples of 4)");
+  SAT_CHECK_ARG(a->D1 % 32 == 0 && a->D1 <= 256 && a->D2 % 32 == 0 && a->D2 <= 64,
+                "sat_attn_step_fwd: D1 % 32 == 0 (<= 256), D2 in {32, 64}");
+  SAT_CHECK_ARG(!a->att1_forward || a->F <= 8, "sat_attn_step_fwd: F <= 8");
   SAT_CHECK_ARG(!a->att1_forward || (a->F <= kMaxF && a->KW <= kMaxKW && a->F * a->D1 <= kMaxF * kMaxD),
                 "sat_attn_step_fwd: location conv too large");
   SAT_CHECK_ARG(a->part_stride >= sat_attn_part_stride(a->M1, a->M2), "sat_attn_step_fwd: part stride");
-  SAT_CHECK_ARG(a->ntiles <= 256 && a->ntiles == ceil_div(a->N, a->NT), "sat_attn_step_fwd: ntiles");
+  SAT_CHECK_ARG(a->ntiles <= 16 && a->ntiles == ceil_div(a->N, a->NT), "sat_attn_step_fwd: ntiles must be <= 16");
+  SAT_CHECK_ARG(a->D2 <= 64, "sat_attn_step_fwd: D2 <= 64");
   SAT_CHECK_ARG(a->q && a->K1 && a->V1 && a->K2 && a->V2 && a->lengths && a->v1 && a->v2 &&
                 a->e1 && a->e2 && a->part && a->s_out && a->a_out && a->s2_out && a->ctx,
                 "sat_attn_step_fwd: null pointer");
@@ -297,7 +405,13 @@ extern "C" int sat_attn_step_fwd(const SatAttnStep* a, void* stream) {
   hipStream_t s = as_stream(stream);
   const int phases = a->phases == 0 ? 3 : a->phases;
   if (phases & 1) {
-    hipLaunchKernelGGL(attn_energy_kernel, dim3(a->ntiles, a->B), dim3(256), 0, s, p);
+    const dim3 grid(a->ntiles * a->B);
+    if (a->att1_forward && a->F == 5 && a->D1 == 224 && a->D2 == 32)
+      hipLaunchKernelGGL((attn_energy_kernel<5, 7, 1, true>), grid, dim3(256), 0, s, p);
+    else if (a->att1_forward)
+      hipLaunchKernelGGL((attn_energy_kernel<8, 8, 2, true>), grid, dim3(256), 0, s, p);
+    else
+      hipLaunchKernelGGL((attn_energy_kernel<0, 8, 2, false>), grid, dim3(256), 0, s, p);
     SAT_LAUNCH_CHECK("sat_attn_step_fwd(energy)");
   }
   if (!(phases & 2)) return SAT_OK;
@@ -333,7 +447,7 @@ struct AttnBwdP {
   const float* dctx; int64_t dctx_sb;
   const float* dalpha_next;
   const float* V1; const float* V2;
-  float* DA; float* DS2;
+  float* DA; float* DS2; float* DSN;
   const float* s_t; const float* a_t; const float* a_prev; const float* s_prev; const float* s2_t;
   const float* stats;
   const float* df_next;
@@ -349,188 +463,299 @@ struct AttnBwdP {
   float* pg; int64_t pg_stride;
 };
 
+// Per-tile first stage of the backward step:
+//   DA[n]  = dctx1 . V1[n] + dalpha_next[n]      (gradient reaching the normalised alignment)
+//   DS2[n] = dctx2 . V2[n]
+//   DSN[n] = sum_{j,f} df_next[n - j + padl][f] convW[j][f]   (transpose of the next step's
+//            location convolution: how s_t feeds f_{t+1}); 0 when there is no next step.
+template <int NT>
 __global__ void __launch_bounds__(256) attn_bwd_ctx_kernel(AttnBwdP p) {
-  __shared__ float dc[2 * kMaxD + kMaxD];
+  constexpr int PPW = NT / 4;
+  __shared__ float dc[2 * kMaxD];
+  __shared__ float dfw[(NT + kMaxKW) * kMaxFb];
+  __shared__ float cws[kMaxKW * kMaxFb];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int b = blockIdx.x % p.B, tile = blockIdx.x / p.B;
-  const int n0 = tile * p.NT, nt = min(p.NT, p.N - n0);
+  const int n0 = tile * NT, nt = min(NT, p.N - n0);
+  const int64_t rb = (int64_t)b * p.N;
+  const int F = p.att1_forward ? p.F : 0;
+  const int padl = (p.KW - 1) / 2;
+  const bool conv = F > 0 && p.df_next != nullptr;
+  float v1r[PPW][4], v2r[PPW], dan[PPW];
+#pragma unroll
+  for (int i = 0; i < PPW; ++i) {
+    const int nl = wave + 4 * i, n = min(n0 + nl, p.N - 1);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int d = lane + 64 * s;
+      v1r[i][s] = d < p.M1 ? p.V1[(rb + n) * p.M1 + d] : 0.f;
+    }
+    v2r[i] = lane < p.M2 ? p.V2[(rb + n) * p.M2 + lane] : 0.f;
+    dan[i] = p.dalpha_next ? p.dalpha_next[rb + n] : 0.f;
+  }
   const float* g = p.dctx + (int64_t)b * p.dctx_sb;
   for (int i = tid; i < p.M1 + p.M2; i += 256) dc[i] = g[i];
+  if (conv) {
+    // window of df_next rows m in [n0 - (KW-1-padl), n0 + nt + padl)
+    const int lo = n0 - (p.KW - 1 - padl), span = nt + p.KW - 1;
+    for (int i = tid; i < span * F; i += 256) {
+      const int r = i / F, m = lo + r;
+      dfw[i] = (m >= 0 && m < p.N) ? p.df_next[(rb + m) * F + (i - r * F)] : 0.f;
+    }
+    for (int i = tid; i < p.KW * F; i += 256) cws[i] = p.convW[i];
+  }
   __syncthreads();
-  for (int nl = wave; nl < nt; nl += 4) {
-    const int n = n0 + nl;
-    const float* v1 = p.V1 + ((int64_t)b * p.N + n) * p.M1;
-    const float* v2 = p.V2 + ((int64_t)b * p.N + n) * p.M2;
-    float a = 0.f, c = 0.f;
-    for (int d = lane; d < p.M1; d += 64) a = fmaf(dc[d], v1[d], a);
-    for (int d = lane; d < p.M2; d += 64) c = fmaf(dc[p.M1 + d], v2[d], c);
+#pragma unroll
+  for (int i = 0; i < PPW; ++i) {
+    const int nl = wave + 4 * i;
+    if (nl >= nt) break;
+    float a = 0.f;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int d = lane + 64 * s;
+      if (d < p.M1) a = fmaf(dc[d], v1r[i][s], a);
+    }
+    float c = lane < p.M2 ? dc[p.M1 + lane] * v2r[i] : 0.f;
     a = wave_sum(a);
     c = wave_sum(c);
     if (lane == 0) {
-      const int64_t i = (int64_t)b * p.N + n;
-      p.DA[i] = a + (p.dalpha_next ? p.dalpha_next[i] : 0.f);
-      p.DS2[i] = c;
+      p.DA[rb + n0 + nl] = a + dan[i];
+      p.DS2[rb + n0 + nl] = c;
     }
+  }
+  // DSN: 8 lanes per position, lanes stride over the KW taps
+  if (tid < NT * 8) {
+    const int nl = tid >> 3, part = tid & 7;
+    float acc = 0.f;
+    if (conv && nl < nt) {
+      // position n uses df_next[m] with m = n - j + padl, i.e. window row nl + (KW-1-padl) + padl - j
+      for (int j = part; j < p.KW; j += 8) {
+        const float* row = dfw + (nl + p.KW - 1 - j) * F;
+        const float* w = cws + j * F;
+        for (int f = 0; f < F; ++f) acc = fmaf(row[f], w[f], acc);
+      }
+    }
+    acc = group8_sum(acc);
+    if (part == 0 && nl < nt) p.DSN[rb + n0 + nl] = acc;
   }
 }
 
+// LDS budget of the energy backward: per-wave accumulator flush (phase 4)
+constexpr int kBwdScratch = 4 * (kMaxD * (2 + kMaxFb) + 128);
+
+__device__ __forceinline__ float2 block_sum2(float a, float b, float* scratch) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  a = wave_sum_dpp(a);
+  b = wave_sum_dpp(b);
+  if (lane == 0) { scratch[w] = a; scratch[4 + w] = b; }
+  __syncthreads();
+  return make_float2((scratch[0] + scratch[1]) + (scratch[2] + scratch[3]),
+                     (scratch[4] + scratch[5]) + (scratch[6] + scratch[7]));
+}
+
+// Second stage: utterance-wide softmax / forward-recursion backward (scalars recomputed per
+// block from 8 N-vectors), then the tile's energies are recomputed and back-propagated through
+// tanh.  One wave per memory position, lanes over the energy dims (4 slots of 64; the LDS copies
+// of q, v, W_loc are zero padded to 256 so padding lanes contribute exact zeros).  F is
+// compile-time (0 = additive attention1), so the inner loop carries no guards.
+template <int NT, int F>
 __global__ void __launch_bounds__(256) attn_bwd_energy_kernel(AttnBwdP p) {
-  __shared__ float dst[kMaxN], dat[kMaxN];
-  __shared__ float qb[kMaxD], vv[kMaxD], q2s[kMaxD], v2s[kMaxD];
-  __shared__ float locw[kMaxFb * kMaxD];
-  __shared__ float fs[kMaxNT][kMaxFb], dfs[kMaxNT][kMaxFb];
-  __shared__ float sp[kMaxNT + kMaxKW];
-  __shared__ float de1[kMaxNT], de2[kMaxNT];
+  constexpr int PPW = NT / 4;
+  constexpr int kPos = kMaxN / 256;      // utterance positions per thread
+  constexpr int kPgr = 8;                // PG entries per thread (pg_stride <= 2048)
+  constexpr int FL = F > 0 ? F : 1;
+  constexpr bool FWD = F > 0;
+  __shared__ float dst[NT + 1], dat[NT + 2], stt[NT + 2];
+  __shared__ float qb[kMaxD], vv[kMaxD], q2s[64], v2s[64];
+  __shared__ float locw[FL * kMaxD];
+  __shared__ float cw[kMaxKW * FL + FL];
+  __shared__ float fs[NT][FL], dfs[NT][FL];
+  __shared__ float sp[NT + kMaxKW];
+  __shared__ float de1[NT], de2[NT];
+  __shared__ float convg[kMaxKW * FL + FL];
   __shared__ float red[16];
-  __shared__ float racc[4][kMaxD * (2 + kMaxFb) + 128];
+  __shared__ float scratch[kBwdScratch];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int b = blockIdx.x % p.B, tile = blockIdx.x / p.B;
-  const int n0 = tile * p.NT, nt = min(p.NT, p.N - n0);
+  const int n0 = tile * NT, nt = min(NT, p.N - n0);
   const int64_t rb = (int64_t)b * p.N;
   const int padl = (p.KW - 1) / 2;
-  const bool fwd = p.att1_forward != 0;
   const float u = p.u;
+  const int D1 = p.D1, D2 = p.D2, N = p.N;
+  const int64_t pgrow = ((int64_t)b * p.ntiles + tile) * p.pg_stride;
 
-  // ---- normaliser sums over the whole utterance
-  float s1 = 0.f, s3 = 0.f;
-  for (int n = tid; n < p.N; n += 256) {
-    if (fwd) s1 += p.DA[rb + n] * p.a_t[rb + n];
-    s3 += p.s2_t[rb + n] * p.DS2[rb + n];
-  }
-  s1 = block_sum(s1, red);
-  s3 = block_sum(s3, red + 4);
-  const float Sa = fwd ? p.stats[b * 4 + 2] : 1.f;
-  float s2sum = 0.f;
-  for (int n = tid; n < p.N; n += 256) {
-    float ds;
-    if (fwd) {
-      const float da = (p.DA[rb + n] - s1) / Sa;
-      const float g = (1.f - u) * p.a_prev[rb + n] + (n > 0 ? u * p.a_prev[rb + n - 1] : 0.f) + 1e-7f;
-      float dsn = 0.f;
-      if (p.df_next) {  // conv-transpose of the next step's location-feature grads
-        for (int j = 0; j < p.KW; ++j) {
-          const int m = n - j + padl;
-          if (m < 0 || m >= p.N) continue;
-          const float* dfr = p.df_next + (rb + m) * p.F;
-          for (int f = 0; f < p.F; ++f) dsn = fmaf(dfr[f], p.convW[j * p.F + f], dsn);
-        }
-      }
-      dat[n] = da;
-      ds = dsn + da * g;
-    } else {
-      ds = p.DA[rb + n];
+  // ---------------- burst: registers (indices clamped: no load behind a branch)
+  float k1r[PPW][4], dk1r[PPW][4], k2r[PPW], dk2r[PPW];
+#pragma unroll
+  for (int i = 0; i < PPW; ++i) {
+    const int n = min(n0 + wave + 4 * i, N - 1);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int d = min(lane + 64 * s, D1 - 1);
+      k1r[i][s] = p.K1[(rb + n) * D1 + d];
+      dk1r[i][s] = p.dK1[(rb + n) * D1 + d];
     }
-    dst[n] = ds;
-    s2sum += p.s_t[rb + n] * ds;
+    const int d2 = min(lane, D2 - 1);
+    k2r[i] = p.K2[(rb + n) * D2 + d2];
+    dk2r[i] = p.dK2[(rb + n) * D2 + d2];
   }
-  s2sum = block_sum(s2sum, red + 8);   // (block_sum syncs: dst/dat visible after)
-
-  // ---- tile: de, de2, dA_prev
-  for (int i = tid; i < nt; i += 256) {
-    const int n = n0 + i;
-    de1[i] = p.s_t[rb + n] * (dst[n] - s2sum);
-    de2[i] = p.s2_t[rb + n] * (p.DS2[rb + n] - s3);
-    if (fwd) {
-      float v = (1.f - u) * dat[n] * p.s_t[rb + n];
-      if (n + 1 < p.N) v += u * dat[n + 1] * p.s_t[rb + n + 1];
-      p.dalpha_prev[rb + n] = v;
+  float rDA[kPos], rDS2[kPos], rat[kPos], rst[kPos], rs2[kPos], rap[kPos], ram[kPos], rsn[kPos];
+#pragma unroll
+  for (int i = 0; i < kPos; ++i) {
+    const int n = tid + 256 * i;
+    const bool ok = n < N;
+    const int64_t o = rb + min(n, N - 1);
+    rDA[i] = ok ? p.DA[o] : 0.f;
+    rDS2[i] = ok ? p.DS2[o] : 0.f;
+    rst[i] = ok ? p.s_t[o] : 0.f;
+    rs2[i] = ok ? p.s2_t[o] : 0.f;
+    if (FWD) {
+      rat[i] = ok ? p.a_t[o] : 0.f;
+      rap[i] = ok ? p.a_prev[o] : 0.f;
+      ram[i] = (ok && n > 0) ? p.a_prev[o - 1] : 0.f;
+      rsn[i] = ok ? p.DSN[o] : 0.f;
     }
   }
+  float pgr[kPgr];
+#pragma unroll
+  for (int i = 0; i < kPgr; ++i) {
+    const int j = min(tid + 256 * i, (int)p.pg_stride - 1);
+    pgr[i] = p.pg[pgrow + j];
+  }
+  // ---------------- burst: LDS (zero padded to 256 / 64)
   const float* q = p.q + (int64_t)b * p.q_sb;
-  for (int d = tid; d < p.D1; d += 256) {
-    qb[d] = q[d] + (p.b1 ? p.b1[d] : 0.f);
-    vv[d] = p.v1[d];
+  {
+    const int d = tid;   // kMaxD == 256 == blockDim
+    const bool ok = d < D1;
+    qb[d] = ok ? q[d] + (p.b1 ? p.b1[d] : 0.f) : 0.f;
+    vv[d] = ok ? p.v1[d] : 0.f;
+    if (d < 64) {
+      q2s[d] = d < D2 ? q[D1 + d] : 0.f;
+      v2s[d] = d < D2 ? p.v2[d] : 0.f;
+    }
+    if (FWD) {
+#pragma unroll
+      for (int f = 0; f < F; ++f) locw[f * kMaxD + d] = ok ? p.locW[f * D1 + d] : 0.f;
+    }
   }
-  for (int d = tid; d < p.D2; d += 256) {
-    q2s[d] = q[p.D1 + d];
-    v2s[d] = p.v2[d];
-  }
-  if (fwd) {
-    for (int i = tid; i < p.F * p.D1; i += 256) locw[i] = p.locW[i];
+  if (FWD) {
+    for (int i = tid; i < p.KW * F; i += 256) cw[i] = p.convW[i];
+    if (tid < F) cw[p.KW * F + tid] = p.convb[tid];
     const int span = nt + p.KW - 1;
     for (int i = tid; i < span; i += 256) {
       const int n = n0 - padl + i;
-      sp[i] = (n >= 0 && n < p.N) ? p.s_prev[rb + n] : 0.f;
+      sp[i] = (n >= 0 && n < N) ? p.s_prev[rb + n] : 0.f;
     }
   }
-  __syncthreads();
-  if (fwd) {
-    for (int i = tid; i < nt * p.F; i += 256) {
-      const int nl = i / p.F, f = i - nl * p.F;
-      float acc = p.convb[f];
-      for (int j = 0; j < p.KW; ++j) acc = fmaf(sp[nl + j], p.convW[j * p.F + f], acc);
+  // ---------------- normaliser sums over the utterance
+  float s1 = 0.f, s3 = 0.f;
+#pragma unroll
+  for (int i = 0; i < kPos; ++i) {
+    if (FWD) s1 = fmaf(rDA[i], rat[i], s1);
+    s3 = fmaf(rs2[i], rDS2[i], s3);
+  }
+  const float2 s13 = block_sum2(s1, s3, red);   // barrier also publishes the LDS burst
+  s1 = s13.x; s3 = s13.y;
+  const float Sa = FWD ? p.stats[b * 4 + 2] : 1.f;
+  const float rSa = 1.f / Sa;
+  float s2sum = 0.f;
+#pragma unroll
+  for (int i = 0; i < kPos; ++i) {
+    const int n = tid + 256 * i;
+    float ds, da = 0.f;
+    if (FWD) {
+      da = (rDA[i] - s1) * rSa;
+      ds = rsn[i] + da * ((1.f - u) * rap[i] + u * ram[i] + 1e-7f);
+    } else {
+      ds = rDA[i];
+    }
+    s2sum = fmaf(rst[i], ds, s2sum);
+    const int r = n - n0;
+    if (r >= 0 && r <= nt) {
+      if (r < nt) dst[r] = ds;
+      dat[r] = da;
+      stt[r] = rst[i];
+    }
+  }
+  if (FWD) {  // location features of the tile
+    if (tid < NT * F) {
+      const int nl = tid / F, f = tid - nl * F;
+      float acc = cw[p.KW * F + f];
+      for (int j = 0; j < p.KW; ++j) acc = fmaf(sp[nl + j], cw[j * F + f], acc);
       fs[nl][f] = acc;
+    }
+  }
+  s2sum = block_sum2(s2sum, 0.f, red + 8).x;   // dst/dat/fs visible after its barrier
+
+  // ---------------- tile: de, de2, dA_prev
+  if (tid < nt) {
+    const int n = n0 + tid;
+    de1[tid] = stt[tid] * (dst[tid] - s2sum);
+    de2[tid] = p.s2_t[rb + n] * (p.DS2[rb + n] - s3);
+    if (FWD) {
+      float v = (1.f - u) * dat[tid] * stt[tid];
+      if (n + 1 < N) v += u * dat[tid + 1] * stt[tid + 1];
+      p.dalpha_prev[rb + n] = v;
     }
   }
   __syncthreads();
 
-  // ---- recompute energies of the tile and back-propagate through tanh
+  // ---------------- recompute the tile's energies, back-propagate through tanh
   float aq[4] = {0, 0, 0, 0}, av[4] = {0, 0, 0, 0};
-  float aw[4][kMaxFb];
+  float aw[4][FL];
 #pragma unroll
   for (int k = 0; k < 4; ++k)
 #pragma unroll
-    for (int f = 0; f < kMaxFb; ++f) aw[k][f] = 0.f;
+    for (int f = 0; f < FL; ++f) aw[k][f] = 0.f;
   float aq2 = 0.f, av2 = 0.f;   // lane owns d2 = lane (D2 <= 64, checked on the host)
-  for (int nl = wave; nl < nt; nl += 4) {
-    const int n = n0 + nl;
-    const float e = de1[nl];
-    const float* k1 = p.K1 + (rb + n) * p.D1;
-    float* dk1 = p.dK1 + (rb + n) * p.D1;
-    float dfp[kMaxFb];
+  const float q2 = q2s[lane], v2 = v2s[lane];
 #pragma unroll
-    for (int f = 0; f < kMaxFb; ++f) dfp[f] = 0.f;
+  for (int i = 0; i < PPW; ++i) {
+    const int nl = wave + 4 * i;
+    if (nl >= nt) break;
+    const int64_t row = rb + n0 + nl;
+    const float e = de1[nl];
+    float fl[FL], dfp[FL];
+#pragma unroll
+    for (int f = 0; f < FL; ++f) { fl[f] = FWD ? fs[nl][f] : 0.f; dfp[f] = 0.f; }
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int d = lane + 64 * k;
-      if (d < p.D1) {
-        float pre = k1[d] + qb[d];
-        if (fwd) {
+      float pre = k1r[i][k] + qb[d];
+      float lw[FL];
 #pragma unroll
-          for (int f = 0; f < kMaxFb; ++f)
-            if (f < p.F) pre = fmaf(fs[nl][f], locw[f * p.D1 + d], pre);
-        }
-        const float z = tanhf(pre);
-        const float dp = e * vv[d] * (1.f - z * z);
-        dk1[d] += dp;
-        aq[k] += dp;
-        av[k] = fmaf(e, z, av[k]);
-        if (fwd) {
+      for (int f = 0; f < F; ++f) { lw[f] = locw[f * kMaxD + d]; pre = fmaf(fl[f], lw[f], pre); }
+      const float z = tanh_fast(pre);
+      const float dp = e * vv[d] * (1.f - z * z);
+      if (d < D1) p.dK1[row * D1 + d] = dk1r[i][k] + dp;
+      aq[k] += dp;
+      av[k] = fmaf(e, z, av[k]);
 #pragma unroll
-          for (int f = 0; f < kMaxFb; ++f)
-            if (f < p.F) {
-              aw[k][f] = fmaf(fs[nl][f], dp, aw[k][f]);
-              dfp[f] = fmaf(dp, locw[f * p.D1 + d], dfp[f]);
-            }
-        }
+      for (int f = 0; f < F; ++f) {
+        aw[k][f] = fmaf(fl[f], dp, aw[k][f]);
+        dfp[f] = fmaf(dp, lw[f], dfp[f]);
       }
     }
-    if (fwd) {
 #pragma unroll
-      for (int f = 0; f < kMaxFb; ++f) {
-        if (f < p.F) {
-          const float s = wave_sum(dfp[f]);
-          if (lane == 0) dfs[nl][f] = s;
-        }
-      }
+    for (int f = 0; f < F; ++f) {
+      const float sdf = wave_sum_dpp(dfp[f]);
+      if (lane == 0) dfs[nl][f] = sdf;
     }
-    const float e2v = de2[nl];
-    const float* k2 = p.K2 + (rb + n) * p.D2;
-    float* dk2 = p.dK2 + (rb + n) * p.D2;
-    if (lane < p.D2) {
-      const int d = lane;
-      const float z = tanhf(k2[d] + q2s[d]);
-      const float dp = e2v * v2s[d] * (1.f - z * z);
-      dk2[d] += dp;
+    {
+      const float e2v = de2[nl];
+      const float z = tanh_fast(k2r[i] + q2);
+      const float dp = e2v * v2 * (1.f - z * z);
+      if (lane < D2) p.dK2[row * D2 + lane] = dk2r[i] + dp;
       aq2 += dp;
       av2 = fmaf(e2v, z, av2);
     }
   }
-  // ---- reduce the per-lane accumulators of the 4 waves
-  // layout per wave: [dq D1][dv1 D1][dWloc F*D1][dq2 64][dv2 64]
-  float* r = racc[wave];
-  const int W = p.D1, F = fwd ? p.F : 0;
+  // ---------------- per-wave accumulators -> LDS (layout per wave:
+  //                  [dq D1][dv1 D1][dWloc F*D1][dq2 64][dv2 64])
+  const int W = D1;
+  constexpr int wstride = kBwdScratch / 4;
+  float* r = scratch + wave * wstride;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int d = lane + 64 * k;
@@ -538,48 +763,70 @@ __global__ void __launch_bounds__(256) attn_bwd_energy_kernel(AttnBwdP p) {
       r[d] = aq[k];
       r[W + d] = av[k];
 #pragma unroll
-      for (int f = 0; f < kMaxFb; ++f)
-        if (f < F) r[2 * W + f * W + d] = aw[k][f];
+      for (int f = 0; f < F; ++f) r[2 * W + f * W + d] = aw[k][f];
     }
   }
   const int off2 = (2 + F) * W;
-  if (lane < 64) {
-    r[off2 + lane] = aq2;
-    r[off2 + 64 + lane] = av2;
-  }
+  r[off2 + lane] = aq2;
+  r[off2 + 64 + lane] = av2;
   __syncthreads();
-  float* dqp = p.dqp + ((int64_t)b * p.ntiles + tile) * (p.D1 + p.D2);
-  float* pg = p.pg + ((int64_t)b * p.ntiles + tile) * p.pg_stride;
-  // pg layout: [dv1 D1][dWloc F*D1][dconvW KW*F][dconvb F][dv2 D2]
-  const int total = off2;
-  for (int i = tid; i < total; i += 256) {
-    const float v = racc[0][i] + racc[1][i] + racc[2][i] + racc[3][i];
-    if (i < W) dqp[i] = v;
-    else pg[i - W] += v;        // dv1 then dWloc
-  }
-  for (int i = tid; i < p.D2; i += 256) {
-    float vq = 0.f, vv2 = 0.f;
-    for (int w = 0; w < 4; ++w) { vq += racc[w][off2 + i]; vv2 += racc[w][off2 + 64 + i]; }
-    dqp[p.D1 + i] = vq;
-    pg[(1 + p.F) * W + p.KW * p.F + p.F + i] += vv2;
-  }
-  if (fwd) {
-    // location conv grads: dconvW[j,f] = sum_n s_prev[n+j-padl] df[n,f], dconvb[f] = sum_n df
-    for (int i = tid; i < p.KW * p.F + p.F; i += 256) {
+  if (FWD) {   // location conv grads of the tile
+    for (int i = tid; i < p.KW * F + F; i += 256) {
       float acc = 0.f;
-      if (i < p.KW * p.F) {
-        const int j = i / p.F, f = i - j * p.F;
+      if (i < p.KW * F) {
+        const int j = i / F, f = i - j * F;
         for (int nl = 0; nl < nt; ++nl) acc = fmaf(sp[nl + j], dfs[nl][f], acc);
       } else {
-        const int f = i - p.KW * p.F;
+        const int f = i - p.KW * F;
         for (int nl = 0; nl < nt; ++nl) acc += dfs[nl][f];
       }
-      pg[(1 + p.F) * W + i] += acc;
+      convg[i] = acc;
     }
-    for (int i = tid; i < nt * p.F; i += 256) {
-      const int nl = i / p.F, f = i - nl * p.F;
-      p.df_out[(rb + n0 + nl) * p.F + f] = dfs[nl][f];
+    if (tid < nt * F) {
+      const int nl = tid / F, f = tid - nl * F;
+      p.df_out[(rb + n0 + nl) * F + f] = dfs[nl][f];
     }
+    __syncthreads();
+  }
+  // ---------------- outputs: dq partials (overwrite) and the PG row (accumulate)
+  float* dqp = p.dqp + ((int64_t)b * p.ntiles + tile) * (D1 + D2);
+  for (int d = tid; d < D1 + D2; d += 256) {
+    const int o = d < D1 ? d : off2 + (d - D1);
+    dqp[d] = (scratch[o] + scratch[wstride + o]) + (scratch[2 * wstride + o] + scratch[3 * wstride + o]);
+  }
+  // pg layout: [dv1 D1][dWloc F*D1][dconvW KW*F][dconvb F][dv2 D2]
+  const int pconv = (1 + F) * W, pv2 = pconv + p.KW * F + F;
+#pragma unroll
+  for (int i = 0; i < kPgr; ++i) {
+    const int j = tid + 256 * i;
+    if (j >= p.pg_stride) break;
+    float c = 0.f;
+    if (j < pconv) {
+      const int o = W + j;   // dv1 at [W, 2W), dWloc at [2W, (2+F)W)
+      c = (scratch[o] + scratch[wstride + o]) + (scratch[2 * wstride + o] + scratch[3 * wstride + o]);
+    } else if (j < pv2) {
+      if (FWD) c = convg[j - pconv];
+    } else if (j < pv2 + D2) {
+      const int o = off2 + 64 + (j - pv2);
+      c = (scratch[o] + scratch[wstride + o]) + (scratch[2 * wstride + o] + scratch[3 * wstride + o]);
+    }
+    p.pg[pgrow + j] = pgr[i] + c;
+  }
+}
+
+template <int NT>
+void launch_attn_bwd(const AttnBwdP& p, int F, int blocks, hipStream_t s) {
+  hipLaunchKernelGGL(attn_bwd_ctx_kernel<NT>, dim3(blocks), dim3(256), 0, s, p);
+  switch (F) {
+    case 0: hipLaunchKernelGGL((attn_bwd_energy_kernel<NT, 0>), dim3(blocks), dim3(256), 0, s, p); break;
+    case 1: hipLaunchKernelGGL((attn_bwd_energy_kernel<NT, 1>), dim3(blocks), dim3(256), 0, s, p); break;
+    case 2: hipLaunchKernelGGL((attn_bwd_energy_kernel<NT, 2>), dim3(blocks), dim3(256), 0, s, p); break;
+    case 3: hipLaunchKernelGGL((attn_bwd_energy_kernel<NT, 3>), dim3(blocks), dim3(256), 0, s, p); break;
+    case 4: hipLaunchKernelGGL((attn_bwd_energy_kernel<NT, 4>), dim3(blocks), dim3(256), 0, s, p); break;
+    case 5: hipLaunchKernelGGL((attn_bwd_energy_kernel<NT, 5>), dim3(blocks), dim3(256), 0, s, p); break;
+    case 6: hipLaunchKernelGGL((attn_bwd_energy_kernel<NT, 6>), dim3(blocks), dim3(256), 0, s, p); break;
+    case 7: hipLaunchKernelGGL((attn_bwd_energy_kernel<NT, 7>), dim3(blocks), dim3(256), 0, s, p); break;
+    default: hipLaunchKernelGGL((attn_bwd_energy_kernel<NT, 8>), dim3(blocks), dim3(256), 0, s, p); break;
   }
 }
 
@@ -594,15 +841,16 @@ extern "C" int sat_attn_pg_stride(int32_t D1, int32_t D2, int32_t F, int32_t KW)
 
 extern "C" int sat_attn_step_bwd(const SatAttnStepBwd* a, void* stream) {
   SAT_CHECK_ARG(a && a->B > 0 && a->N > 0 && a->N <= kMaxN, "sat_attn_step_bwd: bad sizes (N <= 1024)");
-  SAT_CHECK_ARG(a->D1 <= kMaxD && a->D2 <= 64 && a->M1 + a->M2 <= 3 * kMaxD,
+  SAT_CHECK_ARG(a->D1 <= kMaxD && a->D2 <= 64 && a->M2 <= 64 && a->M1 + a->M2 <= 2 * kMaxD,
                 "sat_attn_step_bwd: D1 <= 256, D2 <= 64");
-  SAT_CHECK_ARG(a->NT > 0 && a->NT <= kMaxNT && a->ntiles == ceil_div(a->N, a->NT),
-                "sat_attn_step_bwd: tiles");
+  SAT_CHECK_ARG((a->NT == 8 || a->NT == 16 || a->NT == 32) && a->ntiles == ceil_div(a->N, a->NT),
+                "sat_attn_step_bwd: tile size must be 8, 16 or 32");
+  SAT_CHECK_ARG(a->pg_stride <= 2048 && a->M1 <= 256, "sat_attn_step_bwd: pg_stride <= 2048, M1 <= 256");
   SAT_CHECK_ARG(!a->att1_forward || (a->F <= kMaxFb && a->KW <= kMaxKW),
                 "sat_attn_step_bwd: location conv too large (F <= 8)");
   SAT_CHECK_ARG(a->pg_stride >= sat_attn_pg_stride(a->D1, a->D2, a->F, a->KW), "sat_attn_step_bwd: pg stride");
   SAT_CHECK_ARG(a->dctx && a->V1 && a->V2 && a->DA && a->DS2 && a->s_t && a->s2_t && a->q &&
-                a->K1 && a->K2 && a->v1 && a->v2 && a->dK1 && a->dK2 && a->dqp && a->pg,
+                a->K1 && a->K2 && a->v1 && a->v2 && a->dK1 && a->dK2 && a->dqp && a->pg && a->DSN,
                 "sat_attn_step_bwd: null pointer");
   SAT_CHECK_ARG(!a->att1_forward || (a->a_t && a->a_prev && a->s_prev && a->stats && a->convW &&
                                      a->convb && a->locW && a->dalpha_prev && a->df_out),
@@ -611,7 +859,7 @@ extern "C" int sat_attn_step_bwd(const SatAttnStepBwd* a, void* stream) {
   p.B = a->B; p.N = a->N; p.D1 = a->D1; p.M1 = a->M1; p.D2 = a->D2; p.M2 = a->M2; p.F = a->F;
   p.KW = a->KW; p.NT = a->NT; p.ntiles = a->ntiles; p.att1_forward = a->att1_forward; p.u = a->u;
   p.dctx = a->dctx; p.dctx_sb = a->dctx_sb; p.dalpha_next = a->dalpha_next;
-  p.V1 = a->V1; p.V2 = a->V2; p.DA = a->DA; p.DS2 = a->DS2;
+  p.V1 = a->V1; p.V2 = a->V2; p.DA = a->DA; p.DS2 = a->DS2; p.DSN = a->DSN;
   p.s_t = a->s_t; p.a_t = a->a_t; p.a_prev = a->a_prev; p.s_prev = a->s_prev; p.s2_t = a->s2_t;
   p.stats = a->stats; p.df_next = a->df_next; p.lengths = a->lengths; p.q = a->q; p.q_sb = a->q_sb;
   p.K1 = a->K1; p.K2 = a->K2; p.v1 = a->v1; p.b1 = a->b1; p.convW = a->convW; p.convb = a->convb;
@@ -619,9 +867,10 @@ extern "C" int sat_attn_step_bwd(const SatAttnStepBwd* a, void* stream) {
   p.dK1 = a->dK1; p.dK2 = a->dK2; p.dqp = a->dqp; p.pg = a->pg; p.pg_stride = a->pg_stride;
   hipStream_t s = as_stream(stream);
   const int blocks = a->B * a->ntiles;
-  hipLaunchKernelGGL(attn_bwd_ctx_kernel, dim3(blocks), dim3(256), 0, s, p);
-  SAT_LAUNCH_CHECK("sat_attn_step_bwd(ctx)");
-  hipLaunchKernelGGL(attn_bwd_energy_kernel, dim3(blocks), dim3(256), 0, s, p);
-  SAT_LAUNCH_CHECK("sat_attn_step_bwd(energy)");
+  const int F = a->att1_forward ? a->F : 0;
+  if (a->NT == 8) launch_attn_bwd<8>(p, F, blocks, s);
+  else if (a->NT == 16) launch_attn_bwd<16>(p, F, blocks, s);
+  else launch_attn_bwd<32>(p, F, blocks, s);
+  SAT_LAUNCH_CHECK("sat_attn_step_bwd");
   return SAT_OK;
 }

@@ -347,10 +347,37 @@ __global__ void loss_grad_kernel(const float* __restrict__ mel, const float* __r
   }
 }
 
+// out[c][r] = in[r][c]  (32x32 tiles through LDS)
+__global__ void transpose_kernel(const float* __restrict__ in, int64_t ldi, float* __restrict__ out,
+                                 int64_t ldo, int R, int C) {
+  __shared__ float t[32][33];
+  const int r0 = blockIdx.y * 32, c0 = blockIdx.x * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;   // 256 threads: 8 rows per pass
+  for (int i = ty; i < 32; i += 8) {
+    const int r = r0 + i, c = c0 + tx;
+    t[i][tx] = (r < R && c < C) ? in[(int64_t)r * ldi + c] : 0.f;
+  }
+  __syncthreads();
+  for (int i = ty; i < 32; i += 8) {
+    const int c = c0 + i, r = r0 + tx;
+    if (c < C && r < R) out[(int64_t)c * ldo + r] = t[tx][i];
+  }
+}
+
 }  // namespace
 }  // namespace sat
 
 using namespace sat;
+
+extern "C" int sat_transpose(const float* in, int64_t ldi, float* out, int64_t ldo, int32_t R,
+                             int32_t C, void* stream) {
+  SAT_CHECK_ARG(in && out && R >= 0 && C >= 0, "sat_transpose: bad args");
+  if (R == 0 || C == 0) return SAT_OK;
+  hipLaunchKernelGGL(transpose_kernel, dim3(ceil_div(C, 32), ceil_div(R, 32)), dim3(256), 0,
+                     as_stream(stream), in, ldi, out, ldo, R, C);
+  SAT_LAUNCH_CHECK("sat_transpose");
+  return SAT_OK;
+}
 
 extern "C" int sat_seq_mask(const float* x, float* out, int32_t B, int32_t N, int32_t C,
                             const int64_t* lengths, void* stream) {

@@ -36,41 +36,68 @@ struct LstmFwdP {
   float* gates;
 };
 
+// Forward step.  Every global load is issued up front: the workgroup's weight slice
+// W[:, u0:u0+4, :] (K x 16 floats) and its 8 input rows go global -> LDS in one burst of
+// 16-byte loads, the pointwise operands (xproj, c, h, masks) are prefetched into registers,
+// then the K-split dot products run out of LDS.
 __global__ void __launch_bounds__(256) lstm_fwd_kernel(LstmFwdP p) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int K = p.K;
+  float4* Ws = reinterpret_cast<float4*>(smem);          // [K][UT]
+  float* xs = smem + (size_t)K * UT * 4;                  // [BT][K + 4]
+  const int xld = K + 4;
   const int tid = threadIdx.x;
   const int ks = tid & (KS - 1), pair = tid >> 3;
-  const int u = blockIdx.x * UT + (pair & (UT - 1));
-  const int b = blockIdx.y * BT + (pair >> 2);
+  const int u0 = blockIdx.x * UT, b0 = blockIdx.y * BT;
+  const int u = u0 + (pair & (UT - 1));
+  const int bl = pair >> 2;
+  const int b = b0 + bl;
   const bool active = (u < p.U) && (b < p.B);
+  // prefetch the pointwise operands of this (b, u)
+  const int64_t bu = (int64_t)b * p.U + u;
+  float4 xp = make_float4(0.f, 0.f, 0.f, 0.f);
+  float cp = 0.f, hp = 0.f, mc = 0.f, mh = 0.f;
+  bool valid = true;
+  if (active && ks == 0) {
+    if (p.xproj) xp = reinterpret_cast<const float4*>(p.xproj + (int64_t)b * p.xproj_sb)[u];
+    else if (p.bias) xp = reinterpret_cast<const float4*>(p.bias)[u];
+    cp = p.c_prev ? p.c_prev[bu] : 0.f;
+    hp = p.h_prev ? p.h_prev[(int64_t)b * p.h_prev_sb + u] : 0.f;
+    if (p.mask_c) { mc = p.mask_c[bu]; mh = p.mask_h[bu]; }
+    valid = p.lengths ? (p.t < p.lengths[b]) : true;
+  }
+  // weights: K rows x UT float4 (rows are UT*16 contiguous bytes at stride U*16)
+  const float4* W4 = reinterpret_cast<const float4*>(p.W);
+  const int nu = min(UT, p.U - u0);
+  for (int i = tid; i < K * UT; i += 256) {
+    const int k = i / UT, j = i - k * UT;
+    Ws[i] = j < nu ? W4[(int64_t)k * p.U + u0 + j] : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  const int kq = K >> 2;
+  for (int i = tid; i < BT * kq; i += 256) {
+    const int r = i / kq, c = i - r * kq;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (b0 + r < p.B) v = reinterpret_cast<const float4*>(p.rin + (int64_t)(b0 + r) * p.rin_sb)[c];
+    *reinterpret_cast<float4*>(xs + r * xld + 4 * c) = v;
+  }
+  __syncthreads();
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
-  if (active) {
-    const float* rin = p.rin + (int64_t)b * p.rin_sb;
-    const float4* W4 = reinterpret_cast<const float4*>(p.W);
-    const int nchunk = p.K >> 2;
+  const float* xr = xs + bl * xld;
+  const int ul = pair & (UT - 1);
 #pragma unroll 4
-    for (int c = ks; c < nchunk; c += KS) {
-      const float4 x = *reinterpret_cast<const float4*>(rin + 4 * c);
-      const float xs[4] = {x.x, x.y, x.z, x.w};
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float4 w = W4[(int64_t)(4 * c + r) * p.U + u];
-        acc[0] = fmaf(xs[r], w.x, acc[0]);
-        acc[1] = fmaf(xs[r], w.y, acc[1]);
-        acc[2] = fmaf(xs[r], w.z, acc[2]);
-        acc[3] = fmaf(xs[r], w.w, acc[3]);
-      }
-    }
+  for (int k = ks; k < K; k += KS) {
+    const float xv = xr[k];
+    const float4 w = Ws[k * UT + ul];
+    acc[0] = fmaf(xv, w.x, acc[0]);
+    acc[1] = fmaf(xv, w.y, acc[1]);
+    acc[2] = fmaf(xv, w.z, acc[2]);
+    acc[3] = fmaf(xv, w.w, acc[3]);
   }
 #pragma unroll
   for (int o = 1; o < KS; o <<= 1)
 #pragma unroll
     for (int g = 0; g < 4; ++g) acc[g] += __shfl_xor(acc[g], o, 64);
   if (!active || ks != 0) return;
-
-  const int64_t bu = (int64_t)b * p.U + u;
-  const float cp = p.c_prev ? p.c_prev[bu] : 0.f;
-  const float hp = p.h_prev ? p.h_prev[(int64_t)b * p.h_prev_sb + u] : 0.f;
-  const bool valid = p.lengths ? (p.t < p.lengths[b]) : true;
   if (!valid) {  // bidirectional_dynamic_rnn(sequence_length): state copied, output 0
     p.c_out[bu] = cp;
     p.h_out[(int64_t)b * p.h_out_sb + u] = hp;
@@ -78,10 +105,6 @@ __global__ void __launch_bounds__(256) lstm_fwd_kernel(LstmFwdP p) {
     if (p.gates) reinterpret_cast<float4*>(p.gates)[bu] = make_float4(0.f, 0.f, 0.f, 0.f);
     return;
   }
-  float4 xp;
-  if (p.xproj) xp = reinterpret_cast<const float4*>(p.xproj + (int64_t)b * p.xproj_sb)[u];
-  else if (p.bias) xp = reinterpret_cast<const float4*>(p.bias)[u];
-  else xp = make_float4(0.f, 0.f, 0.f, 0.f);
   const float gi = sigmf(acc[0] + xp.x);
   const float gj = tanhf(acc[1] + xp.y);
   const float gf = sigmf(acc[2] + xp.z + 1.0f);   // forget_bias = 1.0
@@ -90,7 +113,6 @@ __global__ void __launch_bounds__(256) lstm_fwd_kernel(LstmFwdP p) {
   const float hn = go * tanhf(cn);
   float c2, h2;
   if (p.mask_c) {
-    const float mc = p.mask_c[bu], mh = p.mask_h[bu];
     c2 = mc * cn + (1.f - mc) * cp;
     h2 = mh * hn + (1.f - mh) * hp;
   } else {
@@ -126,49 +148,83 @@ struct LstmBwdP {
 // dL/dh_t = dh_carry + sum_g dgates_{t+1}[b, g] * W[hoff + u, g]  (the recurrent product)
 // The optional query-gradient term sum_d dq[b, d] wq[u, d] reads dq as `dq_parts` per-tile
 // partials: the workgroup first sums them for its 8 batch rows into LDS (all 256 threads, loads
-// independent), then every (b, u) group dots the LDS row with wq's row.
+// independent), then every (b, u) group dots the LDS row with wq's row.  dgates_{t+1} rows and
+// the 4 W rows are staged global -> LDS in one burst of 16-byte loads.
 constexpr int kMaxDq = 320;
 
 __global__ void __launch_bounds__(256) lstm_bwd_kernel(LstmBwdP p) {
-  __shared__ float dqs[BT][kMaxDq];
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int G = 4 * p.U;
+  const int D0 = p.dq0 ? p.dq0_n : 0, D1 = p.dq1 ? p.dq1_n : 0, DQ = D0 + D1;
+  float* dgs = smem;                                   // [BT][G + 4]  dgates_{t+1} rows
+  float* wrs = dgs + (size_t)BT * (G + 4);             // [UT][G + 4]  W rows hoff+u
+  float* dqs = wrs + (size_t)UT * (G + 4);             // [BT][DQ]
+  const int ld = G + 4;
   const int tid = threadIdx.x;
   const int ks = tid & (KS - 1), pair = tid >> 3;
-  const int u = blockIdx.x * UT + (pair & (UT - 1));
-  const int bl = pair >> 2;
-  const int b = blockIdx.y * BT + bl;
+  const int u0 = blockIdx.x * UT, b0 = blockIdx.y * BT;
+  const int ul = pair & (UT - 1), bl = pair >> 2;
+  const int u = u0 + ul, b = b0 + bl;
   const bool active = (u < p.U) && (b < p.B);
-  const int D0 = p.dq0 ? p.dq0_n : 0, D1 = p.dq1 ? p.dq1_n : 0;
-  if (D0 + D1 > 0) {
-    for (int i = tid; i < BT * (D0 + D1); i += 256) {
-      const int r = i / (D0 + D1), d = i - r * (D0 + D1);
-      const int bb = blockIdx.y * BT + r;
-      float g = 0.f;
-      if (bb < p.B) {
-        const float* src = d < D0 ? p.dq0 + d : p.dq1 + (d - D0);
-        for (int part = 0; part < p.dq_parts; ++part)
-          g += src[(int64_t)bb * p.dq_bstride + part * p.dq_pstride];
-      }
-      dqs[r][d] = g;
-    }
-    __syncthreads();
+  const int64_t bu = (int64_t)b * p.U + u;
+  // prefetch the pointwise operands
+  float4 g4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  float cp = 0.f, dyv = 0.f, dhc = 0.f, dcc = 0.f, mc = 0.f, mh = 0.f;
+  bool valid = true;
+  if (active && ks == 0) {
+    g4 = reinterpret_cast<const float4*>(p.gates)[bu];
+    cp = p.c_prev ? p.c_prev[bu] : 0.f;
+    dyv = p.dy ? p.dy[(int64_t)b * p.dy_sb + u] : 0.f;
+    dhc = p.dh_carry ? p.dh_carry[bu] : 0.f;
+    dcc = p.dc_carry ? p.dc_carry[bu] : 0.f;
+    if (p.mask_c) { mc = p.mask_c[bu]; mh = p.mask_h[bu]; }
+    valid = p.lengths ? (p.t < p.lengths[b]) : true;
   }
+  const int gq = G >> 2;
+  if (p.dgates_next) {
+    for (int i = tid; i < BT * gq; i += 256) {
+      const int r = i / gq, c = i - r * gq;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (b0 + r < p.B) v = reinterpret_cast<const float4*>(p.dgates_next + (int64_t)(b0 + r) * G)[c];
+      *reinterpret_cast<float4*>(dgs + r * ld + 4 * c) = v;
+    }
+    for (int i = tid; i < UT * gq; i += 256) {
+      const int r = i / gq, c = i - r * gq;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (u0 + r < p.U) v = reinterpret_cast<const float4*>(p.W + (int64_t)(p.hoff + u0 + r) * G)[c];
+      *reinterpret_cast<float4*>(wrs + r * ld + 4 * c) = v;
+    }
+  }
+  for (int i = tid; i < BT * DQ; i += 256) {   // sum the per-tile query-gradient partials
+    const int r = i / DQ, d = i - r * DQ;
+    const int bb = b0 + r;
+    float g = 0.f;
+    if (bb < p.B) {
+      const float* src = d < D0 ? p.dq0 + d : p.dq1 + (d - D0);
+      for (int part = 0; part < p.dq_parts; ++part)
+        g += src[(int64_t)bb * p.dq_bstride + part * p.dq_pstride];
+    }
+    dqs[r * DQ + d] = g;
+  }
+  __syncthreads();
   float rec = 0.f, extra = 0.f;
   if (active && p.dgates_next) {
-    const float4* dg = reinterpret_cast<const float4*>(p.dgates_next + (int64_t)b * p.U * 4);
-    const float4* wr = reinterpret_cast<const float4*>(p.W + (int64_t)(p.hoff + u) * p.U * 4);
-#pragma unroll 8
-    for (int v = ks; v < p.U; v += KS) {
-      const float4 g = dg[v], w = wr[v];
+    const float* dg = dgs + bl * ld;
+    const float* wr = wrs + ul * ld;
+#pragma unroll 4
+    for (int v = 4 * ks; v < G; v += 4 * KS) {
+      const float4 g = *reinterpret_cast<const float4*>(dg + v);
+      const float4 w = *reinterpret_cast<const float4*>(wr + v);
       rec += g.x * w.x + g.y * w.y + g.z * w.z + g.w * w.w;
     }
   }
   if (active && D0 > 0) {
     const float* w0 = p.wq0 + (int64_t)u * D0;
-    for (int d = ks; d < D0; d += KS) extra = fmaf(dqs[bl][d], w0[d], extra);
+    for (int d = ks; d < D0; d += KS) extra = fmaf(dqs[bl * DQ + d], w0[d], extra);
   }
   if (active && D1 > 0) {
     const float* w1 = p.wq1 + (int64_t)u * D1;
-    for (int d = ks; d < D1; d += KS) extra = fmaf(dqs[bl][D0 + d], w1[d], extra);
+    for (int d = ks; d < D1; d += KS) extra = fmaf(dqs[bl * DQ + D0 + d], w1[d], extra);
   }
 #pragma unroll
   for (int o = 1; o < KS; o <<= 1) {
@@ -176,25 +232,19 @@ __global__ void __launch_bounds__(256) lstm_bwd_kernel(LstmBwdP p) {
     extra += __shfl_xor(extra, o, 64);
   }
   if (!active || ks != 0) return;
-  const int64_t bu = (int64_t)b * p.U + u;
-  const float dh_t = rec + (p.dh_carry ? p.dh_carry[bu] : 0.f);
-  const float dc_t = p.dc_carry ? p.dc_carry[bu] : 0.f;
-  const bool valid = p.lengths ? (p.t < p.lengths[b]) : true;
+  const float dh_t = rec + dhc;
+  const float dc_t = dcc;
   if (!valid) {
     reinterpret_cast<float4*>(p.dgates)[bu] = make_float4(0.f, 0.f, 0.f, 0.f);
     p.dh_carry_out[bu] = dh_t;
     p.dc_carry_out[bu] = dc_t;
     return;
   }
-  const float4 g = reinterpret_cast<const float4*>(p.gates)[bu];
-  const float gi = g.x, gj = g.y, gf = g.z, go = g.w;
-  const float cp = p.c_prev ? p.c_prev[bu] : 0.f;
+  const float gi = g4.x, gj = g4.y, gf = g4.z, go = g4.w;
   const float cn = gf * cp + gi * gj;
   const float tc = tanhf(cn);
-  float mc, mh;
-  if (p.mask_c) { mc = p.mask_c[bu]; mh = p.mask_h[bu]; }
-  else { mc = 1.f - p.zc; mh = 1.f - p.zh; }
-  const float dy = (p.dy ? p.dy[(int64_t)b * p.dy_sb + u] : 0.f) + extra;
+  if (!p.mask_c) { mc = 1.f - p.zc; mh = 1.f - p.zh; }
+  const float dy = dyv + extra;
   const float dhn = dy + mh * dh_t;                 // dL/dh'
   const float dcn = mc * dc_t + dhn * go * (1.f - tc * tc);
   const float d_o = dhn * tc * go * (1.f - go);
@@ -226,7 +276,9 @@ extern "C" int sat_lstm_step_fwd(const SatLstmFwd* a, void* stream) {
   p.h_raw = a->h_raw; p.h_raw_sb = a->h_raw_sb;
   p.c_out = a->c_out; p.h_out = a->h_out; p.h_out_sb = a->h_out_sb; p.gates = a->gates;
   dim3 grid(ceil_div(a->U, UT), ceil_div(a->B, BT));
-  hipLaunchKernelGGL(lstm_fwd_kernel, grid, dim3(256), 0, as_stream(stream), p);
+  const size_t shm = ((size_t)a->K * UT * 4 + (size_t)BT * (a->K + 4)) * sizeof(float);
+  SAT_CHECK_ARG(shm <= 160 * 1024, "sat_lstm_step_fwd: K too large for the LDS-staged step");
+  hipLaunchKernelGGL(lstm_fwd_kernel, grid, dim3(256), shm, as_stream(stream), p);
   SAT_LAUNCH_CHECK("sat_lstm_step_fwd");
   return SAT_OK;
 }
@@ -252,7 +304,10 @@ extern "C" int sat_lstm_step_bwd(const SatLstmBwd* a, void* stream) {
   p.lengths = a->lengths; p.t = a->t;
   p.dgates = a->dgates; p.dh_carry_out = a->dh_carry_out; p.dc_carry_out = a->dc_carry_out;
   dim3 grid(ceil_div(a->U, UT), ceil_div(a->B, BT));
-  hipLaunchKernelGGL(lstm_bwd_kernel, grid, dim3(256), 0, as_stream(stream), p);
+  const int DQ = (a->dq0 ? a->dq0_n : 0) + (a->dq1 ? a->dq1_n : 0);
+  const size_t shm = ((size_t)(BT + UT) * (4 * a->U + 4) + (size_t)BT * DQ) * sizeof(float);
+  SAT_CHECK_ARG(shm <= 160 * 1024, "sat_lstm_step_bwd: U too large for the LDS-staged step");
+  hipLaunchKernelGGL(lstm_bwd_kernel, grid, dim3(256), shm, as_stream(stream), p);
   SAT_LAUNCH_CHECK("sat_lstm_step_bwd");
   return SAT_OK;
 }

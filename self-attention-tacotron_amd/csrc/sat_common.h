@@ -72,6 +72,42 @@ __device__ __forceinline__ float block_max(float v, float* scratch) {
   return r;
 }
 
+// DPP lane permutes (VALU, no LDS crossbar): quad_perm xor1 / xor2, row_half_mirror, row_mirror
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+// sum over each aligned group of 8 lanes (result in every lane of the group)
+__device__ __forceinline__ float group8_sum(float v) {
+  v += dpp<0xB1>(v);
+  v += dpp<0x4E>(v);
+  v += dpp<0x141>(v);
+  return v;
+}
+__device__ __forceinline__ float group8_max(float v) {
+  v = fmaxf(v, dpp<0xB1>(v));
+  v = fmaxf(v, dpp<0x4E>(v));
+  v = fmaxf(v, dpp<0x141>(v));
+  return v;
+}
+// full-wave sum: DPP within rows of 16, then 4 readlanes (uniform result)
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+  v = group8_sum(v);
+  v += dpp<0x140>(v);
+  const float a = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
+  const float b = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16));
+  const float c = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
+  const float d = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
+  return (a + b) + (c + d);
+}
+
+// tanh via one v_exp_f32 and one reciprocal: |error| ~2e-7 absolute, saturates correctly
+// (exp overflow -> +1, underflow -> -1).  Used for the attention energies (1.4 M per step).
+__device__ __forceinline__ float tanh_fast(float x) {
+  const float e = __expf(2.f * x);
+  return 1.f - 2.f * __builtin_amdgcn_rcpf(1.f + e);
+}
+
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 inline int ceil_div(int64_t a, int64_t b) { return static_cast<int>((a + b - 1) / b); }

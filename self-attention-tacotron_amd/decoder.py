@@ -54,8 +54,9 @@ def teacher_inputs(targets: torch.Tensor, r: int, n_feed: int) -> torch.Tensor:
 
 def decoder_forward(P: Dict[str, torch.Tensor], hp, d: Dims, m1: torch.Tensor, m2: torch.Tensor,
                     lengths: torch.Tensor, targets: torch.Tensor,
-                    masks: Optional[Dict[str, torch.Tensor]], attn_tile: int = 16,
+                    masks: Optional[Dict[str, torch.Tensor]], attn_tile: int = 32,
                     spk: Optional[torch.Tensor] = None):
+    """Forward of the teacher-forced decoder; returns (D [T', B, dec], DecoderSaved)."""
     dev = m1.device
     B, N, _ = m1.shape
     r, nf = d.r, hp.n_feed_frame
@@ -111,6 +112,11 @@ def decoder_forward(P: Dict[str, torch.Tensor], hp, d: Dims, m1: torch.Tensor, m
         raise NotImplementedError("attention2 must be 'additive' (hparams.py:98)")
     a1 = "decoder/attention1"
     Wr0 = W0[p_w:]
+    # query layers of both mechanisms, transposed once per step so the per-decoder-step query
+    # product is a skinny row-dot ([B, A] x [D1+D2, A]^T)
+    QT = torch.empty(D1 + D2, A, **f32)
+    K.transpose(P[f"{a1}/query_layer/kernel"], QT[:D1])
+    K.transpose(P["decoder/attention2/query_layer/kernel"], QT[D1:])
     zc0, zh0 = mk("dec/lstm0/zc"), mk("dec/lstm0/zh")
     for t in range(Tp):
         K.lstm_step_fwd(B=B, U=A, K=R0, t=t, xproj=X0[t], rin=REC0[t], W=Wr0,
@@ -119,8 +125,7 @@ def decoder_forward(P: Dict[str, torch.Tensor], hp, d: Dims, m1: torch.Tensor, m
                         mask_h=None if zh0 is None else zh0[t], zc=zc, zh=zh,
                         h_raw=H0RAW[t], c_out=C0[t + 1], h_out=REC0[t + 1, :, M1 + M2:],
                         gates=G0[t])
-        K.attn_query(H0RAW[t], P[f"{a1}/query_layer/kernel"],
-                     P["decoder/attention2/query_layer/kernel"], Q[t])
+        K.rowdot(H0RAW[t], QT, Q[t])
         K.attn_step_fwd(
             B=B, N=N, D1=D1, M1=M1, D2=D2, M2=M2, F=d.loc_f, KW=d.loc_k, NT=attn_tile,
             ntiles=ntiles, att1_forward=att1_fwd, u=0.5, q=Q[t], q_sb=D1 + D2,

@@ -20,7 +20,7 @@ from .model import BNState, model_forward
 
 class Tacotron:
     def __init__(self, hp, device, seed: int = 1234,
-                 init_values: Optional[Dict[str, np.ndarray]] = None, attn_tile: int = 16):
+                 init_values: Optional[Dict[str, np.ndarray]] = None, attn_tile: int = 32):
         self.hp = hp
         self.d = PR.resolve_dims(hp)
         self.device = torch.device(device)

@@ -377,3 +377,11 @@ def loss_fwd_bwd(mel, tgt, tmask, stop, done, dmask, out, dmel=None, dstop=None,
     Tp = stop.shape[1]
     _lib.call("sat_loss_fwd_bwd", _p(mel), _p(tgt), _p(tmask), _p(stop), _p(done), _p(dmask),
               B, T, M, Tp, l1_weight, _p(out), _p(dmel), _p(dstop), _stream())
+
+
+def transpose(x: torch.Tensor, out: torch.Tensor = None) -> torch.Tensor:
+    R, C = x.shape
+    if out is None:
+        out = torch.empty(C, R, device=x.device)
+    _lib.call("sat_transpose", _p(x), x.stride(0), _p(out), out.stride(0), R, C, _stream())
+    return out

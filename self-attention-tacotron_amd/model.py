@@ -218,7 +218,7 @@ class Saved(dict):
 
 def model_forward(P, bn: BNState, hp, d: PR.Dims, batch: Dict[str, torch.Tensor],
                   masks: Optional[Dict[str, torch.Tensor]], training: bool, ws: K.Workspace,
-                  compute_grad_seeds: bool = True, attn_tile: int = 16):
+                  compute_grad_seeds: bool = True, attn_tile: int = 32):
     """model_fn forward + loss.  Returns (outputs dict, Saved)."""
     sv = Saved()
     ids, lengths = batch["source"], batch["source_length"]

@@ -50,6 +50,8 @@ def parse():
     ap.add_argument("--cpu-baseline-batch", type=int, default=2)
     ap.add_argument("--cpu-baseline-steps", type=int, default=4)
     ap.add_argument("--attn-tile", type=int, default=32)
+    ap.add_argument("--pipeline-chunk", type=int, default=25,
+                    help="decoder steps per chunk of the multi-stream recurrence pipeline (0 = off)")
     return ap.parse_args()
 
 
@@ -170,12 +172,12 @@ def main():
     dist = world > 1
     if dist:
         torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
-    from sat_amd import data, engine, hparams, train
+    from sat_amd import data, dp, engine, hparams, train
     hp = hparams.ljspeech_hparams()
     B, N, T = args.batch, args.chars, args.frames
-    model = engine.Tacotron(hp, "cuda", seed=1234, attn_tile=args.attn_tile)
-    if dist:   # identical initial weights on every replica
-        torch.distributed.broadcast(model.params, 0)
+    model = engine.Tacotron(hp, "cuda", seed=1234, attn_tile=args.attn_tile,
+                            pipeline_chunk=args.pipeline_chunk)
+    dp.broadcast_params(model.params)   # identical initial weights on every replica
     b = data.synthetic_batch(hp, B, N=N, T=T, shape="max", seed=1000 + rank * 1_000_000)
     batch = {k: torch.tensor(v).cuda() for k, v in b.items()}
     trainer = train.Trainer(model, B, N, T // hp.outputs_per_step, seed=1234 + rank)
@@ -201,10 +203,7 @@ def main():
     if dist:
         torch.distributed.barrier()
     dt = time.perf_counter() - t0
-    if dist:
-        tt = torch.tensor([dt], device="cuda", dtype=torch.float64)
-        torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
-        dt = float(tt.item())
+    dt = dp.max_over_ranks(dt, "cuda")
     loss1 = float(trainer.last_loss.item())
     frames = world * B * T * args.steps
     value = frames / dt

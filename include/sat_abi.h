@@ -302,6 +302,7 @@ int sat_loss_fwd_bwd(const float* mel, const float* tgt, const float* tmask, con
 typedef struct SatAdamConfig {
   float lr0, beta1, beta2, eps, clip_norm;   /* clip_norm <= 0 disables clipping */
   int32_t decay, step_factor;
+  float grad_scale;   /* grads are used as grad_scale * g (1/world after a SUM all-reduce) */
 } SatAdamConfig;
 
 int64_t sat_workspace_adam(void);

@@ -67,7 +67,7 @@ SatLstmBwd = _struct("SatLstmBwd", """
     ptr:dgates ptr:dh_carry_out ptr:dc_carry_out""")
 
 SatAdamConfig = _struct("SatAdamConfig", """
-    f32:lr0 f32:beta1 f32:beta2 f32:eps f32:clip_norm i32:decay i32:step_factor""")
+    f32:lr0 f32:beta1 f32:beta2 f32:eps f32:clip_norm i32:decay i32:step_factor f32:grad_scale""")
 
 SatAttnStepBwd = _struct("SatAttnStepBwd", """
     i32:B i32:N i32:D1 i32:M1 i32:D2 i32:M2 i32:F i32:KW i32:NT i32:ntiles i32:att1_forward
@@ -149,8 +149,34 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     return lib
 
 
-def exported_symbols():
-    return list(SIGNATURES) + list(RESTYPES) + ["sat_last_error_string"]
+HEADER_PATH = os.path.join(os.path.dirname(PKG_DIR), "include", "sat_abi.h")
+
+
+def bound_symbols():
+    """Entry points this binding declares argtypes for."""
+    return set(SIGNATURES) | set(RESTYPES) | {"sat_last_error_string"}
+
+
+def header_symbols(path: str = HEADER_PATH):
+    """Function names declared in include/sat_abi.h (comments stripped)."""
+    import re
+    text = open(path).read()
+    text = re.sub(r"/\*.*?\*/", " ", text, flags=re.S)
+    text = re.sub(r"//[^\n]*", " ", text)
+    return set(re.findall(r"\b(sat_\w+)\s*\(", text))
+
+
+def exported_symbols(path: str = LIB_PATH):
+    """Header symbols the shared library actually exports (dlsym; no device call is made)."""
+    lib = ctypes.CDLL(path)
+    out = set()
+    for name in header_symbols():
+        try:
+            getattr(lib, name)
+            out.add(name)
+        except AttributeError:
+            pass
+    return out
 
 
 def check(rc: int, what: str) -> None:

@@ -17,6 +17,7 @@ import torch
 
 from . import kernels as K
 from .model import _contig_span
+from .pipeline import SEQUENTIAL, Pipeline
 
 
 def lin_bwd(x, dy, W, dW, db, ws, dx=None, beta_dx=0.0, need_dx=True):
@@ -92,67 +93,87 @@ def head_bwd(P, G, hp, d, sv, ws):
     return dz.transpose(0, 1).contiguous()                           # [T', B, D] (data movement)
 
 
+class _LstmBwd:
+    """Reverse recurrence of one LSTM layer, resumable across chunks of steps (the dh/dc carries
+    ping-pong between two buffers)."""
+
+    def __init__(self, B, U, dev):
+        self.hc = [torch.zeros(B, U, device=dev), torch.zeros(B, U, device=dev)]
+        self.cc = [torch.zeros(B, U, device=dev), torch.zeros(B, U, device=dev)]
+        self.first = True
+        self.cur = 0
+
+    def step(self, **kw):
+        c = self.cur
+        K.lstm_step_bwd(dh_carry=None if self.first else self.hc[c],
+                        dc_carry=None if self.first else self.cc[c],
+                        dh_carry_out=self.hc[1 - c], dc_carry_out=self.cc[1 - c], **kw)
+        self.first = False
+        self.cur = 1 - c
+
+
 def _lstm_loop_bwd(*, B, U, Kr, hoff, Tp, Wr, G_, CS, dY, mc, mh, zc, zh, order, nxt_of,
                    cprev_of, lengths=None, extra=None):
     """Reverse recurrence of one LSTM layer; returns DG (same layout as the forward gates)."""
-    dev = G_.device
     DG = torch.empty_like(G_)
-    hc = [torch.zeros(B, U, device=dev), torch.zeros(B, U, device=dev)]
-    cc = [torch.zeros(B, U, device=dev), torch.zeros(B, U, device=dev)]
-    first = True
-    cur = 0
+    run = _LstmBwd(B, U, G_.device)
     for t in order:
         nt = nxt_of(t)
         kw = dict(extra(t)) if extra is not None else {}
-        K.lstm_step_bwd(B=B, U=U, K=Kr, hoff=hoff, t=t, W=Wr,
-                        dgates_next=None if nt is None else DG[nt], gates=G_[t],
-                        c_prev=cprev_of(t), dy=None if dY is None else dY(t),
-                        dh_carry=None if first else hc[cur], dc_carry=None if first else cc[cur],
-                        mask_c=None if mc is None else mc[t], mask_h=None if mh is None else mh[t],
-                        zc=zc, zh=zh, dgates=DG[t], dh_carry_out=hc[1 - cur],
-                        dc_carry_out=cc[1 - cur], lengths=lengths, **kw)
-        first = False
-        cur = 1 - cur
+        run.step(B=B, U=U, K=Kr, hoff=hoff, t=t, W=Wr,
+                 dgates_next=None if nt is None else DG[nt], gates=G_[t], c_prev=cprev_of(t),
+                 dy=None if dY is None else dY(t), mask_c=None if mc is None else mc[t],
+                 mask_h=None if mh is None else mh[t], zc=zc, zh=zh, dgates=DG[t],
+                 lengths=lengths, **kw)
     return DG
 
 
-def decoder_bwd(P, G, hp, d, dsv, dH2, masks, ws, attn_tile=32):
-    """Backward of decoder.decoder_forward.  Returns (dm1, dm2) batch-major."""
+def decoder_bwd(P, G, hp, d, dsv, dH2, masks, ws, attn_tile=32, pipe: Pipeline = SEQUENTIAL):
+    """Backward of decoder.decoder_forward.  Returns (dm1, dm2) batch-major.
+
+    The three reverse recurrences (LSTM2 -> LSTM1 -> attention RNN) are software-pipelined over
+    chunks of steps like the forward: LSTM2 runs on lane 2, LSTM1 on lane 1 (each followed by the
+    chunk's input-gradient GEMM), the attention chain on the current stream; the LSTMs' weight
+    gradients then overlap the tail of the attention chain."""
     S = dsv.tensors
     B, N, Tp = dsv.B, dsv.N, dsv.Tp
     dev = dH2.device
     A, Dd, M1, M2, D1, D2 = d.att_rnn, d.dec, d.m1, d.m2, d.d1, d.d2
     zc, zh = hp.zoneout_factor_cell, hp.zoneout_factor_output
     mk = (lambda n: masks[n]) if masks is not None else (lambda n: None)
-    rev = list(range(Tp - 1, -1, -1))
-    nxt = lambda t: t + 1 if t + 1 < Tp else None
-
-    # ---- LSTM 2
-    W2 = P["decoder/lstm2/kernel"]
-    dW2 = G["decoder/lstm2/kernel"]
-    DG2 = _lstm_loop_bwd(B=B, U=Dd, Kr=Dd, hoff=0, Tp=Tp, Wr=W2[Dd:], G_=S["G2"], CS=S["C2S"],
-                         dY=lambda t: dH2[t], mc=mk("dec/lstm2/zc"), mh=mk("dec/lstm2/zh"),
-                         zc=zc, zh=zh, order=rev, nxt_of=nxt, cprev_of=lambda t: S["C2S"][t])
-    DG2f = DG2.view(Tp * B, 4 * Dd)
-    K.gemm(S["H2S"][:Tp].reshape(Tp * B, Dd).t(), DG2f, dW2[Dd:], beta=1.0)
-    dH1 = lin_bwd(S["H1RAW"], DG2, W2[:Dd], dW2[:Dd], G["decoder/lstm2/bias"], ws)
-
-    # ---- LSTM 1
-    W1 = P["decoder/lstm1/kernel"]
-    dW1 = G["decoder/lstm1/kernel"]
+    f32 = dict(device=dev, dtype=torch.float32)
     R0 = M1 + M2 + A
-    DG1 = _lstm_loop_bwd(B=B, U=Dd, Kr=Dd, hoff=0, Tp=Tp, Wr=W1[A + M1 + M2:], G_=S["G1"],
-                         CS=S["C1S"], dY=lambda t: dH1[t], mc=mk("dec/lstm1/zc"),
-                         mh=mk("dec/lstm1/zh"), zc=zc, zh=zh, order=rev, nxt_of=nxt,
-                         cprev_of=lambda t: S["C1S"][t])
-    DG1f = DG1.view(Tp * B, 4 * Dd)
-    K.gemm(S["H1S"][:Tp].reshape(Tp * B, Dd).t(), DG1f, dW1[A + M1 + M2:], beta=1.0)
-    K.colsum(DG1f, G["decoder/lstm1/bias"], ws)
-    ctx_all = S["REC0"][1:].reshape(Tp * B, R0)[:, :M1 + M2]
-    K.gemm(S["H0RAW"].view(Tp * B, A).t(), DG1f, dW1[:A], beta=1.0)
-    K.gemm(ctx_all.t(), DG1f, dW1[A:A + M1 + M2], beta=1.0)
-    dH0 = K.gemm(DG1f, W1[:A].t()).view(Tp, B, A)
-    DCTX = K.gemm(DG1f, W1[A:A + M1 + M2].t()).view(Tp, B, M1 + M2)
+
+    W2, dW2 = P["decoder/lstm2/kernel"], G["decoder/lstm2/kernel"]
+    W1, dW1 = P["decoder/lstm1/kernel"], G["decoder/lstm1/kernel"]
+    DG2 = torch.empty_like(S["G2"])
+    DG1 = torch.empty_like(S["G1"])
+    dH1 = torch.empty(Tp, B, Dd, **f32)
+    dH0 = torch.empty(Tp, B, A, **f32)
+    DCTX = torch.empty(Tp, B, M1 + M2, **f32)
+    run2, run1 = _LstmBwd(B, Dd, dev), _LstmBwd(B, Dd, dev)
+    m2c, m2h, m1c, m1h = (mk("dec/lstm2/zc"), mk("dec/lstm2/zh"), mk("dec/lstm1/zc"),
+                          mk("dec/lstm1/zh"))
+
+    def lstm2_chunk(a, b):
+        for t in range(b - 1, a - 1, -1):
+            run2.step(B=B, U=Dd, K=Dd, hoff=0, t=t, W=W2[Dd:],
+                      dgates_next=DG2[t + 1] if t + 1 < Tp else None, gates=S["G2"][t],
+                      c_prev=S["C2S"][t], dy=dH2[t], mask_c=None if m2c is None else m2c[t],
+                      mask_h=None if m2h is None else m2h[t], zc=zc, zh=zh, dgates=DG2[t])
+        n = (b - a) * B
+        K.gemm(DG2[a:b].view(n, 4 * Dd), W2[:Dd].t(), dH1[a:b].view(n, Dd))
+
+    def lstm1_chunk(a, b):
+        for t in range(b - 1, a - 1, -1):
+            run1.step(B=B, U=Dd, K=Dd, hoff=0, t=t, W=W1[A + M1 + M2:],
+                      dgates_next=DG1[t + 1] if t + 1 < Tp else None, gates=S["G1"][t],
+                      c_prev=S["C1S"][t], dy=dH1[t], mask_c=None if m1c is None else m1c[t],
+                      mask_h=None if m1h is None else m1h[t], zc=zc, zh=zh, dgates=DG1[t])
+        n = (b - a) * B
+        dg = DG1[a:b].view(n, 4 * Dd)
+        K.gemm(dg, W1[:A].t(), dH0[a:b].view(n, A))
+        K.gemm(dg, W1[A:A + M1 + M2].t(), DCTX[a:b].view(n, M1 + M2))
 
     # ---- attention RNN + dual-source attention recurrence
     W0 = P["decoder/attention_lstm/kernel"]
@@ -163,51 +184,76 @@ def decoder_bwd(P, G, hp, d, dsv, dH2, masks, ws, attn_tile=32):
     fwd = d.att1 == "forward"
     ntiles = (N + attn_tile - 1) // attn_tile
     pgs = K.pg_stride(D1, D2, d.loc_f, d.loc_k)
-    f32 = dict(device=dev, dtype=torch.float32)
     DG0 = torch.empty(Tp, B, 4 * A, **f32)
     DA = torch.empty(B, N, **f32)
     DS2 = torch.empty(B, N, **f32)
     DSN = torch.empty(B, N, **f32)
     DAP = [torch.zeros(B, N, **f32), torch.zeros(B, N, **f32)]
     DF = [torch.zeros(B, N, max(d.loc_f, 1), **f32), torch.zeros(B, N, max(d.loc_f, 1), **f32)]
-    DQP = torch.empty(Tp, B, ntiles, D1 + D2, **f32)
+    DQP = torch.empty(Tp, B, ntiles, D1 + D2, **f32)   # per-step, per-tile query gradients
     dK1 = torch.zeros(B, N, D1, **f32)
     dK2 = torch.zeros(B, N, D2, **f32)
     PG = torch.zeros(B * ntiles, pgs, **f32)
     hc = [torch.zeros(B, A, **f32), torch.zeros(B, A, **f32)]
     cc = [torch.zeros(B, A, **f32), torch.zeros(B, A, **f32)]
     mc0, mh0 = mk("dec/lstm0/zc"), mk("dec/lstm0/zh")
-    cur = 0
-    for i, t in enumerate(rev):
-        last = i == 0
-        if not last:   # gradient of c_t through the attention RNN's input at step t+1
-            K.rowdot(DG0[t + 1], W0r[:M1 + M2], DCTX[t], beta=1.0)
-        K.attn_step_bwd(
-            B=B, N=N, D1=D1, M1=M1, D2=D2, M2=M2, F=d.loc_f, KW=d.loc_k, NT=attn_tile,
-            ntiles=ntiles, att1_forward=1 if fwd else 0, u=0.5, dctx=DCTX[t],
-            dctx_sb=M1 + M2, dalpha_next=None if last else DAP[cur], V1=S["V1"], V2=S["V2"],
-            DA=DA, DS2=DS2, DSN=DSN, s_t=S["S1"][t + 1], a_t=S["AL1"][t + 1], a_prev=S["AL1"][t],
-            s_prev=S["S1"][t], s2_t=S["S2"][t], stats=S["ST"][t],
-            df_next=None if last else DF[cur], lengths=None, q=S["Q"][t], q_sb=D1 + D2,
-            K1=S["K1"], K2=S["K2"],
-            v1=P[f"{a1}/attention_variable"] if fwd else P[f"{a1}/attention_v"],
-            b1=P[f"{a1}/attention_bias"] if fwd else None,
-            convW=P[f"{a1}/location_conv/kernel"] if fwd else None,
-            convb=P[f"{a1}/location_conv/bias"] if fwd else None,
-            locW=P[f"{a1}/location_layer/kernel"] if fwd else None,
-            v2=P[f"{a2}/attention_v"], dalpha_prev=DAP[1 - cur], df_out=DF[1 - cur],
-            dK1=dK1, dK2=dK2, dqp=DQP[t], pg=PG, pg_stride=pgs)
-        K.lstm_step_bwd(B=B, U=A, K=R0, hoff=M1 + M2, t=t, W=W0r,
-                        dgates_next=None if last else DG0[t + 1], gates=S["G0"][t],
-                        c_prev=S["C0"][t], dy=dH0[t], dh_carry=None if last else hc[cur],
-                        dc_carry=None if last else cc[cur],
-                        mask_c=None if mc0 is None else mc0[t],
-                        mask_h=None if mh0 is None else mh0[t], zc=zc, zh=zh, dgates=DG0[t],
-                        dh_carry_out=hc[1 - cur], dc_carry_out=cc[1 - cur],
-                        dq0=DQP[t][:, :, :D1], wq0=P[f"{a1}/query_layer/kernel"],
-                        dq1=DQP[t][:, :, D1:], wq1=P[f"{a2}/query_layer/kernel"],
-                        dq_parts=ntiles, dq_pstride=D1 + D2, dq_bstride=ntiles * (D1 + D2))
-        cur = 1 - cur
+    chain = {"cur": 0}
+
+    def attention_chunk(a, b):
+        for t in range(b - 1, a - 1, -1):
+            cur = chain["cur"]
+            last = t == Tp - 1
+            if not last:   # gradient of c_t through the attention RNN's input at step t+1
+                K.rowdot(DG0[t + 1], W0r[:M1 + M2], DCTX[t], beta=1.0)
+            K.attn_step_bwd(
+                B=B, N=N, D1=D1, M1=M1, D2=D2, M2=M2, F=d.loc_f, KW=d.loc_k, NT=attn_tile,
+                ntiles=ntiles, att1_forward=1 if fwd else 0, u=0.5, dctx=DCTX[t],
+                dctx_sb=M1 + M2, dalpha_next=None if last else DAP[cur], V1=S["V1"], V2=S["V2"],
+                DA=DA, DS2=DS2, DSN=DSN, s_t=S["S1"][t + 1], a_t=S["AL1"][t + 1],
+                a_prev=S["AL1"][t], s_prev=S["S1"][t], s2_t=S["S2"][t], stats=S["ST"][t],
+                df_next=None if last else DF[cur], lengths=None, q=S["Q"][t], q_sb=D1 + D2,
+                K1=S["K1"], K2=S["K2"],
+                v1=P[f"{a1}/attention_variable"] if fwd else P[f"{a1}/attention_v"],
+                b1=P[f"{a1}/attention_bias"] if fwd else None,
+                convW=P[f"{a1}/location_conv/kernel"] if fwd else None,
+                convb=P[f"{a1}/location_conv/bias"] if fwd else None,
+                locW=P[f"{a1}/location_layer/kernel"] if fwd else None,
+                v2=P[f"{a2}/attention_v"], dalpha_prev=DAP[1 - cur], df_out=DF[1 - cur],
+                dK1=dK1, dK2=dK2, dqp=DQP[t], pg=PG, pg_stride=pgs)
+            K.lstm_step_bwd(B=B, U=A, K=R0, hoff=M1 + M2, t=t, W=W0r,
+                            dgates_next=None if last else DG0[t + 1], gates=S["G0"][t],
+                            c_prev=S["C0"][t], dy=dH0[t], dh_carry=None if last else hc[cur],
+                            dc_carry=None if last else cc[cur],
+                            mask_c=None if mc0 is None else mc0[t],
+                            mask_h=None if mh0 is None else mh0[t], zc=zc, zh=zh, dgates=DG0[t],
+                            dh_carry_out=hc[1 - cur], dc_carry_out=cc[1 - cur],
+                            dq0=DQP[t][:, :, :D1], wq0=P[f"{a1}/query_layer/kernel"],
+                            dq1=DQP[t][:, :, D1:], wq1=P[f"{a2}/query_layer/kernel"],
+                            dq_parts=ntiles, dq_pstride=D1 + D2, dq_bstride=ntiles * (D1 + D2))
+            chain["cur"] = 1 - cur
+
+    pipe.fork()
+    for a, b in reversed(pipe.chunks(Tp)):
+        with pipe.lane(2):
+            lstm2_chunk(a, b)
+        pipe.handoff(2, 1)
+        with pipe.lane(1):
+            lstm1_chunk(a, b)
+        pipe.handoff(1, 0)
+        attention_chunk(a, b)
+    # LSTM weight gradients on their own lanes, overlapping the attention chain's tail
+    DG2f = DG2.view(Tp * B, 4 * Dd)
+    DG1f = DG1.view(Tp * B, 4 * Dd)
+    with pipe.lane(2):
+        K.gemm(S["H2S"][:Tp].reshape(Tp * B, Dd).t(), DG2f, dW2[Dd:], beta=1.0)
+        K.gemm(S["H1RAW"].view(Tp * B, Dd).t(), DG2f, dW2[:Dd], beta=1.0)
+        K.colsum(DG2f, G["decoder/lstm2/bias"], ws)
+    with pipe.lane(1):
+        K.gemm(S["H1S"][:Tp].reshape(Tp * B, Dd).t(), DG1f, dW1[A + M1 + M2:], beta=1.0)
+        K.colsum(DG1f, G["decoder/lstm1/bias"], ws)
+        ctx_all = S["REC0"][1:].reshape(Tp * B, R0)[:, :M1 + M2]
+        K.gemm(S["H0RAW"].view(Tp * B, A).t(), DG1f, dW1[:A], beta=1.0)
+        K.gemm(ctx_all.t(), DG1f, dW1[A:A + M1 + M2], beta=1.0)
 
     DG0f = DG0.view(Tp * B, 4 * A)
     K.gemm(S["REC0"][:Tp].reshape(Tp * B, R0).t(), DG0f, dW0[p_w:], beta=1.0)
@@ -238,6 +284,7 @@ def decoder_bwd(P, G, hp, d, dsv, dH2, masks, ws, attn_tile=32):
         o += D1 + 0
         o = (1 + d.loc_f) * D1 + d.loc_k * d.loc_f + d.loc_f
     K.axpby(pg_sum[o:o + D2], G[f"{a2}/attention_v"], 1.0, 1.0)
+    # the per-tile partials of every step sum into the query-layer / bias gradients
     DQf = DQP.view(Tp * B * ntiles, D1 + D2)
     if fwd:
         qsum = torch.zeros(D1 + D2, **f32)
@@ -255,6 +302,7 @@ def decoder_bwd(P, G, hp, d, dsv, dH2, masks, ws, attn_tile=32):
             ws, dx=dV1, beta_dx=1.0)
     lin_bwd(S["V2"], dK2, P[f"{a2}/memory_layer/kernel"], G[f"{a2}/memory_layer/kernel"], None,
             ws, dx=dV2, beta_dx=1.0)
+    pipe.join()
     return dV1, dV2          # caller applies the sequence mask (values were masked memories)
 
 
@@ -371,11 +419,12 @@ def encoder_bwd(P, G, hp, d, sv, dm1, dm2, lengths, masks, ws):
     K.embedding_bwd(dx, sv["batch"]["source"], G["embedding"])
 
 
-def model_backward(P, G, hp, d, sv, ws, attn_tile=32):
+def model_backward(P, G, hp, d, sv, ws, attn_tile=32, pipe: Pipeline = SEQUENTIAL):
     """Accumulate dL/dparams of model_forward's loss into G (caller zeroes G)."""
     masks = sv["masks"]
     dH2 = head_bwd(P, G, hp, d, sv, ws)
-    dV1, dV2 = decoder_bwd(P, G, hp, d, sv["dec"], dH2, masks, ws, attn_tile=attn_tile)
+    dV1, dV2 = decoder_bwd(P, G, hp, d, sv["dec"], dH2, masks, ws, attn_tile=attn_tile,
+                           pipe=pipe)
     lengths = sv["batch"]["source_length"]
     dm1 = K.seq_mask(dV1, lengths)
     dm2 = K.seq_mask(dV2, lengths)

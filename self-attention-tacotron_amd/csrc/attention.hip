@@ -39,6 +39,98 @@ struct AttnFwdP {
 // partial record: [0]=m1 [1]=Z1 [2]=A1 [3]=m2 [4]=Z2 [5..7]=pad [8..8+M1) C1 [8+M1..) C2
 constexpr int kPartHdr = 8;
 
+struct AttnCombineP {
+  int B, N, M1, M2, ntiles, att1_forward;
+  float u;
+  const float* e1; const float* e2; const float* part; int64_t part_stride;
+  const float* a_prev;
+  float* s_out; float* a_out; float* s2_out;   // [B][N]
+  float* ctx; int64_t ctx_sb;                  // [B][M1 + M2] (row stride ctx_sb)
+  float* stats;                                // [B][4]: M1, Z1, A1/Z1 (= sum g s), Z2 for the bwd
+};
+
+// Per-utterance combine: all loads issued at entry, tile headers reduced by one wave.
+// (A last-tile-block fusion into the tile kernel was measured slower: the device-scope fence it
+// needs writes back the XCD's L2, 12 -> 29 us per step.)
+__device__ __forceinline__ void combine_utterance(const AttnCombineP& p, int b) {
+  __shared__ float sc1[64], sc2[64];
+  __shared__ float hdr[6];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t rb = (int64_t)b * p.N;
+  const float* part = p.part + (int64_t)b * p.ntiles * p.part_stride;
+  const int W = p.M1 + p.M2;
+  constexpr int kMaxPos = 4;
+  float ev[kMaxPos], e2v[kMaxPos], apv[kMaxPos], amv[kMaxPos];
+#pragma unroll
+  for (int i = 0; i < kMaxPos; ++i) {
+    const int n = tid + 256 * i;
+    const bool ok = n < p.N;
+    ev[i] = ok ? p.e1[rb + n] : -INFINITY;
+    e2v[i] = ok ? p.e2[rb + n] : -INFINITY;
+    apv[i] = (ok && p.att1_forward) ? p.a_prev[rb + n] : 0.f;
+    amv[i] = (ok && p.att1_forward && n > 0) ? p.a_prev[rb + n - 1] : 0.f;
+  }
+  float cpart[2][16];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int d = tid + 256 * h;
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      cpart[h][j] = (d < W && j < p.ntiles) ? part[j * p.part_stride + kPartHdr + d] : 0.f;
+  }
+  if (wave == 0) {
+    float hm1 = -INFINITY, hz1 = 0.f, ha1 = 0.f, hm2 = -INFINITY, hz2 = 0.f;
+    if (lane < p.ntiles) {
+      const float* r = part + lane * p.part_stride;
+      hm1 = r[0]; hz1 = r[1]; ha1 = r[2]; hm2 = r[3]; hz2 = r[4];
+    }
+    const float M1 = wave_max(hm1), M2 = wave_max(hm2);
+    const float s1 = (hm1 == -INFINITY) ? 0.f : expf(hm1 - M1);
+    const float s2 = (hm2 == -INFINITY) ? 0.f : expf(hm2 - M2);
+    if (lane < p.ntiles) { sc1[lane] = s1; sc2[lane] = s2; }
+    const float Z1 = wave_sum(hz1 * s1), A1 = wave_sum(ha1 * s1), Z2 = wave_sum(hz2 * s2);
+    if (lane == 0) {
+      hdr[0] = M1; hdr[1] = Z1; hdr[2] = A1; hdr[3] = Z2; hdr[4] = M2;
+      if (p.stats) {  // sum_n g[n] s[n] = A1 / Z1 (the forward-attention normaliser) for the bwd
+        p.stats[b * 4 + 0] = M1; p.stats[b * 4 + 1] = Z1; p.stats[b * 4 + 2] = A1 / Z1;
+        p.stats[b * 4 + 3] = Z2;
+      }
+    }
+  }
+  __syncthreads();
+  const float M1 = hdr[0], Z1 = hdr[1], A1 = hdr[2], Z2 = hdr[3], M2 = hdr[4];
+  const float inv1 = 1.f / (p.att1_forward ? A1 : Z1);
+  const float invz1 = 1.f / Z1, invz2 = 1.f / Z2;
+  float* ctx = p.ctx + (int64_t)b * p.ctx_sb;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int d = tid + 256 * h;
+    if (d < W) {
+      const bool first = d < p.M1;
+      float acc = 0.f;
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+        if (j < p.ntiles) acc = fmaf(cpart[h][j], first ? sc1[j] : sc2[j], acc);
+      ctx[d] = acc * (first ? inv1 : invz2);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < kMaxPos; ++i) {
+    const int n = tid + 256 * i;
+    if (n >= p.N) break;
+    const float pe = (ev[i] == -INFINITY) ? 0.f : expf(ev[i] - M1);
+    const float pe2 = (e2v[i] == -INFINITY) ? 0.f : expf(e2v[i] - M2);
+    const float s = pe * invz1;
+    p.s_out[rb + n] = s;
+    p.s2_out[rb + n] = pe2 * invz2;
+    p.a_out[rb + n] = p.att1_forward ? ((1.f - p.u) * apv[i] + p.u * amv[i] + 1e-7f) * pe * inv1 : s;
+  }
+}
+
+__global__ void __launch_bounds__(256) attn_combine_kernel(AttnCombineP p) {
+  combine_utterance(p, blockIdx.x);
+}
+
 // Tile kernel (NT = 32 memory positions per workgroup, 256 threads = 32 positions x 8 lanes).
 // Each lane owns 4*DW4 consecutive energy dims of one position: its K1 slice arrives as DW4
 // 16-byte loads issued at entry (indices clamped so no load sits behind a branch), the energy
@@ -234,93 +326,6 @@ __global__ void __launch_bounds__(256) attn_energy_kernel(AttnFwdP p) {
       s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
     }
     reinterpret_cast<float4*>(part_out + kPartHdr + p.M1)[j] = s;
-  }
-}
-
-struct AttnCombineP {
-  int B, N, M1, M2, ntiles, att1_forward;
-  float u;
-  const float* e1; const float* e2; const float* part; int64_t part_stride;
-  const float* a_prev;
-  float* s_out; float* a_out; float* s2_out;   // [B][N]
-  float* ctx; int64_t ctx_sb;                  // [B][M1 + M2] (row stride ctx_sb)
-  float* stats;                                // [B][4]: M1, Z1, A1/Z1 (= sum g s), Z2 for the bwd
-};
-
-// Per-utterance combine: all loads issued at entry, tile headers reduced by one wave.
-__global__ void __launch_bounds__(256) attn_combine_kernel(AttnCombineP p) {
-  __shared__ float sc1[64], sc2[64];
-  __shared__ float hdr[6];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int b = blockIdx.x;
-  const int64_t rb = (int64_t)b * p.N;
-  const float* part = p.part + (int64_t)b * p.ntiles * p.part_stride;
-  const int W = p.M1 + p.M2;
-  constexpr int kMaxPos = 4;
-  float ev[kMaxPos], e2v[kMaxPos], apv[kMaxPos], amv[kMaxPos];
-#pragma unroll
-  for (int i = 0; i < kMaxPos; ++i) {
-    const int n = tid + 256 * i;
-    const bool ok = n < p.N;
-    ev[i] = ok ? p.e1[rb + n] : -INFINITY;
-    e2v[i] = ok ? p.e2[rb + n] : -INFINITY;
-    apv[i] = (ok && p.att1_forward) ? p.a_prev[rb + n] : 0.f;
-    amv[i] = (ok && p.att1_forward && n > 0) ? p.a_prev[rb + n - 1] : 0.f;
-  }
-  float cpart[2][16];
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int d = tid + 256 * h;
-#pragma unroll
-    for (int j = 0; j < 16; ++j)
-      cpart[h][j] = (d < W && j < p.ntiles) ? part[j * p.part_stride + kPartHdr + d] : 0.f;
-  }
-  if (wave == 0) {
-    float hm1 = -INFINITY, hz1 = 0.f, ha1 = 0.f, hm2 = -INFINITY, hz2 = 0.f;
-    if (lane < p.ntiles) {
-      const float* r = part + lane * p.part_stride;
-      hm1 = r[0]; hz1 = r[1]; ha1 = r[2]; hm2 = r[3]; hz2 = r[4];
-    }
-    const float M1 = wave_max(hm1), M2 = wave_max(hm2);
-    const float s1 = (hm1 == -INFINITY) ? 0.f : expf(hm1 - M1);
-    const float s2 = (hm2 == -INFINITY) ? 0.f : expf(hm2 - M2);
-    if (lane < p.ntiles) { sc1[lane] = s1; sc2[lane] = s2; }
-    const float Z1 = wave_sum(hz1 * s1), A1 = wave_sum(ha1 * s1), Z2 = wave_sum(hz2 * s2);
-    if (lane == 0) {
-      hdr[0] = M1; hdr[1] = Z1; hdr[2] = A1; hdr[3] = Z2; hdr[4] = M2;
-      if (p.stats) {  // sum_n g[n] s[n] = A1 / Z1 (the forward-attention normaliser) for the bwd
-        p.stats[b * 4 + 0] = M1; p.stats[b * 4 + 1] = Z1; p.stats[b * 4 + 2] = A1 / Z1;
-        p.stats[b * 4 + 3] = Z2;
-      }
-    }
-  }
-  __syncthreads();
-  const float M1 = hdr[0], Z1 = hdr[1], A1 = hdr[2], Z2 = hdr[3], M2 = hdr[4];
-  const float inv1 = 1.f / (p.att1_forward ? A1 : Z1);
-  const float invz1 = 1.f / Z1, invz2 = 1.f / Z2;
-  float* ctx = p.ctx + (int64_t)b * p.ctx_sb;
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int d = tid + 256 * h;
-    if (d < W) {
-      const bool first = d < p.M1;
-      float acc = 0.f;
-#pragma unroll
-      for (int j = 0; j < 16; ++j)
-        if (j < p.ntiles) acc = fmaf(cpart[h][j], first ? sc1[j] : sc2[j], acc);
-      ctx[d] = acc * (first ? inv1 : invz2);
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < kMaxPos; ++i) {
-    const int n = tid + 256 * i;
-    if (n >= p.N) break;
-    const float pe = (ev[i] == -INFINITY) ? 0.f : expf(ev[i] - M1);
-    const float pe2 = (e2v[i] == -INFINITY) ? 0.f : expf(e2v[i] - M2);
-    const float s = pe * invz1;
-    p.s_out[rb + n] = s;
-    p.s2_out[rb + n] = pe2 * invz2;
-    p.a_out[rb + n] = p.att1_forward ? ((1.f - p.u) * apv[i] + p.u * amv[i] + 1e-7f) * pe * inv1 : s;
   }
 }
 
@@ -865,6 +870,7 @@ extern "C" int sat_attn_step_bwd(const SatAttnStepBwd* a, void* stream) {
   p.K1 = a->K1; p.K2 = a->K2; p.v1 = a->v1; p.b1 = a->b1; p.convW = a->convW; p.convb = a->convb;
   p.locW = a->locW; p.v2 = a->v2; p.dalpha_prev = a->dalpha_prev; p.df_out = a->df_out;
   p.dK1 = a->dK1; p.dK2 = a->dK2; p.dqp = a->dqp; p.pg = a->pg; p.pg_stride = a->pg_stride;
+
   hipStream_t s = as_stream(stream);
   const int blocks = a->B * a->ntiles;
   const int F = a->att1_forward ? a->F : 0;

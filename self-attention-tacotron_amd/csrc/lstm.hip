@@ -146,20 +146,22 @@ struct LstmBwdP {
 };
 
 // dL/dh_t = dh_carry + sum_g dgates_{t+1}[b, g] * W[hoff + u, g]  (the recurrent product)
-// The optional query-gradient term sum_d dq[b, d] wq[u, d] reads dq as `dq_parts` per-tile
-// partials: the workgroup first sums them for its 8 batch rows into LDS (all 256 threads, loads
-// independent), then every (b, u) group dots the LDS row with wq's row.  dgates_{t+1} rows and
-// the 4 W rows are staged global -> LDS in one burst of 16-byte loads.
+// plus, for the attention RNN, the query-gradient term sum_d dq[b, d] wq[u, d] where dq is the
+// sum of `dq_parts` per-tile partials.  Both are ONE dot product of length 4U + DQ:
+//   row b:  [dgates_{t+1}[b] (4U) | dq[b] (DQ)]         (partials summed while staging)
+//   row u:  [W[hoff + u] (4U) | wq0[u] (D0) | wq1[u] (D1)]
+// staged global -> LDS in one burst of 16-byte loads (all independent), then 8 k-slices per
+// (b, u) and 3 xor-shuffles.
 constexpr int kMaxDq = 320;
 
 __global__ void __launch_bounds__(256) lstm_bwd_kernel(LstmBwdP p) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int G = 4 * p.U;
   const int D0 = p.dq0 ? p.dq0_n : 0, D1 = p.dq1 ? p.dq1_n : 0, DQ = D0 + D1;
-  float* dgs = smem;                                   // [BT][G + 4]  dgates_{t+1} rows
-  float* wrs = dgs + (size_t)BT * (G + 4);             // [UT][G + 4]  W rows hoff+u
-  float* dqs = wrs + (size_t)UT * (G + 4);             // [BT][DQ]
-  const int ld = G + 4;
+  const int L = G + DQ;                                // dot length
+  const int ld = L + 4;
+  float* dgs = smem;                                   // [BT][ld]
+  float* wrs = dgs + (size_t)BT * ld;                  // [UT][ld]
   const int tid = threadIdx.x;
   const int ks = tid & (KS - 1), pair = tid >> 3;
   const int u0 = blockIdx.x * UT, b0 = blockIdx.y * BT;
@@ -180,56 +182,66 @@ __global__ void __launch_bounds__(256) lstm_bwd_kernel(LstmBwdP p) {
     if (p.mask_c) { mc = p.mask_c[bu]; mh = p.mask_h[bu]; }
     valid = p.lengths ? (p.t < p.lengths[b]) : true;
   }
-  const int gq = G >> 2;
-  if (p.dgates_next) {
-    for (int i = tid; i < BT * gq; i += 256) {
-      const int r = i / gq, c = i - r * gq;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (b0 + r < p.B) v = reinterpret_cast<const float4*>(p.dgates_next + (int64_t)(b0 + r) * G)[c];
-      *reinterpret_cast<float4*>(dgs + r * ld + 4 * c) = v;
-    }
-    for (int i = tid; i < UT * gq; i += 256) {
-      const int r = i / gq, c = i - r * gq;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (u0 + r < p.U) v = reinterpret_cast<const float4*>(p.W + (int64_t)(p.hoff + u0 + r) * G)[c];
-      *reinterpret_cast<float4*>(wrs + r * ld + 4 * c) = v;
-    }
-  }
-  for (int i = tid; i < BT * DQ; i += 256) {   // sum the per-tile query-gradient partials
-    const int r = i / DQ, d = i - r * DQ;
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  const int gq = G >> 2, lq = L >> 2, q0 = D0 >> 2;
+  // batch rows: dgates_{t+1} then the summed query gradient
+  for (int i = tid; i < BT * lq; i += 256) {
+    const int r = i / lq, c = i - r * lq;
     const int bb = b0 + r;
-    float g = 0.f;
+    float4 v = z4;
     if (bb < p.B) {
-      const float* src = d < D0 ? p.dq0 + d : p.dq1 + (d - D0);
-      for (int part = 0; part < p.dq_parts; ++part)
-        g += src[(int64_t)bb * p.dq_bstride + part * p.dq_pstride];
+      if (c < gq) {
+        if (p.dgates_next) v = reinterpret_cast<const float4*>(p.dgates_next + (int64_t)bb * G)[c];
+      } else {
+        const int dc = c - gq;
+        const float* src = dc < q0 ? p.dq0 + 4 * dc : p.dq1 + 4 * (dc - q0);
+        src += (int64_t)bb * p.dq_bstride;
+        for (int part = 0; part < p.dq_parts; ++part) {
+          const float4 w = *reinterpret_cast<const float4*>(src + (int64_t)part * p.dq_pstride);
+          v.x += w.x; v.y += w.y; v.z += w.z; v.w += w.w;
+        }
+      }
     }
-    dqs[r * DQ + d] = g;
+    *reinterpret_cast<float4*>(dgs + r * ld + 4 * c) = v;
+  }
+  // unit rows: recurrent weights then the query-layer weights of this unit
+  for (int i = tid; i < UT * lq; i += 256) {
+    const int r = i / lq, c = i - r * lq;
+    const int uu = u0 + r;
+    float4 v = z4;
+    if (uu < p.U) {
+      if (c < gq) v = reinterpret_cast<const float4*>(p.W + (int64_t)(p.hoff + uu) * G)[c];
+      else if (c - gq < q0) v = reinterpret_cast<const float4*>(p.wq0 + (int64_t)uu * D0)[c - gq];
+      else v = reinterpret_cast<const float4*>(p.wq1 + (int64_t)uu * D1)[c - gq - q0];
+    }
+    *reinterpret_cast<float4*>(wrs + r * ld + 4 * c) = v;
   }
   __syncthreads();
-  float rec = 0.f, extra = 0.f;
-  if (active && p.dgates_next) {
+  // the recurrent term belongs to dL/dh_t (the zoneout-blended state), the query term to
+  // dL/dh'_t (it enters through the raw output h'): two accumulators, G % 32 == 0 so every
+  // 32-float stride of the k-slices lies on one side of the split
+  float rec = 0.f, qterm = 0.f;
+  if (active) {
     const float* dg = dgs + bl * ld;
     const float* wr = wrs + ul * ld;
+    if (p.dgates_next) {
 #pragma unroll 4
-    for (int v = 4 * ks; v < G; v += 4 * KS) {
+      for (int v = 4 * ks; v < G; v += 4 * KS) {
+        const float4 g = *reinterpret_cast<const float4*>(dg + v);
+        const float4 w = *reinterpret_cast<const float4*>(wr + v);
+        rec += g.x * w.x + g.y * w.y + g.z * w.z + g.w * w.w;
+      }
+    }
+    for (int v = G + 4 * ks; v < L; v += 4 * KS) {
       const float4 g = *reinterpret_cast<const float4*>(dg + v);
       const float4 w = *reinterpret_cast<const float4*>(wr + v);
-      rec += g.x * w.x + g.y * w.y + g.z * w.z + g.w * w.w;
+      qterm += g.x * w.x + g.y * w.y + g.z * w.z + g.w * w.w;
     }
-  }
-  if (active && D0 > 0) {
-    const float* w0 = p.wq0 + (int64_t)u * D0;
-    for (int d = ks; d < D0; d += KS) extra = fmaf(dqs[bl * DQ + d], w0[d], extra);
-  }
-  if (active && D1 > 0) {
-    const float* w1 = p.wq1 + (int64_t)u * D1;
-    for (int d = ks; d < D1; d += KS) extra = fmaf(dqs[bl * DQ + D0 + d], w1[d], extra);
   }
 #pragma unroll
   for (int o = 1; o < KS; o <<= 1) {
     rec += __shfl_xor(rec, o, 64);
-    extra += __shfl_xor(extra, o, 64);
+    qterm += __shfl_xor(qterm, o, 64);
   }
   if (!active || ks != 0) return;
   const float dh_t = rec + dhc;
@@ -244,7 +256,7 @@ __global__ void __launch_bounds__(256) lstm_bwd_kernel(LstmBwdP p) {
   const float cn = gf * cp + gi * gj;
   const float tc = tanhf(cn);
   if (!p.mask_c) { mc = 1.f - p.zc; mh = 1.f - p.zh; }
-  const float dy = dyv + extra;
+  const float dy = dyv + qterm;
   const float dhn = dy + mh * dh_t;                 // dL/dh'
   const float dcn = mc * dc_t + dhn * go * (1.f - tc * tc);
   const float d_o = dhn * tc * go * (1.f - go);
@@ -260,6 +272,8 @@ __global__ void __launch_bounds__(256) lstm_bwd_kernel(LstmBwdP p) {
 }  // namespace sat
 
 using namespace sat;
+
+static inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 extern "C" int sat_lstm_step_fwd(const SatLstmFwd* a, void* stream) {
   SAT_CHECK_ARG(a && a->B > 0 && a->U > 0 && a->K >= 0, "sat_lstm_step_fwd: bad sizes");
@@ -290,6 +304,11 @@ extern "C" int sat_lstm_step_bwd(const SatLstmBwd* a, void* stream) {
   SAT_CHECK_ARG(a->hoff >= 0 && a->hoff + a->U <= a->K, "sat_lstm_step_bwd: hoff out of range");
   SAT_CHECK_ARG((a->dq0 ? a->dq0_n : 0) + (a->dq1 ? a->dq1_n : 0) <= kMaxDq,
                 "sat_lstm_step_bwd: query width > 320");
+  SAT_CHECK_ARG((!a->dq0 || (a->wq0 && a->dq0_n % 4 == 0 && aligned16(a->dq0) && aligned16(a->wq0))) &&
+                (!a->dq1 || (a->wq1 && a->dq1_n % 4 == 0 && aligned16(a->dq1) && aligned16(a->wq1))) &&
+                a->dq_pstride % 4 == 0 && a->dq_bstride % 4 == 0 && aligned16(a->W) &&
+                aligned16(a->dgates_next),
+                "sat_lstm_step_bwd: query-gradient operands must be 16-byte aligned, widths % 4");
   LstmBwdP p;
   p.B = a->B; p.U = a->U; p.K = a->K; p.hoff = a->hoff;
   p.W = a->W; p.dgates_next = a->dgates_next; p.gates = a->gates; p.c_prev = a->c_prev;
@@ -305,7 +324,7 @@ extern "C" int sat_lstm_step_bwd(const SatLstmBwd* a, void* stream) {
   p.dgates = a->dgates; p.dh_carry_out = a->dh_carry_out; p.dc_carry_out = a->dc_carry_out;
   dim3 grid(ceil_div(a->U, UT), ceil_div(a->B, BT));
   const int DQ = (a->dq0 ? a->dq0_n : 0) + (a->dq1 ? a->dq1_n : 0);
-  const size_t shm = ((size_t)(BT + UT) * (4 * a->U + 4) + (size_t)BT * DQ) * sizeof(float);
+  const size_t shm = (size_t)(BT + UT) * (4 * a->U + DQ + 4) * sizeof(float);
   SAT_CHECK_ARG(shm <= 160 * 1024, "sat_lstm_step_bwd: U too large for the LDS-staged step");
   hipLaunchKernelGGL(lstm_bwd_kernel, grid, dim3(256), shm, as_stream(stream), p);
   SAT_LAUNCH_CHECK("sat_lstm_step_bwd");

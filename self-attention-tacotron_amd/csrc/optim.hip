@@ -33,11 +33,11 @@ __global__ void __launch_bounds__(256) sumsq_kernel(const float* __restrict__ g,
   if (threadIdx.x == 0) part[blockIdx.x] = sh[0] + sh[1] + sh[2] + sh[3];
 }
 
-// scalars: [0] global norm, [1] clip scale, [2] lr (decayed), [3] lr_t (bias corrected)
+// scalars: [0] global norm (of grad_scale * g), [1] total scale applied to g, [2] lr (decayed), [3] lr_t (bias corrected)
 __global__ void adam_prepare_kernel(const double* __restrict__ part, int nparts,
                                     int64_t* __restrict__ global_step, float* __restrict__ scalars,
                                     double lr0, int decay, int step_factor, double b1, double b2,
-                                    double clip, int do_clip) {
+                                    double clip, int do_clip, double gscale) {
   __shared__ double sh[256];
   double acc = 0.0;
   for (int i = threadIdx.x; i < nparts; i += blockDim.x) acc += part[i];
@@ -48,8 +48,8 @@ __global__ void adam_prepare_kernel(const double* __restrict__ part, int nparts,
     __syncthreads();
   }
   if (threadIdx.x == 0) {
-    const double norm = sqrt(sh[0]);
-    const double scale = do_clip ? clip / fmax(norm, clip) : 1.0;
+    const double norm = gscale * sqrt(sh[0]);
+    const double scale = gscale * (do_clip ? clip / fmax(norm, clip) : 1.0);
     const int64_t gs = *global_step;
     double lr = lr0;
     if (decay) {
@@ -103,12 +103,14 @@ extern "C" int sat_adam_step(float* params, const float* grads, float* m, float*
                              const SatAdamConfig* cfg, void* stream) {
   SAT_CHECK_ARG(params && grads && m && v && global_step && scalars && workspace && cfg && n >= 0,
                 "sat_adam_step: bad args");
+  SAT_CHECK_ARG(cfg->grad_scale > 0.f, "sat_adam_step: grad_scale must be > 0");
   hipStream_t s = as_stream(stream);
   double* part = reinterpret_cast<double*>(workspace);
   hipLaunchKernelGGL(sumsq_kernel, dim3(kNormBlocks), dim3(256), 0, s, grads, n, part);
   hipLaunchKernelGGL(adam_prepare_kernel, dim3(1), dim3(256), 0, s, part, kNormBlocks, global_step,
                      scalars, (double)cfg->lr0, cfg->decay, cfg->step_factor, (double)cfg->beta1,
-                     (double)cfg->beta2, (double)cfg->clip_norm, cfg->clip_norm > 0.f ? 1 : 0);
+                     (double)cfg->beta2, (double)cfg->clip_norm, cfg->clip_norm > 0.f ? 1 : 0,
+                     (double)cfg->grad_scale);
   const int blocks = (int)std::min<int64_t>((n + 255) / 256, 8192);
   hipLaunchKernelGGL(adam_update_kernel, dim3(blocks), dim3(256), 0, s, params, grads, m, v, n,
                      scalars, cfg->beta1, cfg->beta2, cfg->eps);

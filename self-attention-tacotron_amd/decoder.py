@@ -9,8 +9,10 @@ MI355X restructuring (same arithmetic, different schedule):
   input projection (x @ W_x + b) are hoisted out of the recurrence into large MFMA GEMMs;
 * the recurrence of the attention RNN (ZoneoutLSTM 256 -> query -> dual-source attention) runs
   first over all steps: 3 launches per step (LSTM step, query GEMV, attention tile+combine);
-* the two decoder LSTMs depend only on the attention RNN's outputs, so they run afterwards as
-  their own recurrences with hoisted input GEMMs (1 launch per step each).
+* the two decoder LSTMs depend only on the attention RNN's outputs, so they run as their own
+  recurrences (1 launch per step each) with input GEMMs hoisted per chunk of steps, software-
+  pipelined behind the attention RNN on two side HIP streams (``pipeline.Pipeline``): chunk k of
+  LSTM1 overlaps chunk k+1 of the attention recurrence, chunk k of LSTM2 overlaps both.
 
 All state histories are kept (step-major ``[T'+1, B, .]``) for the hand-written BPTT.
 """
@@ -24,6 +26,7 @@ import torch
 
 from . import kernels as K
 from .params import Dims
+from .pipeline import SEQUENTIAL, Pipeline
 
 
 @dataclass
@@ -55,7 +58,7 @@ def teacher_inputs(targets: torch.Tensor, r: int, n_feed: int) -> torch.Tensor:
 def decoder_forward(P: Dict[str, torch.Tensor], hp, d: Dims, m1: torch.Tensor, m2: torch.Tensor,
                     lengths: torch.Tensor, targets: torch.Tensor,
                     masks: Optional[Dict[str, torch.Tensor]], attn_tile: int = 32,
-                    spk: Optional[torch.Tensor] = None):
+                    spk: Optional[torch.Tensor] = None, pipe: Pipeline = SEQUENTIAL):
     """Forward of the teacher-forced decoder; returns (D [T', B, dec], DecoderSaved)."""
     dev = m1.device
     B, N, _ = m1.shape
@@ -118,7 +121,8 @@ def decoder_forward(P: Dict[str, torch.Tensor], hp, d: Dims, m1: torch.Tensor, m
     K.transpose(P[f"{a1}/query_layer/kernel"], QT[:D1])
     K.transpose(P["decoder/attention2/query_layer/kernel"], QT[D1:])
     zc0, zh0 = mk("dec/lstm0/zc"), mk("dec/lstm0/zh")
-    for t in range(Tp):
+
+    def attention_step(t):
         K.lstm_step_fwd(B=B, U=A, K=R0, t=t, xproj=X0[t], rin=REC0[t], W=Wr0,
                         c_prev=C0[t], h_prev=REC0[t, :, M1 + M2:],
                         mask_c=None if zc0 is None else zc0[t],
@@ -138,34 +142,59 @@ def decoder_forward(P: Dict[str, torch.Tensor], hp, d: Dims, m1: torch.Tensor, m
             v2=P["decoder/attention2/attention_v"], e1=E1, e2=E2, part=PART, part_stride=pst,
             s_out=S1[t + 1], a_out=AL1[t + 1], s2_out=S2[t], ctx=REC0[t + 1], ctx_sb=R0,
             stats=ST[t])
-    S.update(X0=X0, REC0=REC0, C0=C0, H0RAW=H0RAW, G0=G0, Q=Q, S1=S1, AL1=AL1, S2=S2, ST=ST)
 
     # ---- decoder LSTM 1: input o_t = [h0'_t | c1_t | c2_t]  (ConcatOutputAndAttentionWrapper)
     W1 = P["decoder/lstm1/kernel"]                   # [A + M1 + M2 + D, 4D]
-    X1 = K.linear(H0RAW.view(Tp * B, A), W1[:A], P["decoder/lstm1/bias"])
-    ctx_all = REC0[1:].reshape(Tp * B, R0)[:, :M1 + M2]
-    K.gemm(ctx_all, W1[A:A + M1 + M2], X1, beta=1.0)
-    X1 = X1.view(Tp, B, 4 * Dd)
-    H1RAW, C1S, H1S, G1 = _run_lstm(X1, W1[A + M1 + M2:], Tp, B, Dd, zc, zh,
-                                     mk("dec/lstm1/zc"), mk("dec/lstm1/zh"), f32)
-    # ---- decoder LSTM 2: input h1'_t
-    W2 = P["decoder/lstm2/kernel"]
-    X2 = K.linear(H1RAW.view(Tp * B, Dd), W2[:Dd], P["decoder/lstm2/bias"]).view(Tp, B, 4 * Dd)
-    H2RAW, C2S, H2S, G2 = _run_lstm(X2, W2[Dd:], Tp, B, Dd, zc, zh,
-                                     mk("dec/lstm2/zc"), mk("dec/lstm2/zh"), f32)
+    W2 = P["decoder/lstm2/kernel"]                   # [D + D, 4D]
+    X1 = torch.empty(Tp, B, 4 * Dd, **f32)
+    X2 = torch.empty(Tp, B, 4 * Dd, **f32)
+    L1 = _lstm_buffers(Tp, B, Dd, f32)
+    L2 = _lstm_buffers(Tp, B, Dd, f32)
+    m1c, m1h, m2c, m2h = (mk("dec/lstm1/zc"), mk("dec/lstm1/zh"), mk("dec/lstm2/zc"),
+                          mk("dec/lstm2/zh"))
+
+    def lstm1_chunk(a, b):
+        n = (b - a) * B
+        x1 = X1[a:b].view(n, 4 * Dd)
+        K.linear(H0RAW[a:b].reshape(n, A), W1[:A], P["decoder/lstm1/bias"], out=x1)
+        K.gemm(REC0[a + 1:b + 1].reshape(n, R0)[:, :M1 + M2], W1[A:A + M1 + M2], x1, beta=1.0)
+        _lstm_steps(X1, W1[A + M1 + M2:], a, b, B, Dd, zc, zh, m1c, m1h, L1)
+
+    def lstm2_chunk(a, b):
+        n = (b - a) * B
+        K.linear(L1[0][a:b].reshape(n, Dd), W2[:Dd], P["decoder/lstm2/bias"],
+                 out=X2[a:b].view(n, 4 * Dd))
+        _lstm_steps(X2, W2[Dd:], a, b, B, Dd, zc, zh, m2c, m2h, L2)
+
+    pipe.fork()
+    for a, b in pipe.chunks(Tp):
+        for t in range(a, b):
+            attention_step(t)
+        pipe.handoff(0, 1)
+        with pipe.lane(1):
+            lstm1_chunk(a, b)
+        pipe.handoff(1, 2)
+        with pipe.lane(2):
+            lstm2_chunk(a, b)
+    pipe.join()
+    S.update(X0=X0, REC0=REC0, C0=C0, H0RAW=H0RAW, G0=G0, Q=Q, S1=S1, AL1=AL1, S2=S2, ST=ST)
+    H1RAW, C1S, H1S, G1 = L1
+    H2RAW, C2S, H2S, G2 = L2
     S.update(X1=X1, H1RAW=H1RAW, C1S=C1S, H1S=H1S, G1=G1, X2=X2, H2RAW=H2RAW, C2S=C2S,
              H2S=H2S, G2=G2)
     return H2RAW, DecoderSaved(B, N, Tp, S)
 
 
-def _run_lstm(X, Wr, Tp, B, U, zc, zh, mc, mh, f32):
-    HRAW = torch.empty(Tp, B, U, **f32)
-    CS = torch.zeros(Tp + 1, B, U, **f32)
-    HS = torch.zeros(Tp + 1, B, U, **f32)
-    G = torch.empty(Tp, B, 4 * U, **f32)
-    for t in range(Tp):
+def _lstm_buffers(Tp, B, U, f32):
+    """(h_raw [T',B,U], c [T'+1,B,U], h [T'+1,B,U], gates [T',B,4U]) histories."""
+    return (torch.empty(Tp, B, U, **f32), torch.zeros(Tp + 1, B, U, **f32),
+            torch.zeros(Tp + 1, B, U, **f32), torch.empty(Tp, B, 4 * U, **f32))
+
+
+def _lstm_steps(X, Wr, a, b, B, U, zc, zh, mc, mh, bufs):
+    HRAW, CS, HS, G = bufs
+    for t in range(a, b):
         K.lstm_step_fwd(B=B, U=U, K=U, t=t, xproj=X[t], rin=HS[t], W=Wr, c_prev=CS[t],
                         h_prev=HS[t], mask_c=None if mc is None else mc[t],
                         mask_h=None if mh is None else mh[t], zc=zc, zh=zh, h_raw=HRAW[t],
                         c_out=CS[t + 1], h_out=HS[t + 1], gates=G[t])
-    return HRAW, CS, HS, G

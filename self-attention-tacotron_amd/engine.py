@@ -16,11 +16,13 @@ from . import kernels as K
 from . import params as PR
 from .backward import model_backward
 from .model import BNState, model_forward
+from .pipeline import Pipeline
 
 
 class Tacotron:
     def __init__(self, hp, device, seed: int = 1234,
-                 init_values: Optional[Dict[str, np.ndarray]] = None, attn_tile: int = 32):
+                 init_values: Optional[Dict[str, np.ndarray]] = None, attn_tile: int = 32,
+                 pipeline_chunk: int = 25):
         self.hp = hp
         self.d = PR.resolve_dims(hp)
         self.device = torch.device(device)
@@ -33,17 +35,24 @@ class Tacotron:
         self.bn = BNState(hp, self.device)
         self.ws = K.Workspace(self.device)
         self.attn_tile = attn_tile
+        # chunked multi-stream schedule of the decoder recurrences (0 = one stream, in order).
+        # Forward and backward get their own side-stream pairs: re-forking the same side streams
+        # twice inside one hipGraph capture crashes the capture (measured on ROCm 7.2).
+        self.pipe = Pipeline(self.device, pipeline_chunk)
+        self.pipe_bwd = Pipeline(self.device, pipeline_chunk)
 
     # ------------------------------------------------------------------ steps
     def forward(self, batch: Dict[str, torch.Tensor], masks=None, training: bool = True,
                 need_grad: bool = True):
         return model_forward(self.P, self.bn, self.hp, self.d, batch, masks, training, self.ws,
-                             compute_grad_seeds=need_grad, attn_tile=self.attn_tile)
+                             compute_grad_seeds=need_grad, attn_tile=self.attn_tile,
+                             pipe=self.pipe)
 
     def backward(self, saved, zero: bool = True):
         if zero:
             self.grads.zero_()
-        model_backward(self.P, self.G, self.hp, self.d, saved, self.ws, attn_tile=self.attn_tile)
+        model_backward(self.P, self.G, self.hp, self.d, saved, self.ws, attn_tile=self.attn_tile,
+                       pipe=self.pipe_bwd)
 
     # ------------------------------------------------------------------ host views
     def params_dict(self) -> Dict[str, np.ndarray]:

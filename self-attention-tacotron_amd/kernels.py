@@ -28,13 +28,24 @@ GEMM_WS_BYTES = 32 << 20
 
 
 def _gemm_ws(device):
-    """Per-device split-K scratch (allocated once, before any graph capture)."""
-    key = (device.type, device.index)
+    """Split-K scratch, one per (device, stream): GEMMs on concurrent pipeline lanes never share
+    it.  Allocated on first use on that stream (the eager warm-up, before graph capture)."""
+    key = (device.type, device.index, torch.cuda.current_stream(device).cuda_stream)
     buf = _GEMM_WS.get(key)
     if buf is None:
         buf = torch.empty(GEMM_WS_BYTES, dtype=torch.uint8, device=device)
         _GEMM_WS[key] = buf
     return buf
+
+
+# Optional launch log for tools/gemm_census.py: list of (tag, SatGemmDesc copy) when not None.
+GEMM_LOG = None
+
+
+def _launch_gemm(d, tag):
+    if GEMM_LOG is not None:
+        GEMM_LOG.append((tag, type(d).from_buffer_copy(d)))
+    _lib.check(_lib.load().sat_gemm(ctypes.byref(d), _stream()), tag)
 
 
 def _with_ws(d, device):
@@ -105,7 +116,7 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor = None, *, alpha=1.0,
         d.add_sm = add.stride(-2) if add.dim() >= 2 else 0
         d.add_sbatch = add.stride(0) if add.dim() == 3 else 0
     _with_ws(d, C.device)
-    _lib.check(_lib.load().sat_gemm(ctypes.byref(d), _stream()), "sat_gemm")
+    _launch_gemm(d, "sat_gemm")
     return C
 
 
@@ -147,7 +158,7 @@ def conv1d(x: torch.Tensor, W: torch.Tensor, bias=None, out=None, act=None, beta
     d.b_mode, d.B, d.b_sk, d.b_sn = 0, _p(W), Cout, 1
     d.C, d.c_sm = _p(out), out.stride(1)
     d.bias, d.act, d.alpha, d.beta = _p(bias), ACT[act], 1.0, beta
-    _lib.check(_lib.load().sat_gemm(ctypes.byref(d), _stream()), "sat_gemm(conv1d)")
+    _launch_gemm(d, "sat_gemm(conv1d)")
     return out
 
 
@@ -164,7 +175,7 @@ def conv1d_dx(dy: torch.Tensor, W: torch.Tensor, out=None, beta=0.0):
     d.b_mode, d.b_taps, d.b_C, d.B = 1, taps, Cout, _p(W)
     d.C, d.c_sm = _p(out), out.stride(1)
     d.alpha, d.beta = 1.0, beta
-    _lib.check(_lib.load().sat_gemm(ctypes.byref(d), _stream()), "sat_gemm(conv1d_dx)")
+    _launch_gemm(d, "sat_gemm(conv1d_dx)")
     return out
 
 
@@ -180,7 +191,7 @@ def conv1d_dw(x: torch.Tensor, dy: torch.Tensor, dW: torch.Tensor, beta=0.0):
     d.C, d.c_sm = _p(dW), Cout
     d.alpha, d.beta = 1.0, beta
     _with_ws(d, dW.device)
-    _lib.check(_lib.load().sat_gemm(ctypes.byref(d), _stream()), "sat_gemm(conv1d_dw)")
+    _launch_gemm(d, "sat_gemm(conv1d_dw)")
     return dW
 
 
@@ -274,18 +285,22 @@ def attn_step_fwd(**kw):
 # ---------------------------------------------------------------- elementwise / reductions
 
 class Workspace:
-    """Grow-only fp64 scratch for column reductions (one per stream/model)."""
+    """Grow-only fp64 scratch for column reductions, one buffer per stream (pipeline lanes
+    reduce concurrently)."""
 
     def __init__(self, device):
         self.device = device
-        self.buf = torch.empty(0, dtype=torch.uint8, device=device)
+        self.bufs = {}
 
     def get(self, M, C) -> int:
         need = int(_lib.load().sat_workspace_colreduce(M, C))
-        if self.buf.numel() < need:
-            self.buf = torch.empty(max(need, 2 * self.buf.numel()), dtype=torch.uint8,
-                                   device=self.device)
-        return self.buf.data_ptr()
+        key = torch.cuda.current_stream(self.device).cuda_stream
+        buf = self.bufs.get(key)
+        if buf is None or buf.numel() < need:
+            old = 0 if buf is None else buf.numel()
+            buf = torch.empty(max(need, 2 * old, 1 << 20), dtype=torch.uint8, device=self.device)
+            self.bufs[key] = buf
+        return buf.data_ptr()
 
 
 def embedding_fwd(table, ids, out, offset=0, err=None):

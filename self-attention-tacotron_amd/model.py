@@ -218,7 +218,7 @@ class Saved(dict):
 
 def model_forward(P, bn: BNState, hp, d: PR.Dims, batch: Dict[str, torch.Tensor],
                   masks: Optional[Dict[str, torch.Tensor]], training: bool, ws: K.Workspace,
-                  compute_grad_seeds: bool = True, attn_tile: int = 32):
+                  compute_grad_seeds: bool = True, attn_tile: int = 32, pipe=None):
     """model_fn forward + loss.  Returns (outputs dict, Saved)."""
     sv = Saved()
     ids, lengths = batch["source"], batch["source_length"]
@@ -227,7 +227,8 @@ def model_forward(P, bn: BNState, hp, d: PR.Dims, batch: Dict[str, torch.Tensor]
     if d.multi_speaker:
         raise NotImplementedError("VCTK multi-speaker prenet is the next row (SURVEY 8(f) #3)")
     dout, dsv = decoder_forward(P, hp, d, m1, m2, lengths, batch["mel"], masks,
-                                attn_tile=attn_tile, spk=spk)
+                                attn_tile=attn_tile, spk=spk,
+                                **({} if pipe is None else {"pipe": pipe}))
     sv["dec"] = dsv
     mel_r, stop = head_fwd(P, hp, d, dout, masks, sv)
     B, Tp, _ = mel_r.shape

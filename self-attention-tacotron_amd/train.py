@@ -23,6 +23,7 @@ from typing import Dict, Optional
 import torch
 
 from . import _lib
+from . import dp
 from . import kernels as K
 from .masks import mask_specs
 
@@ -51,10 +52,8 @@ class Trainer:
         self.masks: Dict[str, torch.Tensor] = {
             s.name: torch.empty(s.shape, device=dev) for s in self.specs}
         self.pg = process_group
-        self.world = 1
-        if process_group is not None or (torch.distributed.is_available()
-                                         and torch.distributed.is_initialized()):
-            self.world = torch.distributed.get_world_size(process_group)
+        self.world = dp.world_size(process_group)
+        self.cfg.grad_scale = dp.grad_scale(process_group)
         self.last_loss = None
 
     def draw_masks(self):
@@ -74,11 +73,7 @@ class Trainer:
         return out
 
     def reduce_grads(self):
-        if self.world == 1:
-            return
-        g = self.m.grads
-        torch.distributed.all_reduce(g, op=torch.distributed.ReduceOp.SUM, group=self.pg)
-        K.axpby(g, g, 1.0 / self.world, 0.0)
+        dp.allreduce_grads(self.m.grads, self.pg)
 
     def apply(self):
         m = self.m

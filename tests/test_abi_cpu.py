@@ -1,0 +1,76 @@
+"""The C-ABI boundary without a GPU: libsat_hip.so loads, exports every function that
+include/sat_abi.h declares, the ctypes binding covers exactly that set, and the ctypes structs
+match the C struct sizes.  No device call is made."""
+import ctypes
+import os
+import re
+
+import pytest
+
+import _sat_path  # noqa: E402
+
+_sat_path.load()
+from sat_amd import _lib  # noqa: E402
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _lib_built():
+    return os.path.exists(_lib.LIB_PATH)
+
+
+def test_header_declares_and_binding_covers_the_same_set():
+    h = _lib.header_symbols()
+    assert len(h) >= 30
+    assert h == _lib.bound_symbols()
+
+
+@pytest.mark.skipif(not _lib_built(), reason="libsat_hip.so not built (run __graft_entry__.build())")
+def test_library_exports_every_header_symbol():
+    missing = _lib.header_symbols() - _lib.exported_symbols()
+    assert not missing, missing
+    lib = _lib.load()
+    assert lib.sat_version() > 0
+    # host-only queries (no device touched)
+    assert lib.sat_workspace_adam() > 0
+    assert lib.sat_workspace_colreduce(1000, 256) > 0
+    assert lib.sat_attn_part_stride(256, 32) >= 8 + 256 + 32
+    assert lib.sat_attn_pg_stride(224, 32, 5, 10) % 4 == 0
+
+
+def _c_sizeof(struct):
+    """sizeof(struct) as the C compiler sees include/sat_abi.h (gcc, host only)."""
+    import subprocess
+    import tempfile
+    src = f'#include "sat_abi.h"\n#include <stdio.h>\nint main(){{printf("%zu", sizeof({struct}));}}\n'
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, "s.c")
+        open(c, "w").write(src)
+        exe = os.path.join(d, "s")
+        subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), c, "-o", exe], check=True)
+        return int(subprocess.run([exe], capture_output=True, text=True, check=True).stdout)
+
+
+@pytest.mark.parametrize("name", ["SatGemmDesc", "SatLstmFwd", "SatLstmBwd", "SatAttnStep",
+                                  "SatAttnStepBwd", "SatAdamConfig"])
+def test_ctypes_structs_match_c_layout(name):
+    assert ctypes.sizeof(getattr(_lib, name)) == _c_sizeof(name)
+
+
+def test_errors_are_reported_not_swallowed():
+    """A bad argument returns an error code and a message; check() raises (no silent fallback)."""
+    if not _lib_built():
+        pytest.skip("libsat_hip.so not built")
+    lib = _lib.load()
+    d = _lib.SatAttnStepBwd()   # all-zero sizes
+    rc = lib.sat_attn_step_bwd(ctypes.byref(d), None)
+    assert rc != 0
+    assert b"sat_attn_step_bwd" in lib.sat_last_error_string()
+    with pytest.raises(_lib.SatLibraryError):
+        _lib.check(rc, "sat_attn_step_bwd")
+
+
+def test_header_cites_reference_interfaces():
+    text = open(os.path.join(ROOT, "include", "sat_abi.h")).read()
+    cites = re.findall(r"[\w/]+\.py:\d+", text)
+    assert len(cites) >= 10

@@ -1,0 +1,82 @@
+"""N>1 data-parallel path under ``gloo`` (world_size 2, CPU): the same dp.py functions and
+Trainer.reduce_grads the bench runs over RCCL on the GPUs."""
+import os
+import socket
+import types
+
+import pytest
+import torch
+import torch.distributed as tdist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, q):
+    try:
+        import sys
+        root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+        sys.path.insert(0, root)
+        import _sat_path
+        _sat_path.load()
+        from sat_amd import dp, hparams, train
+        tdist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                                 world_size=world)
+        res = {}
+        # broadcast of the parameter arena: every replica starts from rank 0's weights
+        p = torch.full((1000,), float(rank + 1))
+        dp.broadcast_params(p)
+        res["bcast"] = bool(torch.all(p == 1.0))
+        # one SUM all-reduce of the flat gradient arena + 1/world folded into Adam's config
+        hp = hparams.ljspeech_hparams()
+        model = types.SimpleNamespace(hp=hp, device=torch.device("cpu"),
+                                      params=torch.zeros(4096),
+                                      grads=torch.arange(4096, dtype=torch.float32) * (rank + 1))
+        tr = train.Trainer(model, B=2, N=8, Tp=4)
+        tr.reduce_grads()
+        expect = torch.arange(4096, dtype=torch.float32) * sum(r + 1 for r in range(world))
+        res["sum"] = bool(torch.equal(model.grads, expect))
+        res["scale"] = tr.cfg.grad_scale
+        res["world"] = tr.world
+        # max-over-ranks step time
+        res["max"] = dp.max_over_ranks(0.5 + rank, "cpu")
+        tdist.barrier()
+        tdist.destroy_process_group()
+        q.put((rank, res))
+    except Exception as e:  # pragma: no cover - surfaced by the parent
+        q.put((rank, repr(e)))
+
+
+def test_dp_world2_gloo():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    for r in range(2):
+        res = out[r]
+        assert isinstance(res, dict), res
+        assert res["bcast"] and res["sum"]
+        assert res["scale"] == pytest.approx(0.5) and res["world"] == 2
+        assert res["max"] == pytest.approx(1.5)
+
+
+def test_single_process_is_identity():
+    import _sat_path
+    _sat_path.load()
+    from sat_amd import dp
+    g = torch.ones(8)
+    dp.allreduce_grads(g)
+    assert torch.equal(g, torch.ones(8))
+    assert dp.grad_scale() == 1.0 and dp.world_size() == 1
+    assert dp.max_over_ranks(3.0, "cpu") == 3.0

@@ -50,7 +50,7 @@ def parse():
     ap.add_argument("--cpu-baseline-batch", type=int, default=2)
     ap.add_argument("--cpu-baseline-steps", type=int, default=4)
     ap.add_argument("--attn-tile", type=int, default=32)
-    ap.add_argument("--pipeline-chunk", type=int, default=25,
+    ap.add_argument("--pipeline-chunk", type=int, default=40,
                     help="decoder steps per chunk of the multi-stream recurrence pipeline (0 = off)")
     return ap.parse_args()
 

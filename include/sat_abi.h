@@ -149,7 +149,11 @@ typedef struct SatLstmBwd {
 } SatLstmBwd;
 
 int sat_lstm_step_fwd(const SatLstmFwd* args, void* stream);
+/* 1..4 independent steps (e.g. the attention RNN at t, decoder LSTM1 at t-C, LSTM2 at t-2C) in
+ * ONE launch over disjoint workgroup ranges: one kernel boundary instead of n. */
+int sat_lstm_steps_fwd(const SatLstmFwd* steps, int32_t n, void* stream);
 int sat_lstm_step_bwd(const SatLstmBwd* args, void* stream);
+int sat_lstm_steps_bwd(const SatLstmBwd* steps, int32_t n, void* stream);
 
 /* ---------------------------------------------------------------- dual-source attention step
  * Replaces, for one decoder step, the two attention mechanisms of DualSourceAttentionRNN

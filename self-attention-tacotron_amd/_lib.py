@@ -91,6 +91,8 @@ SIGNATURES = {
     "sat_counter_add": [_P, _U64, _P],
     "sat_lstm_step_fwd": [ctypes.POINTER(SatLstmFwd), _P],
     "sat_lstm_step_bwd": [ctypes.POINTER(SatLstmBwd), _P],
+    "sat_lstm_steps_fwd": [ctypes.POINTER(SatLstmFwd), _I32, _P],
+    "sat_lstm_steps_bwd": [ctypes.POINTER(SatLstmBwd), _I32, _P],
     "sat_attn_part_stride": [_I32, _I32],
     "sat_attn_query": [_I32, _I32, _I32, _I32, _P, _I64, _P, _P, _P, _I64, _P],
     "sat_attn_step_fwd": [ctypes.POINTER(SatAttnStep), _P],

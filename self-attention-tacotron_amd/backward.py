@@ -103,13 +103,18 @@ class _LstmBwd:
         self.first = True
         self.cur = 0
 
-    def step(self, **kw):
+    def desc(self, **kw):
+        """kwargs of the next reverse step (carries filled in); advances the carry state."""
         c = self.cur
-        K.lstm_step_bwd(dh_carry=None if self.first else self.hc[c],
-                        dc_carry=None if self.first else self.cc[c],
-                        dh_carry_out=self.hc[1 - c], dc_carry_out=self.cc[1 - c], **kw)
+        kw.update(dh_carry=None if self.first else self.hc[c],
+                  dc_carry=None if self.first else self.cc[c],
+                  dh_carry_out=self.hc[1 - c], dc_carry_out=self.cc[1 - c])
         self.first = False
         self.cur = 1 - c
+        return kw
+
+    def step(self, **kw):
+        K.lstm_step_bwd(**self.desc(**kw))
 
 
 def _lstm_loop_bwd(*, B, U, Kr, hoff, Tp, Wr, G_, CS, dY, mc, mh, zc, zh, order, nxt_of,
@@ -131,10 +136,11 @@ def _lstm_loop_bwd(*, B, U, Kr, hoff, Tp, Wr, G_, CS, dY, mc, mh, zc, zh, order,
 def decoder_bwd(P, G, hp, d, dsv, dH2, masks, ws, attn_tile=32, pipe: Pipeline = SEQUENTIAL):
     """Backward of decoder.decoder_forward.  Returns (dm1, dm2) batch-major.
 
-    The three reverse recurrences (LSTM2 -> LSTM1 -> attention RNN) are software-pipelined over
-    chunks of steps like the forward: LSTM2 runs on lane 2, LSTM1 on lane 1 (each followed by the
-    chunk's input-gradient GEMM), the attention chain on the current stream; the LSTMs' weight
-    gradients then overlap the tail of the attention chain."""
+    The three reverse recurrences (LSTM2 -> LSTM1 -> attention RNN) run as the mirror image of the
+    forward wavefront (``pipeline.Pipeline``): iteration j holds LSTM2 at step T'-1-j and LSTM1
+    C steps behind in ONE multi-problem launch, the attention chain 2C steps behind; the input
+    gradients of each chunk (dH1, then dH0 and dctx) are chunk GEMMs issued as soon as the
+    producing layer has finished the chunk."""
     S = dsv.tensors
     B, N, Tp = dsv.B, dsv.N, dsv.Tp
     dev = dH2.device
@@ -155,21 +161,23 @@ def decoder_bwd(P, G, hp, d, dsv, dH2, masks, ws, attn_tile=32, pipe: Pipeline =
     m2c, m2h, m1c, m1h = (mk("dec/lstm2/zc"), mk("dec/lstm2/zh"), mk("dec/lstm1/zc"),
                           mk("dec/lstm1/zh"))
 
-    def lstm2_chunk(a, b):
-        for t in range(b - 1, a - 1, -1):
-            run2.step(B=B, U=Dd, K=Dd, hoff=0, t=t, W=W2[Dd:],
-                      dgates_next=DG2[t + 1] if t + 1 < Tp else None, gates=S["G2"][t],
-                      c_prev=S["C2S"][t], dy=dH2[t], mask_c=None if m2c is None else m2c[t],
-                      mask_h=None if m2h is None else m2h[t], zc=zc, zh=zh, dgates=DG2[t])
+    def lstm2_desc(t):
+        return run2.desc(B=B, U=Dd, K=Dd, hoff=0, t=t, W=W2[Dd:],
+                         dgates_next=DG2[t + 1] if t + 1 < Tp else None, gates=S["G2"][t],
+                         c_prev=S["C2S"][t], dy=dH2[t], mask_c=None if m2c is None else m2c[t],
+                         mask_h=None if m2h is None else m2h[t], zc=zc, zh=zh, dgates=DG2[t])
+
+    def lstm1_desc(t):
+        return run1.desc(B=B, U=Dd, K=Dd, hoff=0, t=t, W=W1[A + M1 + M2:],
+                         dgates_next=DG1[t + 1] if t + 1 < Tp else None, gates=S["G1"][t],
+                         c_prev=S["C1S"][t], dy=dH1[t], mask_c=None if m1c is None else m1c[t],
+                         mask_h=None if m1h is None else m1h[t], zc=zc, zh=zh, dgates=DG1[t])
+
+    def dh1_chunk(a, b):
         n = (b - a) * B
         K.gemm(DG2[a:b].view(n, 4 * Dd), W2[:Dd].t(), dH1[a:b].view(n, Dd))
 
-    def lstm1_chunk(a, b):
-        for t in range(b - 1, a - 1, -1):
-            run1.step(B=B, U=Dd, K=Dd, hoff=0, t=t, W=W1[A + M1 + M2:],
-                      dgates_next=DG1[t + 1] if t + 1 < Tp else None, gates=S["G1"][t],
-                      c_prev=S["C1S"][t], dy=dH1[t], mask_c=None if m1c is None else m1c[t],
-                      mask_h=None if m1h is None else m1h[t], zc=zc, zh=zh, dgates=DG1[t])
+    def dh0_chunk(a, b):
         n = (b - a) * B
         dg = DG1[a:b].view(n, 4 * Dd)
         K.gemm(dg, W1[:A].t(), dH0[a:b].view(n, A))
@@ -199,61 +207,77 @@ def decoder_bwd(P, G, hp, d, dsv, dH2, masks, ws, attn_tile=32, pipe: Pipeline =
     mc0, mh0 = mk("dec/lstm0/zc"), mk("dec/lstm0/zh")
     chain = {"cur": 0}
 
-    def attention_chunk(a, b):
-        for t in range(b - 1, a - 1, -1):
-            cur = chain["cur"]
-            last = t == Tp - 1
-            if not last:   # gradient of c_t through the attention RNN's input at step t+1
-                K.rowdot(DG0[t + 1], W0r[:M1 + M2], DCTX[t], beta=1.0)
-            K.attn_step_bwd(
-                B=B, N=N, D1=D1, M1=M1, D2=D2, M2=M2, F=d.loc_f, KW=d.loc_k, NT=attn_tile,
-                ntiles=ntiles, att1_forward=1 if fwd else 0, u=0.5, dctx=DCTX[t],
-                dctx_sb=M1 + M2, dalpha_next=None if last else DAP[cur], V1=S["V1"], V2=S["V2"],
-                DA=DA, DS2=DS2, DSN=DSN, s_t=S["S1"][t + 1], a_t=S["AL1"][t + 1],
-                a_prev=S["AL1"][t], s_prev=S["S1"][t], s2_t=S["S2"][t], stats=S["ST"][t],
-                df_next=None if last else DF[cur], lengths=None, q=S["Q"][t], q_sb=D1 + D2,
-                K1=S["K1"], K2=S["K2"],
-                v1=P[f"{a1}/attention_variable"] if fwd else P[f"{a1}/attention_v"],
-                b1=P[f"{a1}/attention_bias"] if fwd else None,
-                convW=P[f"{a1}/location_conv/kernel"] if fwd else None,
-                convb=P[f"{a1}/location_conv/bias"] if fwd else None,
-                locW=P[f"{a1}/location_layer/kernel"] if fwd else None,
-                v2=P[f"{a2}/attention_v"], dalpha_prev=DAP[1 - cur], df_out=DF[1 - cur],
-                dK1=dK1, dK2=dK2, dqp=DQP[t], pg=PG, pg_stride=pgs)
-            K.lstm_step_bwd(B=B, U=A, K=R0, hoff=M1 + M2, t=t, W=W0r,
-                            dgates_next=None if last else DG0[t + 1], gates=S["G0"][t],
-                            c_prev=S["C0"][t], dy=dH0[t], dh_carry=None if last else hc[cur],
-                            dc_carry=None if last else cc[cur],
-                            mask_c=None if mc0 is None else mc0[t],
-                            mask_h=None if mh0 is None else mh0[t], zc=zc, zh=zh, dgates=DG0[t],
-                            dh_carry_out=hc[1 - cur], dc_carry_out=cc[1 - cur],
-                            dq0=DQP[t][:, :, :D1], wq0=P[f"{a1}/query_layer/kernel"],
-                            dq1=DQP[t][:, :, D1:], wq1=P[f"{a2}/query_layer/kernel"],
-                            dq_parts=ntiles, dq_pstride=D1 + D2, dq_bstride=ntiles * (D1 + D2))
-            chain["cur"] = 1 - cur
+    def attention_step(t):
+        cur = chain["cur"]
+        last = t == Tp - 1
+        if not last:   # gradient of c_t through the attention RNN's input at step t+1
+            K.rowdot(DG0[t + 1], W0r[:M1 + M2], DCTX[t], beta=1.0)
+        K.attn_step_bwd(
+            B=B, N=N, D1=D1, M1=M1, D2=D2, M2=M2, F=d.loc_f, KW=d.loc_k, NT=attn_tile,
+            ntiles=ntiles, att1_forward=1 if fwd else 0, u=0.5, dctx=DCTX[t],
+            dctx_sb=M1 + M2, dalpha_next=None if last else DAP[cur], V1=S["V1"], V2=S["V2"],
+            DA=DA, DS2=DS2, DSN=DSN, s_t=S["S1"][t + 1], a_t=S["AL1"][t + 1],
+            a_prev=S["AL1"][t], s_prev=S["S1"][t], s2_t=S["S2"][t], stats=S["ST"][t],
+            df_next=None if last else DF[cur], lengths=None, q=S["Q"][t], q_sb=D1 + D2,
+            K1=S["K1"], K2=S["K2"],
+            v1=P[f"{a1}/attention_variable"] if fwd else P[f"{a1}/attention_v"],
+            b1=P[f"{a1}/attention_bias"] if fwd else None,
+            convW=P[f"{a1}/location_conv/kernel"] if fwd else None,
+            convb=P[f"{a1}/location_conv/bias"] if fwd else None,
+            locW=P[f"{a1}/location_layer/kernel"] if fwd else None,
+            v2=P[f"{a2}/attention_v"], dalpha_prev=DAP[1 - cur], df_out=DF[1 - cur],
+            dK1=dK1, dK2=dK2, dqp=DQP[t], pg=PG, pg_stride=pgs)
+        K.lstm_step_bwd(B=B, U=A, K=R0, hoff=M1 + M2, t=t, W=W0r,
+                        dgates_next=None if last else DG0[t + 1], gates=S["G0"][t],
+                        c_prev=S["C0"][t], dy=dH0[t], dh_carry=None if last else hc[cur],
+                        dc_carry=None if last else cc[cur],
+                        mask_c=None if mc0 is None else mc0[t],
+                        mask_h=None if mh0 is None else mh0[t], zc=zc, zh=zh, dgates=DG0[t],
+                        dh_carry_out=hc[1 - cur], dc_carry_out=cc[1 - cur],
+                        dq0=DQP[t][:, :, :D1], wq0=P[f"{a1}/query_layer/kernel"],
+                        dq1=DQP[t][:, :, D1:], wq1=P[f"{a2}/query_layer/kernel"],
+                        dq_parts=ntiles, dq_pstride=D1 + D2, dq_bstride=ntiles * (D1 + D2))
+        chain["cur"] = 1 - cur
 
-    pipe.fork()
-    for a, b in reversed(pipe.chunks(Tp)):
-        with pipe.lane(2):
-            lstm2_chunk(a, b)
-        pipe.handoff(2, 1)
-        with pipe.lane(1):
-            lstm1_chunk(a, b)
-        pipe.handoff(1, 0)
-        attention_chunk(a, b)
-    # LSTM weight gradients on their own lanes, overlapping the attention chain's tail
+    if not pipe.enabled:          # layer by layer
+        for t in range(Tp - 1, -1, -1):
+            K.lstm_step_bwd(**lstm2_desc(t))
+        dh1_chunk(0, Tp)
+        for t in range(Tp - 1, -1, -1):
+            K.lstm_step_bwd(**lstm1_desc(t))
+        dh0_chunk(0, Tp)
+        for t in range(Tp - 1, -1, -1):
+            attention_step(t)
+    else:                         # reverse wavefront: LSTM1 C, the attention chain 2C behind
+        C = pipe.chunk
+        dh1_at = pipe.finishing_rev(Tp, 0)
+        dh0_at = pipe.finishing_rev(Tp, C)
+        for j in range(Tp + 2 * C):
+            t2, t1, t0 = Tp - 1 - j, Tp - 1 - j + C, Tp - 1 - j + 2 * C
+            steps = []
+            if t2 >= 0:
+                steps.append(lstm2_desc(t2))
+            if 0 <= t1 < Tp:
+                steps.append(lstm1_desc(t1))
+            if steps:
+                K.lstm_steps_bwd(steps)
+            if 0 <= t0 < Tp:
+                attention_step(t0)
+            if j in dh1_at:
+                dh1_chunk(*dh1_at[j])
+            if j in dh0_at:
+                dh0_chunk(*dh0_at[j])
+    # LSTM weight gradients: one GEMM per weight block over all steps
     DG2f = DG2.view(Tp * B, 4 * Dd)
     DG1f = DG1.view(Tp * B, 4 * Dd)
-    with pipe.lane(2):
-        K.gemm(S["H2S"][:Tp].reshape(Tp * B, Dd).t(), DG2f, dW2[Dd:], beta=1.0)
-        K.gemm(S["H1RAW"].view(Tp * B, Dd).t(), DG2f, dW2[:Dd], beta=1.0)
-        K.colsum(DG2f, G["decoder/lstm2/bias"], ws)
-    with pipe.lane(1):
-        K.gemm(S["H1S"][:Tp].reshape(Tp * B, Dd).t(), DG1f, dW1[A + M1 + M2:], beta=1.0)
-        K.colsum(DG1f, G["decoder/lstm1/bias"], ws)
-        ctx_all = S["REC0"][1:].reshape(Tp * B, R0)[:, :M1 + M2]
-        K.gemm(S["H0RAW"].view(Tp * B, A).t(), DG1f, dW1[:A], beta=1.0)
-        K.gemm(ctx_all.t(), DG1f, dW1[A:A + M1 + M2], beta=1.0)
+    K.gemm(S["H2S"][:Tp].reshape(Tp * B, Dd).t(), DG2f, dW2[Dd:], beta=1.0)
+    K.gemm(S["H1RAW"].view(Tp * B, Dd).t(), DG2f, dW2[:Dd], beta=1.0)
+    K.colsum(DG2f, G["decoder/lstm2/bias"], ws)
+    K.gemm(S["H1S"][:Tp].reshape(Tp * B, Dd).t(), DG1f, dW1[A + M1 + M2:], beta=1.0)
+    K.colsum(DG1f, G["decoder/lstm1/bias"], ws)
+    ctx_all = S["REC0"][1:].reshape(Tp * B, R0)[:, :M1 + M2]
+    K.gemm(S["H0RAW"].view(Tp * B, A).t(), DG1f, dW1[:A], beta=1.0)
+    K.gemm(ctx_all.t(), DG1f, dW1[A:A + M1 + M2], beta=1.0)
 
     DG0f = DG0.view(Tp * B, 4 * A)
     K.gemm(S["REC0"][:Tp].reshape(Tp * B, R0).t(), DG0f, dW0[p_w:], beta=1.0)
@@ -302,7 +326,6 @@ def decoder_bwd(P, G, hp, d, dsv, dH2, masks, ws, attn_tile=32, pipe: Pipeline =
             ws, dx=dV1, beta_dx=1.0)
     lin_bwd(S["V2"], dK2, P[f"{a2}/memory_layer/kernel"], G[f"{a2}/memory_layer/kernel"], None,
             ws, dx=dV2, beta_dx=1.0)
-    pipe.join()
     return dV1, dV2          # caller applies the sequence mask (values were masked memories)
 
 

@@ -14,6 +14,8 @@
 // For U=256, B=32: 64 x 4 = 256 workgroups, one per CU.
 #include "sat_common.h"
 
+#include <algorithm>
+
 namespace sat {
 namespace {
 
@@ -40,15 +42,14 @@ struct LstmFwdP {
 // W[:, u0:u0+4, :] (K x 16 floats) and its 8 input rows go global -> LDS in one burst of
 // 16-byte loads, the pointwise operands (xproj, c, h, masks) are prefetched into registers,
 // then the K-split dot products run out of LDS.
-__global__ void __launch_bounds__(256) lstm_fwd_kernel(LstmFwdP p) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
+__device__ __forceinline__ void lstm_fwd_block(const LstmFwdP& p, int bx, int by, float* smem) {
   const int K = p.K;
   float4* Ws = reinterpret_cast<float4*>(smem);          // [K][UT]
   float* xs = smem + (size_t)K * UT * 4;                  // [BT][K + 4]
   const int xld = K + 4;
   const int tid = threadIdx.x;
   const int ks = tid & (KS - 1), pair = tid >> 3;
-  const int u0 = blockIdx.x * UT, b0 = blockIdx.y * BT;
+  const int u0 = bx * UT, b0 = by * BT;
   const int u = u0 + (pair & (UT - 1));
   const int bl = pair >> 2;
   const int b = b0 + bl;
@@ -125,6 +126,28 @@ __global__ void __launch_bounds__(256) lstm_fwd_kernel(LstmFwdP p) {
   if (p.gates) reinterpret_cast<float4*>(p.gates)[bu] = make_float4(gi, gj, gf, go);
 }
 
+// Up to kMaxProblems independent steps (e.g. the attention RNN at t, decoder LSTM1 at t - C,
+// LSTM2 at t - 2C) in ONE launch: disjoint workgroup ranges, dynamic LDS = the largest need.
+constexpr int kMaxProblems = 4;
+
+struct LstmFwdMulti {
+  LstmFwdP p[kMaxProblems];
+  int first[kMaxProblems + 1];   // first workgroup of each problem (prefix sums)
+  int gx[kMaxProblems];          // unit tiles per problem
+  int n;
+};
+
+__global__ void __launch_bounds__(256) lstm_fwd_kernel(LstmFwdMulti m) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  int i = 0;
+#pragma unroll
+  for (int j = 1; j < kMaxProblems; ++j)
+    if (j < m.n && (int)blockIdx.x >= m.first[j]) i = j;
+  const int local = blockIdx.x - m.first[i];
+  const int by = local / m.gx[i], bx = local - by * m.gx[i];
+  lstm_fwd_block(m.p[i], bx, by, smem);
+}
+
 struct LstmBwdP {
   int B, U, K, hoff;
   const float* W;                       // [K][U][4]
@@ -154,8 +177,7 @@ struct LstmBwdP {
 // (b, u) and 3 xor-shuffles.
 constexpr int kMaxDq = 320;
 
-__global__ void __launch_bounds__(256) lstm_bwd_kernel(LstmBwdP p) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
+__device__ __forceinline__ void lstm_bwd_block(const LstmBwdP& p, int bx, int by, float* smem) {
   const int G = 4 * p.U;
   const int D0 = p.dq0 ? p.dq0_n : 0, D1 = p.dq1 ? p.dq1_n : 0, DQ = D0 + D1;
   const int L = G + DQ;                                // dot length
@@ -164,7 +186,7 @@ __global__ void __launch_bounds__(256) lstm_bwd_kernel(LstmBwdP p) {
   float* wrs = dgs + (size_t)BT * ld;                  // [UT][ld]
   const int tid = threadIdx.x;
   const int ks = tid & (KS - 1), pair = tid >> 3;
-  const int u0 = blockIdx.x * UT, b0 = blockIdx.y * BT;
+  const int u0 = bx * UT, b0 = by * BT;
   const int ul = pair & (UT - 1), bl = pair >> 2;
   const int u = u0 + ul, b = b0 + bl;
   const bool active = (u < p.U) && (b < p.B);
@@ -268,6 +290,24 @@ __global__ void __launch_bounds__(256) lstm_bwd_kernel(LstmBwdP p) {
   p.dh_carry_out[bu] = (1.f - mh) * dh_t;
 }
 
+struct LstmBwdMulti {
+  LstmBwdP p[kMaxProblems];
+  int first[kMaxProblems + 1];
+  int gx[kMaxProblems];
+  int n;
+};
+
+__global__ void __launch_bounds__(256) lstm_bwd_kernel(LstmBwdMulti m) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  int i = 0;
+#pragma unroll
+  for (int j = 1; j < kMaxProblems; ++j)
+    if (j < m.n && (int)blockIdx.x >= m.first[j]) i = j;
+  const int local = blockIdx.x - m.first[i];
+  const int by = local / m.gx[i], bx = local - by * m.gx[i];
+  lstm_bwd_block(m.p[i], bx, by, smem);
+}
+
 }  // namespace
 }  // namespace sat
 
@@ -275,12 +315,11 @@ using namespace sat;
 
 static inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
-extern "C" int sat_lstm_step_fwd(const SatLstmFwd* a, void* stream) {
+static int check_fwd(const SatLstmFwd* a, LstmFwdP& p, size_t& shm) {
   SAT_CHECK_ARG(a && a->B > 0 && a->U > 0 && a->K >= 0, "sat_lstm_step_fwd: bad sizes");
   SAT_CHECK_ARG(a->K % 4 == 0 && a->rin_sb % 4 == 0, "sat_lstm_step_fwd: K and rin stride must be multiples of 4");
   SAT_CHECK_ARG((a->K == 0 || a->rin) && a->W && a->c_out && a->h_out, "sat_lstm_step_fwd: null pointer");
   SAT_CHECK_ARG((a->mask_c == nullptr) == (a->mask_h == nullptr), "sat_lstm_step_fwd: masks come in pairs");
-  LstmFwdP p;
   p.B = a->B; p.U = a->U; p.K = a->K;
   p.xproj = a->xproj; p.xproj_sb = a->xproj_sb; p.bias = a->bias;
   p.rin = a->rin; p.rin_sb = a->rin_sb; p.W = a->W;
@@ -289,15 +328,36 @@ extern "C" int sat_lstm_step_fwd(const SatLstmFwd* a, void* stream) {
   p.lengths = a->lengths; p.t = a->t;
   p.h_raw = a->h_raw; p.h_raw_sb = a->h_raw_sb;
   p.c_out = a->c_out; p.h_out = a->h_out; p.h_out_sb = a->h_out_sb; p.gates = a->gates;
-  dim3 grid(ceil_div(a->U, UT), ceil_div(a->B, BT));
-  const size_t shm = ((size_t)a->K * UT * 4 + (size_t)BT * (a->K + 4)) * sizeof(float);
+  shm = ((size_t)a->K * UT * 4 + (size_t)BT * (a->K + 4)) * sizeof(float);
   SAT_CHECK_ARG(shm <= 160 * 1024, "sat_lstm_step_fwd: K too large for the LDS-staged step");
-  hipLaunchKernelGGL(lstm_fwd_kernel, grid, dim3(256), shm, as_stream(stream), p);
-  SAT_LAUNCH_CHECK("sat_lstm_step_fwd");
   return SAT_OK;
 }
 
-extern "C" int sat_lstm_step_bwd(const SatLstmBwd* a, void* stream) {
+extern "C" int sat_lstm_steps_fwd(const SatLstmFwd* steps, int32_t n, void* stream) {
+  SAT_CHECK_ARG(steps && n >= 1 && n <= kMaxProblems, "sat_lstm_steps_fwd: 1..4 steps");
+  LstmFwdMulti m;
+  m.n = n;
+  m.first[0] = 0;
+  size_t shm = 0;
+  for (int i = 0; i < n; ++i) {
+    size_t s_i = 0;
+    const int rc = check_fwd(steps + i, m.p[i], s_i);
+    if (rc != SAT_OK) return rc;
+    shm = std::max(shm, s_i);
+    m.gx[i] = ceil_div(steps[i].U, UT);
+    m.first[i + 1] = m.first[i] + m.gx[i] * ceil_div(steps[i].B, BT);
+  }
+  for (int i = n; i < kMaxProblems; ++i) { m.gx[i] = 1; m.first[i + 1] = m.first[n]; }
+  hipLaunchKernelGGL(lstm_fwd_kernel, dim3(m.first[n]), dim3(256), shm, as_stream(stream), m);
+  SAT_LAUNCH_CHECK("sat_lstm_steps_fwd");
+  return SAT_OK;
+}
+
+extern "C" int sat_lstm_step_fwd(const SatLstmFwd* a, void* stream) {
+  return sat_lstm_steps_fwd(a, 1, stream);
+}
+
+static int check_bwd(const SatLstmBwd* a, LstmBwdP& p, size_t& shm) {
   SAT_CHECK_ARG(a && a->B > 0 && a->U > 0, "sat_lstm_step_bwd: bad sizes");
   SAT_CHECK_ARG(a->W && a->gates && a->dgates && a->dh_carry_out && a->dc_carry_out,
                 "sat_lstm_step_bwd: null pointer");
@@ -309,7 +369,6 @@ extern "C" int sat_lstm_step_bwd(const SatLstmBwd* a, void* stream) {
                 a->dq_pstride % 4 == 0 && a->dq_bstride % 4 == 0 && aligned16(a->W) &&
                 aligned16(a->dgates_next),
                 "sat_lstm_step_bwd: query-gradient operands must be 16-byte aligned, widths % 4");
-  LstmBwdP p;
   p.B = a->B; p.U = a->U; p.K = a->K; p.hoff = a->hoff;
   p.W = a->W; p.dgates_next = a->dgates_next; p.gates = a->gates; p.c_prev = a->c_prev;
   p.dy = a->dy; p.dy_sb = a->dy_sb;
@@ -322,11 +381,32 @@ extern "C" int sat_lstm_step_bwd(const SatLstmBwd* a, void* stream) {
   p.mask_c = a->mask_c; p.mask_h = a->mask_h; p.zc = a->zc; p.zh = a->zh;
   p.lengths = a->lengths; p.t = a->t;
   p.dgates = a->dgates; p.dh_carry_out = a->dh_carry_out; p.dc_carry_out = a->dc_carry_out;
-  dim3 grid(ceil_div(a->U, UT), ceil_div(a->B, BT));
   const int DQ = (a->dq0 ? a->dq0_n : 0) + (a->dq1 ? a->dq1_n : 0);
-  const size_t shm = (size_t)(BT + UT) * (4 * a->U + DQ + 4) * sizeof(float);
+  shm = (size_t)(BT + UT) * (4 * a->U + DQ + 4) * sizeof(float);
   SAT_CHECK_ARG(shm <= 160 * 1024, "sat_lstm_step_bwd: U too large for the LDS-staged step");
-  hipLaunchKernelGGL(lstm_bwd_kernel, grid, dim3(256), shm, as_stream(stream), p);
-  SAT_LAUNCH_CHECK("sat_lstm_step_bwd");
   return SAT_OK;
+}
+
+extern "C" int sat_lstm_steps_bwd(const SatLstmBwd* steps, int32_t n, void* stream) {
+  SAT_CHECK_ARG(steps && n >= 1 && n <= kMaxProblems, "sat_lstm_steps_bwd: 1..4 steps");
+  LstmBwdMulti m;
+  m.n = n;
+  m.first[0] = 0;
+  size_t shm = 0;
+  for (int i = 0; i < n; ++i) {
+    size_t s_i = 0;
+    const int rc = check_bwd(steps + i, m.p[i], s_i);
+    if (rc != SAT_OK) return rc;
+    shm = std::max(shm, s_i);
+    m.gx[i] = ceil_div(steps[i].U, UT);
+    m.first[i + 1] = m.first[i] + m.gx[i] * ceil_div(steps[i].B, BT);
+  }
+  for (int i = n; i < kMaxProblems; ++i) { m.gx[i] = 1; m.first[i + 1] = m.first[n]; }
+  hipLaunchKernelGGL(lstm_bwd_kernel, dim3(m.first[n]), dim3(256), shm, as_stream(stream), m);
+  SAT_LAUNCH_CHECK("sat_lstm_steps_bwd");
+  return SAT_OK;
+}
+
+extern "C" int sat_lstm_step_bwd(const SatLstmBwd* a, void* stream) {
+  return sat_lstm_steps_bwd(a, 1, stream);
 }

@@ -9,10 +9,11 @@ MI355X restructuring (same arithmetic, different schedule):
   input projection (x @ W_x + b) are hoisted out of the recurrence into large MFMA GEMMs;
 * the recurrence of the attention RNN (ZoneoutLSTM 256 -> query -> dual-source attention) runs
   first over all steps: 3 launches per step (LSTM step, query GEMV, attention tile+combine);
-* the two decoder LSTMs depend only on the attention RNN's outputs, so they run as their own
-  recurrences (1 launch per step each) with input GEMMs hoisted per chunk of steps, software-
-  pipelined behind the attention RNN on two side HIP streams (``pipeline.Pipeline``): chunk k of
-  LSTM1 overlaps chunk k+1 of the attention recurrence, chunk k of LSTM2 overlaps both.
+* the two decoder LSTMs depend only on the attention RNN's outputs, so they run as a wavefront
+  behind it (``pipeline.Pipeline``): ONE multi-problem launch per iteration holds the attention
+  RNN at step i, LSTM1 at i - C and LSTM2 at i - 2C, with the LSTMs' input GEMMs hoisted per
+  chunk of C steps.  Per decoder step: 3 launches for the attention chain, none extra for the
+  two decoder LSTMs.
 
 All state histories are kept (step-major ``[T'+1, B, .]``) for the hand-written BPTT.
 """
@@ -122,13 +123,13 @@ def decoder_forward(P: Dict[str, torch.Tensor], hp, d: Dims, m1: torch.Tensor, m
     K.transpose(P["decoder/attention2/query_layer/kernel"], QT[D1:])
     zc0, zh0 = mk("dec/lstm0/zc"), mk("dec/lstm0/zh")
 
-    def attention_step(t):
-        K.lstm_step_fwd(B=B, U=A, K=R0, t=t, xproj=X0[t], rin=REC0[t], W=Wr0,
-                        c_prev=C0[t], h_prev=REC0[t, :, M1 + M2:],
-                        mask_c=None if zc0 is None else zc0[t],
-                        mask_h=None if zh0 is None else zh0[t], zc=zc, zh=zh,
-                        h_raw=H0RAW[t], c_out=C0[t + 1], h_out=REC0[t + 1, :, M1 + M2:],
-                        gates=G0[t])
+    def lstm0_desc(t):
+        return dict(B=B, U=A, K=R0, t=t, xproj=X0[t], rin=REC0[t], W=Wr0, c_prev=C0[t],
+                    h_prev=REC0[t, :, M1 + M2:], mask_c=None if zc0 is None else zc0[t],
+                    mask_h=None if zh0 is None else zh0[t], zc=zc, zh=zh, h_raw=H0RAW[t],
+                    c_out=C0[t + 1], h_out=REC0[t + 1, :, M1 + M2:], gates=G0[t])
+
+    def attention_rest(t):
         K.rowdot(H0RAW[t], QT, Q[t])
         K.attn_step_fwd(
             B=B, N=N, D1=D1, M1=M1, D2=D2, M2=M2, F=d.loc_f, KW=d.loc_k, NT=attn_tile,
@@ -153,30 +154,53 @@ def decoder_forward(P: Dict[str, torch.Tensor], hp, d: Dims, m1: torch.Tensor, m
     m1c, m1h, m2c, m2h = (mk("dec/lstm1/zc"), mk("dec/lstm1/zh"), mk("dec/lstm2/zc"),
                           mk("dec/lstm2/zh"))
 
-    def lstm1_chunk(a, b):
+    def x1_chunk(a, b):
         n = (b - a) * B
         x1 = X1[a:b].view(n, 4 * Dd)
         K.linear(H0RAW[a:b].reshape(n, A), W1[:A], P["decoder/lstm1/bias"], out=x1)
         K.gemm(REC0[a + 1:b + 1].reshape(n, R0)[:, :M1 + M2], W1[A:A + M1 + M2], x1, beta=1.0)
-        _lstm_steps(X1, W1[A + M1 + M2:], a, b, B, Dd, zc, zh, m1c, m1h, L1)
 
-    def lstm2_chunk(a, b):
+    def x2_chunk(a, b):
         n = (b - a) * B
         K.linear(L1[0][a:b].reshape(n, Dd), W2[:Dd], P["decoder/lstm2/bias"],
                  out=X2[a:b].view(n, 4 * Dd))
-        _lstm_steps(X2, W2[Dd:], a, b, B, Dd, zc, zh, m2c, m2h, L2)
 
-    pipe.fork()
-    for a, b in pipe.chunks(Tp):
-        for t in range(a, b):
-            attention_step(t)
-        pipe.handoff(0, 1)
-        with pipe.lane(1):
-            lstm1_chunk(a, b)
-        pipe.handoff(1, 2)
-        with pipe.lane(2):
-            lstm2_chunk(a, b)
-    pipe.join()
+    def lstm1_desc(t):
+        return _lstm_desc(X1, W1[A + M1 + M2:], t, B, Dd, zc, zh, m1c, m1h, L1)
+
+    def lstm2_desc(t):
+        return _lstm_desc(X2, W2[Dd:], t, B, Dd, zc, zh, m2c, m2h, L2)
+
+    if not pipe.enabled:          # layer by layer
+        for t in range(Tp):
+            K.lstm_step_fwd(**lstm0_desc(t))
+            attention_rest(t)
+        x1_chunk(0, Tp)
+        for t in range(Tp):
+            K.lstm_step_fwd(**lstm1_desc(t))
+        x2_chunk(0, Tp)
+        for t in range(Tp):
+            K.lstm_step_fwd(**lstm2_desc(t))
+    else:                         # wavefront: LSTM1 C steps and LSTM2 2C steps behind
+        C = pipe.chunk
+        x1_at = pipe.finishing(Tp, 0)
+        x2_at = pipe.finishing(Tp, C)
+        for i in range(Tp + 2 * C):
+            steps = []
+            if i < Tp:
+                steps.append(lstm0_desc(i))
+            if 0 <= i - C < Tp:
+                steps.append(lstm1_desc(i - C))
+            if 0 <= i - 2 * C < Tp:
+                steps.append(lstm2_desc(i - 2 * C))
+            if steps:
+                K.lstm_steps_fwd(steps)
+            if i < Tp:
+                attention_rest(i)
+            if i in x1_at:
+                x1_chunk(*x1_at[i])
+            if i in x2_at:
+                x2_chunk(*x2_at[i])
     S.update(X0=X0, REC0=REC0, C0=C0, H0RAW=H0RAW, G0=G0, Q=Q, S1=S1, AL1=AL1, S2=S2, ST=ST)
     H1RAW, C1S, H1S, G1 = L1
     H2RAW, C2S, H2S, G2 = L2
@@ -191,10 +215,8 @@ def _lstm_buffers(Tp, B, U, f32):
             torch.zeros(Tp + 1, B, U, **f32), torch.empty(Tp, B, 4 * U, **f32))
 
 
-def _lstm_steps(X, Wr, a, b, B, U, zc, zh, mc, mh, bufs):
+def _lstm_desc(X, Wr, t, B, U, zc, zh, mc, mh, bufs):
     HRAW, CS, HS, G = bufs
-    for t in range(a, b):
-        K.lstm_step_fwd(B=B, U=U, K=U, t=t, xproj=X[t], rin=HS[t], W=Wr, c_prev=CS[t],
-                        h_prev=HS[t], mask_c=None if mc is None else mc[t],
-                        mask_h=None if mh is None else mh[t], zc=zc, zh=zh, h_raw=HRAW[t],
-                        c_out=CS[t + 1], h_out=HS[t + 1], gates=G[t])
+    return dict(B=B, U=U, K=U, t=t, xproj=X[t], rin=HS[t], W=Wr, c_prev=CS[t], h_prev=HS[t],
+                mask_c=None if mc is None else mc[t], mask_h=None if mh is None else mh[t],
+                zc=zc, zh=zh, h_raw=HRAW[t], c_out=CS[t + 1], h_out=HS[t + 1], gates=G[t])

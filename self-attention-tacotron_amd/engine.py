@@ -22,7 +22,7 @@ from .pipeline import Pipeline
 class Tacotron:
     def __init__(self, hp, device, seed: int = 1234,
                  init_values: Optional[Dict[str, np.ndarray]] = None, attn_tile: int = 32,
-                 pipeline_chunk: int = 25):
+                 pipeline_chunk: int = 40):
         self.hp = hp
         self.d = PR.resolve_dims(hp)
         self.device = torch.device(device)
@@ -35,11 +35,8 @@ class Tacotron:
         self.bn = BNState(hp, self.device)
         self.ws = K.Workspace(self.device)
         self.attn_tile = attn_tile
-        # chunked multi-stream schedule of the decoder recurrences (0 = one stream, in order).
-        # Forward and backward get their own side-stream pairs: re-forking the same side streams
-        # twice inside one hipGraph capture crashes the capture (measured on ROCm 7.2).
+        # wavefront schedule of the decoder recurrences (0 = layer by layer)
         self.pipe = Pipeline(self.device, pipeline_chunk)
-        self.pipe_bwd = Pipeline(self.device, pipeline_chunk)
 
     # ------------------------------------------------------------------ steps
     def forward(self, batch: Dict[str, torch.Tensor], masks=None, training: bool = True,
@@ -52,7 +49,7 @@ class Tacotron:
         if zero:
             self.grads.zero_()
         model_backward(self.P, self.G, self.hp, self.d, saved, self.ws, attn_tile=self.attn_tile,
-                       pipe=self.pipe_bwd)
+                       pipe=self.pipe)
 
     # ------------------------------------------------------------------ host views
     def params_dict(self) -> Dict[str, np.ndarray]:

@@ -215,9 +215,10 @@ def _rs(t) -> int:
     return 0 if t is None else t.stride(0)
 
 
-def lstm_step_fwd(*, B, U, K, t, xproj, rin, W, c_prev, h_prev, mask_c, mask_h, zc, zh,
-                  h_raw, c_out, h_out, gates, lengths=None, bias=None):
-    a = _lib.SatLstmFwd()
+def lstm_fwd_desc(*, B, U, K, t, xproj, rin, W, c_prev, h_prev, mask_c, mask_h, zc, zh,
+                  h_raw, c_out, h_out, gates, lengths=None, bias=None, a=None):
+    """Fill a SatLstmFwd (``a``, or a new one) for one recurrent step."""
+    a = _lib.SatLstmFwd() if a is None else a
     a.B, a.U, a.K, a.t = B, U, K, t
     a.xproj, a.xproj_sb = _p(xproj), _rs(xproj)
     a.bias = _p(bias)
@@ -232,14 +233,27 @@ def lstm_step_fwd(*, B, U, K, t, xproj, rin, W, c_prev, h_prev, mask_c, mask_h, 
     a.c_out = _p(c_out)
     a.h_out, a.h_out_sb = _p(h_out), _rs(h_out)
     a.gates = _p(gates)
+    return a
+
+
+def lstm_step_fwd(**kw):
+    a = lstm_fwd_desc(**kw)
     _lib.check(_lib.load().sat_lstm_step_fwd(ctypes.byref(a), _stream()), "sat_lstm_step_fwd")
 
 
-def lstm_step_bwd(*, B, U, K, hoff, t, W, dgates_next, gates, c_prev, dy, dh_carry, dc_carry,
+def lstm_steps_fwd(steps):
+    """Several independent LSTM steps (list of lstm_step_fwd kwargs) in ONE launch."""
+    arr = (_lib.SatLstmFwd * len(steps))()
+    for i, kw in enumerate(steps):
+        lstm_fwd_desc(a=arr[i], **kw)
+    _lib.check(_lib.load().sat_lstm_steps_fwd(arr, len(steps), _stream()), "sat_lstm_steps_fwd")
+
+
+def lstm_bwd_desc(*, B, U, K, hoff, t, W, dgates_next, gates, c_prev, dy, dh_carry, dc_carry,
                   mask_c, mask_h, zc, zh, dgates, dh_carry_out, dc_carry_out, lengths=None,
                   dq0=None, wq0=None, dq1=None, wq1=None, dq_parts=1, dq_pstride=0,
-                  dq_bstride=0):
-    a = _lib.SatLstmBwd()
+                  dq_bstride=0, a=None):
+    a = _lib.SatLstmBwd() if a is None else a
     a.B, a.U, a.K, a.hoff, a.t = B, U, K, hoff, t
     a.W, a.dgates_next, a.gates, a.c_prev = _p(W), _p(dgates_next), _p(gates), _p(c_prev)
     a.dy, a.dy_sb = _p(dy), _rs(dy)
@@ -251,7 +265,20 @@ def lstm_step_bwd(*, B, U, K, hoff, t, W, dgates_next, gates, c_prev, dy, dh_car
     a.zc, a.zh = zc, zh
     a.lengths = _p(lengths)
     a.dgates, a.dh_carry_out, a.dc_carry_out = _p(dgates), _p(dh_carry_out), _p(dc_carry_out)
+    return a
+
+
+def lstm_step_bwd(**kw):
+    a = lstm_bwd_desc(**kw)
     _lib.check(_lib.load().sat_lstm_step_bwd(ctypes.byref(a), _stream()), "sat_lstm_step_bwd")
+
+
+def lstm_steps_bwd(steps):
+    """Several independent reverse LSTM steps (list of lstm_step_bwd kwargs) in ONE launch."""
+    arr = (_lib.SatLstmBwd * len(steps))()
+    for i, kw in enumerate(steps):
+        lstm_bwd_desc(a=arr[i], **kw)
+    _lib.check(_lib.load().sat_lstm_steps_bwd(arr, len(steps), _stream()), "sat_lstm_steps_bwd")
 
 
 def attn_query(x, W1, W2, q):

@@ -111,14 +111,32 @@ def attention_probe(trainer, hp, d, B, N, tile):
         + B * ntiles * pst                         # partial records written
         + 2 * d.d1 + d.loc_f * d.d1 + d.loc_k * d.loc_f + d.loc_f + d.d2)   # weights
     achieved = bytes_launch / avg_s / 1e9
+    traffic, pmc_src = _pmc_traffic()
     return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
             "kernel": "attn_energy_kernel (sat_attn_step_fwd tile phase)",
             "bytes_per_launch": int(bytes_launch), "avg_launch_us": round(avg_s * 1e6, 3),
             "launches_timed": reps * Tp,
             "note": "avg = HIP-event time of hipGraph-replayed back-to-back launches / count "
-                    "(includes the inter-kernel boundary); K1/V1 (14 MB) are L2/MALL-resident "
-                    "across steps, so achieved > HBM rate is possible"}
+                    "(includes the ~1.5 us inter-kernel boundary); traffic = memory-side bytes "
+                    "per launch from rocprofv3 FETCH_SIZE (x2, gfx950) + WRITE_SIZE passes "
+                    f"({pmc_src}); L2 does not survive the kernel boundary, so K1/V1 are "
+                    "re-fetched every decoder step"}
+
+
+def _pmc_traffic():
+    """Per-launch HBM bytes of the tile kernel from the newest committed PMC summary
+    (profiles/rNN_attn_energy_pmc.json, made by tools/pmc_attention.py + tools/pmc_summary.py)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles",
+                                          "r*_attn_energy_pmc.json")))
+    if not files:
+        return None, "no PMC summary"
+    try:
+        d = json.load(open(files[-1]))
+        return int(d["hbm_bytes_per_launch"]), os.path.basename(files[-1])
+    except (OSError, ValueError, KeyError):
+        return None, "unreadable PMC summary"
 
 
 def cpu_baseline(hp, args):

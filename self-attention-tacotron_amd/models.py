@@ -1,0 +1,222 @@
+"""Model plugin surface: encoder / decoder / model factories and ``model_fn``.
+
+Mirrors models/models.py:20-378: ``encoder_factory(params, is_training)``,
+``decoder_factory(params)``, ``tacotron_model_factory(hparams, model_dir, run_config,
+warm_start_from=None)`` keyed by the ``hparams.encoder`` / ``decoder`` / ``tacotron_model``
+strings (unknown -> ``ValueError``, as the reference), and the Estimator-shaped
+``DualSourceSelfAttentionTacotronModel`` whose ``model_fn(features, labels, mode, params)``
+returns an ``EstimatorSpec``:
+
+* TRAIN  -- one full training step on libsat_hip (masks drawn on the device, forward, BPTT,
+  [RCCL all-reduce], clip_by_global_norm(1.0) + TF Adam + Noam decay), loss = 0.1 L1 + BCE
+  (models/models.py:151-189);
+* EVAL   -- the teacher-forced evaluation loss ``loss_with_teacher`` (dropout off, zoneout
+  blend, BatchNorm moving statistics; models/models.py:208-231) and its metric components;
+* PREDICT -- free-running inference is SURVEY.md 8(f) row 1 (not on this path): raises
+  ``NotImplementedError``.
+
+``features`` / ``labels`` follow the reference's dataset records (``PreprocessedSourceData`` /
+``PreprocessedTargetData``, datasets/codes/dataset.py:45-48; ``codes`` is the mel target for
+LJSpeech/VCTK), as device tensors or numpy arrays.
+"""
+
+from __future__ import annotations
+
+from collections import namedtuple
+from typing import Dict, Optional
+
+import numpy as np
+import torch
+
+from . import params as PR
+from .engine import Tacotron
+from .train import Trainer
+
+
+class ModeKeys:
+    """tf.estimator.ModeKeys values."""
+    TRAIN = "train"
+    EVAL = "eval"
+    PREDICT = "infer"
+
+
+PreprocessedSourceData = namedtuple(
+    "PreprocessedSourceData", ["id", "key", "source", "source_length", "text"])
+PreprocessedTargetData = namedtuple(
+    "PreprocessedTargetData", ["id", "key", "codes", "target_length", "done", "code_loss_mask",
+                               "binary_loss_mask"])
+EstimatorSpec = namedtuple("EstimatorSpec", ["mode", "loss", "train_op", "predictions",
+                                             "eval_metric_ops"])
+
+
+class SelfAttentionCBHGEncoder:
+    """Configuration of modules/module.py:378-438 as built by encoder_factory
+    (models/models.py:325-346); executed by libsat_hip inside the model step."""
+
+    def __init__(self, is_training, **cfg):
+        self.is_training = is_training
+        self.config = cfg
+
+
+class DualSourceTransformerDecoder:
+    """Configuration of modules/module.py:1455-1562 as built by decoder_factory
+    (models/models.py:349-368)."""
+
+    def __init__(self, **cfg):
+        self.config = cfg
+
+
+def encoder_factory(params, is_training):
+    if params.encoder == "SelfAttentionCBHGEncoder":
+        return SelfAttentionCBHGEncoder(
+            is_training, cbhg_out_units=params.cbhg_out_units,
+            conv_channels=params.conv_channels, max_filter_width=params.max_filter_width,
+            projection1_out_channels=params.projection1_out_channels,
+            projection2_out_channels=params.projection2_out_channels,
+            num_highway=params.num_highway,
+            self_attention_out_units=params.self_attention_out_units,
+            self_attention_num_heads=params.self_attention_num_heads,
+            self_attention_num_hop=params.self_attention_num_hop,
+            prenet_out_units=params.encoder_prenet_out_units,
+            drop_rate=params.encoder_prenet_drop_rate,
+            zoneout_factor_cell=params.zoneout_factor_cell,
+            zoneout_factor_output=params.zoneout_factor_output,
+            self_attention_drop_rate=params.self_attention_drop_rate)
+    raise ValueError(f"Unknown encoder: {params.encoder}")
+
+
+def decoder_factory(params):
+    if params.decoder == "DualSourceTransformerDecoder":
+        return DualSourceTransformerDecoder(
+            prenet_out_units=params.decoder_prenet_out_units,
+            drop_rate=params.decoder_prenet_drop_rate,
+            attention_rnn_out_units=params.attention_out_units,
+            decoder_version=params.decoder_version, decoder_out_units=params.decoder_out_units,
+            num_mels=params.num_mels, outputs_per_step=params.outputs_per_step,
+            max_iters=params.max_iters, n_feed_frame=params.n_feed_frame,
+            zoneout_factor_cell=params.zoneout_factor_cell,
+            zoneout_factor_output=params.zoneout_factor_output,
+            self_attention_out_units=params.decoder_self_attention_out_units,
+            self_attention_num_heads=params.decoder_self_attention_num_heads,
+            self_attention_num_hop=params.decoder_self_attention_num_hop,
+            self_attention_drop_rate=params.decoder_self_attention_drop_rate)
+    raise ValueError(f"Unknown decoder: {params.decoder}")
+
+
+def _to_device(x, dev, dtype):
+    if isinstance(x, torch.Tensor):
+        return x.to(device=dev, dtype=dtype)
+    return torch.as_tensor(np.asarray(x), dtype=dtype, device=dev)
+
+
+class DualSourceSelfAttentionTacotronModel:
+    """Estimator-shaped model (models/models.py:20-320) over the libsat_hip engine."""
+
+    def __init__(self, params, model_dir=None, config=None, warm_start_from=None,
+                 device="cuda", seed: int = 1234,
+                 init_values: Optional[Dict[str, np.ndarray]] = None):
+        encoder_factory(params, True)                        # name checks, as the reference
+        if params.decoder not in ("DualSourceDecoder", "DualSourceTransformerDecoder"):
+            raise AssertionError(f"decoder must be a dual-source decoder: {params.decoder}")
+        decoder_factory(params)
+        if params.use_speaker_embedding and params.use_external_speaker_embedding:
+            raise AssertionError("only one of speaker_embedding / external_speaker_embedding")
+        PR.resolve_dims(params)                              # shapes this build supports
+        self.params = params
+        self.model_dir = model_dir
+        self.config = config
+        if warm_start_from is not None:
+            raise NotImplementedError("warm start from TF checkpoints is outside the hot path")
+        self.engine = Tacotron(params, device, seed=seed, init_values=init_values)
+        self._trainers: Dict[tuple, Trainer] = {}
+        self._seed = seed
+
+    @staticmethod
+    def learning_rate_decay(init_rate, global_step, step_factor):
+        """models/models.py:283-287 (host form; the device form lives in sat_adam_step)."""
+        warmup = 4000.0
+        step = float(global_step * step_factor + 1)
+        return init_rate * warmup ** 0.5 * min(step * warmup ** -1.5, step ** -0.5)
+
+    def _batch(self, features, labels):
+        dev = self.engine.device
+        b = {"source": _to_device(features.source, dev, torch.int64),
+             "source_length": _to_device(features.source_length, dev, torch.int64),
+             "mel": _to_device(labels.codes, dev, torch.float32),
+             "mel_mask": _to_device(labels.code_loss_mask, dev, torch.float32),
+             "done": _to_device(labels.done, dev, torch.float32),
+             "done_mask": _to_device(labels.binary_loss_mask, dev, torch.float32),
+             "target_length": _to_device(labels.target_length, dev, torch.int64)}
+        return b
+
+    def _trainer(self, batch) -> Trainer:
+        B, N = batch["source"].shape
+        Tp = batch["mel"].shape[1] // self.params.outputs_per_step
+        key = (B, N, Tp)
+        if key not in self._trainers:
+            shared = next(iter(self._trainers.values()), None)
+            tr = Trainer(self.engine, B, N, Tp, seed=self._seed)
+            if shared is not None:          # one optimiser state per model
+                tr.exp_avg, tr.exp_avg_sq = shared.exp_avg, shared.exp_avg_sq
+                tr.global_step, tr.seed = shared.global_step, shared.seed
+            self._trainers[key] = tr
+        return self._trainers[key]
+
+    def model_fn(self, features, labels, mode, params=None) -> EstimatorSpec:
+        if mode == ModeKeys.PREDICT:
+            raise NotImplementedError("free-running inference (PREDICT) is SURVEY.md 8(f) row 1")
+        batch = self._batch(features, labels)
+        if mode == ModeKeys.TRAIN:
+            tr = self._trainer(batch)
+            out = tr.step(batch)
+            return EstimatorSpec(mode, loss=out["loss"], train_op=tr.global_step,
+                                 predictions=None, eval_metric_ops=None)
+        if mode == ModeKeys.EVAL:
+            with torch.no_grad():
+                out, _ = self.engine.forward(batch, None, training=False, need_grad=False)
+            metrics = {"loss_with_teacher": out["loss"], "code_loss_with_teacher": 0.1 * out["l1"],
+                       "done_loss_with_teacher": out["bce"]}
+            return EstimatorSpec(mode, loss=out["loss"], train_op=None, predictions=None,
+                                 eval_metric_ops=metrics)
+        raise ValueError(f"Unknown mode: {mode}")
+
+    # ---- tf.estimator.Estimator-like drivers
+    def train(self, input_fn, steps: int):
+        loss = None
+        it = iter(input_fn())
+        for _ in range(steps):
+            features, labels = next(it)
+            loss = self.model_fn(features, labels, ModeKeys.TRAIN, self.params).loss
+        return loss
+
+    def evaluate(self, input_fn, steps: int = 1):
+        tot = 0.0
+        it = iter(input_fn())
+        for _ in range(steps):
+            features, labels = next(it)
+            tot += float(self.model_fn(features, labels, ModeKeys.EVAL, self.params).loss.item())
+        return {"loss": tot / steps}
+
+
+def tacotron_model_factory(hparams, model_dir, run_config, warm_start_from=None, **kw):
+    if hparams.tacotron_model == "DualSourceSelfAttentionTacotronModel":
+        return DualSourceSelfAttentionTacotronModel(hparams, model_dir, config=run_config,
+                                                    warm_start_from=warm_start_from, **kw)
+    raise ValueError(f"Unknown Tacotron model: {hparams.tacotron_model}")
+
+
+def synthetic_input_fn(params, batch_size: int, N: int = 200, T: int = 1000, shape="max",
+                       seed: int = 0):
+    """An input_fn over seeded synthetic batches with the dataset contract of SURVEY.md 8(d)."""
+    from . import data
+
+    def input_fn():
+        step = 0
+        while True:
+            b = data.synthetic_batch(params, batch_size, N=N, T=T, seed=seed + step, shape=shape)
+            step += 1
+            ids = np.arange(batch_size)
+            yield (PreprocessedSourceData(ids, ids, b["source"], b["source_length"], None),
+                   PreprocessedTargetData(ids, ids, b["mel"], b["target_length"], b["done"],
+                                          b["mel_mask"], b["done_mask"]))
+    return input_fn

@@ -237,9 +237,13 @@ def _glorot(rng: np.random.Generator, shape: Tuple[int, ...]) -> np.ndarray:
 def init_params(hp, seed: int = 1234) -> Dict[str, np.ndarray]:
     """Seeded synthetic weights (glorot kernels, zero biases, highway T
     bias -1, BN gamma 1 / beta 0).  float32 arrays."""
+    return init_specs(param_specs(hp), seed)
+
+
+def init_specs(specs: List[ParamSpec], seed: int = 1234) -> Dict[str, np.ndarray]:
     rng = np.random.default_rng(seed)
     out: Dict[str, np.ndarray] = {}
-    for p in param_specs(hp):
+    for p in specs:
         if p.init == "glorot":
             a = _glorot(rng, p.shape)
         elif p.init == "zeros":

@@ -1,0 +1,60 @@
+"""Plugin surface without a GPU: AttentionOptions / factory dispatch and error behaviour
+(modules/attentions.py:15-62, models/attention_factories.py:11-37, models/models.py:325-378)."""
+import pytest
+
+import _sat_path
+
+_sat_path.load()
+from sat_amd import attentions as A  # noqa: E402
+from sat_amd import hparams, models as M  # noqa: E402
+
+
+def test_attention_options_fields():
+    assert A.AttentionOptions._fields == ("attention", "num_units", "attention_kernel",
+                                          "attention_filters", "smoothing", "cumulative_weights",
+                                          "use_transition_agent")
+
+
+def test_dual_source_factory_reads_hparams():
+    hp = hparams.ljspeech_hparams()
+    f1, f2 = A.dual_source_attention_factory(hp)
+    assert f1.options == A.AttentionOptions("forward", 224, 10, 5, False, False, False)
+    assert f2.options == A.AttentionOptions("additive", 32, 10, 5, False, False, False)
+    f = A.attention_factory(hp)
+    assert f.options.num_units == hp.attention_out_units
+
+
+def test_mechanism_dispatch_errors():
+    unknown = A.attention_mechanism_factory(A.AttentionOptions("nope", 8, 3, 2, False, False, False))
+    with pytest.raises(ValueError, match="Unknown attention mechanism"):
+        unknown(None, None)
+    for kind in ("location_sensitive", "teacher_forcing_forward", "teacher_forcing_additive"):
+        fn = A.attention_mechanism_factory(A.AttentionOptions(kind, 8, 3, 2, False, False, False))
+        with pytest.raises(NotImplementedError):
+            fn(None, None)
+
+
+@pytest.mark.parametrize("field,factory", [("encoder", lambda hp: M.encoder_factory(hp, True)),
+                                           ("decoder", M.decoder_factory),
+                                           ("tacotron_model",
+                                            lambda hp: M.tacotron_model_factory(hp, None, None))])
+def test_model_factories_reject_unknown_names(field, factory):
+    hp = hparams.ljspeech_hparams()
+    hp.set_hparam(field, "NoSuchThing")
+    with pytest.raises(ValueError, match="Unknown"):
+        factory(hp)
+
+
+def test_factories_build_from_reference_names():
+    hp = hparams.ljspeech_hparams()
+    enc = M.encoder_factory(hp, True)
+    dec = M.decoder_factory(hp)
+    assert enc.config["conv_channels"] == 128 and enc.config["max_filter_width"] == 16
+    assert dec.config["outputs_per_step"] == 2 and dec.config["max_iters"] == 500
+
+
+def test_learning_rate_decay_matches_reference_formula():
+    f = M.DualSourceSelfAttentionTacotronModel.learning_rate_decay
+    assert f(5e-4, 0, 1) == pytest.approx(5e-4 * 4000 ** 0.5 * 4000 ** -1.5)
+    assert f(5e-4, 3999, 1) == pytest.approx(5e-4 * 4000 ** 0.5 * 4000 ** -0.5)
+    assert f(5e-4, 15999, 1) == pytest.approx(5e-4 * 4000 ** 0.5 * 16000 ** -0.5)

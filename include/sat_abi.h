@@ -292,11 +292,13 @@ int sat_softmax_bwd(const float* P, const float* dPd, const float* mask, float* 
 
 /* Loss of models/models.py:159-173: l1_weight * L1(mel, tgt; tmask) + sigmoid xent(stop, done;
  * dmask), tf.losses SUM_BY_NONZERO_WEIGHTS.  out[0..4] = loss, L1, BCE, counts; if dmel/dstop
- * are given, also writes the gradients of out[0]. */
+ * are given, also writes the gradients of out[0].  Deterministic two-pass fp64 reduction over a
+ * caller-provided workspace of sat_workspace_loss() bytes. */
+int64_t sat_workspace_loss(void);
 int sat_loss_fwd_bwd(const float* mel, const float* tgt, const float* tmask, const float* stop,
                      const float* done, const float* dmask, int32_t B, int32_t T, int32_t M,
                      int32_t Tp, float l1_weight, float* out, float* dmel, float* dstop,
-                     void* stream);
+                     void* workspace, void* stream);
 
 /* ---------------------------------------------------------------- optimiser
  * models/models.py:175-189 + :283-287 over the whole flat arena in three launches:

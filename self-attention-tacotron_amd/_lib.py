@@ -114,7 +114,7 @@ SIGNATURES = {
     "sat_axpby": [_P, _P, _I64, _F, _F, _P],
     "sat_softmax_fwd": [_P, _P, _P, _P, _I64, _I32, _I32, _I32, _F, _P],
     "sat_softmax_bwd": [_P, _P, _P, _P, _I64, _I32, _F, _P],
-    "sat_loss_fwd_bwd": [_P, _P, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _F, _P, _P, _P, _P],
+    "sat_loss_fwd_bwd": [_P, _P, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _F, _P, _P, _P, _P, _P],
 }
 
 SIGNATURES.update({
@@ -125,7 +125,8 @@ SIGNATURES.update({
 })
 
 RESTYPES = {"sat_workspace_colreduce": (ctypes.c_int64, [_I32, _I32]),
-            "sat_workspace_adam": (ctypes.c_int64, [])}
+            "sat_workspace_adam": (ctypes.c_int64, []),
+            "sat_workspace_loss": (ctypes.c_int64, [])}
 
 _lib: Optional[ctypes.CDLL] = None
 

@@ -284,19 +284,41 @@ __global__ void softmax_bwd_kernel(const float* __restrict__ P, const float* __r
 
 // ---------------------------------------------------------------- loss (models/models.py:159-173)
 // pass 1 (one workgroup): sums and non-zero-weight counts
-__global__ void __launch_bounds__(1024) loss_reduce_kernel(
+// Loss pass 1: kLossBlocks workgroups, one wave per target row [M] (float4 when M % 4 == 0),
+// fp64 partials {sum w|mel-tgt|, #weighted elements, sum w*xent, #weighted stop entries} per
+// workgroup; pass 1b sums them in a fixed order (deterministic) and writes
+// out = {loss, L1, BCE, count1, count2}.
+constexpr int kLossBlocks = 256;
+
+__global__ void __launch_bounds__(256) loss_partial_kernel(
     const float* __restrict__ mel, const float* __restrict__ tgt, const float* __restrict__ tmask,
     const float* __restrict__ stop, const float* __restrict__ done, const float* __restrict__ dmask,
-    int B, int T, int M, int Tp, float l1w, float* __restrict__ out) {
-  __shared__ double sh[4][16];
+    int B, int T, int M, int Tp, double* __restrict__ part) {
+  __shared__ double sh[4][4];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   double l1 = 0.0, c1 = 0.0, bce = 0.0, c2 = 0.0;
-  const int64_t n1 = (int64_t)B * T * M;
-  for (int64_t i = threadIdx.x; i < n1; i += blockDim.x) {
-    const float w = tmask[i / M];
-    if (w != 0.f) { l1 += (double)w * fabsf(mel[i] - tgt[i]); c1 += 1.0; }
+  const int rows = B * T;
+  const bool vec = (M & 3) == 0;
+  for (int r = blockIdx.x * 4 + wv; r < rows; r += gridDim.x * 4) {
+    const float w = tmask[r];
+    if (w == 0.f) continue;                       // wave-uniform
+    const float* mr = mel + (int64_t)r * M;
+    const float* tr = tgt + (int64_t)r * M;
+    float acc = 0.f;
+    if (vec) {
+      for (int c = lane; c < (M >> 2); c += 64) {
+        const float4 x = reinterpret_cast<const float4*>(mr)[c];
+        const float4 y = reinterpret_cast<const float4*>(tr)[c];
+        acc += fabsf(x.x - y.x) + fabsf(x.y - y.y) + fabsf(x.z - y.z) + fabsf(x.w - y.w);
+      }
+    } else {
+      for (int c = lane; c < M; c += 64) acc += fabsf(mr[c] - tr[c]);
+    }
+    l1 += (double)w * acc;
+    if (lane == 0) c1 += (double)M;
   }
-  const int64_t n2 = (int64_t)B * Tp;
-  for (int64_t i = threadIdx.x; i < n2; i += blockDim.x) {
+  const int n2 = B * Tp;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n2; i += gridDim.x * 256) {
     const float w = dmask[i];
     if (w != 0.f) {
       const float x = stop[i], z = done[i];
@@ -304,19 +326,39 @@ __global__ void __launch_bounds__(1024) loss_reduce_kernel(
       c2 += 1.0;
     }
   }
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   for (int o = 32; o > 0; o >>= 1) {
     l1 += __shfl_xor(l1, o, 64); c1 += __shfl_xor(c1, o, 64);
     bce += __shfl_xor(bce, o, 64); c2 += __shfl_xor(c2, o, 64);
   }
   if (lane == 0) { sh[0][wv] = l1; sh[1][wv] = c1; sh[2][wv] = bce; sh[3][wv] = c2; }
   __syncthreads();
+  if (threadIdx.x < 4) {
+    const int k = threadIdx.x;
+    part[blockIdx.x * 4 + k] = (sh[k][0] + sh[k][1]) + (sh[k][2] + sh[k][3]);
+  }
+}
+
+__global__ void __launch_bounds__(256) loss_finish_kernel(const double* __restrict__ part,
+                                                          int nblocks, float l1w,
+                                                          float* __restrict__ out) {
+  __shared__ double sh[4][4];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  double a[4] = {0, 0, 0, 0};
+  for (int i = threadIdx.x; i < nblocks; i += 256)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) a[k] += part[i * 4 + k];
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    for (int o = 32; o > 0; o >>= 1) a[k] += __shfl_xor(a[k], o, 64);
+  if (lane == 0)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) sh[k][wv] = a[k];
+  __syncthreads();
   if (threadIdx.x == 0) {
-    double a[4] = {0, 0, 0, 0};
-    for (int k = 0; k < 4; ++k)
-      for (int w = 0; w < (int)(blockDim.x >> 6); ++w) a[k] += sh[k][w];
-    const double cl1 = fmax(a[1], 1.0), cb = fmax(a[3], 1.0);
-    const double L1 = a[0] / cl1, BCE = a[2] / cb;
+    double t[4];
+    for (int k = 0; k < 4; ++k) t[k] = (sh[k][0] + sh[k][1]) + (sh[k][2] + sh[k][3]);
+    const double cl1 = fmax(t[1], 1.0), cb = fmax(t[3], 1.0);
+    const double L1 = t[0] / cl1, BCE = t[2] / cb;
     out[0] = (float)(l1w * L1 + BCE);   // loss
     out[1] = (float)L1;
     out[2] = (float)BCE;
@@ -559,14 +601,23 @@ extern "C" int sat_softmax_bwd(const float* P, const float* dPd, const float* ma
   return SAT_OK;
 }
 
+extern "C" int64_t sat_workspace_loss(void) { return (int64_t)kLossBlocks * 4 * sizeof(double); }
+
 extern "C" int sat_loss_fwd_bwd(const float* mel, const float* tgt, const float* tmask,
                                 const float* stop, const float* done, const float* dmask,
                                 int32_t B, int32_t T, int32_t M, int32_t Tp, float l1_weight,
-                                float* out, float* dmel, float* dstop, void* stream) {
-  SAT_CHECK_ARG(mel && tgt && tmask && stop && done && dmask && out, "sat_loss_fwd_bwd: bad args");
+                                float* out, float* dmel, float* dstop, void* workspace,
+                                void* stream) {
+  SAT_CHECK_ARG(mel && tgt && tmask && stop && done && dmask && out && workspace,
+                "sat_loss_fwd_bwd: bad args");
+  SAT_CHECK_ARG(((M & 3) != 0) || (((uintptr_t)mel | (uintptr_t)tgt) & 15) == 0,
+                "sat_loss_fwd_bwd: mel/targets must be 16-byte aligned");
   hipStream_t s = as_stream(stream);
-  hipLaunchKernelGGL(loss_reduce_kernel, dim3(1), dim3(1024), 0, s, mel, tgt, tmask, stop, done,
-                     dmask, B, T, M, Tp, l1_weight, out);
+  double* part = reinterpret_cast<double*>(workspace);
+  hipLaunchKernelGGL(loss_partial_kernel, dim3(kLossBlocks), dim3(256), 0, s, mel, tgt, tmask,
+                     stop, done, dmask, B, T, M, Tp, part);
+  hipLaunchKernelGGL(loss_finish_kernel, dim3(1), dim3(256), 0, s, part, kLossBlocks, l1_weight,
+                     out);
   if (dmel && dstop) {
     const int64_t n = (int64_t)B * T * M + (int64_t)B * Tp;
     hipLaunchKernelGGL(loss_grad_kernel, dim3(grid_for(n)), dim3(256), 0, s, mel, tgt, tmask, stop,

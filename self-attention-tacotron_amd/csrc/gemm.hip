@@ -39,11 +39,16 @@ struct GemmP {
   int64_t a_sbatch2, b_sbatch2, c_sbatch2, mul_sbatch2;
   const float* add;
   int64_t add_sm, add_sbatch;
-  int a_kcontig, b_ncontig, a_vec, b_vec;
   int splits, kchunk;          // split-K: grid.z = splits (batch == 1), partial slabs in ws
   float* ws;
+  int remap;                   // XCD-aware tile order over the xy plane
 };
 
+// Operand loader variants, chosen on the host so the main loop carries no mode branches.
+enum AMode { A_K = 0, A_M = 1, A_IM2COL = 2, A_IM2COLT = 3, A_GEN = 4 };
+enum BMode { B_N = 0, B_K = 1, B_FLIP = 2, B_GEN = 3 };
+
+// generic (scalar) element access, any strides / modes
 __device__ __forceinline__ float load_a(const GemmP& p, const float* A, int m, int k) {
   if (m >= p.M || k >= p.K) return 0.f;
   if (p.a_mode == 0) return A[m * p.a_sm + k * p.a_sk];
@@ -54,7 +59,6 @@ __device__ __forceinline__ float load_a(const GemmP& p, const float* A, int m, i
     if (row < 0 || row >= p.a_L) return 0.f;
     return A[(int64_t)(s * p.a_L + row) * p.a_sm + c * p.a_sk];
   }
-  // mode 2: transposed im2col, (i, k) -> im2col(k, i)
   const int s = k / p.a_L, n = k - s * p.a_L;
   const int tap = m / p.a_C, c = m - tap * p.a_C;
   const int row = n + tap - p.a_shift;
@@ -78,100 +82,180 @@ __device__ __forceinline__ float apply_act(float v, int act) {
   }
 }
 
-template <int BM, int BN>
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+
+template <int BM, int BN, int AM, int BMD>
 __global__ void __launch_bounds__(256) gemm_kernel(GemmP p) {
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int SM = WM / 32, SN = WN / 32;
-  constexpr int EA = BM * BK / 256, EB = BN * BK / 256;   // scalars per thread per tile
-  constexpr int PA = 1, PB = 4;                            // LDS row padding (floats)
-  __shared__ float As[2][BK][BM + PA];
+  constexpr bool A_MC = (AM == A_M || AM == A_IM2COLT);        // loads run along m
+  constexpr bool B_NC = (BMD == B_N);                          // loads run along n
+  constexpr int PA = A_MC ? 4 : 1, PB = B_NC ? 4 : 1;          // LDS row padding
+  constexpr int NA = (AM == A_GEN) ? BM * BK / 256 : BM * BK / 1024;   // per thread
+  constexpr int NB = (BMD == B_GEN) ? BN * BK / 256 : BN * BK / 1024;
+  __shared__ __attribute__((aligned(16))) float As[2][BK][BM + PA];
   __shared__ __attribute__((aligned(16))) float Bs[2][BK][BN + PB];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = (wave >> 1) * WM, wn = (wave & 1) * WN;
+  int tx = blockIdx.x, ty = blockIdx.y;
+  if (p.remap) {   // bijective XCD swizzle: consecutive tiles (one A row panel) share an L2
+    const int nwg = gridDim.x * gridDim.y, orig = blockIdx.y * gridDim.x + blockIdx.x;
+    const int q = nwg >> 3, r = nwg & 7, xcd = orig & 7;
+    const int t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+    ty = t / gridDim.x;
+    tx = t - ty * gridDim.x;
+  }
   int bz, bz2, split;
   if (p.splits > 1) { bz = 0; bz2 = 0; split = blockIdx.z; }
   else { bz = blockIdx.z / p.batch2; bz2 = blockIdx.z - bz * p.batch2; split = 0; }
-  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  const int m0 = ty * BM, n0 = tx * BN;
   const float* A = p.A + bz * p.a_sbatch + bz2 * p.a_sbatch2;
   const float* B = p.B + bz * p.b_sbatch + bz2 * p.b_sbatch2;
   const int kbeg = split * p.kchunk;
   const int kend = min(p.K, kbeg + p.kchunk);
 
-  float ra[EA], rb[EB];
-  auto fetch = [&](int k0) {
-    if (p.a_vec) {   // k-contiguous, 16-B aligned rows: float4 along k
+  // ---- per-thread loader state hoisted out of the K loop
+  const float* arow[NA > 0 ? NA : 1];      // im2col: row base of this thread's output rows
+  int an[NA > 0 ? NA : 1];                 // im2col: position in utterance, -BIG if invalid
+  int aps[NA > 0 ? NA : 1], apn[NA > 0 ? NA : 1];   // im2col-T: (s, n) of the current k
+  if constexpr (AM == A_IM2COL) {
 #pragma unroll
-      for (int i = 0; i < EA / 4; ++i) {
-        const int e = tid + i * 256;            // float4 index within the tile
-        const int m = e / (BK / 4), kq = (e % (BK / 4)) * 4;
+    for (int i = 0; i < NA; ++i) {
+      const int gm = m0 + ((tid + i * 256) >> 3);
+      const int s = gm / p.a_L, n = gm - s * p.a_L;
+      arow[i] = A + (int64_t)s * p.a_L * p.a_sm;
+      an[i] = gm < p.M ? n : -(1 << 28);
+    }
+  }
+  if constexpr (AM == A_IM2COLT) {
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int pos = kbeg + (tid + i * 256) / (BM / 4);
+      aps[i] = pos / p.a_L;
+      apn[i] = pos - aps[i] * p.a_L;
+    }
+  }
+  int atap = 0, ac0 = 0;
+  if constexpr (AM == A_IM2COLT) { atap = m0 / p.a_C; ac0 = m0 - atap * p.a_C; }
+
+  float4 ra4[(AM == A_GEN) ? 1 : NA];
+  float ras[(AM == A_GEN) ? NA : 1];
+  float4 rb4[(BMD == B_GEN) ? 1 : NB];
+  float rbs[(BMD == B_GEN) ? NB : 1];
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+
+  auto fetch = [&](int k0) {
+    if constexpr (AM == A_K) {
+#pragma unroll
+      for (int i = 0; i < NA; ++i) {
+        const int e = tid + i * 256, m = e >> 3, kq = (e & 7) * 4;
         const int gm = m0 + m, gk = k0 + kq;
-        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (gm < p.M && gk < kend) v = *reinterpret_cast<const float4*>(A + gm * p.a_sm + gk);
-        ra[4 * i + 0] = v.x; ra[4 * i + 1] = v.y; ra[4 * i + 2] = v.z; ra[4 * i + 3] = v.w;
+        ra4[i] = (gm < p.M && gk < kend) ? ld4(A + (int64_t)gm * p.a_sm + gk) : z4;
+      }
+    } else if constexpr (AM == A_M) {
+#pragma unroll
+      for (int i = 0; i < NA; ++i) {
+        const int e = tid + i * 256, k = e / (BM / 4), mq = (e % (BM / 4)) * 4;
+        const int gm = m0 + mq, gk = k0 + k;
+        ra4[i] = (gm < p.M && gk < kend) ? ld4(A + (int64_t)gk * p.a_sk + gm) : z4;
+      }
+    } else if constexpr (AM == A_IM2COL) {
+      const int tap = k0 / p.a_C, c0 = k0 - tap * p.a_C;
+#pragma unroll
+      for (int i = 0; i < NA; ++i) {
+        const int kq = ((tid + i * 256) & 7) * 4;
+        const int row = an[i] + tap - p.a_shift;
+        const bool ok = row >= 0 && row < p.a_L && k0 + kq < kend;
+        ra4[i] = ok ? ld4(arow[i] + (int64_t)row * p.a_sm + c0 + kq) : z4;
+      }
+    } else if constexpr (AM == A_IM2COLT) {
+#pragma unroll
+      for (int i = 0; i < NA; ++i) {
+        const int e = tid + i * 256, k = e / (BM / 4), mq = (e % (BM / 4)) * 4;
+        const int row = apn[i] + atap - p.a_shift;
+        const bool ok = (k0 + k < kend) && row >= 0 && row < p.a_L && (m0 + mq < p.M);
+        ra4[i] = ok ? ld4(A + (int64_t)(aps[i] * p.a_L + row) * p.a_sm + ac0 + mq) : z4;
+        apn[i] += BK;                                  // next K-tile of this thread
+        while (apn[i] >= p.a_L) { apn[i] -= p.a_L; ++aps[i]; }
       }
     } else {
 #pragma unroll
-      for (int i = 0; i < EA; ++i) {
-        const int e = tid + i * 256;
-        int m, k;
-        if (p.a_kcontig) { m = e / BK; k = e % BK; } else { k = e / BM; m = e % BM; }
-        ra[i] = (k0 + k < kend) ? load_a(p, A, m0 + m, k0 + k) : 0.f;
+      for (int i = 0; i < NA; ++i) {
+        const int e = tid + i * 256, m = e / BK, k = e % BK;
+        ras[i] = (k0 + k < kend) ? load_a(p, A, m0 + m, k0 + k) : 0.f;
       }
     }
-    if (p.b_vec) {   // n-contiguous, 16-B aligned rows: float4 along n
+    if constexpr (BMD == B_N) {
 #pragma unroll
-      for (int i = 0; i < EB / 4; ++i) {
-        const int e = tid + i * 256;
-        const int k = e / (BN / 4), nq = (e % (BN / 4)) * 4;
+      for (int i = 0; i < NB; ++i) {
+        const int e = tid + i * 256, k = e / (BN / 4), nq = (e % (BN / 4)) * 4;
         const int gk = k0 + k, gn = n0 + nq;
-        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (gk < kend && gn < p.N) v = *reinterpret_cast<const float4*>(B + gk * p.b_sk + gn);
-        rb[4 * i + 0] = v.x; rb[4 * i + 1] = v.y; rb[4 * i + 2] = v.z; rb[4 * i + 3] = v.w;
+        rb4[i] = (gk < kend && gn < p.N) ? ld4(B + (int64_t)gk * p.b_sk + gn) : z4;
+      }
+    } else if constexpr (BMD == B_K) {
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {
+        const int e = tid + i * 256, n = e >> 3, kq = (e & 7) * 4;
+        const int gk = k0 + kq, gn = n0 + n;
+        rb4[i] = (gk < kend && gn < p.N) ? ld4(B + (int64_t)gn * p.b_sn + gk) : z4;
+      }
+    } else if constexpr (BMD == B_FLIP) {
+      const int tap = k0 / p.b_C, o0 = k0 - tap * p.b_C;
+      const float* Wt = B + (int64_t)(p.b_taps - 1 - tap) * p.N * p.b_C + o0;
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {
+        const int e = tid + i * 256, n = e >> 3, kq = (e & 7) * 4;
+        const int gn = n0 + n;
+        rb4[i] = (gn < p.N && k0 + kq < kend) ? ld4(Wt + (int64_t)gn * p.b_C + kq) : z4;
       }
     } else {
 #pragma unroll
-      for (int i = 0; i < EB; ++i) {
-        const int e = tid + i * 256;
-        int k, n;
-        if (p.b_ncontig) { k = e / BN; n = e % BN; } else { n = e / BK; k = e % BK; }
-        rb[i] = (k0 + k < kend) ? load_b(p, B, k0 + k, n0 + n) : 0.f;
+      for (int i = 0; i < NB; ++i) {
+        const int e = tid + i * 256, n = e / BK, k = e % BK;
+        rbs[i] = (k0 + k < kend) ? load_b(p, B, k0 + k, n0 + n) : 0.f;
       }
     }
   };
   auto stash = [&](int buf) {
-    if (p.a_vec) {
+    if constexpr (AM == A_K || AM == A_IM2COL) {
 #pragma unroll
-      for (int i = 0; i < EA / 4; ++i) {
-        const int e = tid + i * 256;
-        const int m = e / (BK / 4), kq = (e % (BK / 4)) * 4;
+      for (int i = 0; i < NA; ++i) {
+        const int e = tid + i * 256, m = e >> 3, kq = (e & 7) * 4;
+        As[buf][kq + 0][m] = ra4[i].x; As[buf][kq + 1][m] = ra4[i].y;
+        As[buf][kq + 2][m] = ra4[i].z; As[buf][kq + 3][m] = ra4[i].w;
+      }
+    } else if constexpr (AM == A_M || AM == A_IM2COLT) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) As[buf][kq + j][m] = ra[4 * i + j];
+      for (int i = 0; i < NA; ++i) {
+        const int e = tid + i * 256, k = e / (BM / 4), mq = (e % (BM / 4)) * 4;
+        *reinterpret_cast<float4*>(&As[buf][k][mq]) = ra4[i];
       }
     } else {
 #pragma unroll
-      for (int i = 0; i < EA; ++i) {
-        const int e = tid + i * 256;
-        int m, k;
-        if (p.a_kcontig) { m = e / BK; k = e % BK; } else { k = e / BM; m = e % BM; }
-        As[buf][k][m] = ra[i];
+      for (int i = 0; i < NA; ++i) {
+        const int e = tid + i * 256, m = e / BK, k = e % BK;
+        As[buf][k][m] = ras[i];
       }
     }
-    if (p.b_vec) {
+    if constexpr (BMD == B_N) {
 #pragma unroll
-      for (int i = 0; i < EB / 4; ++i) {
-        const int e = tid + i * 256;
-        const int k = e / (BN / 4), nq = (e % (BN / 4)) * 4;
-        *reinterpret_cast<float4*>(&Bs[buf][k][nq]) =
-            make_float4(rb[4 * i], rb[4 * i + 1], rb[4 * i + 2], rb[4 * i + 3]);
+      for (int i = 0; i < NB; ++i) {
+        const int e = tid + i * 256, k = e / (BN / 4), nq = (e % (BN / 4)) * 4;
+        *reinterpret_cast<float4*>(&Bs[buf][k][nq]) = rb4[i];
+      }
+    } else if constexpr (BMD == B_K || BMD == B_FLIP) {
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {
+        const int e = tid + i * 256, n = e >> 3, kq = (e & 7) * 4;
+        Bs[buf][kq + 0][n] = rb4[i].x; Bs[buf][kq + 1][n] = rb4[i].y;
+        Bs[buf][kq + 2][n] = rb4[i].z; Bs[buf][kq + 3][n] = rb4[i].w;
       }
     } else {
 #pragma unroll
-      for (int i = 0; i < EB; ++i) {
-        const int e = tid + i * 256;
-        int k, n;
-        if (p.b_ncontig) { k = e / BN; n = e % BN; } else { n = e / BK; k = e % BK; }
-        Bs[buf][k][n] = rb[i];
+      for (int i = 0; i < NB; ++i) {
+        const int e = tid + i * 256, n = e / BK, k = e % BK;
+        Bs[buf][k][n] = rbs[i];
       }
     }
   };
@@ -323,6 +407,27 @@ extern "C" int sat_gemm_rowdot(int32_t M, int32_t N, int32_t K, const float* A, 
   return SAT_OK;
 }
 
+using namespace sat;
+
+template <int BM, int BN>
+static hipError_t launch_tiles(int am, int bm, dim3 grid, hipStream_t s, const GemmP& p) {
+#define SAT_GEMM_CASE(A_, B_)                                                               \
+  if (am == A_ && bm == B_) {                                                               \
+    hipLaunchKernelGGL((gemm_kernel<BM, BN, A_, B_>), grid, dim3(256), 0, s, p);            \
+    return hipGetLastError();                                                               \
+  }
+  SAT_GEMM_CASE(A_K, B_N)
+  SAT_GEMM_CASE(A_K, B_K)
+  SAT_GEMM_CASE(A_M, B_N)
+  SAT_GEMM_CASE(A_M, B_K)
+  SAT_GEMM_CASE(A_IM2COL, B_N)
+  SAT_GEMM_CASE(A_IM2COL, B_FLIP)
+  SAT_GEMM_CASE(A_IM2COLT, B_N)
+#undef SAT_GEMM_CASE
+  hipLaunchKernelGGL((gemm_kernel<BM, BN, A_GEN, B_GEN>), grid, dim3(256), 0, s, p);
+  return hipGetLastError();
+}
+
 extern "C" int sat_gemm(const SatGemmDesc* d, void* stream) {
   using namespace sat;
   SAT_CHECK_ARG(d != nullptr, "sat_gemm: null descriptor");
@@ -349,19 +454,31 @@ extern "C" int sat_gemm(const SatGemmDesc* d, void* stream) {
   p.a_sbatch2 = d->a_sbatch2; p.b_sbatch2 = d->b_sbatch2; p.c_sbatch2 = d->c_sbatch2;
   p.mul_sbatch2 = d->mul_sbatch2;
   p.add = d->add; p.add_sm = d->add_sm; p.add_sbatch = d->add_sbatch;
-  // coalescing order / vector width of the tile loaders
-  p.a_kcontig = (d->a_mode == 1) ? 1 : (d->a_mode == 2 ? 0 : (d->a_sk == 1 ? 1 : 0));
-  p.b_ncontig = (d->b_mode == 1) ? 0 : (d->b_sn == 1 ? 1 : 0);
-  const bool bstr_ok = (p.a_sbatch % 4 == 0) && (p.a_sbatch2 % 4 == 0);
-  p.a_vec = (d->a_mode == 0 && d->a_sk == 1 && d->a_sm % 4 == 0 && d->K % 4 == 0 &&
-             aligned16(d->A) && bstr_ok) ? 1 : 0;
-  p.b_vec = (d->b_mode == 0 && d->b_sn == 1 && d->b_sk % 4 == 0 && d->N % 4 == 0 &&
-             aligned16(d->B) && p.b_sbatch % 4 == 0 && p.b_sbatch2 % 4 == 0) ? 1 : 0;
   hipStream_t s = as_stream(stream);
   const int nb = d->batch * p.batch2;
   const bool big = (int64_t)d->M * d->N * nb >= (int64_t)256 * 128 * 128 && d->N >= 96 && d->M >= 96;
   const int BMs = big ? 128 : 64;
-  const int tiles = ceil_div(d->M, BMs) * ceil_div(d->N, BMs) * nb;
+  // ---- operand loader variants (vector paths need 16-B aligned rows / batch strides)
+  const bool astr = (p.a_sbatch % 4 == 0) && (p.a_sbatch2 % 4 == 0) && aligned16(d->A);
+  const bool bstr = (p.b_sbatch % 4 == 0) && (p.b_sbatch2 % 4 == 0) && aligned16(d->B);
+  int am = A_GEN, bm = B_GEN;
+  if (d->a_mode == 0) {
+    if (astr && d->a_sk == 1 && d->a_sm % 4 == 0 && d->K % 4 == 0) am = A_K;
+    else if (astr && d->a_sm == 1 && d->a_sk % 4 == 0 && d->M % 4 == 0) am = A_M;
+  } else if (d->a_mode == 1) {
+    if (astr && d->a_sk == 1 && d->a_sm % 4 == 0 && d->a_C % BK == 0) am = A_IM2COL;
+  } else {
+    if (astr && d->a_sk == 1 && d->a_sm % 4 == 0 && d->a_C % BMs == 0) am = A_IM2COLT;
+  }
+  if (d->b_mode == 0) {
+    if (bstr && d->b_sn == 1 && d->b_sk % 4 == 0 && d->N % 4 == 0) bm = B_N;
+    else if (bstr && d->b_sk == 1 && d->b_sn % 4 == 0 && d->K % 4 == 0) bm = B_K;
+  } else {
+    if (bstr && d->b_C % BK == 0) bm = B_FLIP;
+  }
+  if (am == A_GEN || bm == B_GEN) { am = A_GEN; bm = B_GEN; }   // instantiated combinations
+  const int gx = ceil_div(d->N, BMs), gy = ceil_div(d->M, BMs);
+  const int tiles = gx * gy * nb;
   // split-K for weight-gradient-shaped products (few output tiles, long reduction)
   p.splits = 1;
   p.kchunk = d->K;
@@ -376,15 +493,15 @@ extern "C" int sat_gemm(const SatGemmDesc* d, void* stream) {
       p.splits = S;
     }
   }
+  p.remap = (gx * gy >= 16) ? 1 : 0;
   const int gz = p.splits > 1 ? p.splits : nb;
-  if (big) {
-    dim3 grid(ceil_div(d->N, 128), ceil_div(d->M, 128), gz);
-    hipLaunchKernelGGL((gemm_kernel<128, 128>), grid, dim3(256), 0, s, p);
-  } else {
-    dim3 grid(ceil_div(d->N, 64), ceil_div(d->M, 64), gz);
-    hipLaunchKernelGGL((gemm_kernel<64, 64>), grid, dim3(256), 0, s, p);
+  const dim3 grid(gx, gy, gz);
+  const hipError_t e = big ? launch_tiles<128, 128>(am, bm, grid, s, p)
+                           : launch_tiles<64, 64>(am, bm, grid, s, p);
+  if (e != hipSuccess) {
+    set_error("sat_gemm: launch failed: %s", hipGetErrorString(e));
+    return SAT_ERR_HIP;
   }
-  SAT_LAUNCH_CHECK("sat_gemm");
   if (p.splits > 1) {
     const int64_t total = (int64_t)d->M * d->N;
     const int blocks = (int)std::min<int64_t>((total + 255) / 256, 2048);

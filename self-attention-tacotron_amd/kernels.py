@@ -38,6 +38,19 @@ def _gemm_ws(device):
     return buf
 
 
+_SCRATCH = {}
+
+
+def _stream_scratch(device, tag: str, nbytes: int) -> int:
+    """Small fixed-size device scratch per (device, stream, tag), allocated on first use."""
+    key = (device.type, device.index, torch.cuda.current_stream(device).cuda_stream, tag)
+    buf = _SCRATCH.get(key)
+    if buf is None or buf.numel() < nbytes:
+        buf = torch.empty(nbytes, dtype=torch.uint8, device=device)
+        _SCRATCH[key] = buf
+    return buf.data_ptr()
+
+
 # Optional launch log for tools/gemm_census.py: list of (tag, SatGemmDesc copy) when not None.
 GEMM_LOG = None
 
@@ -417,8 +430,9 @@ def softmax_bwd(P, dPd, dS, mask=None, scale=1.0):
 def loss_fwd_bwd(mel, tgt, tmask, stop, done, dmask, out, dmel=None, dstop=None, l1_weight=0.1):
     B, T, M = mel.shape
     Tp = stop.shape[1]
+    ws = _stream_scratch(mel.device, "loss", int(_lib.load().sat_workspace_loss()))
     _lib.call("sat_loss_fwd_bwd", _p(mel), _p(tgt), _p(tmask), _p(stop), _p(done), _p(dmask),
-              B, T, M, Tp, l1_weight, _p(out), _p(dmel), _p(dstop), _stream())
+              B, T, M, Tp, l1_weight, _p(out), _p(dmel), _p(dstop), ws, _stream())
 
 
 def transpose(x: torch.Tensor, out: torch.Tensor = None) -> torch.Tensor:

@@ -56,7 +56,7 @@ def main():
     rows = []
     for key, (cnt, us) in groups.items():
         tag, M, N, Kd, nb, nb2, am, bm, ak, bn = key
-        fl = 2.0 * M * N * Kd * nb * nb2
+        fl = 2.0 * M * N * Kd * max(nb, 1) * max(nb2, 1)
         rows.append((cnt * us, cnt, us, fl / us / 1e6, key))
     rows.sort(reverse=True)
     tot = sum(r[0] for r in rows)

@@ -52,7 +52,7 @@ int sat_device_arch(char* buf, int len);       /* gcnArchName of the current dev
  * B modes: 0 dense  B(k,n) = B[k*b_sk + n*b_sn]
  *          1 flipped conv kernel W[taps][N][b_C]: k = tap*b_C + o,
  *                   B = W[((taps-1-tap)*N + n)*b_C + o]                     (conv dX)
- * act: 0 none, 1 relu, 2 tanh, 3 sigmoid.  bias may be NULL.
+ * act: 0 none, 1 relu, 2 tanh, 3 sigmoid, 4 softsign.  bias may be NULL.
  * mul (optional, [M][N] row stride mul_sm): C = act(...) * mul  (fused dropout masks).
  * add (optional, row stride add_sm, 0 = broadcast one row): C = act(...) * mul + add
  *     (fused residual connections, e.g. SelfAttentionTransformer x + tanh(Dense(.))).
@@ -273,7 +273,7 @@ int sat_highway_fwd(const float* h, const float* t, const float* x, float* y, in
 int sat_highway_bwd(const float* h, const float* t, const float* x, const float* dy,
                     float* dh_pre, float* dt_pre, float* dx, int64_t n, void* stream);
 
-/* dx = beta*dx + dy * act'(y) [* mask]; act 0 identity, 1 relu, 2 tanh, 3 sigmoid. */
+/* dx = beta*dx + dy * act'(y) [* mask]; act 0 identity, 1 relu, 2 tanh, 3 sigmoid, 4 softsign. */
 int sat_act_bwd(const float* dy, const float* y, const float* mask, float* dx, int64_t n,
                 int32_t act, float beta, void* stream);
 /* out[c][r] = in[r][c]  (weight re-layouts, e.g. query-layer kernels for the per-step rowdot) */

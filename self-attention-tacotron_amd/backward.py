@@ -284,12 +284,16 @@ def decoder_bwd(P, G, hp, d, dsv, dH2, masks, ws, attn_tile=32, pipe: Pipeline =
     dP = lin_bwd(S["prenet"][-1], DG0, W0[:p_w], dW0[:p_w], G["decoder/attention_lstm/bias"], ws)
     # decoder prenets (inputs are teacher frames: no input gradient needed for the first one)
     pres = S["prenet"]
+    ms = S.get("ms_prenet")
     for i in reversed(range(len(d.dec_prenet))):
         y = pres[i + 1]
         dpre = torch.empty_like(y)
         K.act_bwd(dP, y, dpre, "relu", mask=mk(f"dec/prenet{i}"))
-        dP = lin_bwd(pres[i], dpre, P[f"decoder/prenet{i}/kernel"], G[f"decoder/prenet{i}/kernel"],
-                     G[f"decoder/prenet{i}/bias"], ws, need_dx=i > 0)
+        sc = "decoder/prenet0/dense" if (ms is not None and i == 0) else f"decoder/prenet{i}"
+        dP = lin_bwd(pres[i], dpre, P[f"{sc}/kernel"], G[f"{sc}/kernel"], G[f"{sc}/bias"], ws,
+                     need_dx=i > 0 or ms is not None)
+    if ms is not None:
+        multi_speaker_prenet_bwd(P, G, d, S, ms, dP, ws)
 
     # ---- attention parameters from the per-tile partials
     pg_sum = torch.zeros(pgs, **f32)
@@ -327,6 +331,26 @@ def decoder_bwd(P, G, hp, d, dsv, dH2, masks, ws, attn_tile=32, pipe: Pipeline =
     lin_bwd(S["V2"], dK2, P[f"{a2}/memory_layer/kernel"], G[f"{a2}/memory_layer/kernel"], None,
             ws, dx=dV2, beta_dx=1.0)
     return dV1, dV2          # caller applies the sequence mask (values were masked memories)
+
+
+def multi_speaker_prenet_bwd(P, G, d, S, ms, dd0, ws):
+    """Backward of MultiSpeakerPreNet's first stage (modules/multi_speaker_modules.py:27-29):
+    d0 = relu(x W0 + b0) + softsign(spk Ws + bs), spk = speaker_embedding[id - offset].
+    The speaker row's gradient is the sum of dd0 over the T' steps (a column sum of the
+    step-major [T', B*p0] view)."""
+    Tp, B, p0 = dd0.shape
+    sc = "decoder/prenet0"
+    dsp = torch.empty(B, p0, device=dd0.device)
+    K.colsum(dd0.view(Tp, B * p0), dsp.view(-1), ws, beta=0.0)
+    dspre = torch.empty_like(dsp)
+    K.act_bwd(dsp, ms["sp"], dspre, "softsign")
+    dspk = lin_bwd(ms["spk"], dspre, P[f"{sc}/speaker_projection/kernel"],
+                   G[f"{sc}/speaker_projection/kernel"], G[f"{sc}/speaker_projection/bias"], ws)
+    K.embedding_bwd(dspk, ms["ids"], G["speaker_embedding"], offset=d.spk_offset)
+    dpre0 = torch.empty_like(dd0)
+    K.act_bwd(dd0, ms["y0"], dpre0, "relu")
+    lin_bwd(S["xin"], dpre0, P[f"{sc}/dense0/kernel"], G[f"{sc}/dense0/kernel"],
+            G[f"{sc}/dense0/bias"], ws, need_dx=False)
 
 
 def encoder_bwd(P, G, hp, d, sv, dm1, dm2, lengths, masks, ws):

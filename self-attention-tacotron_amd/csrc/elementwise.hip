@@ -217,7 +217,8 @@ __global__ void highway_bwd_kernel(const float* __restrict__ h, const float* __r
 }
 
 // ---------------------------------------------------------------- activation backward
-// dx = dy * act'(y) [* mask], act: 1 relu (y>0), 2 tanh (1-y^2), 3 sigmoid y(1-y), 0 identity
+// dx = dy * act'(y) [* mask], act: 1 relu (y>0), 2 tanh (1-y^2), 3 sigmoid y(1-y),
+// 4 softsign (1-|y|)^2, 0 identity
 __global__ void act_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ y,
                                const float* __restrict__ mask, float* __restrict__ dx, int64_t n,
                                int act, float beta) {
@@ -228,6 +229,7 @@ __global__ void act_bwd_kernel(const float* __restrict__ dy, const float* __rest
     if (act == 1) g = yv > 0.f ? g : 0.f;
     else if (act == 2) g *= 1.f - yv * yv;
     else if (act == 3) g *= yv * (1.f - yv);
+    else if (act == 4) { const float a = 1.f - fabsf(yv); g *= a * a; }
     dx[i] = beta != 0.f ? beta * dx[i] + g : g;
   }
 }
@@ -567,7 +569,7 @@ extern "C" int sat_highway_bwd(const float* h, const float* t, const float* x, c
 
 extern "C" int sat_act_bwd(const float* dy, const float* y, const float* mask, float* dx, int64_t n,
                            int32_t act, float beta, void* stream) {
-  SAT_CHECK_ARG(dy && dx && n >= 0 && act >= 0 && act <= 3, "sat_act_bwd: bad args");
+  SAT_CHECK_ARG(dy && dx && n >= 0 && act >= 0 && act <= 4, "sat_act_bwd: bad args");
   SAT_CHECK_ARG(act == 0 || y, "sat_act_bwd: activation output needed");
   hipLaunchKernelGGL(act_bwd_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), dy, y,
                      mask, dx, n, act, beta);

@@ -78,6 +78,7 @@ __device__ __forceinline__ float apply_act(float v, int act) {
     case 1: return fmaxf(v, 0.f);
     case 2: return tanhf(v);
     case 3: return 1.f / (1.f + expf(-v));
+    case 4: return v / (1.f + fabsf(v));   // softsign (MultiSpeakerPreNet speaker_projection)
     default: return v;
   }
 }
@@ -437,7 +438,7 @@ extern "C" int sat_gemm(const SatGemmDesc* d, void* stream) {
   SAT_CHECK_ARG(d->a_mode == 0 || d->a_L > 0, "sat_gemm: conv mode needs a_L > 0");
   SAT_CHECK_ARG(d->a_mode == 0 || d->a_C > 0, "sat_gemm: im2col mode needs a_C > 0");
   SAT_CHECK_ARG(d->b_mode != 1 || (d->b_C > 0 && d->b_taps > 0), "sat_gemm: bad conv kernel");
-  SAT_CHECK_ARG(d->act >= 0 && d->act <= 3, "sat_gemm: bad activation");
+  SAT_CHECK_ARG(d->act >= 0 && d->act <= 4, "sat_gemm: bad activation");
   if (d->M == 0 || d->N == 0) return SAT_OK;
   SAT_CHECK_ARG(d->A && d->B && d->C, "sat_gemm: null operand");
   GemmP p;

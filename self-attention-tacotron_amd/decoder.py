@@ -81,15 +81,30 @@ def decoder_forward(P: Dict[str, torch.Tensor], hp, d: Dims, m1: torch.Tensor, m
 
     # ---- prenets over all frames (teacher forcing), dropout fused as a multiplicative epilogue
     xin = teacher_inputs(targets, r, nf)
-    if spk is not None:
-        raise NotImplementedError("multi-speaker prenet: see decoder_forward_ms (next row)")
     pre = xin
     pres = [xin]
-    for i in range(len(d.dec_prenet)):
+    if spk is not None:
+        # MultiSpeakerPreNet (modules/multi_speaker_modules.py:27-32): the speaker term is one
+        # [B, p0] row per utterance, broadcast over the T' steps by a zero batch stride of the
+        # step-major [T', B, .] GEMM's residual operand
+        p0 = d.dec_prenet[0]
+        ms = "decoder/prenet0"
+        sp = K.linear(spk, P[f"{ms}/speaker_projection/kernel"],
+                      P[f"{ms}/speaker_projection/bias"], act="softsign")          # [B, p0]
+        y0 = K.linear(xin, P[f"{ms}/dense0/kernel"], P[f"{ms}/dense0/bias"], act="relu")
+        d0 = K.gemm(xin, P[f"{ms}/dense0/kernel"], bias=P[f"{ms}/dense0/bias"], act="relu",
+                    add=sp.unsqueeze(0).expand(Tp, B, p0))
+        S["ms_prenet"] = dict(spk=spk, sp=sp, y0=y0)
+        pres = [d0]
+        pre = K.linear(d0, P[f"{ms}/dense/kernel"], P[f"{ms}/dense/bias"], act="relu",
+                       mul=mk("dec/prenet0"))
+        pres.append(pre)
+    for i in range(len(pres) - 1, len(d.dec_prenet)):
         pre = K.linear(pre, P[f"decoder/prenet{i}/kernel"], P[f"decoder/prenet{i}/bias"],
                        act="relu", mul=mk(f"dec/prenet{i}"))
         pres.append(pre)
     S["prenet"] = pres
+    S["xin"] = xin
     p_w = pre.shape[-1]
 
     # ---- attention RNN (ZoneoutLSTM A) input projection of the prenet part

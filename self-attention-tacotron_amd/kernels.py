@@ -12,7 +12,7 @@ import torch
 
 from . import _lib
 
-ACT = {None: 0, "none": 0, "relu": 1, "tanh": 2, "sigmoid": 3}
+ACT = {None: 0, "none": 0, "relu": 1, "tanh": 2, "sigmoid": 3, "softsign": 4}
 
 
 def _stream() -> int:

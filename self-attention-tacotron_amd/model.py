@@ -224,12 +224,17 @@ def model_forward(P, bn: BNState, hp, d: PR.Dims, batch: Dict[str, torch.Tensor]
     ids, lengths = batch["source"], batch["source_length"]
     m1, m2 = encoder_fwd(P, bn, hp, d, ids, lengths, masks, training, ws, sv)
     spk = None
-    if d.multi_speaker:
-        raise NotImplementedError("VCTK multi-speaker prenet is the next row (SURVEY 8(f) #3)")
+    if d.multi_speaker:                                               # models/models.py:43-46,69
+        ids_s = batch["speaker_id"]
+        spk = torch.empty(ids_s.shape[0], d.spk_dim, device=m1.device)
+        sv["spk_err"] = torch.zeros(1, dtype=torch.int32, device=m1.device)
+        K.embedding_fwd(P["speaker_embedding"], ids_s, spk, d.spk_offset, sv["spk_err"])
     dout, dsv = decoder_forward(P, hp, d, m1, m2, lengths, batch["mel"], masks,
                                 attn_tile=attn_tile, spk=spk,
                                 **({} if pipe is None else {"pipe": pipe}))
     sv["dec"] = dsv
+    if spk is not None:
+        dsv.tensors["ms_prenet"]["ids"] = batch["speaker_id"]
     mel_r, stop = head_fwd(P, hp, d, dout, masks, sv)
     B, Tp, _ = mel_r.shape
     mel = mel_r.view(B, Tp * d.r, d.num_mels)                         # module.py:1561

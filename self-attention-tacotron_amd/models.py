@@ -45,6 +45,13 @@ PreprocessedSourceData = namedtuple(
 PreprocessedTargetData = namedtuple(
     "PreprocessedTargetData", ["id", "key", "codes", "target_length", "done", "code_loss_mask",
                                "binary_loss_mask"])
+# VCTK records (datasets/vctk/dataset.py:31-46): source carries speaker_id / age / gender, and
+# the target is MelData with spec_loss_mask in place of code_loss_mask.
+SourceData = namedtuple(
+    "SourceData", ["id", "key", "source", "source_length", "speaker_id", "age", "gender", "text"])
+MelData = namedtuple(
+    "MelData", ["id", "key", "mel", "mel_width", "target_length", "done", "spec_loss_mask",
+                "binary_loss_mask"])
 EstimatorSpec = namedtuple("EstimatorSpec", ["mode", "loss", "train_op", "predictions",
                                              "eval_metric_ops"])
 
@@ -140,13 +147,20 @@ class DualSourceSelfAttentionTacotronModel:
 
     def _batch(self, features, labels):
         dev = self.engine.device
+        codes = labels.codes if hasattr(labels, "codes") else labels.mel
+        cmask = (labels.code_loss_mask if hasattr(labels, "code_loss_mask")
+                 else labels.spec_loss_mask)
         b = {"source": _to_device(features.source, dev, torch.int64),
              "source_length": _to_device(features.source_length, dev, torch.int64),
-             "mel": _to_device(labels.codes, dev, torch.float32),
-             "mel_mask": _to_device(labels.code_loss_mask, dev, torch.float32),
+             "mel": _to_device(codes, dev, torch.float32),
+             "mel_mask": _to_device(cmask, dev, torch.float32),
              "done": _to_device(labels.done, dev, torch.float32),
              "done_mask": _to_device(labels.binary_loss_mask, dev, torch.float32),
              "target_length": _to_device(labels.target_length, dev, torch.int64)}
+        if self.params.use_speaker_embedding:                 # models/models.py:69-70
+            if getattr(features, "speaker_id", None) is None:
+                raise ValueError("use_speaker_embedding=True needs features.speaker_id")
+            b["speaker_id"] = _to_device(features.speaker_id, dev, torch.int64)
         return b
 
     def _trainer(self, batch) -> Trainer:
@@ -216,6 +230,12 @@ def synthetic_input_fn(params, batch_size: int, N: int = 200, T: int = 1000, sha
             b = data.synthetic_batch(params, batch_size, N=N, T=T, seed=seed + step, shape=shape)
             step += 1
             ids = np.arange(batch_size)
+            if "speaker_id" in b:
+                yield (SourceData(ids, ids, b["source"], b["source_length"], b["speaker_id"],
+                                  None, None, None),
+                       MelData(ids, ids, b["mel"], params.num_mels, b["target_length"],
+                               b["done"], b["mel_mask"], b["done_mask"]))
+                continue
             yield (PreprocessedSourceData(ids, ids, b["source"], b["source_length"], None),
                    PreprocessedTargetData(ids, ids, b["mel"], b["target_length"], b["done"],
                                           b["mel_mask"], b["done_mask"]))

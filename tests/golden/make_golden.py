@@ -12,6 +12,8 @@ Files:
   golden_model.npz  -- LJSpeech hparams, weights init_params(seed=5), one ragged batch
                        (B=2, N=12, T=16, r=2), its dropout/zoneout masks, and the oracle's
                        eval- and train-mode outputs + per-parameter gradient summaries.
+  golden_model_vctk.npz -- the same for the VCTK multi-speaker config (speaker Embedding
+                       152x16 offset 225 -> MultiSpeakerPreNet), B=3, N=10, T=12.
   golden_ops.npz    -- single-op vectors: zoneout LSTM step (train/eval), causal MHA,
                        SAME conv with an even kernel, MaxPool(2,1,SAME), the loss.
 """
@@ -34,13 +36,19 @@ _sat_path.load()
 from sat_amd import data, hparams, params  # noqa: E402
 from oracle import sat_oracle as O  # noqa: E402
 
-MODEL_CASE = dict(B=2, N=12, T=16, shape="ljs", batch_seed=1, mask_seed=7, init_seed=5)
+MODEL_CASES = {
+    "ljspeech": dict(B=2, N=12, T=16, shape="ljs", batch_seed=1, mask_seed=7, init_seed=5,
+                     file="golden_model.npz"),
+    "vctk": dict(B=3, N=10, T=12, shape="ljs", batch_seed=4, mask_seed=8, init_seed=5,
+                 file="golden_model_vctk.npz"),
+}
+MODEL_CASE = MODEL_CASES["ljspeech"]
 N_HEAD = 8   # leading gradient entries stored per parameter
 
 
-def model_case():
-    c = MODEL_CASE
-    hp = hparams.ljspeech_hparams()
+def model_case(preset="ljspeech"):
+    c = MODEL_CASES[preset]
+    hp = getattr(hparams, f"{preset}_hparams")()
     vals = params.init_params(hp, seed=c["init_seed"])
     batch = data.synthetic_batch(hp, c["B"], N=c["N"], T=c["T"], shape=c["shape"],
                                  seed=c["batch_seed"])
@@ -113,18 +121,20 @@ def ops_case():
 
 
 def main():
-    hp, vals, batch, masks = model_case()
-    names, cks = param_checksums(vals)
-    rec = {"param_names": np.array(names), "param_checksums": cks}
-    rec.update({f"batch__{k}": v for k, v in batch.items()})
-    rec.update({f"mask__{k}": v for k, v in masks.items()})
-    for mode in ("eval", "train"):
-        r = oracle_model(hp, vals, batch, masks, mode == "train")
-        for k, v in r.items():
-            rec[f"{mode}__{k}"] = np.asarray(v)
-    np.savez_compressed(os.path.join(HERE, "golden_model.npz"), **rec)
+    for preset, c in MODEL_CASES.items():
+        hp, vals, batch, masks = model_case(preset)
+        names, cks = param_checksums(vals)
+        rec = {"param_names": np.array(names), "param_checksums": cks}
+        rec.update({f"batch__{k}": v for k, v in batch.items()})
+        rec.update({f"mask__{k}": v for k, v in masks.items()})
+        for mode in ("eval", "train"):
+            r = oracle_model(hp, vals, batch, masks, mode == "train")
+            for k, v in r.items():
+                rec[f"{mode}__{k}"] = np.asarray(v)
+        np.savez_compressed(os.path.join(HERE, c["file"]), **rec)
+        print("wrote", c["file"])
     np.savez_compressed(os.path.join(HERE, "golden_ops.npz"), **ops_case())
-    print("wrote golden_model.npz, golden_ops.npz")
+    print("wrote golden_ops.npz")
 
 
 if __name__ == "__main__":

@@ -6,6 +6,7 @@ import os
 import sys
 
 import numpy as np
+import pytest
 import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -14,12 +15,14 @@ sys.path.insert(0, os.path.join(HERE, "golden"))
 import make_golden as MG  # noqa: E402
 from oracle import sat_oracle as O  # noqa: E402
 
-G = np.load(os.path.join(HERE, "golden", "golden_model.npz"))
+GOLD = {p: np.load(os.path.join(HERE, "golden", c["file"])) for p, c in MG.MODEL_CASES.items()}
 OPS = np.load(os.path.join(HERE, "golden", "golden_ops.npz"))
 
 
-def test_generator_inputs_unchanged():
-    hp, vals, batch, masks = MG.model_case()
+@pytest.mark.parametrize("preset", sorted(MG.MODEL_CASES))
+def test_generator_inputs_unchanged(preset):
+    G = GOLD[preset]
+    hp, vals, batch, masks = MG.model_case(preset)
     names, cks = MG.param_checksums(vals)
     assert list(G["param_names"]) == names
     np.testing.assert_allclose(cks, G["param_checksums"], rtol=1e-12)
@@ -29,8 +32,10 @@ def test_generator_inputs_unchanged():
         np.testing.assert_array_equal(v, G[f"mask__{k}"])
 
 
-def test_oracle_model_matches_golden():
-    hp, vals, batch, masks = MG.model_case()
+@pytest.mark.parametrize("preset", sorted(MG.MODEL_CASES))
+def test_oracle_model_matches_golden(preset):
+    G = GOLD[preset]
+    hp, vals, batch, masks = MG.model_case(preset)
     for mode in ("eval", "train"):
         r = MG.oracle_model(hp, vals, batch, masks, mode == "train")
         for k in ("loss", "l1", "bce"):

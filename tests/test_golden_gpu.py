@@ -9,14 +9,16 @@ import torch
 
 pytestmark = pytest.mark.gpu
 
-G = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden",
-                         "golden_model.npz"))
+FILES = {"ljspeech": "golden_model.npz", "vctk": "golden_model_vctk.npz"}
 
 
+@pytest.mark.parametrize("preset", sorted(FILES))
 @pytest.mark.parametrize("mode", ["eval", "train"])
-def test_hip_path_matches_golden(cuda, mode):
+def test_hip_path_matches_golden(cuda, mode, preset):
     from sat_amd import engine, hparams, params
-    hp = hparams.ljspeech_hparams()
+    G = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden",
+                             FILES[preset]))
+    hp = getattr(hparams, f"{preset}_hparams")()
     vals = params.init_params(hp, seed=5)
     names = sorted(vals)
     assert list(G["param_names"]) == names

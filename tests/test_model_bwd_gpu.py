@@ -6,10 +6,10 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def _run(cuda, train, B=3, N=17, T=24, shape="ljs", seed=0, hp_over=None):
+def _run(cuda, train, B=3, N=17, T=24, shape="ljs", seed=0, hp_over=None, preset="ljspeech"):
     from sat_amd import hparams, params, data, engine
     from oracle import sat_oracle as O
-    hp = hparams.ljspeech_hparams(**(hp_over or {}))
+    hp = getattr(hparams, f"{preset}_hparams")(**(hp_over or {}))
     vals = params.init_params(hp, seed=5)
     m = engine.Tacotron(hp, cuda, init_values=vals)
     batch = data.synthetic_batch(hp, B, N=N, T=T, shape=shape, seed=seed)
@@ -56,3 +56,19 @@ def test_gradients_max_shape_full_lengths(cuda):
     grads, p64, out, ref = _run(cuda, True, B=2, N=40, T=48, shape="max", seed=3)
     bad = _compare(grads, p64)
     assert not bad, bad
+
+
+@pytest.mark.parametrize("train", [False, True])
+def test_vctk_multi_speaker_gradients_match_oracle(cuda, train):
+    """C4: VCTK self-attention-tacotron.json -- speaker Embedding(152, 16, offset 225)
+    (models/models.py:43-46) feeding MultiSpeakerPreNet (modules/multi_speaker_modules.py:27-32);
+    the speaker embedding and projection gradients are covered by the same comparison."""
+    grads, p64, out, ref = _run(cuda, train, B=4, N=15, T=20, seed=11, preset="vctk")
+    assert "speaker_embedding" in p64 and "decoder/prenet0/speaker_projection/kernel" in p64
+    assert abs(float(out["loss"].item()) - float(ref["loss"].detach())) < 1e-5
+    np.testing.assert_allclose(out["mel"].cpu().numpy(), ref["mel"].detach().numpy(), atol=2e-5)
+    bad = _compare(grads, p64)
+    assert not bad, bad
+    # only the rows of the speakers present in the batch receive gradient
+    g = grads["speaker_embedding"]
+    assert np.count_nonzero(np.abs(g).sum(1)) <= 4

@@ -117,22 +117,6 @@ class _LstmBwd:
         K.lstm_step_bwd(**self.desc(**kw))
 
 
-def _lstm_loop_bwd(*, B, U, Kr, hoff, Tp, Wr, G_, CS, dY, mc, mh, zc, zh, order, nxt_of,
-                   cprev_of, lengths=None, extra=None):
-    """Reverse recurrence of one LSTM layer; returns DG (same layout as the forward gates)."""
-    DG = torch.empty_like(G_)
-    run = _LstmBwd(B, U, G_.device)
-    for t in order:
-        nt = nxt_of(t)
-        kw = dict(extra(t)) if extra is not None else {}
-        run.step(B=B, U=U, K=Kr, hoff=hoff, t=t, W=Wr,
-                 dgates_next=None if nt is None else DG[nt], gates=G_[t], c_prev=cprev_of(t),
-                 dy=None if dY is None else dY(t), mask_c=None if mc is None else mc[t],
-                 mask_h=None if mh is None else mh[t], zc=zc, zh=zh, dgates=DG[t],
-                 lengths=lengths, **kw)
-    return DG
-
-
 def decoder_bwd(P, G, hp, d, dsv, dH2, masks, ws, attn_tile=32, pipe: Pipeline = SEQUENTIAL):
     """Backward of decoder.decoder_forward.  Returns (dm1, dm2) batch-major.
 
@@ -207,8 +191,9 @@ def decoder_bwd(P, G, hp, d, dsv, dH2, masks, ws, attn_tile=32, pipe: Pipeline =
     mc0, mh0 = mk("dec/lstm0/zc"), mk("dec/lstm0/zh")
     chain = {"cur": 0}
 
-    def attention_step(t):
-        cur = chain["cur"]
+    def attention_part(t, cur):
+        """Context gradient of step t (through the attention RNN's input at t+1) and the
+        dual-source attention backward of step t."""
         last = t == Tp - 1
         if not last:   # gradient of c_t through the attention RNN's input at step t+1
             K.rowdot(DG0[t + 1], W0r[:M1 + M2], DCTX[t], beta=1.0)
@@ -227,17 +212,27 @@ def decoder_bwd(P, G, hp, d, dsv, dH2, masks, ws, attn_tile=32, pipe: Pipeline =
             locW=P[f"{a1}/location_layer/kernel"] if fwd else None,
             v2=P[f"{a2}/attention_v"], dalpha_prev=DAP[1 - cur], df_out=DF[1 - cur],
             dK1=dK1, dK2=dK2, dqp=DQP[t], pg=PG, pg_stride=pgs)
-        K.lstm_step_bwd(B=B, U=A, K=R0, hoff=M1 + M2, t=t, W=W0r,
-                        dgates_next=None if last else DG0[t + 1], gates=S["G0"][t],
-                        c_prev=S["C0"][t], dy=dH0[t], dh_carry=None if last else hc[cur],
-                        dc_carry=None if last else cc[cur],
-                        mask_c=None if mc0 is None else mc0[t],
-                        mask_h=None if mh0 is None else mh0[t], zc=zc, zh=zh, dgates=DG0[t],
-                        dh_carry_out=hc[1 - cur], dc_carry_out=cc[1 - cur],
-                        dq0=DQP[t][:, :, :D1], wq0=P[f"{a1}/query_layer/kernel"],
-                        dq1=DQP[t][:, :, D1:], wq1=P[f"{a2}/query_layer/kernel"],
-                        dq_parts=ntiles, dq_pstride=D1 + D2, dq_bstride=ntiles * (D1 + D2))
+
+    def lstm0_desc(t, cur):
+        """Reverse step t of the attention RNN: recurrent + query gradients in one dot."""
+        last = t == Tp - 1
+        return dict(B=B, U=A, K=R0, hoff=M1 + M2, t=t, W=W0r,
+                    dgates_next=None if last else DG0[t + 1], gates=S["G0"][t],
+                    c_prev=S["C0"][t], dy=dH0[t], dh_carry=None if last else hc[cur],
+                    dc_carry=None if last else cc[cur],
+                    mask_c=None if mc0 is None else mc0[t],
+                    mask_h=None if mh0 is None else mh0[t], zc=zc, zh=zh, dgates=DG0[t],
+                    dh_carry_out=hc[1 - cur], dc_carry_out=cc[1 - cur],
+                    dq0=DQP[t][:, :, :D1], wq0=P[f"{a1}/query_layer/kernel"],
+                    dq1=DQP[t][:, :, D1:], wq1=P[f"{a2}/query_layer/kernel"],
+                    dq_parts=ntiles, dq_pstride=D1 + D2, dq_bstride=ntiles * (D1 + D2))
+
+    def attention_step(t):
+        """attention part of step t; returns the attention RNN's reverse step t (not launched)."""
+        cur = chain["cur"]
+        attention_part(t, cur)
         chain["cur"] = 1 - cur
+        return lstm0_desc(t, cur)
 
     if not pipe.enabled:          # layer by layer
         for t in range(Tp - 1, -1, -1):
@@ -247,26 +242,34 @@ def decoder_bwd(P, G, hp, d, dsv, dH2, masks, ws, attn_tile=32, pipe: Pipeline =
             K.lstm_step_bwd(**lstm1_desc(t))
         dh0_chunk(0, Tp)
         for t in range(Tp - 1, -1, -1):
-            attention_step(t)
-    else:                         # reverse wavefront: LSTM1 C, the attention chain 2C behind
+            K.lstm_step_bwd(**attention_step(t))
+    else:
+        # reverse wavefront: LSTM1 C and the attention chain 2C behind LSTM2.  Iteration j
+        # issues ONE multi-problem launch {LSTM2 at T'-1-j, LSTM1 C behind, the attention RNN's
+        # step deferred from the previous iteration}, then the attention backward 2C behind.
         C = pipe.chunk
         dh1_at = pipe.finishing_rev(Tp, 0)
         dh0_at = pipe.finishing_rev(Tp, C)
-        for j in range(Tp + 2 * C):
+        pending = None
+        for j in range(Tp + 2 * C + 1):
             t2, t1, t0 = Tp - 1 - j, Tp - 1 - j + C, Tp - 1 - j + 2 * C
             steps = []
             if t2 >= 0:
                 steps.append(lstm2_desc(t2))
             if 0 <= t1 < Tp:
                 steps.append(lstm1_desc(t1))
+            if pending is not None:
+                steps.append(pending)
+                pending = None
             if steps:
                 K.lstm_steps_bwd(steps)
             if 0 <= t0 < Tp:
-                attention_step(t0)
+                pending = attention_step(t0)
             if j in dh1_at:
                 dh1_chunk(*dh1_at[j])
             if j in dh0_at:
                 dh0_chunk(*dh0_at[j])
+        assert pending is None
     # LSTM weight gradients: one GEMM per weight block over all steps
     DG2f = DG2.view(Tp * B, 4 * Dd)
     DG1f = DG1.view(Tp * B, 4 * Dd)
@@ -373,22 +376,31 @@ def encoder_bwd(P, G, hp, d, sv, dm1, dm2, lengths, masks, ws):
     hw_sm = hw.transpose(0, 1).contiguous()                          # [N, B, Win] (data movement)
     dhw = torch.empty(B, N, Win, device=dev)
     zc, zh = hp.zoneout_factor_cell, hp.zoneout_factor_output
-    for i, (dr, rev) in enumerate((("fw", False), ("bw", True))):
+    # reverse recurrences of both directions, one multi-problem launch per step (the forward
+    # cell walks n = N-1 .. 0, the backward cell n = 0 .. N-1)
+    dirs = (("fw", False), ("bw", True))
+    DGs = {dr: torch.empty_like(sv["enc_lstm"][dr]["G"]) for dr, _ in dirs}
+    runs = {dr: _LstmBwd(B, U, dev) for dr, _ in dirs}
+
+    def enc_bwd_desc(dr, rev, n):
+        st = sv["enc_lstm"][dr]
+        half = slice(U, 2 * U) if rev else slice(0, U)
+        nt = (n - 1 if n > 0 else None) if rev else (n + 1 if n + 1 < N else None)
+        mc, mh = mk(f"enc/lstm_{dr}/zc"), mk(f"enc/lstm_{dr}/zh")
+        return runs[dr].desc(
+            B=B, U=U, K=U, hoff=0, t=n, W=P[f"encoder/cbhg/lstm_{dr}/kernel"][Win:],
+            dgates_next=None if nt is None else DGs[dr][nt], gates=st["G"][n],
+            c_prev=st["CS"][n + 1] if rev else st["CS"][n], dy=dm1[:, n, half],
+            mask_c=None if mc is None else mc[n], mask_h=None if mh is None else mh[n],
+            zc=zc, zh=zh, dgates=DGs[dr][n], lengths=lengths)
+
+    for i in range(N):
+        K.lstm_steps_bwd([enc_bwd_desc("fw", False, N - 1 - i), enc_bwd_desc("bw", True, i)])
+    for i, (dr, rev) in enumerate(dirs):
         st = sv["enc_lstm"][dr]
         Wk = P[f"encoder/cbhg/lstm_{dr}/kernel"]
         dWk = G[f"encoder/cbhg/lstm_{dr}/kernel"]
-        half = slice(U, 2 * U) if rev else slice(0, U)
-        dmh = dm1[:, :, half]
-        if rev:
-            order, nxt_of = list(range(N)), (lambda n: n - 1 if n > 0 else None)
-            cprev_of = lambda n, CS=st["CS"]: CS[n + 1]
-        else:
-            order, nxt_of = list(range(N - 1, -1, -1)), (lambda n: n + 1 if n + 1 < N else None)
-            cprev_of = lambda n, CS=st["CS"]: CS[n]
-        DG = _lstm_loop_bwd(B=B, U=U, Kr=U, hoff=0, Tp=N, Wr=Wk[Win:], G_=st["G"], CS=st["CS"],
-                            dY=lambda n, dmh=dmh: dmh[:, n], mc=mk(f"enc/lstm_{dr}/zc"),
-                            mh=mk(f"enc/lstm_{dr}/zh"), zc=zc, zh=zh, order=order,
-                            nxt_of=nxt_of, cprev_of=cprev_of, lengths=lengths)
+        DG = DGs[dr]
         DGf = DG.view(N * B, 4 * U)
         hprev = st["HS"][1:N + 1] if rev else st["HS"][:N]
         K.gemm(hprev.reshape(N * B, U).t(), DGf, dWk[Win:], beta=1.0)

@@ -152,25 +152,30 @@ def encoder_fwd(P, bn: BNState, hp, d: PR.Dims, ids, lengths, masks, training, w
     U = d.cbhg_half
     m1 = torch.empty(B, N, 2 * U, device=dev)
     zc, zh = hp.zoneout_factor_cell, hp.zoneout_factor_output
+    # the two directions are independent recurrences: step n of the forward cell and step
+    # N-1-n of the backward cell run as ONE multi-problem launch (sat_lstm_steps_fwd)
     lstm = {}
-    for dr, rev in (("fw", False), ("bw", True)):
+    for dr in ("fw", "bw"):
         Wk = P[f"encoder/cbhg/lstm_{dr}/kernel"]
-        X = K.linear(hw, Wk[:hw.shape[-1]], P[f"encoder/cbhg/lstm_{dr}/bias"])   # [B, N, 4U]
-        CS = torch.zeros(N + 1, B, U, device=dev)
-        HS = torch.zeros(N + 1, B, U, device=dev)
-        G = torch.empty(N, B, 4 * U, device=dev)
+        lstm[dr] = dict(
+            X=K.linear(hw, Wk[:hw.shape[-1]], P[f"encoder/cbhg/lstm_{dr}/bias"]),  # [B, N, 4U]
+            CS=torch.zeros(N + 1, B, U, device=dev), HS=torch.zeros(N + 1, B, U, device=dev),
+            G=torch.empty(N, B, 4 * U, device=dev))
+
+    def enc_step(dr, rev, n):
+        st = lstm[dr]
+        Wk = P[f"encoder/cbhg/lstm_{dr}/kernel"]
         mc, mh = mk(f"enc/lstm_{dr}/zc"), mk(f"enc/lstm_{dr}/zh")
         out = m1[:, :, U:] if rev else m1[:, :, :U]
-        order = range(N - 1, -1, -1) if rev else range(N)
-        for n in order:
-            prev, nxt = (n + 1, n) if rev else (n, n + 1)
-            K.lstm_step_fwd(B=B, U=U, K=U, t=n, xproj=X[:, n], rin=HS[prev], W=Wk[hw.shape[-1]:],
-                            c_prev=CS[prev], h_prev=HS[prev],
-                            mask_c=None if mc is None else mc[n],
-                            mask_h=None if mh is None else mh[n], zc=zc, zh=zh,
-                            h_raw=out[:, n], c_out=CS[nxt], h_out=HS[nxt], gates=G[n],
-                            lengths=lengths)
-        lstm[dr] = dict(X=X, CS=CS, HS=HS, G=G)
+        prev, nxt = (n + 1, n) if rev else (n, n + 1)
+        return dict(B=B, U=U, K=U, t=n, xproj=st["X"][:, n], rin=st["HS"][prev],
+                    W=Wk[hw.shape[-1]:], c_prev=st["CS"][prev], h_prev=st["HS"][prev],
+                    mask_c=None if mc is None else mc[n], mask_h=None if mh is None else mh[n],
+                    zc=zc, zh=zh, h_raw=out[:, n], c_out=st["CS"][nxt], h_out=st["HS"][nxt],
+                    gates=st["G"][n], lengths=lengths)
+
+    for n in range(N):
+        K.lstm_steps_fwd([enc_step("fw", False, n), enc_step("bw", True, N - 1 - n)])
     sv["enc_lstm"] = lstm
     sv["m1"] = m1
     s0 = K.linear(m1, P["encoder/self_attention_projection/kernel"],

@@ -47,6 +47,8 @@ def parse():
     ap.add_argument("--frames", type=int, default=1000)
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-roofline", action="store_true",
+                    help="skip the attention-kernel probe (profiling runs of the step alone)")
     ap.add_argument("--cpu-baseline-batch", type=int, default=2)
     ap.add_argument("--cpu-baseline-steps", type=int, default=4)
     ap.add_argument("--attn-tile", type=int, default=32)
@@ -225,7 +227,8 @@ def main():
     loss1 = float(trainer.last_loss.item())
     frames = world * B * T * args.steps
     value = frames / dt
-    roof = attention_probe(trainer, hp, model.d, B, N, args.attn_tile)
+    roof = None if args.no_roofline else attention_probe(trainer, hp, model.d, B, N,
+                                                         args.attn_tile)
     if rank == 0:
         cpu = None if args.no_cpu_baseline else cpu_baseline(hp, args)
         line = {

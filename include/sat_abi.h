@@ -184,6 +184,7 @@ typedef struct SatAttnStep {
   float* s_out; float* a_out; float* s2_out;/* [B][N] */
   float* ctx; int64_t ctx_sb;               /* [B][M1 + M2] */
   float* stats;                             /* [B][4] or NULL */
+  float* loc_out;                           /* [B][N][F] location features (bwd history) or NULL */
   int32_t phases;                           /* 0 or 3: both kernels; 1: tile kernel only;
                                                2: combine only (profiling / split launches) */
 } SatAttnStep;
@@ -194,38 +195,66 @@ int sat_attn_query(int32_t B, int32_t K, int32_t N1, int32_t N2, const float* x,
                    const float* W1, const float* W2, float* q, int64_t q_sb, void* stream);
 int sat_attn_step_fwd(const SatAttnStep* args, void* stream);
 
-/* Backward of one attention step (reverse time t).  Inputs: dctx = dL/d[c1|c2] at t (all
- * sources), dalpha_next / df_next = the gradients the step t+1 backward sent to alpha_t and to
- * the location features (NULL at the last step); the forward state of step t (s_t = s_out,
- * a_t = a_out, a_prev, s_prev, s2_t, stats, q).  Outputs: dalpha_prev, df_out (for step t-1),
- * dqp [B][ntiles][D1+D2] per-tile query-gradient partials (overwritten), and ACCUMULATED
- * dK1 [B][N][D1], dK2 [B][N][D2], pg [B*ntiles][pg_stride] = per-tile partial parameter grads
- * [dv1 D1 | dW_loc F*D1 | dconvW KW*F | dconvb F | dv2 D2].  DA, DS2, DSN are [B][N] scratch.
- * The value gradients dV = alignments^T dctx are left to one batched GEMM after the loop. */
+/* Backward of one attention step (reverse time t), one launch.  Inputs: dctx = dL/d[c1|c2] at
+ * t (all sources); ctx_t = the forward context [c1|c2] of step t (row stride ctx_sb: the
+ * utterance-wide softmax / recursion sums are dots with it, so no cross-tile pass is needed);
+ * y_next / df_next = what the step t+1 backward sent back (Y[n] = s_{t+1}[n] dL/dprior[n], the
+ * alignment recursion's gradient, dalpha_t[n] = (1-u) Y[n] + u Y[n+1]; and the location-feature
+ * gradient [B][N][F]) -- both NULL at the last step; the forward state of step t (s_t = s_out,
+ * a_t = a_out, a_prev, s_prev, s2_t, stats, q).  Outputs: y_out, df_out (for step t-1), dqp
+ * [B][ntiles][D1+D2] per-tile query-gradient partials (overwritten), de1_out / de2_out [B][N]
+ * the energy gradients of step t (history rows for sat_attn_param_grads).  Only the critical
+ * path runs per step: parameter gradients are one pass after the loop (sat_attn_param_grads),
+ * the value gradients dV = alignments^T dctx one batched GEMM. */
 typedef struct SatAttnStepBwd {
   int32_t B, N, D1, M1, D2, M2, F, KW, NT, ntiles, att1_forward;
   float u;
   const float* dctx; int64_t dctx_sb;
-  const float* dalpha_next;
+  const float* ctx_t; int64_t ctx_sb;
+  const float* y_next;
   const float* V1; const float* V2;
-  float* DA; float* DS2; float* DSN;
   const float* s_t; const float* a_t; const float* a_prev; const float* s_prev; const float* s2_t;
   const float* stats;
   const float* df_next;
-  const int64_t* lengths;
   const float* q; int64_t q_sb;
   const float* K1; const float* K2;
   const float* v1; const float* b1; const float* convW; const float* convb; const float* locW;
   const float* v2;
-  float* dalpha_prev;
+  float* y_out;
   float* df_out;
-  float* dK1; float* dK2;
+  float* de1_out; float* de2_out;
   float* dqp;
-  float* pg; int64_t pg_stride;
+  int32_t waves;                            /* waves per block: 0 (= 16), 4, 8 or 16 */
 } SatAttnStepBwd;
 
-int sat_attn_pg_stride(int32_t D1, int32_t D2, int32_t F, int32_t KW);
 int sat_attn_step_bwd(const SatAttnStepBwd* args, void* stream);
+
+/* All attention-parameter gradients of the T reverse steps in one pass over (t, b, n)
+ * (ForwardAttention variables modules/forward_attention.py:16-23,68-78 and the Bahdanau
+ * memory/score of attention2): energies recomputed from K1/K2 + the query history q
+ * (q_t[b] = q + t*q_tstride + b*q_bstride, [D1 | D2]) + b1 + the location-feature history
+ * loc [T][B][N][F]; with the energy-gradient histories de1/de2 [T][B][N] and the
+ * location-gradient history df [T][B][N][F] (s_prev: s_{t-1}[b][n] = s_prev + t*s_tstride +
+ * b*N + n).  Writes dK1 [B][N][D1], dK2 [B][N][D2] (overwritten) and one partial row per
+ * workgroup, pg [sat_attn_param_grad_rows(B, N)][pg_stride] =
+ * [dv1 D1 | dW_loc F*D1 | dconvW KW*F | dconvb F | dv2 D2] (F = KW = 0 when !att1_forward),
+ * to be column-summed. */
+typedef struct SatAttnParamGrad {
+  int32_t T, B, N, D1, D2, F, KW, att1_forward;
+  const float* K1; const float* K2;
+  const float* q; int64_t q_tstride, q_bstride;
+  const float* b1; const float* v1; const float* locW; const float* v2;
+  const float* loc;
+  const float* s_prev; int64_t s_tstride;
+  const float* de1; const float* de2;
+  const float* df;
+  float* dK1; float* dK2;
+  float* pg; int64_t pg_stride;
+} SatAttnParamGrad;
+
+int sat_attn_pg_stride(int32_t D1, int32_t D2, int32_t F, int32_t KW);
+int sat_attn_param_grad_rows(int32_t B, int32_t N);
+int sat_attn_param_grads(const SatAttnParamGrad* args, void* stream);
 
 /* ---------------------------------------------------------------- elementwise
  * out[b,n,:] = x[b,n,:] * (n < lengths[b])  -- TF _prepare_memory (memory_sequence_length). */

@@ -71,16 +71,21 @@ SatAdamConfig = _struct("SatAdamConfig", """
 
 SatAttnStepBwd = _struct("SatAttnStepBwd", """
     i32:B i32:N i32:D1 i32:M1 i32:D2 i32:M2 i32:F i32:KW i32:NT i32:ntiles i32:att1_forward
-    f32:u ptr:dctx i64:dctx_sb ptr:dalpha_next ptr:V1 ptr:V2 ptr:DA ptr:DS2 ptr:DSN ptr:s_t ptr:a_t
-    ptr:a_prev ptr:s_prev ptr:s2_t ptr:stats ptr:df_next ptr:lengths ptr:q i64:q_sb ptr:K1 ptr:K2
-    ptr:v1 ptr:b1 ptr:convW ptr:convb ptr:locW ptr:v2 ptr:dalpha_prev ptr:df_out ptr:dK1 ptr:dK2
-    ptr:dqp ptr:pg i64:pg_stride""")
+    f32:u ptr:dctx i64:dctx_sb ptr:ctx_t i64:ctx_sb ptr:y_next ptr:V1 ptr:V2 ptr:s_t ptr:a_t
+    ptr:a_prev ptr:s_prev ptr:s2_t ptr:stats ptr:df_next ptr:q i64:q_sb ptr:K1 ptr:K2
+    ptr:v1 ptr:b1 ptr:convW ptr:convb ptr:locW ptr:v2 ptr:y_out ptr:df_out ptr:de1_out ptr:de2_out
+    ptr:dqp i32:waves""")
+
+SatAttnParamGrad = _struct("SatAttnParamGrad", """
+    i32:T i32:B i32:N i32:D1 i32:D2 i32:F i32:KW i32:att1_forward ptr:K1 ptr:K2
+    ptr:q i64:q_tstride i64:q_bstride ptr:b1 ptr:v1 ptr:locW ptr:v2 ptr:loc
+    ptr:s_prev i64:s_tstride ptr:de1 ptr:de2 ptr:df ptr:dK1 ptr:dK2 ptr:pg i64:pg_stride""")
 
 SatAttnStep = _struct("SatAttnStep", """
     i32:B i32:N i32:D1 i32:M1 i32:D2 i32:M2 i32:F i32:KW i32:NT i32:ntiles i32:att1_forward
     f32:u ptr:q i64:q_sb ptr:K1 ptr:V1 ptr:K2 ptr:V2 ptr:lengths ptr:s_prev ptr:a_prev
     ptr:v1 ptr:b1 ptr:convW ptr:convb ptr:locW ptr:v2 ptr:e1 ptr:e2 ptr:part i64:part_stride
-    ptr:s_out ptr:a_out ptr:s2_out ptr:ctx i64:ctx_sb ptr:stats i32:phases""")
+    ptr:s_out ptr:a_out ptr:s2_out ptr:ctx i64:ctx_sb ptr:stats ptr:loc_out i32:phases""")
 
 # name -> argtypes (restype is int for all but sat_last_error_string)
 SIGNATURES = {
@@ -98,6 +103,8 @@ SIGNATURES = {
     "sat_attn_step_fwd": [ctypes.POINTER(SatAttnStep), _P],
     "sat_attn_pg_stride": [_I32, _I32, _I32, _I32],
     "sat_attn_step_bwd": [ctypes.POINTER(SatAttnStepBwd), _P],
+    "sat_attn_param_grad_rows": [_I32, _I32],
+    "sat_attn_param_grads": [ctypes.POINTER(SatAttnParamGrad), _P],
     "sat_seq_mask": [_P, _P, _I32, _I32, _I32, _P, _P],
     "sat_embedding_fwd": [_P, _P, _P, _I64, _I32, _I32, _I64, _P, _P],
     "sat_embedding_bwd": [_P, _P, _P, _I64, _I32, _I32, _I64, _P],

@@ -175,17 +175,12 @@ def decoder_bwd(P, G, hp, d, dsv, dH2, masks, ws, attn_tile=32, pipe: Pipeline =
     a1, a2 = "decoder/attention1", "decoder/attention2"
     fwd = d.att1 == "forward"
     ntiles = (N + attn_tile - 1) // attn_tile
-    pgs = K.pg_stride(D1, D2, d.loc_f, d.loc_k)
     DG0 = torch.empty(Tp, B, 4 * A, **f32)
-    DA = torch.empty(B, N, **f32)
-    DS2 = torch.empty(B, N, **f32)
-    DSN = torch.empty(B, N, **f32)
-    DAP = [torch.zeros(B, N, **f32), torch.zeros(B, N, **f32)]
-    DF = [torch.zeros(B, N, max(d.loc_f, 1), **f32), torch.zeros(B, N, max(d.loc_f, 1), **f32)]
+    YA = [torch.zeros(B, N, **f32), torch.zeros(B, N, **f32)]   # alignment-recursion grads
+    DFH = torch.empty(Tp, B, N, max(d.loc_f, 1), **f32)     # location-feature gradient history
+    DE1 = torch.empty(Tp, B, N, **f32)                      # energy-gradient histories
+    DE2 = torch.empty(Tp, B, N, **f32)
     DQP = torch.empty(Tp, B, ntiles, D1 + D2, **f32)   # per-step, per-tile query gradients
-    dK1 = torch.zeros(B, N, D1, **f32)
-    dK2 = torch.zeros(B, N, D2, **f32)
-    PG = torch.zeros(B * ntiles, pgs, **f32)
     hc = [torch.zeros(B, A, **f32), torch.zeros(B, A, **f32)]
     cc = [torch.zeros(B, A, **f32), torch.zeros(B, A, **f32)]
     mc0, mh0 = mk("dec/lstm0/zc"), mk("dec/lstm0/zh")
@@ -200,18 +195,19 @@ def decoder_bwd(P, G, hp, d, dsv, dH2, masks, ws, attn_tile=32, pipe: Pipeline =
         K.attn_step_bwd(
             B=B, N=N, D1=D1, M1=M1, D2=D2, M2=M2, F=d.loc_f, KW=d.loc_k, NT=attn_tile,
             ntiles=ntiles, att1_forward=1 if fwd else 0, u=0.5, dctx=DCTX[t],
-            dctx_sb=M1 + M2, dalpha_next=None if last else DAP[cur], V1=S["V1"], V2=S["V2"],
-            DA=DA, DS2=DS2, DSN=DSN, s_t=S["S1"][t + 1], a_t=S["AL1"][t + 1],
+            dctx_sb=M1 + M2, ctx_t=S["REC0"][t + 1], ctx_sb=R0,
+            y_next=None if last else YA[cur], V1=S["V1"], V2=S["V2"],
+            s_t=S["S1"][t + 1], a_t=S["AL1"][t + 1],
             a_prev=S["AL1"][t], s_prev=S["S1"][t], s2_t=S["S2"][t], stats=S["ST"][t],
-            df_next=None if last else DF[cur], lengths=None, q=S["Q"][t], q_sb=D1 + D2,
+            df_next=None if last or not fwd else DFH[t + 1], q=S["Q"][t], q_sb=D1 + D2,
             K1=S["K1"], K2=S["K2"],
             v1=P[f"{a1}/attention_variable"] if fwd else P[f"{a1}/attention_v"],
             b1=P[f"{a1}/attention_bias"] if fwd else None,
             convW=P[f"{a1}/location_conv/kernel"] if fwd else None,
             convb=P[f"{a1}/location_conv/bias"] if fwd else None,
             locW=P[f"{a1}/location_layer/kernel"] if fwd else None,
-            v2=P[f"{a2}/attention_v"], dalpha_prev=DAP[1 - cur], df_out=DF[1 - cur],
-            dK1=dK1, dK2=dK2, dqp=DQP[t], pg=PG, pg_stride=pgs)
+            v2=P[f"{a2}/attention_v"], y_out=YA[1 - cur], df_out=DFH[t],
+            de1_out=DE1[t], de2_out=DE2[t], dqp=DQP[t])
 
     def lstm0_desc(t, cur):
         """Reverse step t of the attention RNN: recurrent + query gradients in one dot."""
@@ -298,12 +294,26 @@ def decoder_bwd(P, G, hp, d, dsv, dH2, masks, ws, attn_tile=32, pipe: Pipeline =
     if ms is not None:
         multi_speaker_prenet_bwd(P, G, d, S, ms, dP, ws)
 
-    # ---- attention parameters from the per-tile partials
+    # ---- attention parameters: one pass over all steps (sat_attn_param_grads), then a column
+    #      sum of its per-workgroup partial rows
+    F, KW = (d.loc_f, d.loc_k) if fwd else (0, 0)
+    pgs = K.pg_stride(D1, D2, F, KW)
+    PG = torch.empty(K.attn_param_grad_rows(B, N), pgs, **f32)
+    dK1 = torch.empty(B, N, D1, **f32)
+    dK2 = torch.empty(B, N, D2, **f32)
+    Qh = S["Q"]
+    K.attn_param_grads(
+        T=Tp, B=B, N=N, D1=D1, D2=D2, F=F, KW=KW, att1_forward=1 if fwd else 0,
+        K1=S["K1"], K2=S["K2"], q=Qh, q_tstride=Qh.stride(0), q_bstride=Qh.stride(1),
+        b1=P[f"{a1}/attention_bias"] if fwd else None,
+        v1=P[f"{a1}/attention_variable"] if fwd else P[f"{a1}/attention_v"],
+        locW=P[f"{a1}/location_layer/kernel"] if fwd else None, v2=P[f"{a2}/attention_v"],
+        loc=S["LOC"] if fwd else None, s_prev=S["S1"], s_tstride=S["S1"].stride(0),
+        de1=DE1, de2=DE2, df=DFH if fwd else None, dK1=dK1, dK2=dK2, pg=PG, pg_stride=pgs)
     pg_sum = torch.zeros(pgs, **f32)
     K.colsum(PG, pg_sum, ws, beta=0.0)
     o = 0
     if fwd:
-        F, KW = d.loc_f, d.loc_k
         K.axpby(pg_sum[o:o + D1], G[f"{a1}/attention_variable"], 1.0, 1.0); o += D1
         K.axpby(pg_sum[o:o + F * D1], G[f"{a1}/location_layer/kernel"].view(-1), 1.0, 1.0)
         o += F * D1
@@ -311,9 +321,7 @@ def decoder_bwd(P, G, hp, d, dsv, dH2, masks, ws, attn_tile=32, pipe: Pipeline =
         o += KW * F
         K.axpby(pg_sum[o:o + F], G[f"{a1}/location_conv/bias"], 1.0, 1.0); o += F
     else:
-        K.axpby(pg_sum[o:o + D1], G[f"{a1}/attention_v"], 1.0, 1.0)
-        o += D1 + 0
-        o = (1 + d.loc_f) * D1 + d.loc_k * d.loc_f + d.loc_f
+        K.axpby(pg_sum[o:o + D1], G[f"{a1}/attention_v"], 1.0, 1.0); o += D1
     K.axpby(pg_sum[o:o + D2], G[f"{a2}/attention_v"], 1.0, 1.0)
     # the per-tile partials of every step sum into the query-layer / bias gradients
     DQf = DQP.view(Tp * B * ntiles, D1 + D2)

@@ -34,6 +34,7 @@ struct AttnFwdP {
   float u;
   float* e1; float* e2;                  // [B][N]
   float* part; int64_t part_stride;      // [B][ntiles][part_stride]
+  float* loc_out;                        // [B][N][F] location features (history for the bwd), nullable
 };
 
 // partial record: [0]=m1 [1]=Z1 [2]=A1 [3]=m2 [4]=Z2 [5..7]=pad [8..8+M1) C1 [8+M1..) C2
@@ -230,6 +231,7 @@ __global__ void __launch_bounds__(256) attn_energy_kernel(AttnFwdP p) {
         for (int j = 0; j < p.KW; ++j) acc = fmaf(sp[i + j], cw[j * p.F + f], acc);
       }
       fs[i][f] = acc;
+      if (p.loc_out && i < nt && f < p.F) p.loc_out[(rb + n0 + i) * p.F + f] = acc;
     }
     __syncthreads();
   }
@@ -407,6 +409,7 @@ extern "C" int sat_attn_step_fwd(const SatAttnStep* a, void* stream) {
   p.v1 = a->v1; p.b1 = a->b1; p.convW = a->convW; p.convb = a->convb; p.locW = a->locW;
   p.v2 = a->v2; p.u = a->u; p.e1 = a->e1; p.e2 = a->e2; p.part = a->part;
   p.part_stride = a->part_stride;
+  p.loc_out = a->att1_forward ? a->loc_out : nullptr;
   hipStream_t s = as_stream(stream);
   const int phases = a->phases == 0 ? 3 : a->phases;
   if (phases & 1) {
@@ -432,15 +435,24 @@ extern "C" int sat_attn_step_fwd(const SatAttnStep* a, void* stream) {
 }
 
 // ============================================================================ backward
-// Reverse step t of the dual-source attention (see the forward formulas at the top).
-// K_b1 (per utterance x tile):  dA[n] = dA_next[n] + dc1 . V1[n],  dS2[n] = dc2 . V2[n]
-// K_b2 (per utterance x tile):  the normaliser sums over all n (cheap: [N] vectors), then for the
-//   tile: de, de2, dA_prev (recursion), the energies' tanh recomputed from K1 (no [T',B,N,224]
-//   tensor is ever stored), dK1/dK2 accumulated in place (each element owned by one thread),
-//   per-tile dq partials, location-conv grads df (conv-transposed by the NEXT reverse step into
-//   dS_prev), and the small parameter grads accumulated per (utterance, tile) without atomics.
-// Utterance b's tiles are mapped to blocks b, b+B, b+2B, ... so (B % 8 == 0) all of b's tiles
-// run on one XCD every step and K1[b], V1[b], dK1[b] stay in that XCD's L2.
+// Reverse step t of the dual-source attention (see the forward formulas at the top), ONE
+// launch per step: (utterance, tile) workgroups.
+//
+// The utterance-wide scalars of the softmax / forward-recursion backward need no cross-tile
+// pass over the values, because the forward context of step t is already a weighted sum of them:
+//   DA[n] = dc1 . V1[n] + dalpha_next[n]              (gradient reaching alpha_t[n])
+//   s1    = sum_n DA[n] alpha_t[n] = dc1 . c1_t + sum_n dalpha_next[n] alpha_t[n]
+//   s3    = sum_n DS2[n] s2_t[n]   = dc2 . c2_t
+//   s2sum = sum_n s_t[n] ds[n]     = sum_n s_t[n] DSN[n]   (the alpha path cancels: sum alpha = 1)
+// where DSN[n] = sum_{j,f} df_next[n - j + padl][f] convW[j][f] is the transposed location
+// convolution of the next reverse step's feature gradient (whole utterance, from LDS).  So each
+// block needs only its own tile's V1/V2 rows, and the [B,N] alpha-gradient crosses steps as
+//   Y[n] = s_t[n] (DA[n] - s1) / Sa,   dalpha_{t-1}[n] = (1-u) Y[n] + u Y[n+1].
+// Then the tile's energies are recomputed from K1 (no [T',B,N,224] tensor is stored) and
+// back-propagated through tanh: dK1/dK2 accumulated in place (each element owned by one thread),
+// per-tile dq partials, location-feature gradients df (-> DSN of step t-1), and the small
+// parameter grads accumulated per (utterance, tile) without atomics.
+// Utterance b's tiles are blocks b, b+B, b+2B, ... (B % 8 == 0: one XCD, K1[b] stays in its L2).
 namespace sat {
 namespace {
 
@@ -450,135 +462,45 @@ struct AttnBwdP {
   int B, N, D1, M1, D2, M2, F, KW, NT, ntiles, att1_forward;
   float u;
   const float* dctx; int64_t dctx_sb;
-  const float* dalpha_next;
+  const float* ctx_t; int64_t ctx_sb;
+  const float* y_next;
   const float* V1; const float* V2;
-  float* DA; float* DS2; float* DSN;
   const float* s_t; const float* a_t; const float* a_prev; const float* s_prev; const float* s2_t;
   const float* stats;
   const float* df_next;
-  const int64_t* lengths;
   const float* q; int64_t q_sb;
   const float* K1; const float* K2;
   const float* v1; const float* b1; const float* convW; const float* convb; const float* locW;
   const float* v2;
-  float* dalpha_prev;
+  float* y_out;
   float* df_out;
-  float* dK1; float* dK2;
+  float* de1_out; float* de2_out;
   float* dqp;
-  float* pg; int64_t pg_stride;
 };
 
-// Per-tile first stage of the backward step:
-//   DA[n]  = dctx1 . V1[n] + dalpha_next[n]      (gradient reaching the normalised alignment)
-//   DS2[n] = dctx2 . V2[n]
-//   DSN[n] = sum_{j,f} df_next[n - j + padl][f] convW[j][f]   (transpose of the next step's
-//            location convolution: how s_t feeds f_{t+1}); 0 when there is no next step.
-template <int NT>
-__global__ void __launch_bounds__(256) attn_bwd_ctx_kernel(AttnBwdP p) {
-  constexpr int PPW = NT / 4;
-  __shared__ float dc[2 * kMaxD];
-  __shared__ float dfw[(NT + kMaxKW) * kMaxFb];
-  __shared__ float cws[kMaxKW * kMaxFb];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int b = blockIdx.x % p.B, tile = blockIdx.x / p.B;
-  const int n0 = tile * NT, nt = min(NT, p.N - n0);
-  const int64_t rb = (int64_t)b * p.N;
-  const int F = p.att1_forward ? p.F : 0;
-  const int padl = (p.KW - 1) / 2;
-  const bool conv = F > 0 && p.df_next != nullptr;
-  float v1r[PPW][4], v2r[PPW], dan[PPW];
-#pragma unroll
-  for (int i = 0; i < PPW; ++i) {
-    const int nl = wave + 4 * i, n = min(n0 + nl, p.N - 1);
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int d = lane + 64 * s;
-      v1r[i][s] = d < p.M1 ? p.V1[(rb + n) * p.M1 + d] : 0.f;
-    }
-    v2r[i] = lane < p.M2 ? p.V2[(rb + n) * p.M2 + lane] : 0.f;
-    dan[i] = p.dalpha_next ? p.dalpha_next[rb + n] : 0.f;
-  }
-  const float* g = p.dctx + (int64_t)b * p.dctx_sb;
-  for (int i = tid; i < p.M1 + p.M2; i += 256) dc[i] = g[i];
-  if (conv) {
-    // window of df_next rows m in [n0 - (KW-1-padl), n0 + nt + padl)
-    const int lo = n0 - (p.KW - 1 - padl), span = nt + p.KW - 1;
-    for (int i = tid; i < span * F; i += 256) {
-      const int r = i / F, m = lo + r;
-      dfw[i] = (m >= 0 && m < p.N) ? p.df_next[(rb + m) * F + (i - r * F)] : 0.f;
-    }
-    for (int i = tid; i < p.KW * F; i += 256) cws[i] = p.convW[i];
-  }
-  __syncthreads();
-#pragma unroll
-  for (int i = 0; i < PPW; ++i) {
-    const int nl = wave + 4 * i;
-    if (nl >= nt) break;
-    float a = 0.f;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int d = lane + 64 * s;
-      if (d < p.M1) a = fmaf(dc[d], v1r[i][s], a);
-    }
-    float c = lane < p.M2 ? dc[p.M1 + lane] * v2r[i] : 0.f;
-    a = wave_sum(a);
-    c = wave_sum(c);
-    if (lane == 0) {
-      p.DA[rb + n0 + nl] = a + dan[i];
-      p.DS2[rb + n0 + nl] = c;
-    }
-  }
-  // DSN: 8 lanes per position, lanes stride over the KW taps
-  if (tid < NT * 8) {
-    const int nl = tid >> 3, part = tid & 7;
-    float acc = 0.f;
-    if (conv && nl < nt) {
-      // position n uses df_next[m] with m = n - j + padl, i.e. window row nl + (KW-1-padl) + padl - j
-      for (int j = part; j < p.KW; j += 8) {
-        const float* row = dfw + (nl + p.KW - 1 - j) * F;
-        const float* w = cws + j * F;
-        for (int f = 0; f < F; ++f) acc = fmaf(row[f], w[f], acc);
-      }
-    }
-    acc = group8_sum(acc);
-    if (part == 0 && nl < nt) p.DSN[rb + n0 + nl] = acc;
-  }
-}
+// LDS: df_next of the whole utterance early, the per-wave dq partials late
+constexpr int kBwdScratch = kMaxN * kMaxFb;
+static_assert(kBwdScratch >= 16 * (kMaxD + 64), "dq flush must fit the scratch");
 
-// LDS budget of the energy backward: per-wave accumulator flush (phase 4)
-constexpr int kBwdScratch = 4 * (kMaxD * (2 + kMaxFb) + 128);
-
-__device__ __forceinline__ float2 block_sum2(float a, float b, float* scratch) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  a = wave_sum_dpp(a);
-  b = wave_sum_dpp(b);
-  if (lane == 0) { scratch[w] = a; scratch[4 + w] = b; }
-  __syncthreads();
-  return make_float2((scratch[0] + scratch[1]) + (scratch[2] + scratch[3]),
-                     (scratch[4] + scratch[5]) + (scratch[6] + scratch[7]));
-}
-
-// Second stage: utterance-wide softmax / forward-recursion backward (scalars recomputed per
-// block from 8 N-vectors), then the tile's energies are recomputed and back-propagated through
-// tanh.  One wave per memory position, lanes over the energy dims (4 slots of 64; the LDS copies
-// of q, v, W_loc are zero padded to 256 so padding lanes contribute exact zeros).  F is
-// compile-time (0 = additive attention1), so the inner loop carries no guards.
-template <int NT, int F>
-__global__ void __launch_bounds__(256) attn_bwd_energy_kernel(AttnBwdP p) {
-  constexpr int PPW = NT / 4;
-  constexpr int kPos = kMaxN / 256;      // utterance positions per thread
-  constexpr int kPgr = 8;                // PG entries per thread (pg_stride <= 2048)
+// WAVES waves per block (NT / WAVES tile positions per wave): the step is latency-bound, so
+// more, shorter per-wave chains (8 waves = 2 per SIMD) hide the LDS / transcendental latencies.
+template <int NT, int F, int WAVES>
+__global__ void __launch_bounds__(64 * WAVES) attn_bwd_kernel(AttnBwdP p) {
+  constexpr int NTH = 64 * WAVES;
+  constexpr int PPW = NT / WAVES;
+  constexpr int kPos = (kMaxN + NTH - 1) / NTH;   // utterance positions per thread
   constexpr int FL = F > 0 ? F : 1;
   constexpr bool FWD = F > 0;
-  __shared__ float dst[NT + 1], dat[NT + 2], stt[NT + 2];
+  static_assert(NT % WAVES == 0 && NTH >= kMaxD, "tile / wave split");
+  __shared__ float dc[2 * kMaxD];
+  __shared__ float dsn_t[NT], dan_t[NT], stv[NT], s2v[NT], apv[NT + 1];
   __shared__ float qb[kMaxD], vv[kMaxD], q2s[64], v2s[64];
   __shared__ float locw[FL * kMaxD];
   __shared__ float cw[kMaxKW * FL + FL];
   __shared__ float fs[NT][FL], dfs[NT][FL];
   __shared__ float sp[NT + kMaxKW];
   __shared__ float de1[NT], de2[NT];
-  __shared__ float convg[kMaxKW * FL + FL];
-  __shared__ float red[16];
+  __shared__ float red[3 * WAVES];
   __shared__ float scratch[kBwdScratch];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -587,51 +509,49 @@ __global__ void __launch_bounds__(256) attn_bwd_energy_kernel(AttnBwdP p) {
   const int64_t rb = (int64_t)b * p.N;
   const int padl = (p.KW - 1) / 2;
   const float u = p.u;
-  const int D1 = p.D1, D2 = p.D2, N = p.N;
-  const int64_t pgrow = ((int64_t)b * p.ntiles + tile) * p.pg_stride;
+  const int D1 = p.D1, D2 = p.D2, N = p.N, M1 = p.M1, M2 = p.M2;
+  const bool has_next = p.y_next != nullptr;     // false at the last decoder step
 
   // ---------------- burst: registers (indices clamped: no load behind a branch)
-  float k1r[PPW][4], dk1r[PPW][4], k2r[PPW], dk2r[PPW];
+  float k1r[PPW][4], k2r[PPW], v1r[PPW][4], v2r[PPW];
 #pragma unroll
   for (int i = 0; i < PPW; ++i) {
-    const int n = min(n0 + wave + 4 * i, N - 1);
+    const int n = min(n0 + wave + WAVES * i, N - 1);
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       const int d = min(lane + 64 * s, D1 - 1);
       k1r[i][s] = p.K1[(rb + n) * D1 + d];
-      dk1r[i][s] = p.dK1[(rb + n) * D1 + d];
+      v1r[i][s] = p.V1[(rb + n) * M1 + min(lane + 64 * s, M1 - 1)];
     }
-    const int d2 = min(lane, D2 - 1);
-    k2r[i] = p.K2[(rb + n) * D2 + d2];
-    dk2r[i] = p.dK2[(rb + n) * D2 + d2];
+    k2r[i] = p.K2[(rb + n) * D2 + min(lane, D2 - 1)];
+    v2r[i] = p.V2[(rb + n) * M2 + min(lane, M2 - 1)];
   }
-  float rDA[kPos], rDS2[kPos], rat[kPos], rst[kPos], rs2[kPos], rap[kPos], ram[kPos], rsn[kPos];
+  float ry0[kPos], ry1[kPos], rat[kPos], rst[kPos];
 #pragma unroll
   for (int i = 0; i < kPos; ++i) {
-    const int n = tid + 256 * i;
-    const bool ok = n < N;
+    const int n = tid + NTH * i;
     const int64_t o = rb + min(n, N - 1);
-    rDA[i] = ok ? p.DA[o] : 0.f;
-    rDS2[i] = ok ? p.DS2[o] : 0.f;
-    rst[i] = ok ? p.s_t[o] : 0.f;
-    rs2[i] = ok ? p.s2_t[o] : 0.f;
-    if (FWD) {
-      rat[i] = ok ? p.a_t[o] : 0.f;
-      rap[i] = ok ? p.a_prev[o] : 0.f;
-      ram[i] = (ok && n > 0) ? p.a_prev[o - 1] : 0.f;
-      rsn[i] = ok ? p.DSN[o] : 0.f;
-    }
+    ry0[i] = (has_next && n < N) ? p.y_next[o] : 0.f;
+    ry1[i] = (has_next && n + 1 < N) ? p.y_next[o + 1] : 0.f;
+    rat[i] = n < N ? p.a_t[o] : 0.f;
+    rst[i] = n < N ? p.s_t[o] : 0.f;
   }
-  float pgr[kPgr];
-#pragma unroll
-  for (int i = 0; i < kPgr; ++i) {
-    const int j = min(tid + 256 * i, (int)p.pg_stride - 1);
-    pgr[i] = p.pg[pgrow + j];
+  // dc . c_t (the forward context of step t)
+  float dcc1 = 0.f, dcc2 = 0.f;
+  {
+    const float* g = p.dctx + (int64_t)b * p.dctx_sb;
+    const float* c = p.ctx_t + (int64_t)b * p.ctx_sb;
+    for (int d = tid; d < M1 + M2; d += NTH) {
+      const float gv = g[d];
+      dc[d] = gv;
+      if (d < M1) dcc1 = fmaf(gv, c[d], dcc1);
+      else dcc2 = fmaf(gv, c[d], dcc2);
+    }
   }
   // ---------------- burst: LDS (zero padded to 256 / 64)
   const float* q = p.q + (int64_t)b * p.q_sb;
-  {
-    const int d = tid;   // kMaxD == 256 == blockDim
+  if (tid < kMaxD) {
+    const int d = tid;
     const bool ok = d < D1;
     qb[d] = ok ? q[d] + (p.b1 ? p.b1[d] : 0.f) : 0.f;
     vv[d] = ok ? p.v1[d] : 0.f;
@@ -644,44 +564,46 @@ __global__ void __launch_bounds__(256) attn_bwd_energy_kernel(AttnBwdP p) {
       for (int f = 0; f < F; ++f) locw[f * kMaxD + d] = ok ? p.locW[f * D1 + d] : 0.f;
     }
   }
+  float* dfall = scratch;   // [N][F] df_next of the whole utterance (free until the flush)
+  if (tid < nt) {
+    stv[tid] = p.s_t[rb + n0 + tid];
+    s2v[tid] = p.s2_t[rb + n0 + tid];
+  }
   if (FWD) {
-    for (int i = tid; i < p.KW * F; i += 256) cw[i] = p.convW[i];
+    if (tid <= nt) apv[tid] = (n0 - 1 + tid >= 0 && n0 - 1 + tid < N) ? p.a_prev[rb + n0 - 1 + tid] : 0.f;
+    for (int i = tid; i < p.KW * F; i += NTH) cw[i] = p.convW[i];
     if (tid < F) cw[p.KW * F + tid] = p.convb[tid];
     const int span = nt + p.KW - 1;
-    for (int i = tid; i < span; i += 256) {
+    for (int i = tid; i < span; i += NTH) {
       const int n = n0 - padl + i;
       sp[i] = (n >= 0 && n < N) ? p.s_prev[rb + n] : 0.f;
     }
+    if (has_next)
+      for (int i = tid; i < N * F; i += NTH) dfall[i] = p.df_next[rb * F + i];
   }
-  // ---------------- normaliser sums over the utterance
-  float s1 = 0.f, s3 = 0.f;
+  __syncthreads();
+
+  // ---------------- utterance-wide sums: s1 = dc1.c1 + sum dalpha_next alpha, s3 = dc2.c2,
+  //                  s2sum = sum s DSN; the tile keeps its own DSN / dalpha_next
+  float s1 = dcc1, s3 = dcc2, s2 = 0.f;
 #pragma unroll
   for (int i = 0; i < kPos; ++i) {
-    if (FWD) s1 = fmaf(rDA[i], rat[i], s1);
-    s3 = fmaf(rs2[i], rDS2[i], s3);
-  }
-  const float2 s13 = block_sum2(s1, s3, red);   // barrier also publishes the LDS burst
-  s1 = s13.x; s3 = s13.y;
-  const float Sa = FWD ? p.stats[b * 4 + 2] : 1.f;
-  const float rSa = 1.f / Sa;
-  float s2sum = 0.f;
+    const int n = tid + NTH * i;
+    if (n >= N) break;
+    const float dan = (1.f - u) * ry0[i] + u * ry1[i];
+    s1 = fmaf(dan, rat[i], s1);
+    float dsn = 0.f;
+    if (FWD && has_next) {
+      for (int j = 0; j < p.KW; ++j) {
+        const int m = n - j + padl;
+        if (m < 0 || m >= N) continue;
 #pragma unroll
-  for (int i = 0; i < kPos; ++i) {
-    const int n = tid + 256 * i;
-    float ds, da = 0.f;
-    if (FWD) {
-      da = (rDA[i] - s1) * rSa;
-      ds = rsn[i] + da * ((1.f - u) * rap[i] + u * ram[i] + 1e-7f);
-    } else {
-      ds = rDA[i];
+        for (int f = 0; f < F; ++f) dsn = fmaf(dfall[m * F + f], cw[j * F + f], dsn);
+      }
+      s2 = fmaf(rst[i], dsn, s2);
     }
-    s2sum = fmaf(rst[i], ds, s2sum);
     const int r = n - n0;
-    if (r >= 0 && r <= nt) {
-      if (r < nt) dst[r] = ds;
-      dat[r] = da;
-      stt[r] = rst[i];
-    }
+    if (r >= 0 && r < nt) { dsn_t[r] = dsn; dan_t[r] = dan; }
   }
   if (FWD) {  // location features of the tile
     if (tid < NT * F) {
@@ -691,35 +613,66 @@ __global__ void __launch_bounds__(256) attn_bwd_energy_kernel(AttnBwdP p) {
       fs[nl][f] = acc;
     }
   }
-  s2sum = block_sum2(s2sum, 0.f, red + 8).x;   // dst/dat/fs visible after its barrier
+  s1 = wave_sum_dpp(s1);
+  s3 = wave_sum_dpp(s3);
+  s2 = wave_sum_dpp(s2);
+  if (lane == 0) { red[wave] = s1; red[WAVES + wave] = s3; red[2 * WAVES + wave] = s2; }
+  __syncthreads();   // also publishes dsn_t / dan_t / fs
+  s1 = 0.f; s3 = 0.f; s2 = 0.f;
+#pragma unroll
+  for (int w = 0; w < WAVES; ++w) {
+    s1 += red[w]; s3 += red[WAVES + w]; s2 += red[2 * WAVES + w];
+  }
+  const float s2sum = FWD ? s2 : s1;
+  const float Sa = FWD ? p.stats[b * 4 + 2] : 1.f;
+  const float rSa = 1.f / Sa;
 
-  // ---------------- tile: de, de2, dA_prev
-  if (tid < nt) {
-    const int n = n0 + tid;
-    de1[tid] = stt[tid] * (dst[tid] - s2sum);
-    de2[tid] = p.s2_t[rb + n] * (p.DS2[rb + n] - s3);
-    if (FWD) {
-      float v = (1.f - u) * dat[tid] * stt[tid];
-      if (n + 1 < N) v += u * dat[tid + 1] * stt[tid + 1];
-      p.dalpha_prev[rb + n] = v;
+  // ---------------- tile: DA, DS2 (wave per position, lanes over the value dims) -> de, de2, Y
+#pragma unroll
+  for (int i = 0; i < PPW; ++i) {
+    const int nl = wave + WAVES * i;
+    if (nl >= nt) break;
+    float a = 0.f;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int d = lane + 64 * s;
+      if (d < M1) a = fmaf(dc[d], v1r[i][s], a);
+    }
+    float c = lane < M2 ? dc[M1 + lane] * v2r[i] : 0.f;
+    a = wave_sum(a);
+    c = wave_sum(c);
+    if (lane == 0) {
+      const int n = n0 + nl;
+      const float DA = a + dan_t[nl];
+      const float st = stv[nl];
+      float ds;
+      if (FWD) {
+        const float da = (DA - s1) * rSa;
+        const float prior = (1.f - u) * apv[nl + 1] + u * apv[nl] + 1e-7f;
+        ds = dsn_t[nl] + da * prior;
+        p.y_out[rb + n] = st * da;
+      } else {
+        ds = DA;
+      }
+      const float e1v = st * (ds - s2sum), e2v = s2v[nl] * (c - s3);
+      de1[nl] = e1v;
+      de2[nl] = e2v;
+      p.de1_out[rb + n] = e1v;
+      p.de2_out[rb + n] = e2v;
     }
   }
   __syncthreads();
 
-  // ---------------- recompute the tile's energies, back-propagate through tanh
-  float aq[4] = {0, 0, 0, 0}, av[4] = {0, 0, 0, 0};
-  float aw[4][FL];
-#pragma unroll
-  for (int k = 0; k < 4; ++k)
-#pragma unroll
-    for (int f = 0; f < FL; ++f) aw[k][f] = 0.f;
-  float aq2 = 0.f, av2 = 0.f;   // lane owns d2 = lane (D2 <= 64, checked on the host)
+  // ---------------- recompute the tile's energies, back-propagate through tanh: the query
+  //                  gradient and the location-feature gradient (the critical path); the
+  //                  parameter gradients are left to sat_attn_param_grads after the loop
+  float aq[4] = {0, 0, 0, 0};
+  float aq2 = 0.f;   // lane owns d2 = lane (D2 <= 64, checked on the host)
   const float q2 = q2s[lane], v2 = v2s[lane];
 #pragma unroll
   for (int i = 0; i < PPW; ++i) {
-    const int nl = wave + 4 * i;
+    const int nl = wave + WAVES * i;
     if (nl >= nt) break;
-    const int64_t row = rb + n0 + nl;
     const float e = de1[nl];
     float fl[FL], dfp[FL];
 #pragma unroll
@@ -733,14 +686,9 @@ __global__ void __launch_bounds__(256) attn_bwd_energy_kernel(AttnBwdP p) {
       for (int f = 0; f < F; ++f) { lw[f] = locw[f * kMaxD + d]; pre = fmaf(fl[f], lw[f], pre); }
       const float z = tanh_fast(pre);
       const float dp = e * vv[d] * (1.f - z * z);
-      if (d < D1) p.dK1[row * D1 + d] = dk1r[i][k] + dp;
       aq[k] += dp;
-      av[k] = fmaf(e, z, av[k]);
 #pragma unroll
-      for (int f = 0; f < F; ++f) {
-        aw[k][f] = fmaf(fl[f], dp, aw[k][f]);
-        dfp[f] = fmaf(dp, lw[f], dfp[f]);
-      }
+      for (int f = 0; f < F; ++f) dfp[f] = fmaf(dp, lw[f], dfp[f]);
     }
 #pragma unroll
     for (int f = 0; f < F; ++f) {
@@ -748,90 +696,189 @@ __global__ void __launch_bounds__(256) attn_bwd_energy_kernel(AttnBwdP p) {
       if (lane == 0) dfs[nl][f] = sdf;
     }
     {
-      const float e2v = de2[nl];
       const float z = tanh_fast(k2r[i] + q2);
-      const float dp = e2v * v2 * (1.f - z * z);
-      if (lane < D2) p.dK2[row * D2 + lane] = dk2r[i] + dp;
-      aq2 += dp;
-      av2 = fmaf(e2v, z, av2);
+      aq2 = fmaf(de2[nl] * v2, 1.f - z * z, aq2);
     }
   }
-  // ---------------- per-wave accumulators -> LDS (layout per wave:
-  //                  [dq D1][dv1 D1][dWloc F*D1][dq2 64][dv2 64])
-  const int W = D1;
-  constexpr int wstride = kBwdScratch / 4;
+  // ---------------- per-wave dq partials -> LDS ([dq D1 (256)][dq2 64] per wave; dfall is dead)
+  constexpr int wstride = kMaxD + 64;
   float* r = scratch + wave * wstride;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int d = lane + 64 * k;
-    if (d < W) {
-      r[d] = aq[k];
-      r[W + d] = av[k];
-#pragma unroll
-      for (int f = 0; f < F; ++f) r[2 * W + f * W + d] = aw[k][f];
-    }
-  }
-  const int off2 = (2 + F) * W;
-  r[off2 + lane] = aq2;
-  r[off2 + 64 + lane] = av2;
   __syncthreads();
-  if (FWD) {   // location conv grads of the tile
-    for (int i = tid; i < p.KW * F + F; i += 256) {
-      float acc = 0.f;
-      if (i < p.KW * F) {
-        const int j = i / F, f = i - j * F;
-        for (int nl = 0; nl < nt; ++nl) acc = fmaf(sp[nl + j], dfs[nl][f], acc);
-      } else {
-        const int f = i - p.KW * F;
-        for (int nl = 0; nl < nt; ++nl) acc += dfs[nl][f];
-      }
-      convg[i] = acc;
-    }
-    if (tid < nt * F) {
-      const int nl = tid / F, f = tid - nl * F;
-      p.df_out[(rb + n0 + nl) * F + f] = dfs[nl][f];
-    }
-    __syncthreads();
-  }
-  // ---------------- outputs: dq partials (overwrite) and the PG row (accumulate)
-  float* dqp = p.dqp + ((int64_t)b * p.ntiles + tile) * (D1 + D2);
-  for (int d = tid; d < D1 + D2; d += 256) {
-    const int o = d < D1 ? d : off2 + (d - D1);
-    dqp[d] = (scratch[o] + scratch[wstride + o]) + (scratch[2 * wstride + o] + scratch[3 * wstride + o]);
-  }
-  // pg layout: [dv1 D1][dWloc F*D1][dconvW KW*F][dconvb F][dv2 D2]
-  const int pconv = (1 + F) * W, pv2 = pconv + p.KW * F + F;
 #pragma unroll
-  for (int i = 0; i < kPgr; ++i) {
-    const int j = tid + 256 * i;
-    if (j >= p.pg_stride) break;
-    float c = 0.f;
-    if (j < pconv) {
-      const int o = W + j;   // dv1 at [W, 2W), dWloc at [2W, (2+F)W)
-      c = (scratch[o] + scratch[wstride + o]) + (scratch[2 * wstride + o] + scratch[3 * wstride + o]);
-    } else if (j < pv2) {
-      if (FWD) c = convg[j - pconv];
-    } else if (j < pv2 + D2) {
-      const int o = off2 + 64 + (j - pv2);
-      c = (scratch[o] + scratch[wstride + o]) + (scratch[2 * wstride + o] + scratch[3 * wstride + o]);
-    }
-    p.pg[pgrow + j] = pgr[i] + c;
+  for (int k = 0; k < 4; ++k) r[lane + 64 * k] = aq[k];
+  r[kMaxD + lane] = aq2;
+  __syncthreads();
+  if (FWD && tid < nt * F) {
+    const int nl = tid / F, f = tid - nl * F;
+    p.df_out[(rb + n0 + nl) * F + f] = dfs[nl][f];
+  }
+  float* dqp = p.dqp + ((int64_t)b * p.ntiles + tile) * (D1 + D2);
+  for (int d = tid; d < D1 + D2; d += NTH) {
+    const int o = d < D1 ? d : kMaxD + (d - D1);
+    float acc = 0.f;
+#pragma unroll
+    for (int w = 0; w < WAVES; ++w) acc += scratch[w * wstride + o];
+    dqp[d] = acc;
   }
 }
 
-template <int NT>
+// ---------------------------------------------------------------- parameter gradients
+// After the reverse loop, every per-step contribution to the attention parameters is summed in
+// ONE pass over (t, b, n): the energy pre-activations are recomputed from K1/K2, the stored
+// processed queries and location features, and the stored energy gradients de1/de2 (scalars per
+// step and position):
+//   dp[d] = de1 v1[d] (1 - z[d]^2),  z = tanh(K1[n] + q_t + b1 + f_t[n] W_loc)
+//   dK1[n] = sum_t dp,  dv1 = sum z de1,  dW_loc[f] = sum f_t[n][f] dp,
+//   dconvW[j][f] = sum s_{t-1}[n + j - padl] df_t[n][f],  dconvb[f] = sum df_t[n][f]
+// (the same for source 2 without the location terms).  One wave per memory position, lanes
+// over float4 slots of [D1 | D2]; the wave loops over the T' steps; the four positions of a
+// workgroup are reduced through LDS into one partial row (summed by a column reduction).
+template <int SLOTS, int F>
+__global__ void __launch_bounds__(256) attn_param_grad_kernel(SatAttnParamGrad p) {
+  constexpr int FL = F > 0 ? F : 1;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int nq = (p.N + 3) / 4;
+  const int b = blockIdx.x / nq, n = 4 * (blockIdx.x - b * nq) + wave;
+  const bool live = n < p.N;
+  const int nn = min(n, p.N - 1);
+  const int Q1 = p.D1 / 4, Q = Q1 + p.D2 / 4;
+  const int padl = (p.KW - 1) / 2;
+  const int64_t bn = (int64_t)b * p.N + nn;
+  const int64_t TBN = (int64_t)p.B * p.N;
+
+  float4 kk[SLOTS], bb[SLOTS], vv[SLOTS], lw[SLOTS][FL];
+  float4 adk[SLOTS], adv[SLOTS], adw[SLOTS][FL];
+  bool m1[SLOTS], ok[SLOTS];
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int s = 0; s < SLOTS; ++s) {
+    const int c = lane + 64 * s;
+    ok[s] = c < Q;
+    m1[s] = c < Q1;
+    const int c1 = min(c, Q1 - 1), c2 = min(max(c - Q1, 0), p.D2 / 4 - 1);
+    kk[s] = m1[s] ? reinterpret_cast<const float4*>(p.K1 + bn * p.D1)[c1]
+                  : reinterpret_cast<const float4*>(p.K2 + bn * p.D2)[c2];
+    bb[s] = (m1[s] && p.b1) ? reinterpret_cast<const float4*>(p.b1)[c1] : z4;
+    vv[s] = m1[s] ? reinterpret_cast<const float4*>(p.v1)[c1] : reinterpret_cast<const float4*>(p.v2)[c2];
+#pragma unroll
+    for (int f = 0; f < F; ++f)
+      lw[s][f] = m1[s] ? reinterpret_cast<const float4*>(p.locW + (int64_t)f * p.D1)[c1] : z4;
+    adk[s] = z4; adv[s] = z4;
+#pragma unroll
+    for (int f = 0; f < FL; ++f) adw[s][f] = z4;
+  }
+  // location-conv roles: lane < KW*F owns (j, f) of convW, the next F lanes own convb
+  const int nconv = F > 0 ? p.KW * F : 0;
+  const int cj = F > 0 ? lane / FL : 0, cf = F > 0 ? lane - cj * FL : 0;
+  float acw = 0.f;
+  const int qoff = 4 * min(lane, Q1 - 1);   // (unused lanes read a valid address)
+  (void)qoff;
+  for (int t = 0; t < p.T; ++t) {
+    const int64_t tb = (int64_t)t * TBN + bn;
+    const float e1 = p.de1[tb], e2 = p.de2[tb];
+    float fl[FL];
+#pragma unroll
+    for (int f = 0; f < F; ++f) fl[f] = p.loc[tb * F + f];
+    const float* qt = p.q + (int64_t)t * p.q_tstride + (int64_t)b * p.q_bstride;
+#pragma unroll
+    for (int s = 0; s < SLOTS; ++s) {
+      const int c = lane + 64 * s;
+      const int cq = min(c, Q - 1);
+      const float4 qv = reinterpret_cast<const float4*>(qt)[cq];
+      float pre[4] = {kk[s].x + qv.x + bb[s].x, kk[s].y + qv.y + bb[s].y,
+                      kk[s].z + qv.z + bb[s].z, kk[s].w + qv.w + bb[s].w};
+      if (m1[s]) {
+#pragma unroll
+        for (int f = 0; f < F; ++f) {
+          pre[0] = fmaf(fl[f], lw[s][f].x, pre[0]); pre[1] = fmaf(fl[f], lw[s][f].y, pre[1]);
+          pre[2] = fmaf(fl[f], lw[s][f].z, pre[2]); pre[3] = fmaf(fl[f], lw[s][f].w, pre[3]);
+        }
+      }
+      const float e = m1[s] ? e1 : e2;
+      float z[4], dp[4];
+      const float vs[4] = {vv[s].x, vv[s].y, vv[s].z, vv[s].w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        z[k] = tanh_fast(pre[k]);
+        dp[k] = e * vs[k] * (1.f - z[k] * z[k]);
+      }
+      adk[s].x += dp[0]; adk[s].y += dp[1]; adk[s].z += dp[2]; adk[s].w += dp[3];
+      adv[s].x = fmaf(e, z[0], adv[s].x); adv[s].y = fmaf(e, z[1], adv[s].y);
+      adv[s].z = fmaf(e, z[2], adv[s].z); adv[s].w = fmaf(e, z[3], adv[s].w);
+#pragma unroll
+      for (int f = 0; f < F; ++f) {
+        adw[s][f].x = fmaf(fl[f], dp[0], adw[s][f].x); adw[s][f].y = fmaf(fl[f], dp[1], adw[s][f].y);
+        adw[s][f].z = fmaf(fl[f], dp[2], adw[s][f].z); adw[s][f].w = fmaf(fl[f], dp[3], adw[s][f].w);
+      }
+    }
+    if (F > 0 && lane < nconv + F) {
+      if (lane < nconv) {
+        const int m = nn + cj - padl;
+        const float sv = (m >= 0 && m < p.N) ? p.s_prev[(int64_t)t * p.s_tstride + (int64_t)b * p.N + m] : 0.f;
+        acw = fmaf(sv, p.df[tb * F + cf], acw);
+      } else {
+        acw += p.df[tb * F + (lane - nconv)];
+      }
+    }
+  }
+  // ---- outputs: dK rows (overwrite); partial parameter row of the workgroup (4 positions)
+  if (live) {
+#pragma unroll
+    for (int s = 0; s < SLOTS; ++s) {
+      const int c = lane + 64 * s;
+      if (!ok[s]) continue;
+      if (m1[s]) reinterpret_cast<float4*>(p.dK1 + bn * p.D1)[c] = adk[s];
+      else reinterpret_cast<float4*>(p.dK2 + bn * p.D2)[c - Q1] = adk[s];
+    }
+  }
+  // pg layout: [dv1 D1][dWloc F*D1][dconvW KW*F][dconvb F][dv2 D2]
+  extern __shared__ float red[];     // [4][pg_stride]
+  float* r = red + wave * p.pg_stride;
+  for (int i = lane; i < p.pg_stride; i += 64) r[i] = 0.f;
+  __syncthreads();
+  if (live) {
+    const int D1 = p.D1;
+    const int pconv = (1 + F) * D1, pv2 = pconv + nconv + F;
+#pragma unroll
+    for (int s = 0; s < SLOTS; ++s) {
+      const int c = lane + 64 * s;
+      if (!ok[s]) continue;
+      if (m1[s]) {
+        float* dv = r + 4 * c;
+        dv[0] = adv[s].x; dv[1] = adv[s].y; dv[2] = adv[s].z; dv[3] = adv[s].w;
+#pragma unroll
+        for (int f = 0; f < F; ++f) {
+          float* w = r + D1 + f * D1 + 4 * c;
+          w[0] = adw[s][f].x; w[1] = adw[s][f].y; w[2] = adw[s][f].z; w[3] = adw[s][f].w;
+        }
+      } else {
+        float* dv = r + pv2 + 4 * (c - Q1);
+        dv[0] = adv[s].x; dv[1] = adv[s].y; dv[2] = adv[s].z; dv[3] = adv[s].w;
+      }
+    }
+    if (F > 0 && lane < nconv + F) r[pconv + lane] = acw;
+  }
+  __syncthreads();
+  float* out = p.pg + (int64_t)blockIdx.x * p.pg_stride;
+  for (int i = threadIdx.x; i < p.pg_stride; i += 256) {
+    const int ps = p.pg_stride;
+    out[i] = (red[i] + red[ps + i]) + (red[2 * ps + i] + red[3 * ps + i]);
+  }
+}
+
+template <int NT, int WAVES>
 void launch_attn_bwd(const AttnBwdP& p, int F, int blocks, hipStream_t s) {
-  hipLaunchKernelGGL(attn_bwd_ctx_kernel<NT>, dim3(blocks), dim3(256), 0, s, p);
+  const dim3 g(blocks), blk(64 * WAVES);
   switch (F) {
-    case 0: hipLaunchKernelGGL((attn_bwd_energy_kernel<NT, 0>), dim3(blocks), dim3(256), 0, s, p); break;
-    case 1: hipLaunchKernelGGL((attn_bwd_energy_kernel<NT, 1>), dim3(blocks), dim3(256), 0, s, p); break;
-    case 2: hipLaunchKernelGGL((attn_bwd_energy_kernel<NT, 2>), dim3(blocks), dim3(256), 0, s, p); break;
-    case 3: hipLaunchKernelGGL((attn_bwd_energy_kernel<NT, 3>), dim3(blocks), dim3(256), 0, s, p); break;
-    case 4: hipLaunchKernelGGL((attn_bwd_energy_kernel<NT, 4>), dim3(blocks), dim3(256), 0, s, p); break;
-    case 5: hipLaunchKernelGGL((attn_bwd_energy_kernel<NT, 5>), dim3(blocks), dim3(256), 0, s, p); break;
-    case 6: hipLaunchKernelGGL((attn_bwd_energy_kernel<NT, 6>), dim3(blocks), dim3(256), 0, s, p); break;
-    case 7: hipLaunchKernelGGL((attn_bwd_energy_kernel<NT, 7>), dim3(blocks), dim3(256), 0, s, p); break;
-    default: hipLaunchKernelGGL((attn_bwd_energy_kernel<NT, 8>), dim3(blocks), dim3(256), 0, s, p); break;
+    case 0: hipLaunchKernelGGL((attn_bwd_kernel<NT, 0, WAVES>), g, blk, 0, s, p); break;
+    case 1: hipLaunchKernelGGL((attn_bwd_kernel<NT, 1, WAVES>), g, blk, 0, s, p); break;
+    case 2: hipLaunchKernelGGL((attn_bwd_kernel<NT, 2, WAVES>), g, blk, 0, s, p); break;
+    case 3: hipLaunchKernelGGL((attn_bwd_kernel<NT, 3, WAVES>), g, blk, 0, s, p); break;
+    case 4: hipLaunchKernelGGL((attn_bwd_kernel<NT, 4, WAVES>), g, blk, 0, s, p); break;
+    case 5: hipLaunchKernelGGL((attn_bwd_kernel<NT, 5, WAVES>), g, blk, 0, s, p); break;
+    case 6: hipLaunchKernelGGL((attn_bwd_kernel<NT, 6, WAVES>), g, blk, 0, s, p); break;
+    case 7: hipLaunchKernelGGL((attn_bwd_kernel<NT, 7, WAVES>), g, blk, 0, s, p); break;
+    default: hipLaunchKernelGGL((attn_bwd_kernel<NT, 8, WAVES>), g, blk, 0, s, p); break;
   }
 }
 
@@ -844,39 +891,87 @@ extern "C" int sat_attn_pg_stride(int32_t D1, int32_t D2, int32_t F, int32_t KW)
   return (D1 + F * D1 + KW * F + F + D2 + 3) / 4 * 4;
 }
 
+extern "C" int sat_attn_param_grad_rows(int32_t B, int32_t N) { return B * ((N + 3) / 4); }
+
+extern "C" int sat_attn_param_grads(const SatAttnParamGrad* a, void* stream) {
+  SAT_CHECK_ARG(a && a->T > 0 && a->B > 0 && a->N > 0, "sat_attn_param_grads: bad sizes");
+  SAT_CHECK_ARG(a->D1 % 4 == 0 && a->D2 % 4 == 0 && a->D1 > 0 && a->D2 > 0 &&
+                (a->D1 + a->D2) / 4 <= 128, "sat_attn_param_grads: D1, D2 multiples of 4, D1+D2 <= 512");
+  const int F = a->att1_forward ? a->F : 0, KW = a->att1_forward ? a->KW : 0;
+  SAT_CHECK_ARG(F == 0 || F == 5 || (F >= 1 && F <= 8), "sat_attn_param_grads: F <= 8");
+  SAT_CHECK_ARG(KW * F + F <= 64, "sat_attn_param_grads: location conv needs KW*F + F <= 64");
+  SAT_CHECK_ARG(a->pg_stride >= sat_attn_pg_stride(a->D1, a->D2, F, KW) && a->pg_stride <= 8192,
+                "sat_attn_param_grads: pg stride");
+  SAT_CHECK_ARG(a->K1 && a->K2 && a->q && a->v1 && a->v2 && a->de1 && a->de2 && a->dK1 &&
+                a->dK2 && a->pg, "sat_attn_param_grads: null pointer");
+  SAT_CHECK_ARG(F == 0 || (a->locW && a->loc && a->s_prev && a->df),
+                "sat_attn_param_grads: forward attention needs loc / s_prev / df histories");
+  SAT_CHECK_ARG(aligned16(a->K1) && aligned16(a->K2) && aligned16(a->q) && aligned16(a->v1) &&
+                aligned16(a->v2) && aligned16(a->dK1) && aligned16(a->dK2) &&
+                (!a->b1 || aligned16(a->b1)) && (!a->locW || aligned16(a->locW)) &&
+                a->q_tstride % 4 == 0 && a->q_bstride % 4 == 0,
+                "sat_attn_param_grads: 16-byte aligned operands");
+  SatAttnParamGrad p = *a;
+  p.F = F; p.KW = KW;
+  const int slots = ((a->D1 + a->D2) / 4 + 63) / 64;
+  const dim3 grid(sat_attn_param_grad_rows(a->B, a->N));
+  const size_t shm = 4 * (size_t)a->pg_stride * sizeof(float);
+  hipStream_t s = as_stream(stream);
+  if (slots == 1 && F == 5) hipLaunchKernelGGL((attn_param_grad_kernel<1, 5>), grid, dim3(256), shm, s, p);
+  else if (slots == 1 && F == 0) hipLaunchKernelGGL((attn_param_grad_kernel<1, 0>), grid, dim3(256), shm, s, p);
+  else if (F == 0) hipLaunchKernelGGL((attn_param_grad_kernel<2, 0>), grid, dim3(256), shm, s, p);
+  else hipLaunchKernelGGL((attn_param_grad_kernel<2, 8>), grid, dim3(256), shm, s, p);
+  SAT_LAUNCH_CHECK("sat_attn_param_grads");
+  return SAT_OK;
+}
+
 extern "C" int sat_attn_step_bwd(const SatAttnStepBwd* a, void* stream) {
   SAT_CHECK_ARG(a && a->B > 0 && a->N > 0 && a->N <= kMaxN, "sat_attn_step_bwd: bad sizes (N <= 1024)");
   SAT_CHECK_ARG(a->D1 <= kMaxD && a->D2 <= 64 && a->M2 <= 64 && a->M1 + a->M2 <= 2 * kMaxD,
                 "sat_attn_step_bwd: D1 <= 256, D2 <= 64");
+  SAT_CHECK_ARG(a->M1 <= 256 && a->M1 > 0 && a->M2 > 0 && a->D1 > 0 && a->D2 > 0,
+                "sat_attn_step_bwd: M1 <= 256");
   SAT_CHECK_ARG((a->NT == 8 || a->NT == 16 || a->NT == 32) && a->ntiles == ceil_div(a->N, a->NT),
                 "sat_attn_step_bwd: tile size must be 8, 16 or 32");
-  SAT_CHECK_ARG(a->pg_stride <= 2048 && a->M1 <= 256, "sat_attn_step_bwd: pg_stride <= 2048, M1 <= 256");
   SAT_CHECK_ARG(!a->att1_forward || (a->F <= kMaxFb && a->KW <= kMaxKW),
                 "sat_attn_step_bwd: location conv too large (F <= 8)");
-  SAT_CHECK_ARG(a->pg_stride >= sat_attn_pg_stride(a->D1, a->D2, a->F, a->KW), "sat_attn_step_bwd: pg stride");
-  SAT_CHECK_ARG(a->dctx && a->V1 && a->V2 && a->DA && a->DS2 && a->s_t && a->s2_t && a->q &&
-                a->K1 && a->K2 && a->v1 && a->v2 && a->dK1 && a->dK2 && a->dqp && a->pg && a->DSN,
+  SAT_CHECK_ARG(a->dctx && a->ctx_t && a->V1 && a->V2 && a->s_t && a->a_t && a->s2_t && a->q &&
+                a->K1 && a->K2 && a->v1 && a->v2 && a->de1_out && a->de2_out && a->dqp,
                 "sat_attn_step_bwd: null pointer");
-  SAT_CHECK_ARG(!a->att1_forward || (a->a_t && a->a_prev && a->s_prev && a->stats && a->convW &&
-                                     a->convb && a->locW && a->dalpha_prev && a->df_out),
+  SAT_CHECK_ARG(!a->att1_forward || (a->a_prev && a->s_prev && a->stats && a->convW &&
+                                     a->convb && a->locW && a->y_out && a->df_out &&
+                                     (a->y_next == nullptr) == (a->df_next == nullptr)),
                 "sat_attn_step_bwd: forward attention state missing");
   AttnBwdP p;
   p.B = a->B; p.N = a->N; p.D1 = a->D1; p.M1 = a->M1; p.D2 = a->D2; p.M2 = a->M2; p.F = a->F;
   p.KW = a->KW; p.NT = a->NT; p.ntiles = a->ntiles; p.att1_forward = a->att1_forward; p.u = a->u;
-  p.dctx = a->dctx; p.dctx_sb = a->dctx_sb; p.dalpha_next = a->dalpha_next;
-  p.V1 = a->V1; p.V2 = a->V2; p.DA = a->DA; p.DS2 = a->DS2; p.DSN = a->DSN;
+  p.dctx = a->dctx; p.dctx_sb = a->dctx_sb; p.ctx_t = a->ctx_t; p.ctx_sb = a->ctx_sb;
+  p.y_next = a->att1_forward ? a->y_next : nullptr;
+  p.V1 = a->V1; p.V2 = a->V2;
   p.s_t = a->s_t; p.a_t = a->a_t; p.a_prev = a->a_prev; p.s_prev = a->s_prev; p.s2_t = a->s2_t;
-  p.stats = a->stats; p.df_next = a->df_next; p.lengths = a->lengths; p.q = a->q; p.q_sb = a->q_sb;
+  p.stats = a->stats; p.df_next = a->df_next; p.q = a->q; p.q_sb = a->q_sb;
   p.K1 = a->K1; p.K2 = a->K2; p.v1 = a->v1; p.b1 = a->b1; p.convW = a->convW; p.convb = a->convb;
-  p.locW = a->locW; p.v2 = a->v2; p.dalpha_prev = a->dalpha_prev; p.df_out = a->df_out;
-  p.dK1 = a->dK1; p.dK2 = a->dK2; p.dqp = a->dqp; p.pg = a->pg; p.pg_stride = a->pg_stride;
+  p.locW = a->locW; p.v2 = a->v2; p.y_out = a->y_out; p.df_out = a->df_out;
+  p.de1_out = a->de1_out; p.de2_out = a->de2_out; p.dqp = a->dqp;
 
   hipStream_t s = as_stream(stream);
   const int blocks = a->B * a->ntiles;
   const int F = a->att1_forward ? a->F : 0;
-  if (a->NT == 8) launch_attn_bwd<8>(p, F, blocks, s);
-  else if (a->NT == 16) launch_attn_bwd<16>(p, F, blocks, s);
-  else launch_attn_bwd<32>(p, F, blocks, s);
+  // waves per block: 0 = default (16: two positions per wave at NT = 32, measured fastest);
+  // the tile size picks the per-wave position count
+  const int waves = a->waves == 0 ? 16 : a->waves;
+  SAT_CHECK_ARG(waves == 4 || waves == 8 || waves == 16, "sat_attn_step_bwd: waves in {4, 8, 16}");
+  SAT_CHECK_ARG(a->NT >= waves || a->NT == 8, "sat_attn_step_bwd: NT >= waves");
+  if (a->NT == 8) launch_attn_bwd<8, 4>(p, F, blocks, s);
+  else if (a->NT == 16) {
+    if (waves == 4) launch_attn_bwd<16, 4>(p, F, blocks, s);
+    else if (waves == 8) launch_attn_bwd<16, 8>(p, F, blocks, s);
+    else launch_attn_bwd<16, 16>(p, F, blocks, s);
+  } else {
+    if (waves == 4) launch_attn_bwd<32, 4>(p, F, blocks, s);
+    else if (waves == 8) launch_attn_bwd<32, 8>(p, F, blocks, s);
+    else launch_attn_bwd<32, 16>(p, F, blocks, s);
+  }
   SAT_LAUNCH_CHECK("sat_attn_step_bwd");
   return SAT_OK;
 }

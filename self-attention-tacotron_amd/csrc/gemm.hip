@@ -359,7 +359,6 @@ __global__ void __launch_bounds__(256) gemm_splitk_reduce(GemmP p) {
   }
 }
 
-inline bool aligned16(const void* ptr) { return (reinterpret_cast<uintptr_t>(ptr) & 15) == 0; }
 
 // Skinny product C[M][N] = alpha * A[M][K] . Bt[N][K]^T + beta * C with both operands' rows
 // contiguous in K (a per-decoder-step [B=32] x [4U=1024] x [288] gradient product): 8 lanes

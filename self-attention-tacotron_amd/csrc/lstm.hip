@@ -313,7 +313,6 @@ __global__ void __launch_bounds__(256) lstm_bwd_kernel(LstmBwdMulti m) {
 
 using namespace sat;
 
-static inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 static int check_fwd(const SatLstmFwd* a, LstmFwdP& p, size_t& shm) {
   SAT_CHECK_ARG(a && a->B > 0 && a->U > 0 && a->K >= 0, "sat_lstm_step_fwd: bad sizes");

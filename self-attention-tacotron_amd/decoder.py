@@ -121,6 +121,9 @@ def decoder_forward(P: Dict[str, torch.Tensor], hp, d: Dims, m1: torch.Tensor, m
     AL1[0, :, 0] = 1.0                               # forward_attention.py:131-133
     S2 = torch.empty(Tp, B, N, **f32)
     ST = torch.empty(Tp, B, 4, **f32)
+    # location features f_t of every step (forward attention): the backward's parameter-gradient
+    # pass recomputes the energies from them
+    LOC = torch.empty(Tp, B, N, max(d.loc_f, 1), **f32) if d.att1 == "forward" else None
     ntiles = (N + attn_tile - 1) // attn_tile
     pst = K.part_stride(M1, M2)
     E1 = torch.empty(B, N, **f32)
@@ -157,7 +160,7 @@ def decoder_forward(P: Dict[str, torch.Tensor], hp, d: Dims, m1: torch.Tensor, m
             locW=P[f"{a1}/location_layer/kernel"] if att1_fwd else None,
             v2=P["decoder/attention2/attention_v"], e1=E1, e2=E2, part=PART, part_stride=pst,
             s_out=S1[t + 1], a_out=AL1[t + 1], s2_out=S2[t], ctx=REC0[t + 1], ctx_sb=R0,
-            stats=ST[t])
+            stats=ST[t], loc_out=None if LOC is None else LOC[t])
 
     # ---- decoder LSTM 1: input o_t = [h0'_t | c1_t | c2_t]  (ConcatOutputAndAttentionWrapper)
     W1 = P["decoder/lstm1/kernel"]                   # [A + M1 + M2 + D, 4D]
@@ -216,7 +219,8 @@ def decoder_forward(P: Dict[str, torch.Tensor], hp, d: Dims, m1: torch.Tensor, m
                 x1_chunk(*x1_at[i])
             if i in x2_at:
                 x2_chunk(*x2_at[i])
-    S.update(X0=X0, REC0=REC0, C0=C0, H0RAW=H0RAW, G0=G0, Q=Q, S1=S1, AL1=AL1, S2=S2, ST=ST)
+    S.update(X0=X0, REC0=REC0, C0=C0, H0RAW=H0RAW, G0=G0, Q=Q, S1=S1, AL1=AL1, S2=S2, ST=ST,
+             LOC=LOC)
     H1RAW, C1S, H1S, G1 = L1
     H2RAW, C2S, H2S, G2 = L2
     S.update(X1=X1, H1RAW=H1RAW, C1S=C1S, H1S=H1S, G1=G1, X2=X2, H2RAW=H2RAW, C2S=C2S,

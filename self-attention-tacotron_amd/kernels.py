@@ -304,6 +304,18 @@ def part_stride(M1, M2) -> int:
     return _lib.load().sat_attn_part_stride(M1, M2)
 
 
+def attn_param_grad_rows(B: int, N: int) -> int:
+    return int(_lib.load().sat_attn_param_grad_rows(B, N))
+
+
+def attn_param_grads(**kw):
+    a = _lib.SatAttnParamGrad()
+    for k, v in kw.items():
+        setattr(a, k, _p(v) if isinstance(v, torch.Tensor) else v)
+    _lib.check(_lib.load().sat_attn_param_grads(ctypes.byref(a), _stream()),
+               "sat_attn_param_grads")
+
+
 def attn_step_bwd(**kw):
     a = _lib.SatAttnStepBwd()
     for k, v in kw.items():

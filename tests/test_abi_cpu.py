@@ -51,10 +51,32 @@ def _c_sizeof(struct):
         return int(subprocess.run([exe], capture_output=True, text=True, check=True).stdout)
 
 
-@pytest.mark.parametrize("name", ["SatGemmDesc", "SatLstmFwd", "SatLstmBwd", "SatAttnStep",
-                                  "SatAttnStepBwd", "SatAdamConfig"])
+STRUCTS = ["SatGemmDesc", "SatLstmFwd", "SatLstmBwd", "SatAttnStep", "SatAttnStepBwd",
+           "SatAttnParamGrad", "SatAdamConfig"]
+
+
+def _c_offsets(struct, fields):
+    """offsetof every field as gcc lays out include/sat_abi.h."""
+    import subprocess
+    import tempfile
+    body = "".join(f'printf("%zu\\n", offsetof({struct}, {f}));' for f in fields)
+    src = (f'#include "sat_abi.h"\n#include <stdio.h>\n#include <stddef.h>\n'
+           f'int main(){{{body}}}\n')
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, "s.c")
+        open(c, "w").write(src)
+        exe = os.path.join(d, "s")
+        subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), c, "-o", exe], check=True)
+        out = subprocess.run([exe], capture_output=True, text=True, check=True).stdout
+    return [int(x) for x in out.split()]
+
+
+@pytest.mark.parametrize("name", STRUCTS)
 def test_ctypes_structs_match_c_layout(name):
-    assert ctypes.sizeof(getattr(_lib, name)) == _c_sizeof(name)
+    st = getattr(_lib, name)
+    assert ctypes.sizeof(st) == _c_sizeof(name)
+    fields = [f for f, _ in st._fields_ if not f.startswith("pad")]
+    assert [getattr(st, f).offset for f in fields] == _c_offsets(name, fields)
 
 
 def test_errors_are_reported_not_swallowed():

@@ -101,28 +101,30 @@ def main():
             ctx_sb=M1 + M2, stats=st, phases=phases)
     res["attn fwd energy tile (phase 1)"] = timed_graph(lambda t: attn(t, 1), Tp)
     res["attn fwd energy + combine (2 launches)"] = timed_graph(lambda t: attn(t, 3), Tp)
-    pgs = K.pg_stride(D1, D2, d.loc_f, d.loc_k)
-    DA, DS2, DSN = (torch.empty(B, N, **f) for _ in range(3))
-    DAP = torch.zeros(B, N, **f)
+    YA = torch.zeros(B, N, **f)
     DF = torch.zeros(B, N, d.loc_f, **f)
     DQ = torch.empty(B, ntiles, D1 + D2, **f)
     DQR = torch.empty(B, D1 + D2, **f)
-    dK1, dK2 = torch.zeros(B, N, D1, **f), torch.zeros(B, N, D2, **f)
-    PG = torch.zeros(B * ntiles, pgs, **f)
+    DE = torch.empty(B, N, **f)
+    DQ8 = torch.empty(B, (N + 7) // 8, D1 + D2, **f)
     dctx = torch.randn(Tp, B, M1 + M2, **f) * 1e-3
 
-    def attn_bwd(t):
+    def attn_bwd(t, nt=32, waves=0):
+        ntl = (N + nt - 1) // nt
         K.attn_step_bwd(
-            B=B, N=N, D1=D1, M1=M1, D2=D2, M2=M2, F=d.loc_f, KW=d.loc_k, NT=32, ntiles=ntiles,
-            att1_forward=1, u=0.5, dctx=dctx[t], dctx_sb=M1 + M2, dalpha_next=DAP, V1=S["V1"],
-            V2=S["V2"], DA=DA, DS2=DS2, DSN=DSN, s_t=S["S1"][t + 1], a_t=S["AL1"][t + 1],
+            B=B, N=N, D1=D1, M1=M1, D2=D2, M2=M2, F=d.loc_f, KW=d.loc_k, NT=nt, ntiles=ntl,
+            att1_forward=1, u=0.5, dctx=dctx[t], dctx_sb=M1 + M2, ctx_t=S["REC0"][t + 1],
+            ctx_sb=S["REC0"].shape[-1], y_next=YA, V1=S["V1"],
+            V2=S["V2"], s_t=S["S1"][t + 1], a_t=S["AL1"][t + 1],
             a_prev=S["AL1"][t], s_prev=S["S1"][t], s2_t=S["S2"][t], stats=S["ST"][t],
-            df_next=DF, lengths=None, q=S["Q"][t], q_sb=D1 + D2, K1=S["K1"], K2=S["K2"],
+            df_next=DF, q=S["Q"][t], q_sb=D1 + D2, K1=S["K1"], K2=S["K2"],
             v1=P[f"{a1}/attention_variable"], b1=P[f"{a1}/attention_bias"],
             convW=P[f"{a1}/location_conv/kernel"], convb=P[f"{a1}/location_conv/bias"],
             locW=P[f"{a1}/location_layer/kernel"], v2=P["decoder/attention2/attention_v"],
-            dalpha_prev=DAP, df_out=DF, dK1=dK1, dK2=dK2, dqp=DQ, pg=PG, pg_stride=pgs)
-    res["attn bwd (ctx + energy)"] = timed_graph(attn_bwd, Tp)
+            y_out=YA, df_out=DF, de1_out=DE, de2_out=DE, dqp=DQ8, waves=waves)
+    for nt, w in ((16, 4), (16, 8), (16, 16), (32, 4), (32, 8), (32, 16)):
+        res[f"attn bwd NT={nt} waves={w}"] = timed_graph(
+            lambda t, nt=nt, w=w: attn_bwd(t, nt, w), Tp)
     dy = torch.randn(Tp, B, A, **f) * 1e-3
 
     def lstm_bwd(t, dq):

@@ -185,6 +185,8 @@ typedef struct SatAttnStep {
   float* ctx; int64_t ctx_sb;               /* [B][M1 + M2] */
   float* stats;                             /* [B][4] or NULL */
   float* loc_out;                           /* [B][N][F] location features (bwd history) or NULL */
+  int32_t lpp;                              /* lanes per memory position of the tile kernel:
+                                               0 (= 16), 8, 16 or 32 */
   int32_t phases;                           /* 0 or 3: both kernels; 1: tile kernel only;
                                                2: combine only (profiling / split launches) */
 } SatAttnStep;

@@ -85,7 +85,7 @@ SatAttnStep = _struct("SatAttnStep", """
     i32:B i32:N i32:D1 i32:M1 i32:D2 i32:M2 i32:F i32:KW i32:NT i32:ntiles i32:att1_forward
     f32:u ptr:q i64:q_sb ptr:K1 ptr:V1 ptr:K2 ptr:V2 ptr:lengths ptr:s_prev ptr:a_prev
     ptr:v1 ptr:b1 ptr:convW ptr:convb ptr:locW ptr:v2 ptr:e1 ptr:e2 ptr:part i64:part_stride
-    ptr:s_out ptr:a_out ptr:s2_out ptr:ctx i64:ctx_sb ptr:stats ptr:loc_out i32:phases""")
+    ptr:s_out ptr:a_out ptr:s2_out ptr:ctx i64:ctx_sb ptr:stats ptr:loc_out i32:lpp i32:phases""")
 
 # name -> argtypes (restype is int for all but sat_last_error_string)
 SIGNATURES = {

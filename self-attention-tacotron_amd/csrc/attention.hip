@@ -331,6 +331,198 @@ __global__ void __launch_bounds__(256) attn_energy_kernel(AttnFwdP p) {
   }
 }
 
+// Wide tile kernel: the same step with LPP lanes per memory position (NT * LPP threads, 512 or
+// 1024), so each lane's serial chain is 64 / LPP float4 of the (zero padded to 256) energy row;
+// the step is latency-bound, and more, shorter chains per block hide the exp / rcp / LDS
+// latencies.  Source 2 (D2 <= 4 * LPP) takes one float4 per lane.  Same partial record.
+template <int F, int LPP, bool FWD>
+__global__ void __launch_bounds__(kNT * LPP) attn_energy_wide_kernel(AttnFwdP p) {
+  constexpr int NT = kNT, NTH = NT * LPP, NW = NTH / 64;
+  constexpr int J = 64 / LPP;                      // float4 of the padded energy row per lane
+  constexpr int G = NTH / 64;                      // position groups of the context phase
+  constexpr int PG = NT / G;                       // positions per group
+  constexpr int FL = F > 0 ? F : 1;
+  __shared__ __attribute__((aligned(16))) float qb[kMaxD];
+  __shared__ __attribute__((aligned(16))) float vv[kMaxD];
+  __shared__ __attribute__((aligned(16))) float locw[FL * kMaxD];
+  __shared__ __attribute__((aligned(16))) float q2s[64];
+  __shared__ __attribute__((aligned(16))) float v2s[64];
+  __shared__ float cw[kMaxKW * kMaxF + kMaxF];
+  __shared__ float fs[NT][FL];
+  __shared__ float sp[NT + kMaxKW], ap[NT + 1];
+  __shared__ float e1s[NT], e2s[NT], w1s[NT], w2s[NT];
+  __shared__ __attribute__((aligned(16))) float4 cred[G][64];
+  __shared__ __attribute__((aligned(16))) float4 c2red[NT][16];
+  __shared__ float red[8];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int b = blockIdx.x % p.B, tile = blockIdx.x / p.B;
+  const int n0 = tile * NT;
+  const int nt = min(NT, p.N - n0);
+  const int64_t rb = (int64_t)b * p.N;
+  const int padl = (p.KW - 1) / 2;
+  const int D1 = p.D1;
+  const int nl = tid / LPP, part = tid - nl * LPP;
+  const int nc = min(n0 + nl, p.N - 1);       // clamped position for this lane's loads
+
+  // ---- burst: K1 / K2 slices of this lane's position, V1 / V2 rows of the context phase
+  float4 k1r[J];
+  {
+    const int d1q = D1 / 4;
+    const float4* k1p = reinterpret_cast<const float4*>(p.K1 + (rb + nc) * D1);
+#pragma unroll
+    for (int j = 0; j < J; ++j) k1r[j] = k1p[min(part + LPP * j, d1q - 1)];
+  }
+  const int d2q = p.D2 / 4;
+  const float4 k2r = reinterpret_cast<const float4*>(p.K2 + (rb + nc) * p.D2)[min(part, d2q - 1)];
+  const int c4 = lane, g = wave;               // context phase: group g, float4 column c4
+  const int M1q = p.M1 / 4, M2q = p.M2 / 4;
+  float4 v1r[PG];
+#pragma unroll
+  for (int i = 0; i < PG; ++i) {
+    const int n = min(n0 + g * PG + i, p.N - 1);
+    v1r[i] = reinterpret_cast<const float4*>(p.V1 + (rb + n) * p.M1)[min(c4, M1q - 1)];
+  }
+  const float4 v2r = reinterpret_cast<const float4*>(p.V2 + (rb + nc) * p.M2)[min(part, M2q - 1)];
+  // ---- burst: small per-step vectors and weights (LDS, zero padded)
+  const float* q = p.q + (int64_t)b * p.q_sb;
+  if (tid < kMaxD) {
+    const int d = tid;
+    const bool ok = d < D1;
+    qb[d] = ok ? q[d] + (p.b1 ? p.b1[d] : 0.f) : 0.f;
+    vv[d] = ok ? p.v1[d] : 0.f;
+    if (d < 64) {
+      q2s[d] = d < p.D2 ? q[D1 + d] : 0.f;
+      v2s[d] = d < p.D2 ? p.v2[d] : 0.f;
+    }
+    if (FWD) {
+#pragma unroll
+      for (int f = 0; f < F; ++f) locw[f * kMaxD + d] = (ok && f < p.F) ? p.locW[f * D1 + d] : 0.f;
+    }
+  }
+  if (FWD) {
+    if (tid < p.KW * p.F) cw[tid] = p.convW[tid];
+    if (tid < p.F) cw[p.KW * p.F + tid] = p.convb[tid];
+    const int span = nt + p.KW - 1;
+    if (tid < span) {
+      const int n = n0 - padl + tid;
+      sp[tid] = (n >= 0 && n < p.N) ? p.s_prev[rb + n] : 0.f;
+    }
+    if (tid <= nt) ap[tid] = (n0 - 1 + tid >= 0) ? p.a_prev[rb + n0 - 1 + tid] : 0.f;
+  }
+  const int len = (int)p.lengths[b];
+  __syncthreads();
+  if (FWD) {  // location features f = Conv1D_SAME(s_{t-1}) + bias
+    if (tid < NT * F) {
+      const int i = tid / F, f = tid - i * F;    // padded filters (f >= p.F) are zero
+      float acc = 0.f;
+      if (f < p.F) {
+        acc = cw[p.KW * p.F + f];
+        for (int j = 0; j < p.KW; ++j) acc = fmaf(sp[i + j], cw[j * p.F + f], acc);
+        if (p.loc_out && i < nt) p.loc_out[(rb + n0 + i) * p.F + f] = acc;
+      }
+      fs[i][f] = acc;
+    }
+    __syncthreads();
+  }
+  // ---- energies: J float4 per lane, LPP-lane reduction
+  float fl[FL];
+#pragma unroll
+  for (int f = 0; f < FL; ++f) fl[f] = FWD ? fs[nl][f] : 0.f;
+  float acc = 0.f;
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const int d = 4 * (part + LPP * j);
+    const float4 qv = *reinterpret_cast<const float4*>(&qb[d]);
+    const float4 vw = *reinterpret_cast<const float4*>(&vv[d]);
+    float4 pre = make_float4(k1r[j].x + qv.x, k1r[j].y + qv.y, k1r[j].z + qv.z, k1r[j].w + qv.w);
+    if (FWD) {
+#pragma unroll
+      for (int f = 0; f < F; ++f) {
+        const float4 lw = *reinterpret_cast<const float4*>(&locw[f * kMaxD + d]);
+        pre.x = fmaf(fl[f], lw.x, pre.x); pre.y = fmaf(fl[f], lw.y, pre.y);
+        pre.z = fmaf(fl[f], lw.z, pre.z); pre.w = fmaf(fl[f], lw.w, pre.w);
+      }
+    }
+    acc = fmaf(vw.x, tanh_fast(pre.x), acc);
+    acc = fmaf(vw.y, tanh_fast(pre.y), acc);
+    acc = fmaf(vw.z, tanh_fast(pre.z), acc);
+    acc = fmaf(vw.w, tanh_fast(pre.w), acc);
+  }
+  float acc2 = 0.f;
+  if (part < 16) {
+    const int d = 4 * part;
+    const float4 qv = *reinterpret_cast<const float4*>(&q2s[d]);
+    const float4 vw = *reinterpret_cast<const float4*>(&v2s[d]);
+    acc2 = fmaf(vw.x, tanh_fast(k2r.x + qv.x), acc2);
+    acc2 = fmaf(vw.y, tanh_fast(k2r.y + qv.y), acc2);
+    acc2 = fmaf(vw.z, tanh_fast(k2r.z + qv.z), acc2);
+    acc2 = fmaf(vw.w, tanh_fast(k2r.w + qv.w), acc2);
+  }
+  if (LPP == 16) { acc = group16_sum(acc); acc2 = group16_sum(acc2); }
+  else { acc = group32_sum(acc); acc2 = group32_sum(acc2); }
+  if (part == 0 && nl < nt) {
+    const bool valid = n0 + nl < len;
+    e1s[nl] = valid ? acc : -INFINITY;
+    e2s[nl] = valid ? acc2 : -INFINITY;
+  }
+  __syncthreads();
+  // ---- tile statistics (wave 0)
+  if (wave == 0) {
+    const float e1v = lane < nt ? e1s[lane] : -INFINITY;
+    const float e2v = lane < nt ? e2s[lane] : -INFINITY;
+    const float m1 = wave_max(e1v), m2 = wave_max(e2v);
+    const float pe = (e1v == -INFINITY) ? 0.f : expf(e1v - m1);
+    const float pe2 = (e2v == -INFINITY) ? 0.f : expf(e2v - m2);
+    float w = pe;
+    if (FWD && lane < nt) w = ((1.f - p.u) * ap[lane + 1] + p.u * ap[lane] + 1e-7f) * pe;
+    if (lane < NT) { w1s[lane] = lane < nt ? w : 0.f; w2s[lane] = lane < nt ? pe2 : 0.f; }
+    const float z1 = wave_sum_dpp(pe), a1 = wave_sum_dpp(lane < nt ? w : 0.f),
+                z2 = wave_sum_dpp(pe2);
+    if (lane == 0) { red[0] = m1; red[1] = z1; red[2] = a1; red[3] = m2; red[4] = z2; }
+  }
+  __syncthreads();
+  float* part_out = p.part + ((int64_t)b * p.ntiles + tile) * p.part_stride;
+  if (tid < kPartHdr) part_out[tid] = tid < 5 ? red[tid] : 0.f;
+  if (tid < nt) {
+    p.e1[rb + n0 + tid] = e1s[tid];
+    p.e2[rb + n0 + tid] = e2s[tid];
+  }
+  // ---- unnormalised partial contexts
+  float4 c = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int i = 0; i < PG; ++i) {
+    const float w = w1s[g * PG + i];
+    c.x = fmaf(w, v1r[i].x, c.x); c.y = fmaf(w, v1r[i].y, c.y);
+    c.z = fmaf(w, v1r[i].z, c.z); c.w = fmaf(w, v1r[i].w, c.w);
+  }
+  cred[g][c4] = c;
+  if (part < 16) {
+    const float w = w2s[nl];
+    c2red[nl][part] = make_float4(w * v2r.x, w * v2r.y, w * v2r.z, w * v2r.w);
+  }
+  __syncthreads();
+  if (tid < M1q) {
+    float4 sum = cred[0][tid];
+#pragma unroll
+    for (int j = 1; j < G; ++j) {
+      const float4 v = cred[j][tid];
+      sum.x += v.x; sum.y += v.y; sum.z += v.z; sum.w += v.w;
+    }
+    reinterpret_cast<float4*>(part_out + kPartHdr)[tid] = sum;
+  } else if (tid >= 64 && tid < 64 + M2q) {
+    const int j = tid - 64;
+    float4 sum = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 8
+    for (int i = 0; i < NT; ++i) {
+      const float4 v = c2red[i][j];
+      sum.x += v.x; sum.y += v.y; sum.z += v.z; sum.w += v.w;
+    }
+    reinterpret_cast<float4*>(part_out + kPartHdr + p.M1)[j] = sum;
+  }
+  (void)NW;
+}
+
 // q[b, :] = x[b, :] @ [W1 | W2]   (query layers of both mechanisms, no bias)
 __global__ void __launch_bounds__(256) query_kernel(int B, int K, int N1, int N2, const float* x,
                                                    int64_t x_sb, const float* W1, const float* W2,
@@ -414,7 +606,17 @@ extern "C" int sat_attn_step_fwd(const SatAttnStep* a, void* stream) {
   const int phases = a->phases == 0 ? 3 : a->phases;
   if (phases & 1) {
     const dim3 grid(a->ntiles * a->B);
-    if (a->att1_forward && a->F == 5 && a->D1 == 224 && a->D2 == 32)
+    const int lpp = a->lpp == 0 ? 16 : a->lpp;
+    SAT_CHECK_ARG(lpp == 8 || lpp == 16 || lpp == 32, "sat_attn_step_fwd: lpp in {8, 16, 32}");
+    if (lpp == 16 && a->att1_forward && a->F == 5)
+      hipLaunchKernelGGL((attn_energy_wide_kernel<5, 16, true>), grid, dim3(kNT * 16), 0, s, p);
+    else if (lpp == 32 && a->att1_forward && a->F == 5)
+      hipLaunchKernelGGL((attn_energy_wide_kernel<5, 32, true>), grid, dim3(kNT * 32), 0, s, p);
+    else if (lpp != 8 && a->att1_forward)
+      hipLaunchKernelGGL((attn_energy_wide_kernel<8, 16, true>), grid, dim3(kNT * 16), 0, s, p);
+    else if (lpp != 8)
+      hipLaunchKernelGGL((attn_energy_wide_kernel<0, 16, false>), grid, dim3(kNT * 16), 0, s, p);
+    else if (a->att1_forward && a->F == 5 && a->D1 == 224 && a->D2 == 32)
       hipLaunchKernelGGL((attn_energy_kernel<5, 7, 1, true>), grid, dim3(256), 0, s, p);
     else if (a->att1_forward)
       hipLaunchKernelGGL((attn_energy_kernel<8, 8, 2, true>), grid, dim3(256), 0, s, p);
@@ -771,53 +973,67 @@ __global__ void __launch_bounds__(256) attn_param_grad_kernel(SatAttnParamGrad p
   const int nconv = F > 0 ? p.KW * F : 0;
   const int cj = F > 0 ? lane / FL : 0, cf = F > 0 ? lane - cj * FL : 0;
   float acw = 0.f;
-  const int qoff = 4 * min(lane, Q1 - 1);   // (unused lanes read a valid address)
-  (void)qoff;
-  for (int t = 0; t < p.T; ++t) {
-    const int64_t tb = (int64_t)t * TBN + bn;
-    const float e1 = p.de1[tb], e2 = p.de2[tb];
-    float fl[FL];
+  // the step loop is latency-bound (a handful of dependent loads per step): issue the loads of
+  // kU steps at once, then do their arithmetic
+  constexpr int kU = 4;
+  for (int t0 = 0; t0 < p.T; t0 += kU) {
+    float e1s[kU], e2s[kU], fls[kU][FL], sv[kU], dfv[kU];
+    float4 qv[kU][SLOTS];
 #pragma unroll
-    for (int f = 0; f < F; ++f) fl[f] = p.loc[tb * F + f];
-    const float* qt = p.q + (int64_t)t * p.q_tstride + (int64_t)b * p.q_bstride;
+    for (int u = 0; u < kU; ++u) {
+      const int t = min(t0 + u, p.T - 1);
+      const bool on = t0 + u < p.T;
+      const int64_t tb = (int64_t)t * TBN + bn;
+      e1s[u] = on ? p.de1[tb] : 0.f;       // a step past T contributes exactly zero
+      e2s[u] = on ? p.de2[tb] : 0.f;
 #pragma unroll
-    for (int s = 0; s < SLOTS; ++s) {
-      const int c = lane + 64 * s;
-      const int cq = min(c, Q - 1);
-      const float4 qv = reinterpret_cast<const float4*>(qt)[cq];
-      float pre[4] = {kk[s].x + qv.x + bb[s].x, kk[s].y + qv.y + bb[s].y,
-                      kk[s].z + qv.z + bb[s].z, kk[s].w + qv.w + bb[s].w};
-      if (m1[s]) {
+      for (int f = 0; f < F; ++f) fls[u][f] = p.loc[tb * F + f];
+      const float* qt = p.q + (int64_t)t * p.q_tstride + (int64_t)b * p.q_bstride;
 #pragma unroll
-        for (int f = 0; f < F; ++f) {
-          pre[0] = fmaf(fl[f], lw[s][f].x, pre[0]); pre[1] = fmaf(fl[f], lw[s][f].y, pre[1]);
-          pre[2] = fmaf(fl[f], lw[s][f].z, pre[2]); pre[3] = fmaf(fl[f], lw[s][f].w, pre[3]);
+      for (int s = 0; s < SLOTS; ++s)
+        qv[u][s] = reinterpret_cast<const float4*>(qt)[min(lane + 64 * s, Q - 1)];
+      sv[u] = 0.f; dfv[u] = 0.f;
+      if (F > 0 && on && lane < nconv + F) {
+        if (lane < nconv) {
+          const int m = nn + cj - padl;
+          sv[u] = (m >= 0 && m < p.N) ? p.s_prev[(int64_t)t * p.s_tstride + (int64_t)b * p.N + m] : 0.f;
+          dfv[u] = p.df[tb * F + cf];
+        } else {
+          sv[u] = 1.f;
+          dfv[u] = p.df[tb * F + (lane - nconv)];
         }
       }
-      const float e = m1[s] ? e1 : e2;
-      float z[4], dp[4];
-      const float vs[4] = {vv[s].x, vv[s].y, vv[s].z, vv[s].w};
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        z[k] = tanh_fast(pre[k]);
-        dp[k] = e * vs[k] * (1.f - z[k] * z[k]);
-      }
-      adk[s].x += dp[0]; adk[s].y += dp[1]; adk[s].z += dp[2]; adk[s].w += dp[3];
-      adv[s].x = fmaf(e, z[0], adv[s].x); adv[s].y = fmaf(e, z[1], adv[s].y);
-      adv[s].z = fmaf(e, z[2], adv[s].z); adv[s].w = fmaf(e, z[3], adv[s].w);
-#pragma unroll
-      for (int f = 0; f < F; ++f) {
-        adw[s][f].x = fmaf(fl[f], dp[0], adw[s][f].x); adw[s][f].y = fmaf(fl[f], dp[1], adw[s][f].y);
-        adw[s][f].z = fmaf(fl[f], dp[2], adw[s][f].z); adw[s][f].w = fmaf(fl[f], dp[3], adw[s][f].w);
-      }
     }
-    if (F > 0 && lane < nconv + F) {
-      if (lane < nconv) {
-        const int m = nn + cj - padl;
-        const float sv = (m >= 0 && m < p.N) ? p.s_prev[(int64_t)t * p.s_tstride + (int64_t)b * p.N + m] : 0.f;
-        acw = fmaf(sv, p.df[tb * F + cf], acw);
-      } else {
-        acw += p.df[tb * F + (lane - nconv)];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      acw = fmaf(sv[u], dfv[u], acw);
+#pragma unroll
+      for (int s = 0; s < SLOTS; ++s) {
+        float pre[4] = {kk[s].x + qv[u][s].x + bb[s].x, kk[s].y + qv[u][s].y + bb[s].y,
+                        kk[s].z + qv[u][s].z + bb[s].z, kk[s].w + qv[u][s].w + bb[s].w};
+        if (m1[s]) {
+#pragma unroll
+          for (int f = 0; f < F; ++f) {
+            pre[0] = fmaf(fls[u][f], lw[s][f].x, pre[0]); pre[1] = fmaf(fls[u][f], lw[s][f].y, pre[1]);
+            pre[2] = fmaf(fls[u][f], lw[s][f].z, pre[2]); pre[3] = fmaf(fls[u][f], lw[s][f].w, pre[3]);
+          }
+        }
+        const float e = m1[s] ? e1s[u] : e2s[u];
+        float z[4], dp[4];
+        const float vs[4] = {vv[s].x, vv[s].y, vv[s].z, vv[s].w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          z[k] = tanh_fast(pre[k]);
+          dp[k] = e * vs[k] * (1.f - z[k] * z[k]);
+        }
+        adk[s].x += dp[0]; adk[s].y += dp[1]; adk[s].z += dp[2]; adk[s].w += dp[3];
+        adv[s].x = fmaf(e, z[0], adv[s].x); adv[s].y = fmaf(e, z[1], adv[s].y);
+        adv[s].z = fmaf(e, z[2], adv[s].z); adv[s].w = fmaf(e, z[3], adv[s].w);
+#pragma unroll
+        for (int f = 0; f < F; ++f) {
+          adw[s][f].x = fmaf(fls[u][f], dp[0], adw[s][f].x); adw[s][f].y = fmaf(fls[u][f], dp[1], adw[s][f].y);
+          adw[s][f].z = fmaf(fls[u][f], dp[2], adw[s][f].z); adw[s][f].w = fmaf(fls[u][f], dp[3], adw[s][f].w);
+        }
       }
     }
   }

@@ -92,6 +92,15 @@ __device__ __forceinline__ float group8_max(float v) {
   v = fmaxf(v, dpp<0x141>(v));
   return v;
 }
+// sum over each aligned group of 16 / 32 lanes (result in every lane of the group)
+__device__ __forceinline__ float group16_sum(float v) {
+  v = group8_sum(v);
+  return v + dpp<0x140>(v);
+}
+__device__ __forceinline__ float group32_sum(float v) {
+  v = group16_sum(v);
+  return v + __shfl_xor(v, 16, 64);
+}
 // full-wave sum: DPP within rows of 16, then 4 readlanes (uniform result)
 __device__ __forceinline__ float wave_sum_dpp(float v) {
   v = group8_sum(v);

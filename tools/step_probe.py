@@ -89,7 +89,7 @@ def main():
     st = torch.empty(B, 4, **f)
     a1 = "decoder/attention1"
 
-    def attn(t, phases):
+    def attn(t, phases, lpp=0):
         K.attn_step_fwd(
             B=B, N=N, D1=D1, M1=M1, D2=D2, M2=M2, F=d.loc_f, KW=d.loc_k, NT=32, ntiles=ntiles,
             att1_forward=1, u=0.5, q=S["Q"][t], q_sb=D1 + D2, K1=S["K1"], V1=S["V1"], K2=S["K2"],
@@ -98,8 +98,9 @@ def main():
             convW=P[f"{a1}/location_conv/kernel"], convb=P[f"{a1}/location_conv/bias"],
             locW=P[f"{a1}/location_layer/kernel"], v2=P["decoder/attention2/attention_v"],
             e1=E1, e2=E2, part=PART, part_stride=pst, s_out=so, a_out=ao, s2_out=s2o, ctx=ctx,
-            ctx_sb=M1 + M2, stats=st, phases=phases)
-    res["attn fwd energy tile (phase 1)"] = timed_graph(lambda t: attn(t, 1), Tp)
+            ctx_sb=M1 + M2, stats=st, phases=phases, lpp=lpp)
+    for lpp in (8, 16, 32):
+        res[f"attn fwd energy tile lpp={lpp}"] = timed_graph(lambda t, l=lpp: attn(t, 1, l), Tp)
     res["attn fwd energy + combine (2 launches)"] = timed_graph(lambda t: attn(t, 3), Tp)
     YA = torch.zeros(B, N, **f)
     DF = torch.zeros(B, N, d.loc_f, **f)

@@ -127,7 +127,8 @@ typedef struct SatLstmFwd {
 } SatLstmFwd;
 
 /* Backward of one step (reverse time).  dL/dh_t = dh_carry + dgates_{t+1} . W[hoff+u, :]
- * (the recurrent product is done here), dL/dh'_t = dy + sum(dq_i . wq_i[u]) + m_h dL/dh_t. */
+ * (the recurrent product is done here unless the caller passes it precomputed in `rec`),
+ * dL/dh'_t = dy + sum(dq_i . wq_i[u]) + m_h dL/dh_t. */
 typedef struct SatLstmBwd {
   int32_t B, U, K, hoff, t;
   const float* W;
@@ -146,6 +147,9 @@ typedef struct SatLstmBwd {
   float* dgates;
   float* dh_carry_out;
   float* dc_carry_out;
+  const float* rec; int64_t rec_sb;   /* optional [B][U]: the recurrent product
+                                         dgates_next . W[hoff + u] precomputed by the caller
+                                         (then dgates_next is not read) */
 } SatLstmBwd;
 
 int sat_lstm_step_fwd(const SatLstmFwd* args, void* stream);

@@ -64,7 +64,7 @@ SatLstmBwd = _struct("SatLstmBwd", """
     i32:B i32:U i32:K i32:hoff i32:t ptr:W ptr:dgates_next ptr:gates ptr:c_prev
     ptr:dy i64:dy_sb ptr:dq0 ptr:wq0 i32:dq0_n ptr:dq1 ptr:wq1 i32:dq1_n
     i32:dq_parts i64:dq_pstride i64:dq_bstride ptr:dh_carry ptr:dc_carry ptr:mask_c ptr:mask_h f32:zc f32:zh ptr:lengths
-    ptr:dgates ptr:dh_carry_out ptr:dc_carry_out""")
+    ptr:dgates ptr:dh_carry_out ptr:dc_carry_out ptr:rec i64:rec_sb""")
 
 SatAdamConfig = _struct("SatAdamConfig", """
     f32:lr0 f32:beta1 f32:beta2 f32:eps f32:clip_norm i32:decay i32:step_factor f32:grad_scale""")

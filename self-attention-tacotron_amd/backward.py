@@ -140,7 +140,11 @@ def decoder_bwd(P, G, hp, d, dsv, dH2, masks, ws, attn_tile=32, pipe: Pipeline =
     DG1 = torch.empty_like(S["G1"])
     dH1 = torch.empty(Tp, B, Dd, **f32)
     dH0 = torch.empty(Tp, B, A, **f32)
-    DCTX = torch.empty(Tp, B, M1 + M2, **f32)
+    # [dL/dctx_t | recurrent product of the attention RNN] per step: the per-step row-dot with
+    # DG0[t+1] fills both halves at once (the ctx half on top of LSTM1's contribution), so the
+    # attention RNN's reverse step only does the query-gradient dot
+    RD = torch.zeros(Tp, B, M1 + M2 + A, **f32)
+    DCTX = RD[:, :, :M1 + M2]
     run2, run1 = _LstmBwd(B, Dd, dev), _LstmBwd(B, Dd, dev)
     m2c, m2h, m1c, m1h = (mk("dec/lstm2/zc"), mk("dec/lstm2/zh"), mk("dec/lstm1/zc"),
                           mk("dec/lstm1/zh"))
@@ -165,7 +169,7 @@ def decoder_bwd(P, G, hp, d, dsv, dH2, masks, ws, attn_tile=32, pipe: Pipeline =
         n = (b - a) * B
         dg = DG1[a:b].view(n, 4 * Dd)
         K.gemm(dg, W1[:A].t(), dH0[a:b].view(n, A))
-        K.gemm(dg, W1[A:A + M1 + M2].t(), DCTX[a:b].view(n, M1 + M2))
+        K.gemm(dg, W1[A:A + M1 + M2].t(), RD[a:b].view(n, R0)[:, :M1 + M2])
 
     # ---- attention RNN + dual-source attention recurrence
     W0 = P["decoder/attention_lstm/kernel"]
@@ -190,12 +194,12 @@ def decoder_bwd(P, G, hp, d, dsv, dH2, masks, ws, attn_tile=32, pipe: Pipeline =
         """Context gradient of step t (through the attention RNN's input at t+1) and the
         dual-source attention backward of step t."""
         last = t == Tp - 1
-        if not last:   # gradient of c_t through the attention RNN's input at step t+1
-            K.rowdot(DG0[t + 1], W0r[:M1 + M2], DCTX[t], beta=1.0)
+        if not last:   # [c_t | h_t] through the attention RNN's input at step t+1
+            K.rowdot(DG0[t + 1], W0r, RD[t], beta=1.0)
         K.attn_step_bwd(
             B=B, N=N, D1=D1, M1=M1, D2=D2, M2=M2, F=d.loc_f, KW=d.loc_k, NT=attn_tile,
-            ntiles=ntiles, att1_forward=1 if fwd else 0, u=0.5, dctx=DCTX[t],
-            dctx_sb=M1 + M2, ctx_t=S["REC0"][t + 1], ctx_sb=R0,
+            ntiles=ntiles, att1_forward=1 if fwd else 0, u=0.5, dctx=RD[t],
+            dctx_sb=R0, ctx_t=S["REC0"][t + 1], ctx_sb=R0,
             y_next=None if last else YA[cur], V1=S["V1"], V2=S["V2"],
             s_t=S["S1"][t + 1], a_t=S["AL1"][t + 1],
             a_prev=S["AL1"][t], s_prev=S["S1"][t], s2_t=S["S2"][t], stats=S["ST"][t],
@@ -212,8 +216,8 @@ def decoder_bwd(P, G, hp, d, dsv, dH2, masks, ws, attn_tile=32, pipe: Pipeline =
     def lstm0_desc(t, cur):
         """Reverse step t of the attention RNN: recurrent + query gradients in one dot."""
         last = t == Tp - 1
-        return dict(B=B, U=A, K=R0, hoff=M1 + M2, t=t, W=W0r,
-                    dgates_next=None if last else DG0[t + 1], gates=S["G0"][t],
+        return dict(B=B, U=A, K=R0, hoff=M1 + M2, t=t, W=W0r, rec=RD[t][:, M1 + M2:],
+                    dgates_next=None, gates=S["G0"][t],
                     c_prev=S["C0"][t], dy=dH0[t], dh_carry=None if last else hc[cur],
                     dc_carry=None if last else cc[cur],
                     mask_c=None if mc0 is None else mc0[t],

@@ -166,6 +166,7 @@ struct LstmBwdP {
   float* dgates;                        // [B][U][4]
   float* dh_carry_out;                  // [B][U]
   float* dc_carry_out;                  // [B][U]
+  const float* rec; int64_t rec_sb;     // precomputed recurrent product [B][U] (nullable)
 };
 
 // dL/dh_t = dh_carry + sum_g dgates_{t+1}[b, g] * W[hoff + u, g]  (the recurrent product)
@@ -178,7 +179,8 @@ struct LstmBwdP {
 constexpr int kMaxDq = 320;
 
 __device__ __forceinline__ void lstm_bwd_block(const LstmBwdP& p, int bx, int by, float* smem) {
-  const int G = 4 * p.U;
+  // with a precomputed recurrent product (p.rec) only the query term is a dot here
+  const int G = p.rec ? 0 : 4 * p.U;
   const int D0 = p.dq0 ? p.dq0_n : 0, D1 = p.dq1 ? p.dq1_n : 0, DQ = D0 + D1;
   const int L = G + DQ;                                // dot length
   const int ld = L + 4;
@@ -201,6 +203,7 @@ __device__ __forceinline__ void lstm_bwd_block(const LstmBwdP& p, int bx, int by
     dyv = p.dy ? p.dy[(int64_t)b * p.dy_sb + u] : 0.f;
     dhc = p.dh_carry ? p.dh_carry[bu] : 0.f;
     dcc = p.dc_carry ? p.dc_carry[bu] : 0.f;
+    if (p.rec) dhc += p.rec[(int64_t)b * p.rec_sb + u];
     if (p.mask_c) { mc = p.mask_c[bu]; mh = p.mask_h[bu]; }
     valid = p.lengths ? (p.t < p.lengths[b]) : true;
   }
@@ -213,7 +216,7 @@ __device__ __forceinline__ void lstm_bwd_block(const LstmBwdP& p, int bx, int by
     float4 v = z4;
     if (bb < p.B) {
       if (c < gq) {
-        if (p.dgates_next) v = reinterpret_cast<const float4*>(p.dgates_next + (int64_t)bb * G)[c];
+        if (p.dgates_next) v = reinterpret_cast<const float4*>(p.dgates_next + (int64_t)bb * 4 * p.U)[c];
       } else {
         const int dc = c - gq;
         const float* src = dc < q0 ? p.dq0 + 4 * dc : p.dq1 + 4 * (dc - q0);
@@ -232,7 +235,7 @@ __device__ __forceinline__ void lstm_bwd_block(const LstmBwdP& p, int bx, int by
     const int uu = u0 + r;
     float4 v = z4;
     if (uu < p.U) {
-      if (c < gq) v = reinterpret_cast<const float4*>(p.W + (int64_t)(p.hoff + uu) * G)[c];
+      if (c < gq) v = reinterpret_cast<const float4*>(p.W + (int64_t)(p.hoff + uu) * 4 * p.U)[c];
       else if (c - gq < q0) v = reinterpret_cast<const float4*>(p.wq0 + (int64_t)uu * D0)[c - gq];
       else v = reinterpret_cast<const float4*>(p.wq1 + (int64_t)uu * D1)[c - gq - q0];
     }
@@ -246,7 +249,7 @@ __device__ __forceinline__ void lstm_bwd_block(const LstmBwdP& p, int bx, int by
   if (active) {
     const float* dg = dgs + bl * ld;
     const float* wr = wrs + ul * ld;
-    if (p.dgates_next) {
+    if (p.dgates_next && G > 0) {
 #pragma unroll 4
       for (int v = 4 * ks; v < G; v += 4 * KS) {
         const float4 g = *reinterpret_cast<const float4*>(dg + v);
@@ -380,8 +383,9 @@ static int check_bwd(const SatLstmBwd* a, LstmBwdP& p, size_t& shm) {
   p.mask_c = a->mask_c; p.mask_h = a->mask_h; p.zc = a->zc; p.zh = a->zh;
   p.lengths = a->lengths; p.t = a->t;
   p.dgates = a->dgates; p.dh_carry_out = a->dh_carry_out; p.dc_carry_out = a->dc_carry_out;
+  p.rec = a->rec; p.rec_sb = a->rec_sb;
   const int DQ = (a->dq0 ? a->dq0_n : 0) + (a->dq1 ? a->dq1_n : 0);
-  shm = (size_t)(BT + UT) * (4 * a->U + DQ + 4) * sizeof(float);
+  shm = (size_t)(BT + UT) * ((a->rec ? 0 : 4 * a->U) + DQ + 4) * sizeof(float);
   SAT_CHECK_ARG(shm <= 160 * 1024, "sat_lstm_step_bwd: U too large for the LDS-staged step");
   return SAT_OK;
 }

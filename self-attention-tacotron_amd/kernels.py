@@ -265,7 +265,7 @@ def lstm_steps_fwd(steps):
 def lstm_bwd_desc(*, B, U, K, hoff, t, W, dgates_next, gates, c_prev, dy, dh_carry, dc_carry,
                   mask_c, mask_h, zc, zh, dgates, dh_carry_out, dc_carry_out, lengths=None,
                   dq0=None, wq0=None, dq1=None, wq1=None, dq_parts=1, dq_pstride=0,
-                  dq_bstride=0, a=None):
+                  dq_bstride=0, rec=None, a=None):
     a = _lib.SatLstmBwd() if a is None else a
     a.B, a.U, a.K, a.hoff, a.t = B, U, K, hoff, t
     a.W, a.dgates_next, a.gates, a.c_prev = _p(W), _p(dgates_next), _p(gates), _p(c_prev)
@@ -278,6 +278,7 @@ def lstm_bwd_desc(*, B, U, K, hoff, t, W, dgates_next, gates, c_prev, dy, dh_car
     a.zc, a.zh = zc, zh
     a.lengths = _p(lengths)
     a.dgates, a.dh_carry_out, a.dc_carry_out = _p(dgates), _p(dh_carry_out), _p(dc_carry_out)
+    a.rec, a.rec_sb = _p(rec), _rs(rec)
     return a
 
 

@@ -100,6 +100,13 @@ int sat_rng_fill(float* out, int64_t n, const uint64_t* seed_ptr, uint64_t strea
                  float keep, float on_value, void* stream);
 int sat_counter_add(uint64_t* counter, uint64_t inc, void* stream);
 
+/* Free-running decoding: the termination test of the tacotron2 StopTokenBasedInferenceHelper
+ * (analog modules/helpers.py:154-158) after decoder step t -- finished iff t > min_iters and
+ * sigmoid(stop[b * stride]) > 0.5 for every b; the first finished t is latched into state[0]
+ * (the caller initialises it to -1). */
+int sat_stop_check(const float* stop, int64_t stride, int32_t B, int32_t t, int32_t min_iters,
+                   int32_t* state, void* stream);
+
 /* ---------------------------------------------------------------- (Zoneout)LSTM step
  * One time step of TF LSTMCell wrapped in ext tacotron2 ZoneoutLSTMCell,
  * as used by ZoneoutCBHG's BiLSTM (modules/module.py:93-108) and DecoderRNNV2 /

@@ -434,6 +434,84 @@ def model_forward(p: Dict[str, Tensor], bufs, hp, batch: Dict[str, Tensor],
     return out
 
 
+def infer_free_running(p: Dict[str, Tensor], bufs, hp, batch: Dict[str, Tensor],
+                       max_iters: Optional[int] = None, min_iters: int = 10):
+    """PREDICT branch of model_fn (models/models.py:84-97, 252-277) with the inference decoder
+    of RNNTransformer (modules/module.py:766-784): dynamic_decode over
+    OutputAndStopTokenTransparentWrapper(TransformerWrapper(RNNStateHistoryWrapper(DecoderRNNV2)))
+    driven by the tacotron2 StopTokenBasedInferenceHelper (analog modules/helpers.py:111-160):
+      * step 0 input = go frame (zeros); step t+1 input = mel_t[:, -num_mels*n_feed:] (the last
+        predicted frame of the r-group);
+      * every step appends h2_t to the state history and re-runs the causal self-attention
+        transformer over the whole history, keeping the last row (rnn_wrappers.py:111-124);
+        mel_t / stop_t are the out / stop-token projections of that row (:209-214);
+      * finished after step t iff t > min_iters and sigmoid(stop_t) > 0.5 for EVERY utterance
+        (reduce_all); the loop also ends at max_iters (hparams max_iters, JSON 500).
+    Eval semantics throughout: no dropout (apply_dropout_on_inference=False, hparams.py:105),
+    zoneout blend, BatchNorm moving statistics.  Returns mel [B, T_out*r, mels], stop
+    [B, T_out], alignments, the decoder-self-attention probabilities of the last step and
+    T_out (the number of decoder steps run)."""
+    max_iters = hp.max_iters if max_iters is None else max_iters
+    m1, m2, enc_al = encoder(batch["source"], batch["source_length"], p, bufs, hp, None, False)
+    spk = None
+    if hp.use_speaker_embedding and hp.speaker_embedd_to_prenet:
+        spk = p["speaker_embedding"][batch["speaker_id"] - hp.speaker_embedding_offset]
+    lengths = batch["source_length"]
+    B, N, _ = m1.shape
+    M, r, nf = hp.num_mels, hp.outputs_per_step, hp.n_feed_frame
+    att1 = make_attention(hp.attention, p, "decoder/attention1", m1, lengths)
+    att2 = make_attention(hp.attention2, p, "decoder/attention2", m2, lengths)
+    dt = m1.dtype
+    A, D = hp.attention_out_units, hp.decoder_out_units
+    st1 = att1.initial_state(B, N, dt)
+    st2 = att2.initial_state(B, N, dt)
+    c1 = m1.new_zeros(B, m1.shape[2])
+    c2 = m2.new_zeros(B, m2.shape[2])
+    c0 = h0 = m1.new_zeros(B, A)
+    cc1 = hh1 = m1.new_zeros(B, D)
+    cc2 = hh2 = m1.new_zeros(B, D)
+    zc, zh = hp.zoneout_factor_cell, hp.zoneout_factor_output
+    x = m1.new_zeros(B, M * nf)                                        # _go_frames
+    hist, mels, stops, al1, al2 = [], [], [], [], []
+    probs = None
+    for t in range(max_iters):
+        pre = decoder_prenets(x, p, hp, None, spk)
+        cell_in = torch.cat([pre, c1, c2], dim=-1)
+        h0_out, c0, h0 = zoneout_lstm_step(cell_in, c0, h0, p["decoder/attention_lstm/kernel"],
+                                           p["decoder/attention_lstm/bias"], zc, zh, None, None)
+        a1, st1 = att1(h0_out, st1)
+        a2, st2 = att2(h0_out, st2)
+        c1 = (a1.unsqueeze(1) @ att1.values).squeeze(1)
+        c2 = (a2.unsqueeze(1) @ att2.values).squeeze(1)
+        o = torch.cat([h0_out, c1, c2], dim=-1)
+        h1_out, cc1, hh1 = zoneout_lstm_step(o, cc1, hh1, p["decoder/lstm1/kernel"],
+                                             p["decoder/lstm1/bias"], zc, zh, None, None)
+        h2_out, cc2, hh2 = zoneout_lstm_step(h1_out, cc2, hh2, p["decoder/lstm2/kernel"],
+                                             p["decoder/lstm2/bias"], zc, zh, None, None)
+        hist.append(h2_out)
+        z = torch.stack(hist, dim=1)
+        probs = []
+        for h in range(hp.decoder_self_attention_num_hop):
+            z, a = sa_transformer(z, p, f"decoder/self_attention{h}",
+                                  hp.decoder_self_attention_num_heads, True, None)
+            probs.append(a)
+        last = z[:, -1]
+        mel_t = dense(last, p, "decoder/out_projection")              # [B, M*r]
+        stop_t = dense(last, p, "decoder/stop_token_projection")[:, 0]
+        mels.append(mel_t)
+        stops.append(stop_t)
+        al1.append(a1)
+        al2.append(a2)
+        x = mel_t[:, -M * nf:]
+        if t > min_iters and bool((torch.sigmoid(stop_t) > 0.5).all()):
+            break
+    T_out = len(mels)
+    mel = torch.stack(mels, dim=1).reshape(B, T_out * r, M)
+    return {"mel": mel, "stop": torch.stack(stops, dim=1), "alignment1": torch.stack(al1, 1),
+            "alignment2": torch.stack(al2, 1), "decoder_self_alignments": probs,
+            "encoder_self_alignments": enc_al, "steps": T_out, "m1": m1, "m2": m2}
+
+
 def to_torch(d, dtype=torch.float64):
     out = {}
     for k, v in d.items():

@@ -94,6 +94,7 @@ SIGNATURES = {
     "sat_gemm": [ctypes.POINTER(SatGemmDesc), _P],
     "sat_rng_fill": [_P, _I64, _P, _U64, _F, _F, _P],
     "sat_counter_add": [_P, _U64, _P],
+    "sat_stop_check": [_P, _I64, _I32, _I32, _I32, _P, _P],
     "sat_lstm_step_fwd": [ctypes.POINTER(SatLstmFwd), _P],
     "sat_lstm_step_bwd": [ctypes.POINTER(SatLstmBwd), _P],
     "sat_lstm_steps_fwd": [ctypes.POINTER(SatLstmFwd), _I32, _P],

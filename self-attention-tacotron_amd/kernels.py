@@ -208,6 +208,12 @@ def conv1d_dw(x: torch.Tensor, dy: torch.Tensor, dW: torch.Tensor, beta=0.0):
     return dW
 
 
+def stop_check(stop: torch.Tensor, t: int, min_iters: int, state: torch.Tensor):
+    """state[0] := t if (no earlier finish) and t > min_iters and all sigmoid(stop) > 0.5."""
+    _lib.call("sat_stop_check", _p(stop), stop.stride(0), stop.shape[0], t, min_iters,
+              _p(state), _stream())
+
+
 def rng_fill(out: torch.Tensor, seed_dev: torch.Tensor, stream_id: int, keep: float,
              on_value: float):
     _lib.call("sat_rng_fill", _p(out), out.numel(), _p(seed_dev), stream_id, keep, on_value,

@@ -12,8 +12,9 @@ returns an ``EstimatorSpec``:
   (models/models.py:151-189);
 * EVAL   -- the teacher-forced evaluation loss ``loss_with_teacher`` (dropout off, zoneout
   blend, BatchNorm moving statistics; models/models.py:208-231) and its metric components;
-* PREDICT -- free-running inference is SURVEY.md 8(f) row 1 (not on this path): raises
-  ``NotImplementedError``.
+* PREDICT -- free-running inference (BASELINE configs[4]; inference.FreeRunningDecoder: the
+  stop-token helper + the KV-cached incremental decoder self-attention), returning the
+  reference's predictions dict (models/models.py:252-277).
 
 ``features`` / ``labels`` follow the reference's dataset records (``PreprocessedSourceData`` /
 ``PreprocessedTargetData``, datasets/codes/dataset.py:45-48; ``codes`` is the mel target for
@@ -176,9 +177,44 @@ class DualSourceSelfAttentionTacotronModel:
             self._trainers[key] = tr
         return self._trainers[key]
 
+    def _predict(self, features) -> EstimatorSpec:
+        """PREDICT (models/models.py:84-97, 252-277): free-running decode (inference.py) and
+        the reference's predictions dict.  ``codes`` follows the fork's one-hot of the argmax
+        over the feature bins of each frame (:99-100); ``mel`` is the raw decoder output
+        (code_output_raw) the one-hot is taken from."""
+        from .inference import FreeRunningDecoder
+        dev = self.engine.device
+        batch = {"source": _to_device(features.source, dev, torch.int64),
+                 "source_length": _to_device(features.source_length, dev, torch.int64)}
+        if self.params.use_speaker_embedding:
+            if getattr(features, "speaker_id", None) is None:
+                raise ValueError("use_speaker_embedding=True needs features.speaker_id")
+            batch["speaker_id"] = _to_device(features.speaker_id, dev, torch.int64)
+        out = FreeRunningDecoder(self.engine, max_iters=self.params.max_iters).run(batch)
+        mel = out["mel"]
+        codes = torch.zeros_like(mel)
+        codes.scatter_(2, mel.argmax(dim=2, keepdim=True), 1.0)       # tf.one_hot(argmax)
+        preds = {"id": features.id, "key": features.key, "codes": codes, "mel": mel,
+                 "stop_token": out["stop"], "alignment": out["alignment1"],
+                 "alignment2": out["alignment2"], "source": features.source,
+                 "text": getattr(features, "text", None)}
+        # decoder self-attention alignments (per hop, per head, transposed as :108-109), then
+        # the encoder's (alignment5..8)
+        dec = [a[:, h].transpose(1, 2) for a in out["decoder_self_alignments"]
+               for h in range(a.shape[1])]
+        for i, a in enumerate(dec[:2]):
+            preds[f"alignment{3 + i}"] = a
+        enc = [a[:, h].transpose(1, 2) for a in out["encoder_self_alignments"]
+               for h in range(a.shape[1])]
+        for i, a in enumerate(enc[:4]):
+            preds[f"alignment{5 + i}"] = a
+        preds = {k: v for k, v in preds.items() if v is not None}
+        return EstimatorSpec(ModeKeys.PREDICT, loss=None, train_op=None, predictions=preds,
+                             eval_metric_ops=None)
+
     def model_fn(self, features, labels, mode, params=None) -> EstimatorSpec:
         if mode == ModeKeys.PREDICT:
-            raise NotImplementedError("free-running inference (PREDICT) is SURVEY.md 8(f) row 1")
+            return self._predict(features)
         batch = self._batch(features, labels)
         if mode == ModeKeys.TRAIN:
             tr = self._trainer(batch)
@@ -195,6 +231,10 @@ class DualSourceSelfAttentionTacotronModel:
         raise ValueError(f"Unknown mode: {mode}")
 
     # ---- tf.estimator.Estimator-like drivers
+    def predict(self, input_fn):
+        for features, _ in input_fn():
+            yield self.model_fn(features, None, ModeKeys.PREDICT, self.params).predictions
+
     def train(self, input_fn, steps: int):
         loss = None
         it = iter(input_fn())

@@ -175,3 +175,44 @@ def test_oracle_gradients_flow_everywhere():
     out["loss"].backward()
     missing = [k for k, v in p.items() if v.grad is None]
     assert missing == []
+
+
+@pytest.mark.parametrize("preset", ["ljspeech", "vctk"])
+def test_free_running_equals_teacher_forced_on_its_own_predictions(preset):
+    """The PREDICT restatement (StopTokenBasedInferenceHelper feeding back the last predicted
+    frame + TransformerWrapper re-running the causal self-attention over the history) equals
+    the teacher-forced eval path (TransformerTrainingHelper + post-hoc causal self-attention,
+    modules/module.py:743-764) when the teacher frames ARE the free-running predictions --
+    exactly the modules/transformer_test.py:44-90 equivalence, closed over the feedback loop."""
+    from sat_amd import data, hparams, params
+    hp = getattr(hparams, f"{preset}_hparams")()
+    vals = params.init_params(hp, seed=5)
+    p = O.to_torch(vals)
+    bufs = O.to_torch(params.init_bn_buffers(hp))
+    b = O.to_torch(data.synthetic_batch(hp, 2, N=9, T=16, shape="ljs", seed=3))
+    inf = O.infer_free_running(p, bufs, hp, b, max_iters=8, min_iters=100)
+    assert inf["steps"] == 8
+    tb = dict(b)
+    T = inf["mel"].shape[1]
+    tb["mel"] = inf["mel"]
+    tb["mel_mask"] = torch.ones(2, T, dtype=torch.float64)
+    tb["done"] = torch.zeros(2, T // hp.outputs_per_step, dtype=torch.float64)
+    tb["done_mask"] = torch.ones_like(tb["done"])
+    tf = O.model_forward(p, bufs, hp, tb, None, training=False)
+    np.testing.assert_allclose(tf["mel"].numpy(), inf["mel"].numpy(), rtol=1e-10, atol=1e-12)
+    np.testing.assert_allclose(tf["stop"][..., 0].numpy(), inf["stop"].numpy(), rtol=1e-10,
+                               atol=1e-12)
+    np.testing.assert_allclose(tf["alignment1"].numpy(), inf["alignment1"].numpy(), atol=1e-12)
+
+
+def test_free_running_stop_rule():
+    """is_finished: t > min_iters and sigmoid(stop) > 0.5 for every utterance (reduce_all)."""
+    from sat_amd import data, hparams, params
+    hp = hparams.ljspeech_hparams()
+    vals = params.init_params(hp, seed=5)
+    bufs = O.to_torch(params.init_bn_buffers(hp))
+    b = O.to_torch(data.synthetic_batch(hp, 2, N=7, T=8, shape="ljs", seed=1))
+    for bias, steps in ((9.0, 6), (-9.0, 15)):
+        vals["decoder/stop_token_projection/bias"] = np.full((1,), bias, np.float32)
+        out = O.infer_free_running(O.to_torch(vals), bufs, hp, b, max_iters=15, min_iters=4)
+        assert out["steps"] == steps

@@ -50,8 +50,14 @@ def test_model_fn_eval_matches_golden_and_train_learns(cuda):
     losses = [float(model.model_fn(feats, labels, M.ModeKeys.TRAIN, hp).loss.item())
               for _ in range(8)]
     assert losses[-1] < losses[0]
-    with pytest.raises(NotImplementedError):
-        model.model_fn(feats, None, M.ModeKeys.PREDICT, hp)
+    spec = model.model_fn(feats, None, M.ModeKeys.PREDICT, hp)
+    pr = spec.predictions
+    B = b["source"].shape[0]
+    T = pr["mel"].shape[1]
+    assert pr["mel"].shape == (B, T, hp.num_mels) and pr["codes"].shape == pr["mel"].shape
+    assert torch.all(pr["codes"].sum(-1) == 1)                       # one-hot per frame
+    assert pr["alignment"].shape == (B, b["source"].shape[1], T // hp.outputs_per_step)
+    assert "alignment3" in pr and "alignment5" in pr
 
 
 def test_model_fn_vctk_multi_speaker_records(cuda):

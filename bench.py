@@ -116,7 +116,7 @@ def attention_probe(trainer, hp, d, B, N, tile):
     traffic, pmc_src = _pmc_traffic()
     return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-            "kernel": "attn_energy_kernel (sat_attn_step_fwd tile phase)",
+            "kernel": "attn_energy_wide_kernel<5,16> (sat_attn_step_fwd tile phase)",
             "bytes_per_launch": int(bytes_launch), "avg_launch_us": round(avg_s * 1e6, 3),
             "launches_timed": reps * Tp,
             "note": "avg = HIP-event time of hipGraph-replayed back-to-back launches / count "

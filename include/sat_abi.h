@@ -269,6 +269,40 @@ int sat_attn_pg_stride(int32_t D1, int32_t D2, int32_t F, int32_t KW);
 int sat_attn_param_grad_rows(int32_t B, int32_t N);
 int sat_attn_param_grads(const SatAttnParamGrad* args, void* stream);
 
+/* ---------------------------------------------------------------- persistent decoder chain
+ * ALL T' steps of the decoder's attention chain in one launch (DualSourceAttentionRNN,
+ * modules/module.py:1017-1048: ZoneoutLSTM attention RNN -> query layers -> ForwardAttention
+ * modules/forward_attention.py:88-122 + BahdanauAttention -> contexts), teacher-forced inputs
+ * X0 [T][B][4U] = prenet(x_t) @ W0[:p] + b0 precomputed.  8 groups x 32 workgroups; each
+ * (utterance, 32-position tile) K/V slice stays in LDS and each workgroup's LSTM / query weight
+ * columns in registers for the whole decode; steps are separated by in-kernel group barriers
+ * (sc1 hand-offs, bounded spins: a timeout sets err[0] != 0 and the kernel drains).
+ * Compiled for the self-attention-tacotron shapes (U=256, M1=256, M2=32, D1=224, D2=32, F=5,
+ * KW=10), B in {8,16,24,32}, (B/8) * ceil(N/32) <= 32; requires 256 co-resident workgroups.
+ * Writes the same histories as the per-step path: REC0 [T+1][B][M1+M2+U] (rows 1..T),
+ * C0 [T+1][B][U], H0RAW, G0, Q [T][B][.], S1/AL1 [T+1][B][N] (rows 1..T; row 0 = initial
+ * state, set by the caller), S2 [T][B][N], ST [T][B][4], LOC [T][B][N][F] (nullable).
+ * Scratch: E, PART, QP (sat_decoder_attention_scratch), ctr [sat_decoder_attention_scratch()]
+ * words and err [2] (both zeroed by the call). */
+typedef struct SatDecAttnFwd {
+  int32_t B, N, T, U, M1, M2, D1, D2, F, KW;
+  float u, zc, zh;
+  const float* X0; const float* W0r; const float* Wq1; const float* Wq2;
+  const float* K1; const float* V1; const float* K2; const float* V2;
+  const int64_t* lengths;
+  const float* v1; const float* b1; const float* convW; const float* convb; const float* locW;
+  const float* v2;
+  const float* mask_c; const float* mask_h;
+  float* REC0; float* C0; float* H0RAW; float* G0; float* Q;
+  float* S1; float* AL1; float* S2; float* ST; float* LOC;
+  float* E; float* PART; float* QP; uint32_t* ctr; int32_t* err;
+  int64_t* prof;   /* optional [256][8] per-workgroup segment clocks (100 MHz), NULL = off */
+} SatDecAttnFwd;
+
+int sat_decoder_attention_fwd(const SatDecAttnFwd* args, void* stream);
+int64_t sat_decoder_attention_scratch(int32_t B, int32_t N, int64_t* e_floats, int64_t* part_floats,
+                                      int64_t* qp_floats);
+
 /* ---------------------------------------------------------------- elementwise
  * out[b,n,:] = x[b,n,:] * (n < lengths[b])  -- TF _prepare_memory (memory_sequence_length). */
 int sat_seq_mask(const float* x, float* out, int32_t B, int32_t N, int32_t C,

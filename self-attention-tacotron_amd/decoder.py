@@ -56,11 +56,23 @@ def teacher_inputs(targets: torch.Tensor, r: int, n_feed: int) -> torch.Tensor:
     return x
 
 
+def persistent_eligible(d: Dims, B: int, N: int, attn_tile: int = 32) -> bool:
+    """Shapes sat_decoder_attention_fwd is compiled for (the self-attention-tacotron configs)."""
+    return (d.att1 == "forward" and d.att2 == "additive" and attn_tile == 32 and
+            (d.att_rnn, d.m1, d.m2, d.d1, d.d2, d.loc_f, d.loc_k) == (256, 256, 32, 224, 32, 5, 10)
+            and B % 8 == 0 and B // 8 <= 4 and (B // 8) * ((N + 31) // 32) <= 32)
+
+
 def decoder_forward(P: Dict[str, torch.Tensor], hp, d: Dims, m1: torch.Tensor, m2: torch.Tensor,
                     lengths: torch.Tensor, targets: torch.Tensor,
                     masks: Optional[Dict[str, torch.Tensor]], attn_tile: int = 32,
-                    spk: Optional[torch.Tensor] = None, pipe: Pipeline = SEQUENTIAL):
-    """Forward of the teacher-forced decoder; returns (D [T', B, dec], DecoderSaved)."""
+                    spk: Optional[torch.Tensor] = None, pipe: Pipeline = SEQUENTIAL,
+                    persistent: bool = False, scratch=None):
+    """Forward of the teacher-forced decoder; returns (D [T', B, dec], DecoderSaved).
+
+    ``persistent`` runs the attention chain (attention RNN + query + dual-source attention) for
+    all steps as ONE persistent launch (``sat_decoder_attention_fwd``) when the shapes allow,
+    then the two decoder LSTMs as a two-problem wavefront; otherwise the per-step launches."""
     dev = m1.device
     B, N, _ = m1.shape
     r, nf = d.r, hp.n_feed_frame
@@ -189,7 +201,43 @@ def decoder_forward(P: Dict[str, torch.Tensor], hp, d: Dims, m1: torch.Tensor, m
     def lstm2_desc(t):
         return _lstm_desc(X2, W2[Dd:], t, B, Dd, zc, zh, m2c, m2h, L2)
 
-    if not pipe.enabled:          # layer by layer
+    if persistent and persistent_eligible(d, B, N, attn_tile):
+        if scratch is None:
+            scratch = K.DecoderAttentionScratch(B, N, dev)
+        K.decoder_attention_fwd(
+            B=B, N=N, T=Tp, U=A, M1=M1, M2=M2, D1=D1, D2=D2, F=d.loc_f, KW=d.loc_k, u=0.5,
+            zc=zc, zh=zh, X0=X0, W0r=Wr0, Wq1=P[f"{a1}/query_layer/kernel"],
+            Wq2=P["decoder/attention2/query_layer/kernel"], K1=K1, V1=V1, K2=K2, V2=V2,
+            lengths=lengths, v1=P[f"{a1}/attention_variable"], b1=P[f"{a1}/attention_bias"],
+            convW=P[f"{a1}/location_conv/kernel"], convb=P[f"{a1}/location_conv/bias"],
+            locW=P[f"{a1}/location_layer/kernel"], v2=P["decoder/attention2/attention_v"],
+            mask_c=zc0, mask_h=zh0, REC0=REC0, C0=C0, H0RAW=H0RAW, G0=G0, Q=Q, S1=S1, AL1=AL1,
+            S2=S2, ST=ST, LOC=LOC, E=scratch.E, PART=scratch.PART, QP=scratch.QP, ctr=scratch.ctr,
+            err=scratch.err)
+        S["attn_scratch"] = scratch
+        # decoder LSTMs: all of LSTM1's input projection at once, then LSTM1 at i with LSTM2
+        # C steps behind in one two-problem launch per iteration
+        x1_chunk(0, Tp)
+        C = pipe.chunk if pipe.enabled else Tp
+        x2_at = pipe.finishing(Tp, 0) if pipe.enabled else {}     # LSTM1 runs at lag 0 here
+        if not pipe.enabled:
+            for t in range(Tp):
+                K.lstm_step_fwd(**lstm1_desc(t))
+            x2_chunk(0, Tp)
+            for t in range(Tp):
+                K.lstm_step_fwd(**lstm2_desc(t))
+        else:
+            for i in range(Tp + C):
+                steps = []
+                if i < Tp:
+                    steps.append(lstm1_desc(i))
+                if 0 <= i - C < Tp:
+                    steps.append(lstm2_desc(i - C))
+                if steps:
+                    K.lstm_steps_fwd(steps)
+                if i in x2_at:
+                    x2_chunk(*x2_at[i])
+    elif not pipe.enabled:          # layer by layer
         for t in range(Tp):
             K.lstm_step_fwd(**lstm0_desc(t))
             attention_rest(t)

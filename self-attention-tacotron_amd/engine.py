@@ -22,7 +22,7 @@ from .pipeline import Pipeline
 class Tacotron:
     def __init__(self, hp, device, seed: int = 1234,
                  init_values: Optional[Dict[str, np.ndarray]] = None, attn_tile: int = 32,
-                 pipeline_chunk: int = 40):
+                 pipeline_chunk: int = 40, persistent_decoder: bool = True):
         self.hp = hp
         self.d = PR.resolve_dims(hp)
         self.device = torch.device(device)
@@ -37,13 +37,24 @@ class Tacotron:
         self.attn_tile = attn_tile
         # wavefront schedule of the decoder recurrences (0 = layer by layer)
         self.pipe = Pipeline(self.device, pipeline_chunk)
+        # attention chain of the decoder forward as one persistent launch (when eligible)
+        self.persistent_decoder = persistent_decoder
+        self._scratch = {}
 
     # ------------------------------------------------------------------ steps
     def forward(self, batch: Dict[str, torch.Tensor], masks=None, training: bool = True,
                 need_grad: bool = True):
+        B, N = batch["source"].shape
+        scratch = None
+        if self.persistent_decoder:
+            key = (B, N)
+            if key not in self._scratch:
+                self._scratch[key] = K.DecoderAttentionScratch(B, N, self.device)
+            scratch = self._scratch[key]
         return model_forward(self.P, self.bn, self.hp, self.d, batch, masks, training, self.ws,
                              compute_grad_seeds=need_grad, attn_tile=self.attn_tile,
-                             pipe=self.pipe)
+                             pipe=self.pipe, persistent=self.persistent_decoder,
+                             scratch=scratch)
 
     def backward(self, saved, zero: bool = True):
         if zero:

@@ -323,6 +323,35 @@ def attn_param_grads(**kw):
                "sat_attn_param_grads")
 
 
+class DecoderAttentionScratch:
+    """Device scratch of sat_decoder_attention_fwd for one (B, N): raw energies, tile partials,
+    group counters and the error word (allocated before graph capture)."""
+
+    def __init__(self, B: int, N: int, device):
+        e, pt, qp = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+        words = int(_lib.load().sat_decoder_attention_scratch(B, N, ctypes.byref(e),
+                                                              ctypes.byref(pt), ctypes.byref(qp)))
+        self.E = torch.empty(e.value, device=device)
+        self.PART = torch.empty(pt.value, device=device)
+        self.QP = torch.empty(qp.value, device=device)
+        self.ctr = torch.zeros(words, dtype=torch.int32, device=device)
+        self.err = torch.zeros(2, dtype=torch.int32, device=device)
+
+    def check(self):
+        """Host check of the in-kernel barrier timeout flag (synchronises)."""
+        if int(self.err[0].item()) != 0:
+            raise _lib.SatLibraryError("sat_decoder_attention_fwd: a group barrier timed out "
+                                       "(workgroups not co-resident?)")
+
+
+def decoder_attention_fwd(**kw):
+    a = _lib.SatDecAttnFwd()
+    for k, v in kw.items():
+        setattr(a, k, _p(v) if isinstance(v, torch.Tensor) else v)
+    _lib.check(_lib.load().sat_decoder_attention_fwd(ctypes.byref(a), _stream()),
+               "sat_decoder_attention_fwd")
+
+
 def attn_step_bwd(**kw):
     a = _lib.SatAttnStepBwd()
     for k, v in kw.items():

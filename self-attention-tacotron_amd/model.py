@@ -223,7 +223,8 @@ class Saved(dict):
 
 def model_forward(P, bn: BNState, hp, d: PR.Dims, batch: Dict[str, torch.Tensor],
                   masks: Optional[Dict[str, torch.Tensor]], training: bool, ws: K.Workspace,
-                  compute_grad_seeds: bool = True, attn_tile: int = 32, pipe=None):
+                  compute_grad_seeds: bool = True, attn_tile: int = 32, pipe=None,
+                  persistent: bool = False, scratch=None):
     """model_fn forward + loss.  Returns (outputs dict, Saved)."""
     sv = Saved()
     ids, lengths = batch["source"], batch["source_length"]
@@ -235,8 +236,8 @@ def model_forward(P, bn: BNState, hp, d: PR.Dims, batch: Dict[str, torch.Tensor]
         sv["spk_err"] = torch.zeros(1, dtype=torch.int32, device=m1.device)
         K.embedding_fwd(P["speaker_embedding"], ids_s, spk, d.spk_offset, sv["spk_err"])
     dout, dsv = decoder_forward(P, hp, d, m1, m2, lengths, batch["mel"], masks,
-                                attn_tile=attn_tile, spk=spk,
-                                **({} if pipe is None else {"pipe": pipe}))
+                                attn_tile=attn_tile, spk=spk, persistent=persistent,
+                                scratch=scratch, **({} if pipe is None else {"pipe": pipe}))
     sv["dec"] = dsv
     if spk is not None:
         dsv.tensors["ms_prenet"]["ids"] = batch["speaker_id"]

@@ -52,7 +52,7 @@ def _c_sizeof(struct):
 
 
 STRUCTS = ["SatGemmDesc", "SatLstmFwd", "SatLstmBwd", "SatAttnStep", "SatAttnStepBwd",
-           "SatAttnParamGrad", "SatAdamConfig"]
+           "SatAttnParamGrad", "SatDecAttnFwd", "SatAdamConfig"]
 
 
 def _c_offsets(struct, fields):

@@ -303,6 +303,33 @@ int sat_decoder_attention_fwd(const SatDecAttnFwd* args, void* stream);
 int64_t sat_decoder_attention_scratch(int32_t B, int32_t N, int64_t* e_floats, int64_t* part_floats,
                                       int64_t* qp_floats);
 
+/* Persistent BPTT of the same chain: all T reverse steps of the dual-source attention backward
+ * + the attention RNN's reverse step in ONE launch.  Replaces, per step, sat_rowdot (the
+ * attention RNN's input gradient) + sat_attn_step_bwd + the attention RNN's sat_lstm_steps_bwd
+ * (backward.py decoder_bwd's launch path; reference graph: the TF gradients of
+ * modules/module.py:1522-1540 AttentionRNN + forward_attention.py / tf additive attention).
+ * Inputs: the forward histories (decoder_forward), DH0 = dL/dh0'_t from LSTM1 (all steps) and
+ * RD[:, :, :M1+M2] = LSTM1's dL/dctx_t.  Outputs: DG0, the full dL/dctx_t in RD[:, :, :M1+M2],
+ * DE1/DE2, DFH, DQP (the inputs of the post-loop parameter-gradient pass).  Same shape limits
+ * as the forward; RDP [2][B][32][M1+M2+U] and YA [2][B][N] are scratch. */
+typedef struct SatDecAttnBwd {
+  int32_t B, N, T, U, M1, M2, D1, D2, F, KW;
+  float u, zc, zh;
+  const float* REC0; const float* C0; const float* G0; const float* Q;
+  const float* S1; const float* AL1; const float* S2; const float* ST; const float* LOC;
+  const float* K1; const float* V1; const float* K2; const float* V2;
+  const float* v1; const float* b1; const float* convW; const float* locW; const float* v2;
+  const float* W0r; const float* Wq1; const float* Wq2;
+  const float* mask_c; const float* mask_h;
+  const float* DH0;
+  float* RD; float* DG0; float* DE1; float* DE2; float* DFH; float* DQP;
+  float* RDP; float* YA; uint32_t* ctr; int32_t* err;
+} SatDecAttnBwd;
+
+int sat_decoder_attention_bwd(const SatDecAttnBwd* args, void* stream);
+int64_t sat_decoder_attention_bwd_scratch(int32_t B, int32_t N, int64_t* rdp_floats,
+                                          int64_t* ya_floats);
+
 /* ---------------------------------------------------------------- elementwise
  * out[b,n,:] = x[b,n,:] * (n < lengths[b])  -- TF _prepare_memory (memory_sequence_length). */
 int sat_seq_mask(const float* x, float* out, int32_t B, int32_t N, int32_t C,

@@ -88,6 +88,13 @@ SatDecAttnFwd = _struct("SatDecAttnFwd", """
     ptr:REC0 ptr:C0 ptr:H0RAW ptr:G0 ptr:Q ptr:S1 ptr:AL1 ptr:S2 ptr:ST ptr:LOC
     ptr:E ptr:PART ptr:QP ptr:ctr ptr:err ptr:prof""")
 
+SatDecAttnBwd = _struct("SatDecAttnBwd", """
+    i32:B i32:N i32:T i32:U i32:M1 i32:M2 i32:D1 i32:D2 i32:F i32:KW f32:u f32:zc f32:zh
+    ptr:REC0 ptr:C0 ptr:G0 ptr:Q ptr:S1 ptr:AL1 ptr:S2 ptr:ST ptr:LOC
+    ptr:K1 ptr:V1 ptr:K2 ptr:V2 ptr:v1 ptr:b1 ptr:convW ptr:locW ptr:v2
+    ptr:W0r ptr:Wq1 ptr:Wq2 ptr:mask_c ptr:mask_h ptr:DH0
+    ptr:RD ptr:DG0 ptr:DE1 ptr:DE2 ptr:DFH ptr:DQP ptr:RDP ptr:YA ptr:ctr ptr:err""")
+
 SatAttnStep = _struct("SatAttnStep", """
     i32:B i32:N i32:D1 i32:M1 i32:D2 i32:M2 i32:F i32:KW i32:NT i32:ntiles i32:att1_forward
     f32:u ptr:q i64:q_sb ptr:K1 ptr:V1 ptr:K2 ptr:V2 ptr:lengths ptr:s_prev ptr:a_prev
@@ -112,6 +119,7 @@ SIGNATURES = {
     "sat_attn_pg_stride": [_I32, _I32, _I32, _I32],
     "sat_attn_step_bwd": [ctypes.POINTER(SatAttnStepBwd), _P],
     "sat_decoder_attention_fwd": [ctypes.POINTER(SatDecAttnFwd), _P],
+    "sat_decoder_attention_bwd": [ctypes.POINTER(SatDecAttnBwd), _P],
     "sat_attn_param_grad_rows": [_I32, _I32],
     "sat_attn_param_grads": [ctypes.POINTER(SatAttnParamGrad), _P],
     "sat_seq_mask": [_P, _P, _I32, _I32, _I32, _P, _P],
@@ -143,7 +151,8 @@ SIGNATURES.update({
 RESTYPES = {"sat_workspace_colreduce": (ctypes.c_int64, [_I32, _I32]),
             "sat_workspace_adam": (ctypes.c_int64, []),
             "sat_workspace_loss": (ctypes.c_int64, []),
-            "sat_decoder_attention_scratch": (ctypes.c_int64, [_I32, _I32, _P, _P, _P])}
+            "sat_decoder_attention_scratch": (ctypes.c_int64, [_I32, _I32, _P, _P, _P]),
+            "sat_decoder_attention_bwd_scratch": (ctypes.c_int64, [_I32, _I32, _P, _P])}
 
 _lib: Optional[ctypes.CDLL] = None
 

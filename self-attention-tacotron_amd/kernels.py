@@ -336,12 +336,14 @@ class DecoderAttentionScratch:
         self.QP = torch.empty(qp.value, device=device)
         self.ctr = torch.zeros(words, dtype=torch.int32, device=device)
         self.err = torch.zeros(2, dtype=torch.int32, device=device)
+        self.bwd = DecoderAttentionBwdScratch(B, N, device)   # the persistent BPTT's own
 
     def check(self):
-        """Host check of the in-kernel barrier timeout flag (synchronises)."""
+        """Host check of the in-kernel barrier timeout flags (synchronises)."""
         if int(self.err[0].item()) != 0:
             raise _lib.SatLibraryError("sat_decoder_attention_fwd: a group barrier timed out "
                                        "(workgroups not co-resident?)")
+        self.bwd.check()
 
 
 def decoder_attention_fwd(**kw):
@@ -350,6 +352,33 @@ def decoder_attention_fwd(**kw):
         setattr(a, k, _p(v) if isinstance(v, torch.Tensor) else v)
     _lib.check(_lib.load().sat_decoder_attention_fwd(ctypes.byref(a), _stream()),
                "sat_decoder_attention_fwd")
+
+
+class DecoderAttentionBwdScratch:
+    """Device scratch of sat_decoder_attention_bwd for one (B, N): row-dot partials, the
+    alignment-recursion gradient ping-pong, group counters and the error word."""
+
+    def __init__(self, B: int, N: int, device):
+        rdp, ya = ctypes.c_int64(), ctypes.c_int64()
+        words = int(_lib.load().sat_decoder_attention_bwd_scratch(B, N, ctypes.byref(rdp),
+                                                                  ctypes.byref(ya)))
+        self.RDP = torch.empty(rdp.value, device=device)
+        self.YA = torch.empty(ya.value, device=device)
+        self.ctr = torch.zeros(words, dtype=torch.int32, device=device)
+        self.err = torch.zeros(2, dtype=torch.int32, device=device)
+
+    def check(self):
+        if int(self.err[0].item()) != 0:
+            raise _lib.SatLibraryError("sat_decoder_attention_bwd: a group barrier timed out "
+                                       "(workgroups not co-resident?)")
+
+
+def decoder_attention_bwd(**kw):
+    a = _lib.SatDecAttnBwd()
+    for k, v in kw.items():
+        setattr(a, k, _p(v) if isinstance(v, torch.Tensor) else v)
+    _lib.check(_lib.load().sat_decoder_attention_bwd(ctypes.byref(a), _stream()),
+               "sat_decoder_attention_bwd")
 
 
 def attn_step_bwd(**kw):

@@ -52,7 +52,7 @@ def _c_sizeof(struct):
 
 
 STRUCTS = ["SatGemmDesc", "SatLstmFwd", "SatLstmBwd", "SatAttnStep", "SatAttnStepBwd",
-           "SatAttnParamGrad", "SatDecAttnFwd", "SatAdamConfig"]
+           "SatAttnParamGrad", "SatDecAttnFwd", "SatDecAttnBwd", "SatAdamConfig"]
 
 
 def _c_offsets(struct, fields):

@@ -297,6 +297,8 @@ typedef struct SatDecAttnFwd {
   float* S1; float* AL1; float* S2; float* ST; float* LOC;
   float* E; float* PART; float* QP; uint32_t* ctr; int32_t* err;
   int64_t* prof;   /* optional [256][8] per-workgroup segment clocks (100 MHz), NULL = off */
+  float* ZH;       /* optional [T][B][N][D1+D2]: tanh of every energy pre-activation, kept for
+                      sat_decoder_attention_bwd (which then recomputes no transcendental) */
 } SatDecAttnFwd;
 
 int sat_decoder_attention_fwd(const SatDecAttnFwd* args, void* stream);
@@ -311,19 +313,22 @@ int64_t sat_decoder_attention_scratch(int32_t B, int32_t N, int64_t* e_floats, i
  * Inputs: the forward histories (decoder_forward), DH0 = dL/dh0'_t from LSTM1 (all steps) and
  * RD[:, :, :M1+M2] = LSTM1's dL/dctx_t.  Outputs: DG0, the full dL/dctx_t in RD[:, :, :M1+M2],
  * DE1/DE2, DFH, DQP (the inputs of the post-loop parameter-gradient pass).  Same shape limits
- * as the forward; RDP [2][B][32][M1+M2+U] and YA [2][B][N] are scratch. */
+ * as the forward; RDP and YA (sizes from sat_decoder_attention_bwd_scratch) are scratch. */
 typedef struct SatDecAttnBwd {
   int32_t B, N, T, U, M1, M2, D1, D2, F, KW;
   float u, zc, zh;
-  const float* REC0; const float* C0; const float* G0; const float* Q;
+  const float* REC0; const float* C0; const float* G0;
   const float* S1; const float* AL1; const float* S2; const float* ST; const float* LOC;
-  const float* K1; const float* V1; const float* K2; const float* V2;
-  const float* v1; const float* b1; const float* convW; const float* locW; const float* v2;
+  const float* V1; const float* V2;
+  const float* v1; const float* convW; const float* convb; const float* locW;
+  const float* v2;
   const float* W0r; const float* Wq1; const float* Wq2;
   const float* mask_c; const float* mask_h;
   const float* DH0;
+  const float* ZH;   /* the forward's energy tanh history (SatDecAttnFwd.ZH), required */
   float* RD; float* DG0; float* DE1; float* DE2; float* DFH; float* DQP;
   float* RDP; float* YA; uint32_t* ctr; int32_t* err;
+  int64_t* prof;   /* optional [256][16] per-workgroup segment clocks (100 MHz), NULL = off */
 } SatDecAttnBwd;
 
 int sat_decoder_attention_bwd(const SatDecAttnBwd* args, void* stream);

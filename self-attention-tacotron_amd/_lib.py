@@ -86,14 +86,14 @@ SatDecAttnFwd = _struct("SatDecAttnFwd", """
     ptr:X0 ptr:W0r ptr:Wq1 ptr:Wq2 ptr:K1 ptr:V1 ptr:K2 ptr:V2 ptr:lengths
     ptr:v1 ptr:b1 ptr:convW ptr:convb ptr:locW ptr:v2 ptr:mask_c ptr:mask_h
     ptr:REC0 ptr:C0 ptr:H0RAW ptr:G0 ptr:Q ptr:S1 ptr:AL1 ptr:S2 ptr:ST ptr:LOC
-    ptr:E ptr:PART ptr:QP ptr:ctr ptr:err ptr:prof""")
+    ptr:E ptr:PART ptr:QP ptr:ctr ptr:err ptr:prof ptr:ZH""")
 
 SatDecAttnBwd = _struct("SatDecAttnBwd", """
     i32:B i32:N i32:T i32:U i32:M1 i32:M2 i32:D1 i32:D2 i32:F i32:KW f32:u f32:zc f32:zh
-    ptr:REC0 ptr:C0 ptr:G0 ptr:Q ptr:S1 ptr:AL1 ptr:S2 ptr:ST ptr:LOC
-    ptr:K1 ptr:V1 ptr:K2 ptr:V2 ptr:v1 ptr:b1 ptr:convW ptr:locW ptr:v2
-    ptr:W0r ptr:Wq1 ptr:Wq2 ptr:mask_c ptr:mask_h ptr:DH0
-    ptr:RD ptr:DG0 ptr:DE1 ptr:DE2 ptr:DFH ptr:DQP ptr:RDP ptr:YA ptr:ctr ptr:err""")
+    ptr:REC0 ptr:C0 ptr:G0 ptr:S1 ptr:AL1 ptr:S2 ptr:ST ptr:LOC
+    ptr:V1 ptr:V2 ptr:v1 ptr:convW ptr:convb ptr:locW ptr:v2
+    ptr:W0r ptr:Wq1 ptr:Wq2 ptr:mask_c ptr:mask_h ptr:DH0 ptr:ZH
+    ptr:RD ptr:DG0 ptr:DE1 ptr:DE2 ptr:DFH ptr:DQP ptr:RDP ptr:YA ptr:ctr ptr:err ptr:prof""")
 
 SatAttnStep = _struct("SatAttnStep", """
     i32:B i32:N i32:D1 i32:M1 i32:D2 i32:M2 i32:F i32:KW i32:NT i32:ntiles i32:att1_forward

@@ -236,6 +236,8 @@ def decoder_bwd(P, G, hp, d, dsv, dH2, masks, ws, attn_tile=32, pipe: Pipeline =
 
     scratch = S.get("attn_scratch")
     if scratch is not None:
+        if S.get("ZH") is None:
+            raise RuntimeError("decoder_bwd: the forward ran without keep_tanh (inference mode)")
         # the forward ran the attention chain as one persistent launch: the decoder LSTMs'
         # reverse recurrences first (LSTM1 C steps behind LSTM2 in one two-problem launch per
         # iteration), their input gradients into the chain as whole-sequence GEMMs, then the
@@ -264,13 +266,13 @@ def decoder_bwd(P, G, hp, d, dsv, dH2, masks, ws, attn_tile=32, pipe: Pipeline =
         sb = scratch.bwd
         K.decoder_attention_bwd(
             B=B, N=N, T=Tp, U=A, M1=M1, M2=M2, D1=D1, D2=D2, F=d.loc_f, KW=d.loc_k, u=0.5,
-            zc=zc, zh=zh, REC0=S["REC0"], C0=S["C0"], G0=S["G0"], Q=S["Q"], S1=S["S1"],
-            AL1=S["AL1"], S2=S["S2"], ST=S["ST"], LOC=S["LOC"], K1=S["K1"], V1=S["V1"],
-            K2=S["K2"], V2=S["V2"], v1=P[f"{a1}/attention_variable"],
-            b1=P[f"{a1}/attention_bias"], convW=P[f"{a1}/location_conv/kernel"],
-            locW=P[f"{a1}/location_layer/kernel"], v2=P[f"{a2}/attention_v"], W0r=W0r,
+            zc=zc, zh=zh, REC0=S["REC0"], C0=S["C0"], G0=S["G0"], S1=S["S1"],
+            AL1=S["AL1"], S2=S["S2"], ST=S["ST"], LOC=S["LOC"], V1=S["V1"], V2=S["V2"],
+            v1=P[f"{a1}/attention_variable"], convW=P[f"{a1}/location_conv/kernel"],
+            convb=P[f"{a1}/location_conv/bias"], locW=P[f"{a1}/location_layer/kernel"],
+            v2=P[f"{a2}/attention_v"], W0r=W0r,
             Wq1=P[f"{a1}/query_layer/kernel"], Wq2=P[f"{a2}/query_layer/kernel"],
-            mask_c=mc0, mask_h=mh0, DH0=dH0, RD=RD, DG0=DG0, DE1=DE1, DE2=DE2, DFH=DFH,
+            mask_c=mc0, mask_h=mh0, DH0=dH0, ZH=S["ZH"], RD=RD, DG0=DG0, DE1=DE1, DE2=DE2, DFH=DFH,
             DQP=DQP, RDP=sb.RDP, YA=sb.YA, ctr=sb.ctr, err=sb.err)
     elif not pipe.enabled:          # layer by layer
         for t in range(Tp - 1, -1, -1):

@@ -61,6 +61,7 @@ struct DecAttnP {
   const float* mask_c; const float* mask_h;          // [T][B][U] or null (eval blend)
   float* REC0; float* C0; float* H0RAW; float* G0; float* Q;
   float* S1; float* AL1; float* S2; float* ST; float* LOC;
+  float* ZH;                                         // [T][B][N][D1+D2] energy tanh (nullable)
   float* E;                                          // [2][B][2][N] raw energies
   float* PART;                                       // [2][B][ntiles][kPST]
   float* QP;                                         // [2][B][kGW][kQ] query partials
@@ -409,6 +410,8 @@ __global__ void __launch_bounds__(256) dec_attn_fwd_kernel(DecAttnP p) {
       __syncthreads();
       // energies: 8 lanes per position, 28 dims (7 float4) of K1 per lane, 4 dims of K2
       const int nl = tid >> 3, part = tid & 7;
+      // the tanh values are kept for the BPTT (decoder_persistent_bwd.hip recomputes nothing)
+      float* zrow = (p.ZH && nl < nt) ? p.ZH + ((((int64_t)t * B + tb) * N) + n0 + nl) * kQ : nullptr;
       float acc = 0.f;
       {
         float fl[kF];
@@ -427,10 +430,13 @@ __global__ void __launch_bounds__(256) dec_attn_fwd_kernel(DecAttnP p) {
             pre.x = fmaf(fl[f], lw.x, pre.x); pre.y = fmaf(fl[f], lw.y, pre.y);
             pre.z = fmaf(fl[f], lw.z, pre.z); pre.w = fmaf(fl[f], lw.w, pre.w);
           }
-          acc = fmaf(vw.x, tanh_fast(pre.x), acc);
-          acc = fmaf(vw.y, tanh_fast(pre.y), acc);
-          acc = fmaf(vw.z, tanh_fast(pre.z), acc);
-          acc = fmaf(vw.w, tanh_fast(pre.w), acc);
+          const float4 z = make_float4(tanh_fast(pre.x), tanh_fast(pre.y), tanh_fast(pre.z),
+                                       tanh_fast(pre.w));
+          if (zrow) *reinterpret_cast<float4*>(zrow + d) = z;
+          acc = fmaf(vw.x, z.x, acc);
+          acc = fmaf(vw.y, z.y, acc);
+          acc = fmaf(vw.z, z.z, acc);
+          acc = fmaf(vw.w, z.w, acc);
         }
       }
       float acc2;
@@ -439,10 +445,13 @@ __global__ void __launch_bounds__(256) dec_attn_fwd_kernel(DecAttnP p) {
         const float4 kv = *reinterpret_cast<const float4*>(&k2s[nl][d]);
         const float4 qv = *reinterpret_cast<const float4*>(&q2s[d]);
         const float4 vw = *reinterpret_cast<const float4*>(&vv2[d]);
-        acc2 = vw.x * tanh_fast(kv.x + qv.x);
-        acc2 = fmaf(vw.y, tanh_fast(kv.y + qv.y), acc2);
-        acc2 = fmaf(vw.z, tanh_fast(kv.z + qv.z), acc2);
-        acc2 = fmaf(vw.w, tanh_fast(kv.w + qv.w), acc2);
+        const float4 z = make_float4(tanh_fast(kv.x + qv.x), tanh_fast(kv.y + qv.y),
+                                     tanh_fast(kv.z + qv.z), tanh_fast(kv.w + qv.w));
+        if (zrow) *reinterpret_cast<float4*>(zrow + kD1 + d) = z;
+        acc2 = vw.x * z.x;
+        acc2 = fmaf(vw.y, z.y, acc2);
+        acc2 = fmaf(vw.z, z.z, acc2);
+        acc2 = fmaf(vw.w, z.w, acc2);
       }
       acc = group8_sum(acc);
       acc2 = group8_sum(acc2);
@@ -558,6 +567,7 @@ extern "C" int sat_decoder_attention_fwd(const SatDecAttnFwd* a, void* stream) {
   p.S1 = a->S1; p.AL1 = a->AL1; p.S2 = a->S2; p.ST = a->ST; p.LOC = a->LOC;
   p.E = a->E; p.PART = a->PART; p.QP = a->QP; p.ctr = a->ctr; p.err = a->err;
   p.prof = reinterpret_cast<long long*>(a->prof);
+  p.ZH = a->ZH;
   hipStream_t s = as_stream(stream);
   if (hipMemsetAsync(a->ctr, 0, kG * 64 * sizeof(unsigned), s) != hipSuccess ||
       hipMemsetAsync(a->err, 0, 2 * sizeof(int), s) != hipSuccess) {

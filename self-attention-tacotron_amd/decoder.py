@@ -67,12 +67,13 @@ def decoder_forward(P: Dict[str, torch.Tensor], hp, d: Dims, m1: torch.Tensor, m
                     lengths: torch.Tensor, targets: torch.Tensor,
                     masks: Optional[Dict[str, torch.Tensor]], attn_tile: int = 32,
                     spk: Optional[torch.Tensor] = None, pipe: Pipeline = SEQUENTIAL,
-                    persistent: bool = False, scratch=None):
+                    persistent: bool = False, scratch=None, keep_tanh: bool = True):
     """Forward of the teacher-forced decoder; returns (D [T', B, dec], DecoderSaved).
 
     ``persistent`` runs the attention chain (attention RNN + query + dual-source attention) for
     all steps as ONE persistent launch (``sat_decoder_attention_fwd``) when the shapes allow,
-    then the two decoder LSTMs as a two-problem wavefront; otherwise the per-step launches."""
+    then the two decoder LSTMs as a two-problem wavefront; otherwise the per-step launches.
+    ``keep_tanh`` keeps the energies' tanh for the persistent BPTT (off for inference)."""
     dev = m1.device
     B, N, _ = m1.shape
     r, nf = d.r, hp.n_feed_frame
@@ -204,6 +205,11 @@ def decoder_forward(P: Dict[str, torch.Tensor], hp, d: Dims, m1: torch.Tensor, m
     if persistent and persistent_eligible(d, B, N, attn_tile):
         if scratch is None:
             scratch = K.DecoderAttentionScratch(B, N, dev)
+        # tanh of every energy pre-activation, kept for the persistent BPTT ([T', B, N, D1+D2]:
+        # 3.3 GB at the LJSpeech batch-32 bench shape -- HBM is 288 GB, transcendentals are not
+        # cheap on the BPTT's critical path)
+        ZH = torch.empty(Tp, B, N, D1 + D2, **f32) if keep_tanh else None
+        S["ZH"] = ZH
         K.decoder_attention_fwd(
             B=B, N=N, T=Tp, U=A, M1=M1, M2=M2, D1=D1, D2=D2, F=d.loc_f, KW=d.loc_k, u=0.5,
             zc=zc, zh=zh, X0=X0, W0r=Wr0, Wq1=P[f"{a1}/query_layer/kernel"],
@@ -213,7 +219,7 @@ def decoder_forward(P: Dict[str, torch.Tensor], hp, d: Dims, m1: torch.Tensor, m
             locW=P[f"{a1}/location_layer/kernel"], v2=P["decoder/attention2/attention_v"],
             mask_c=zc0, mask_h=zh0, REC0=REC0, C0=C0, H0RAW=H0RAW, G0=G0, Q=Q, S1=S1, AL1=AL1,
             S2=S2, ST=ST, LOC=LOC, E=scratch.E, PART=scratch.PART, QP=scratch.QP, ctr=scratch.ctr,
-            err=scratch.err)
+            err=scratch.err, ZH=ZH)
         S["attn_scratch"] = scratch
         # decoder LSTMs: all of LSTM1's input projection at once, then LSTM1 at i with LSTM2
         # C steps behind in one two-problem launch per iteration

@@ -237,7 +237,8 @@ def model_forward(P, bn: BNState, hp, d: PR.Dims, batch: Dict[str, torch.Tensor]
         K.embedding_fwd(P["speaker_embedding"], ids_s, spk, d.spk_offset, sv["spk_err"])
     dout, dsv = decoder_forward(P, hp, d, m1, m2, lengths, batch["mel"], masks,
                                 attn_tile=attn_tile, spk=spk, persistent=persistent,
-                                scratch=scratch, **({} if pipe is None else {"pipe": pipe}))
+                                scratch=scratch, keep_tanh=compute_grad_seeds,
+                                **({} if pipe is None else {"pipe": pipe}))
     sv["dec"] = dsv
     if spk is not None:
         dsv.tensors["ms_prenet"]["ids"] = batch["speaker_id"]

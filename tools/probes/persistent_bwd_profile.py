@@ -1,0 +1,49 @@
+"""Segment clocks of the persistent decoder-attention BPTT kernel (tools only): per workgroup,
+the wall-clock (100 MHz) time of each segment of the reverse step over a full training step."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+import _sat_path  # noqa: E402
+
+_sat_path.load()
+import torch  # noqa: E402
+
+from sat_amd import data, engine, hparams  # noqa: E402
+from sat_amd import kernels as K  # noqa: E402
+
+orig = K.decoder_attention_bwd
+PROF = {}
+
+
+def wrapped(**kw):
+    PROF["buf"] = torch.zeros(256 * 16, dtype=torch.int64, device="cuda")
+    kw["prof"] = PROF["buf"]
+    orig(**kw)
+
+
+K.decoder_attention_bwd = wrapped
+
+hp = hparams.ljspeech_hparams()
+m = engine.Tacotron(hp, "cuda", seed=1)
+B = int(sys.argv[1]) if len(sys.argv) > 1 else 32
+b = data.synthetic_batch(hp, B, N=200, T=1000, shape="max", seed=1)
+gb = {k: torch.tensor(v).cuda() for k, v in b.items()}
+mk = {k: torch.tensor(v).cuda() for k, v in data.synthetic_masks(hp, B, 200, 500, seed=2).items()}
+for _ in range(2):
+    out, sv = m.forward(gb, mk, training=True)
+    m.backward(sv)
+torch.cuda.synchronize()
+sv["dec"].tensors["attn_scratch"].check()
+pr = PROF["buf"].view(256, 16).cpu().double() / 100.0   # us
+Tp = 500
+names = ["Y: loads", "Y: dctx reduce + sums", "Y: DA / Y", "Y: energy bwd + flush",
+         "barrier Y", "Z: loads + dq stage", "Z: rowdot", "barrier Z", "Z: qterm + rec sums",
+         "Z: pointwise", "Z: sync"]
+for i, n in enumerate(names):
+    col = pr[:, i]
+    print(f"{n:30s} mean {col.mean() / Tp:7.2f} us/step  min {col.min() / Tp:7.2f}  "
+          f"max {col.max() / Tp:7.2f}")
+tile = pr[[g + 8 * j for g in range(8) for j in range(28)]]
+print("tile WGs:", " ".join(f"{float(tile[:, i].mean() / Tp):.2f}" for i in range(11)))
+print("total us/step", float(pr.sum(1).mean() / Tp))

@@ -335,6 +335,43 @@ int sat_decoder_attention_bwd(const SatDecAttnBwd* args, void* stream);
 int64_t sat_decoder_attention_bwd_scratch(int32_t B, int32_t N, int64_t* rdp_floats,
                                           int64_t* ya_floats);
 
+/* Persistent decoder LSTM stack: all T steps of DecoderRNNV2's two ZoneoutLSTM(U) layers
+ * (ext tacotron2 DecoderRNNV2, built at modules/module.py:1531-1540) in ONE launch, LSTM2 one
+ * step behind LSTM1, one in-kernel group barrier per step.  Replaces the per-step
+ * sat_lstm_steps_fwd / sat_lstm_steps_bwd launches of the two layers (decoder.py /
+ * backward.py launch paths); same arithmetic.  U = 256, B in {8,16,24,32}; ctr
+ * [sat_decoder_attention_scratch() words] and err [2] are zeroed by the call.
+ * Forward inputs: X1 = LSTM1's hoisted input projection + bias [T][B][4U], W1r = LSTM1's
+ * recurrent kernel rows [U][U][4], W2 = LSTM2's kernel [2U][U][4] (input rows, then recurrent),
+ * b2 [4U], zoneout masks [T][B][U] (all four or none: eval blend).  Histories as the launch path:
+ * H*RAW [T][B][U] raw outputs, C*S/H*S [T+1][B][U] states (row 0 = initial state, read),
+ * G* [T][B][4U] activated gates. */
+typedef struct SatDecLstmFwd {
+  int32_t B, T, U;
+  float zc, zh;
+  const float* X1; const float* W1r; const float* W2; const float* b2;
+  const float* mask1_c; const float* mask1_h; const float* mask2_c; const float* mask2_h;
+  float* H1RAW; float* C1S; float* H1S; float* G1;
+  float* H2RAW; float* C2S; float* H2S; float* G2;
+  uint32_t* ctr; int32_t* err;
+} SatDecLstmFwd;
+
+/* Its BPTT: DH2 = dL/dh2'_t [T][B][U] (from the decoder head) -> DG2, DG1 [T][B][4U], the
+ * gate gradients of both layers (their input / weight gradients are whole-sequence GEMMs). */
+typedef struct SatDecLstmBwd {
+  int32_t B, T, U;
+  float zc, zh;
+  const float* W1r; const float* W2;
+  const float* G1; const float* C1S; const float* G2; const float* C2S;
+  const float* DH2;
+  const float* mask1_c; const float* mask1_h; const float* mask2_c; const float* mask2_h;
+  float* DG1; float* DG2;
+  uint32_t* ctr; int32_t* err;
+} SatDecLstmBwd;
+
+int sat_decoder_lstms_fwd(const SatDecLstmFwd* args, void* stream);
+int sat_decoder_lstms_bwd(const SatDecLstmBwd* args, void* stream);
+
 /* ---------------------------------------------------------------- elementwise
  * out[b,n,:] = x[b,n,:] * (n < lengths[b])  -- TF _prepare_memory (memory_sequence_length). */
 int sat_seq_mask(const float* x, float* out, int32_t B, int32_t N, int32_t C,

@@ -95,6 +95,15 @@ SatDecAttnBwd = _struct("SatDecAttnBwd", """
     ptr:W0r ptr:Wq1 ptr:Wq2 ptr:mask_c ptr:mask_h ptr:DH0 ptr:ZH
     ptr:RD ptr:DG0 ptr:DE1 ptr:DE2 ptr:DFH ptr:DQP ptr:RDP ptr:YA ptr:ctr ptr:err ptr:prof""")
 
+SatDecLstmFwd = _struct("SatDecLstmFwd", """
+    i32:B i32:T i32:U f32:zc f32:zh ptr:X1 ptr:W1r ptr:W2 ptr:b2
+    ptr:mask1_c ptr:mask1_h ptr:mask2_c ptr:mask2_h
+    ptr:H1RAW ptr:C1S ptr:H1S ptr:G1 ptr:H2RAW ptr:C2S ptr:H2S ptr:G2 ptr:ctr ptr:err""")
+
+SatDecLstmBwd = _struct("SatDecLstmBwd", """
+    i32:B i32:T i32:U f32:zc f32:zh ptr:W1r ptr:W2 ptr:G1 ptr:C1S ptr:G2 ptr:C2S ptr:DH2
+    ptr:mask1_c ptr:mask1_h ptr:mask2_c ptr:mask2_h ptr:DG1 ptr:DG2 ptr:ctr ptr:err""")
+
 SatAttnStep = _struct("SatAttnStep", """
     i32:B i32:N i32:D1 i32:M1 i32:D2 i32:M2 i32:F i32:KW i32:NT i32:ntiles i32:att1_forward
     f32:u ptr:q i64:q_sb ptr:K1 ptr:V1 ptr:K2 ptr:V2 ptr:lengths ptr:s_prev ptr:a_prev
@@ -120,6 +129,8 @@ SIGNATURES = {
     "sat_attn_step_bwd": [ctypes.POINTER(SatAttnStepBwd), _P],
     "sat_decoder_attention_fwd": [ctypes.POINTER(SatDecAttnFwd), _P],
     "sat_decoder_attention_bwd": [ctypes.POINTER(SatDecAttnBwd), _P],
+    "sat_decoder_lstms_fwd": [ctypes.POINTER(SatDecLstmFwd), _P],
+    "sat_decoder_lstms_bwd": [ctypes.POINTER(SatDecLstmBwd), _P],
     "sat_attn_param_grad_rows": [_I32, _I32],
     "sat_attn_param_grads": [ctypes.POINTER(SatAttnParamGrad), _P],
     "sat_seq_mask": [_P, _P, _I32, _I32, _I32, _P, _P],

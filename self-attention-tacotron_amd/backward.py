@@ -239,29 +239,15 @@ def decoder_bwd(P, G, hp, d, dsv, dH2, masks, ws, attn_tile=32, pipe: Pipeline =
         if S.get("ZH") is None:
             raise RuntimeError("decoder_bwd: the forward ran without keep_tanh (inference mode)")
         # the forward ran the attention chain as one persistent launch: the decoder LSTMs'
-        # reverse recurrences first (LSTM1 C steps behind LSTM2 in one two-problem launch per
-        # iteration), their input gradients into the chain as whole-sequence GEMMs, then the
-        # attention chain's BPTT as ONE persistent launch (sat_decoder_attention_bwd)
-        C = pipe.chunk if pipe.enabled else Tp
-        if not pipe.enabled:
-            for t in range(Tp - 1, -1, -1):
-                K.lstm_step_bwd(**lstm2_desc(t))
-            dh1_chunk(0, Tp)
-            for t in range(Tp - 1, -1, -1):
-                K.lstm_step_bwd(**lstm1_desc(t))
-        else:
-            dh1_at = pipe.finishing_rev(Tp, 0)
-            for j in range(Tp + C):
-                t2, t1 = Tp - 1 - j, Tp - 1 - j + C
-                steps = []
-                if t2 >= 0:
-                    steps.append(lstm2_desc(t2))
-                if 0 <= t1 < Tp:
-                    steps.append(lstm1_desc(t1))
-                if steps:
-                    K.lstm_steps_bwd(steps)
-                if j in dh1_at:
-                    dh1_chunk(*dh1_at[j])
+        # reverse recurrences first (both layers in ONE persistent launch, LSTM1 one step
+        # behind LSTM2, dL/dh1' formed in-kernel from LSTM2's input rows), their input
+        # gradients into the chain as whole-sequence GEMMs, then the attention chain's BPTT as
+        # ONE persistent launch (sat_decoder_attention_bwd)
+        K.decoder_lstms_bwd(
+            B=B, T=Tp, U=Dd, zc=zc, zh=zh, W1r=W1[A + M1 + M2:], W2=W2, G1=S["G1"],
+            C1S=S["C1S"], G2=S["G2"], C2S=S["C2S"], DH2=dH2, mask1_c=m1c, mask1_h=m1h,
+            mask2_c=m2c, mask2_h=m2h, DG1=DG1, DG2=DG2, ctr=scratch.lstm_ctr[1],
+            err=scratch.lstm_err[1])
         dh0_chunk(0, Tp)
         sb = scratch.bwd
         K.decoder_attention_bwd(

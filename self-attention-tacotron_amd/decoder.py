@@ -57,9 +57,11 @@ def teacher_inputs(targets: torch.Tensor, r: int, n_feed: int) -> torch.Tensor:
 
 
 def persistent_eligible(d: Dims, B: int, N: int, attn_tile: int = 32) -> bool:
-    """Shapes sat_decoder_attention_fwd is compiled for (the self-attention-tacotron configs)."""
+    """Shapes sat_decoder_attention_fwd and sat_decoder_lstms_fwd are compiled for (the
+    self-attention-tacotron configs)."""
     return (d.att1 == "forward" and d.att2 == "additive" and attn_tile == 32 and
-            (d.att_rnn, d.m1, d.m2, d.d1, d.d2, d.loc_f, d.loc_k) == (256, 256, 32, 224, 32, 5, 10)
+            (d.att_rnn, d.m1, d.m2, d.d1, d.d2, d.loc_f, d.loc_k, d.dec) ==
+            (256, 256, 32, 224, 32, 5, 10, 256)
             and B % 8 == 0 and B // 8 <= 4 and (B // 8) * ((N + 31) // 32) <= 32)
 
 
@@ -221,28 +223,16 @@ def decoder_forward(P: Dict[str, torch.Tensor], hp, d: Dims, m1: torch.Tensor, m
             S2=S2, ST=ST, LOC=LOC, E=scratch.E, PART=scratch.PART, QP=scratch.QP, ctr=scratch.ctr,
             err=scratch.err, ZH=ZH)
         S["attn_scratch"] = scratch
-        # decoder LSTMs: all of LSTM1's input projection at once, then LSTM1 at i with LSTM2
-        # C steps behind in one two-problem launch per iteration
+        # decoder LSTMs: all of LSTM1's input projection at once, then both layers' recurrences
+        # as ONE persistent launch (LSTM2 one step behind LSTM1, in-kernel group barriers);
+        # LSTM2's input projection happens inside it, so X2 is never materialised
         x1_chunk(0, Tp)
-        C = pipe.chunk if pipe.enabled else Tp
-        x2_at = pipe.finishing(Tp, 0) if pipe.enabled else {}     # LSTM1 runs at lag 0 here
-        if not pipe.enabled:
-            for t in range(Tp):
-                K.lstm_step_fwd(**lstm1_desc(t))
-            x2_chunk(0, Tp)
-            for t in range(Tp):
-                K.lstm_step_fwd(**lstm2_desc(t))
-        else:
-            for i in range(Tp + C):
-                steps = []
-                if i < Tp:
-                    steps.append(lstm1_desc(i))
-                if 0 <= i - C < Tp:
-                    steps.append(lstm2_desc(i - C))
-                if steps:
-                    K.lstm_steps_fwd(steps)
-                if i in x2_at:
-                    x2_chunk(*x2_at[i])
+        X2 = None
+        K.decoder_lstms_fwd(
+            B=B, T=Tp, U=Dd, zc=zc, zh=zh, X1=X1, W1r=W1[A + M1 + M2:], W2=W2,
+            b2=P["decoder/lstm2/bias"], mask1_c=m1c, mask1_h=m1h, mask2_c=m2c, mask2_h=m2h,
+            H1RAW=L1[0], C1S=L1[1], H1S=L1[2], G1=L1[3], H2RAW=L2[0], C2S=L2[1], H2S=L2[2],
+            G2=L2[3], ctr=scratch.lstm_ctr[0], err=scratch.lstm_err[0])
     elif not pipe.enabled:          # layer by layer
         for t in range(Tp):
             K.lstm_step_fwd(**lstm0_desc(t))

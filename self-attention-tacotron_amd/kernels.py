@@ -338,11 +338,19 @@ class DecoderAttentionScratch:
         self.err = torch.zeros(2, dtype=torch.int32, device=device)
         self.bwd = DecoderAttentionBwdScratch(B, N, device)   # the persistent BPTT's own
 
+        # the persistent decoder LSTM stack's own counters / error words (fwd, bwd)
+        self.lstm_ctr = torch.zeros(2, words, dtype=torch.int32, device=device)
+        self.lstm_err = torch.zeros(2, 2, dtype=torch.int32, device=device)
+
     def check(self):
         """Host check of the in-kernel barrier timeout flags (synchronises)."""
         if int(self.err[0].item()) != 0:
             raise _lib.SatLibraryError("sat_decoder_attention_fwd: a group barrier timed out "
                                        "(workgroups not co-resident?)")
+        for i, nm in enumerate(("sat_decoder_lstms_fwd", "sat_decoder_lstms_bwd")):
+            if int(self.lstm_err[i, 0].item()) != 0:
+                raise _lib.SatLibraryError(f"{nm}: a group barrier timed out "
+                                           "(workgroups not co-resident?)")
         self.bwd.check()
 
 
@@ -379,6 +387,22 @@ def decoder_attention_bwd(**kw):
         setattr(a, k, _p(v) if isinstance(v, torch.Tensor) else v)
     _lib.check(_lib.load().sat_decoder_attention_bwd(ctypes.byref(a), _stream()),
                "sat_decoder_attention_bwd")
+
+
+def decoder_lstms_fwd(**kw):
+    a = _lib.SatDecLstmFwd()
+    for k, v in kw.items():
+        setattr(a, k, _p(v) if isinstance(v, torch.Tensor) else v)
+    _lib.check(_lib.load().sat_decoder_lstms_fwd(ctypes.byref(a), _stream()),
+               "sat_decoder_lstms_fwd")
+
+
+def decoder_lstms_bwd(**kw):
+    a = _lib.SatDecLstmBwd()
+    for k, v in kw.items():
+        setattr(a, k, _p(v) if isinstance(v, torch.Tensor) else v)
+    _lib.check(_lib.load().sat_decoder_lstms_bwd(ctypes.byref(a), _stream()),
+               "sat_decoder_lstms_bwd")
 
 
 def attn_step_bwd(**kw):

@@ -52,7 +52,8 @@ def _c_sizeof(struct):
 
 
 STRUCTS = ["SatGemmDesc", "SatLstmFwd", "SatLstmBwd", "SatAttnStep", "SatAttnStepBwd",
-           "SatAttnParamGrad", "SatDecAttnFwd", "SatDecAttnBwd", "SatAdamConfig"]
+           "SatAttnParamGrad", "SatDecAttnFwd", "SatDecAttnBwd", "SatDecLstmFwd",
+           "SatDecLstmBwd", "SatAdamConfig"]
 
 
 def _c_offsets(struct, fields):

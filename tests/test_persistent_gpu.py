@@ -1,6 +1,7 @@
-"""Persistent decoder attention chain (sat_decoder_attention_fwd: all T' steps of attention RNN
-+ query + dual-source attention in ONE launch, K/V resident in LDS, in-kernel group barriers)
-vs the per-step launch path and vs the CPU oracle."""
+"""Persistent decoder kernels (sat_decoder_attention_fwd/bwd: all T' steps of attention RNN
++ query + dual-source attention in ONE launch, K/V resident in LDS; sat_decoder_lstms_fwd/bwd:
+both decoder LSTM layers in ONE launch; in-kernel group barriers) vs the per-step launch path
+and vs the CPU oracle."""
 import numpy as np
 import pytest
 import torch
@@ -38,7 +39,8 @@ def test_persistent_equals_per_step(cuda, B, N, T, train):
     np.testing.assert_allclose(o1["mel"].cpu().numpy(), o0["mel"].cpu().numpy(), atol=2e-5)
     np.testing.assert_allclose(o1["stop"].cpu().numpy(), o0["stop"].cpu().numpy(), atol=2e-5)
     assert abs(float(o1["loss"].item()) - float(o0["loss"].item())) < 1e-5
-    for name in ("REC0", "C0", "H0RAW", "G0", "Q", "S1", "AL1", "S2", "LOC"):
+    for name in ("REC0", "C0", "H0RAW", "G0", "Q", "S1", "AL1", "S2", "LOC",
+                 "H1RAW", "C1S", "H1S", "G1", "H2RAW", "C2S", "H2S", "G2"):
         a, r = s1["dec"].tensors[name], s0["dec"].tensors[name]
         np.testing.assert_allclose(a.cpu().numpy(), r.cpu().numpy(), atol=2e-5, err_msg=name)
     st0, st1 = s0["dec"].tensors["ST"], s1["dec"].tensors["ST"]

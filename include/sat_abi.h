@@ -354,6 +354,7 @@ typedef struct SatDecLstmFwd {
   float* H1RAW; float* C1S; float* H1S; float* G1;
   float* H2RAW; float* C2S; float* H2S; float* G2;
   uint32_t* ctr; int32_t* err;
+  int64_t* prof;   /* optional [256][4] per-workgroup segment clocks (100 MHz), NULL = off */
 } SatDecLstmFwd;
 
 /* Its BPTT: DH2 = dL/dh2'_t [T][B][U] (from the decoder head) -> DG2, DG1 [T][B][4U], the
@@ -367,6 +368,7 @@ typedef struct SatDecLstmBwd {
   const float* mask1_c; const float* mask1_h; const float* mask2_c; const float* mask2_h;
   float* DG1; float* DG2;
   uint32_t* ctr; int32_t* err;
+  int64_t* prof;   /* optional [256][4] per-workgroup segment clocks (100 MHz), NULL = off */
 } SatDecLstmBwd;
 
 int sat_decoder_lstms_fwd(const SatDecLstmFwd* args, void* stream);

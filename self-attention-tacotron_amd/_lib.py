@@ -98,11 +98,11 @@ SatDecAttnBwd = _struct("SatDecAttnBwd", """
 SatDecLstmFwd = _struct("SatDecLstmFwd", """
     i32:B i32:T i32:U f32:zc f32:zh ptr:X1 ptr:W1r ptr:W2 ptr:b2
     ptr:mask1_c ptr:mask1_h ptr:mask2_c ptr:mask2_h
-    ptr:H1RAW ptr:C1S ptr:H1S ptr:G1 ptr:H2RAW ptr:C2S ptr:H2S ptr:G2 ptr:ctr ptr:err""")
+    ptr:H1RAW ptr:C1S ptr:H1S ptr:G1 ptr:H2RAW ptr:C2S ptr:H2S ptr:G2 ptr:ctr ptr:err ptr:prof""")
 
 SatDecLstmBwd = _struct("SatDecLstmBwd", """
     i32:B i32:T i32:U f32:zc f32:zh ptr:W1r ptr:W2 ptr:G1 ptr:C1S ptr:G2 ptr:C2S ptr:DH2
-    ptr:mask1_c ptr:mask1_h ptr:mask2_c ptr:mask2_h ptr:DG1 ptr:DG2 ptr:ctr ptr:err""")
+    ptr:mask1_c ptr:mask1_h ptr:mask2_c ptr:mask2_h ptr:DG1 ptr:DG2 ptr:ctr ptr:err ptr:prof""")
 
 SatAttnStep = _struct("SatAttnStep", """
     i32:B i32:N i32:D1 i32:M1 i32:D2 i32:M2 i32:F i32:KW i32:NT i32:ntiles i32:att1_forward

@@ -51,6 +51,7 @@ struct DecLstmFwdP {
   float* H1RAW; float* C1S; float* H1S; float* G1;
   float* H2RAW; float* C2S; float* H2S; float* G2;
   unsigned* ctr; int* err;
+  long long* prof;                                    // [256][4] segment clocks (nullable)
 };
 
 __device__ __forceinline__ float dot4(float4 a, float4 b, float acc) {
@@ -105,6 +106,16 @@ __global__ void __launch_bounds__(256) dec_lstm_fwd_kernel(DecLstmFwdP p) {
   const bool masked = p.m1c != nullptr;
   const auto rH1S = rsrc(p.H1S), rH1R = rsrc(p.H1RAW), rH2S = rsrc(p.H2S);
 
+  // optional segment clocks (thread 0): barrier wait, staging loads, dots, pointwise
+  long long tp[4] = {0, 0, 0, 0};
+  long long t0 = wall_clock64();
+  auto tick = [&](int seg) {
+    if (p.prof) {
+      const long long t1 = wall_clock64();
+      tp[seg] += t1 - t0;
+      t0 = t1;
+    }
+  };
   for (int i = 0; i <= T; ++i) {
     const bool do1 = i < T, do2 = i >= 1;
     const int t = layer == 0 ? i : i - 1;
@@ -134,6 +145,7 @@ __global__ void __launch_bounds__(256) dec_lstm_fwd_kernel(DecLstmFwdP p) {
       *reinterpret_cast<float4*>(&xs[ub][4 * q]) = v;
     }
     __syncthreads();
+    tick(1);
     float a1[kUBmax], a2[kUBmax];
 #pragma unroll
     for (int ub = 0; ub < kUBmax; ++ub) {
@@ -166,6 +178,7 @@ __global__ void __launch_bounds__(256) dec_lstm_fwd_kernel(DecLstmFwdP p) {
       }
     }
     __syncthreads();
+    tick(2);
     if (pw_step) {
       const float* gg = gs[layer][pub] + 4 * pul;
       const float gi = sigmf(gg[0] + xp.x);
@@ -192,8 +205,12 @@ __global__ void __launch_bounds__(256) dec_lstm_fwd_kernel(DecLstmFwdP p) {
         reinterpret_cast<float4*>(p.G2)[bu] = make_float4(gi, gj, gf, go);
       }
     }
+    tick(3);
     if (i < T) group_barrier(ctr, (unsigned)(i + 1) * kGW, p.err);
+    tick(0);
   }
+  if (p.prof && tid == 0)
+    for (int i = 0; i < 4; ++i) p.prof[blockIdx.x * 4 + i] = tp[i];
 }
 
 struct DecLstmBwdP {
@@ -206,6 +223,7 @@ struct DecLstmBwdP {
   const float* m1c; const float* m1h; const float* m2c; const float* m2h;
   float* DG1; float* DG2;                             // [T][B][4U]
   unsigned* ctr; int* err;
+  long long* prof;                                    // [256][4] segment clocks (nullable)
 };
 
 // TF LSTMCell + zoneout backward of one (utterance, unit) (lstm.hip lstm_bwd_block's pointwise):
@@ -264,6 +282,16 @@ __global__ void __launch_bounds__(256) dec_lstm_bwd_kernel(DecLstmBwdP p) {
   const bool masked = p.m1c != nullptr;
   const auto rDG1 = rsrc(p.DG1), rDG2 = rsrc(p.DG2);
 
+  // optional segment clocks (thread 0): barrier wait, staging loads, dots, pointwise
+  long long tp[4] = {0, 0, 0, 0};
+  long long t0 = wall_clock64();
+  auto tick = [&](int seg) {
+    if (p.prof) {
+      const long long t1 = wall_clock64();
+      tp[seg] += t1 - t0;
+      t0 = t1;
+    }
+  };
   for (int jj = 0; jj <= T; ++jj) {
     const int t2 = T - 1 - jj, t1 = T - jj;
     const bool has2 = t2 >= 0, has1 = jj >= 1;
@@ -302,6 +330,7 @@ __global__ void __launch_bounds__(256) dec_lstm_bwd_kernel(DecLstmBwdP p) {
       }
     }
     __syncthreads();
+    tick(1);
     float r2[kUBmax], y1[kUBmax], r1[kUBmax];
 #pragma unroll
     for (int ub = 0; ub < kUBmax; ++ub) {
@@ -333,6 +362,7 @@ __global__ void __launch_bounds__(256) dec_lstm_bwd_kernel(DecLstmBwdP p) {
         y1[ub] += __shfl_xor(y1[ub], o, 64);
         r1[ub] += __shfl_xor(r1[ub], o, 64);
       }
+    tick(2);
     if (pw_step) {
       float rec = 0.f, dy = dyv;
 #pragma unroll
@@ -345,9 +375,13 @@ __global__ void __launch_bounds__(256) dec_lstm_bwd_kernel(DecLstmBwdP p) {
       const int64_t bu = ((int64_t)t * B + pb) * kU + u;
       stc4(layer == 2 ? rDG2 : rDG1, (int)bu, dg);
     }
+    tick(3);
     if (jj < T) group_barrier(ctr, (unsigned)(jj + 1) * kGW, p.err);
     else __syncthreads();
+    tick(0);
   }
+  if (p.prof && tid == 0)
+    for (int i = 0; i < 4; ++i) p.prof[blockIdx.x * 4 + i] = tp[i];
 }
 
 int check_coresident(const void* kernel, const char* name) {
@@ -401,6 +435,7 @@ extern "C" int sat_decoder_lstms_fwd(const SatDecLstmFwd* a, void* stream) {
   p.H1RAW = a->H1RAW; p.C1S = a->C1S; p.H1S = a->H1S; p.G1 = a->G1;
   p.H2RAW = a->H2RAW; p.C2S = a->C2S; p.H2S = a->H2S; p.G2 = a->G2;
   p.ctr = a->ctr; p.err = a->err;
+  p.prof = reinterpret_cast<long long*>(a->prof);
   hipStream_t s = as_stream(stream);
   rc = reset_sync(a->ctr, a->err, s, nm);
   if (rc != SAT_OK) return rc;
@@ -431,6 +466,7 @@ extern "C" int sat_decoder_lstms_bwd(const SatDecLstmBwd* a, void* stream) {
   p.DH2 = a->DH2;
   p.m1c = a->mask1_c; p.m1h = a->mask1_h; p.m2c = a->mask2_c; p.m2h = a->mask2_h;
   p.DG1 = a->DG1; p.DG2 = a->DG2; p.ctr = a->ctr; p.err = a->err;
+  p.prof = reinterpret_cast<long long*>(a->prof);
   hipStream_t s = as_stream(stream);
   rc = reset_sync(a->ctr, a->err, s, nm);
   if (rc != SAT_OK) return rc;

@@ -2,7 +2,8 @@
 bytes, with the gfx950 corrections of MI355X_MICROARCH.md (HBM section):
   * FETCH_SIZE and WRITE_SIZE are reported in KiB;
   * FETCH_SIZE counts exactly half the bytes of wide (16 B/lane) coalesced streaming reads on
-    gfx950 -> doubled here (the tile kernel's bulk reads are 16-byte float4 loads);
+    gfx950 -> doubled here (the attention kernels' bulk reads are 16-byte float4 loads; other
+    widths are uncalibrated, so the doubled figure is an upper estimate for them);
   * WRITE_SIZE is exact for 16-B stores and is taken as is.
 
     python3 tools/pmc_summary.py <fetch_dir> <write_dir> [kernel_regex]

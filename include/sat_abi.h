@@ -337,10 +337,10 @@ int64_t sat_decoder_attention_bwd_scratch(int32_t B, int32_t N, int64_t* rdp_flo
 
 /* Persistent decoder LSTM stack: all T steps of DecoderRNNV2's two ZoneoutLSTM(U) layers
  * (ext tacotron2 DecoderRNNV2, built at modules/module.py:1531-1540) in ONE launch, LSTM2 one
- * step behind LSTM1, one in-kernel group barrier per step.  Replaces the per-step
+ * step behind LSTM1, one in-kernel hand-off per step.  Replaces the per-step
  * sat_lstm_steps_fwd / sat_lstm_steps_bwd launches of the two layers (decoder.py /
- * backward.py launch paths); same arithmetic.  U = 256, B in {8,16,24,32}; ctr
- * [sat_decoder_attention_scratch() words] and err [2] are zeroed by the call.
+ * backward.py launch paths); same arithmetic.  U = 256, B <= 32; the hand-off scratch
+ * (forward: xch; backward: ctr) and err [2] are zeroed by the call.
  * Forward inputs: X1 = LSTM1's hoisted input projection + bias [T][B][4U], W1r = LSTM1's
  * recurrent kernel rows [U][U][4], W2 = LSTM2's kernel [2U][U][4] (input rows, then recurrent),
  * b2 [4U], zoneout masks [T][B][U] (all four or none: eval blend).  Histories as the launch path:
@@ -353,7 +353,8 @@ typedef struct SatDecLstmFwd {
   const float* mask1_c; const float* mask1_h; const float* mask2_c; const float* mask2_h;
   float* H1RAW; float* C1S; float* H1S; float* G1;
   float* H2RAW; float* C2S; float* H2S; float* G2;
-  uint32_t* ctr; int32_t* err;
+  float* xch;      /* hand-off granules, sat_decoder_lstms_scratch(B) floats, zeroed by the call */
+  int32_t* err;
   int64_t* prof;   /* optional [256][4] per-workgroup segment clocks (100 MHz), NULL = off */
 } SatDecLstmFwd;
 
@@ -367,11 +368,14 @@ typedef struct SatDecLstmBwd {
   const float* DH2;
   const float* mask1_c; const float* mask1_h; const float* mask2_c; const float* mask2_h;
   float* DG1; float* DG2;
-  uint32_t* ctr; int32_t* err;
+  uint32_t* ctr;   /* sat_decoder_lstms_bwd_scratch(B) words, zeroed by the call */
+  int32_t* err;
   int64_t* prof;   /* optional [256][4] per-workgroup segment clocks (100 MHz), NULL = off */
 } SatDecLstmBwd;
 
 int sat_decoder_lstms_fwd(const SatDecLstmFwd* args, void* stream);
+int64_t sat_decoder_lstms_scratch(int32_t B);
+int64_t sat_decoder_lstms_bwd_scratch(int32_t B);
 int sat_decoder_lstms_bwd(const SatDecLstmBwd* args, void* stream);
 
 /* ---------------------------------------------------------------- elementwise

@@ -98,7 +98,7 @@ SatDecAttnBwd = _struct("SatDecAttnBwd", """
 SatDecLstmFwd = _struct("SatDecLstmFwd", """
     i32:B i32:T i32:U f32:zc f32:zh ptr:X1 ptr:W1r ptr:W2 ptr:b2
     ptr:mask1_c ptr:mask1_h ptr:mask2_c ptr:mask2_h
-    ptr:H1RAW ptr:C1S ptr:H1S ptr:G1 ptr:H2RAW ptr:C2S ptr:H2S ptr:G2 ptr:ctr ptr:err ptr:prof""")
+    ptr:H1RAW ptr:C1S ptr:H1S ptr:G1 ptr:H2RAW ptr:C2S ptr:H2S ptr:G2 ptr:xch ptr:err ptr:prof""")
 
 SatDecLstmBwd = _struct("SatDecLstmBwd", """
     i32:B i32:T i32:U f32:zc f32:zh ptr:W1r ptr:W2 ptr:G1 ptr:C1S ptr:G2 ptr:C2S ptr:DH2
@@ -163,7 +163,9 @@ RESTYPES = {"sat_workspace_colreduce": (ctypes.c_int64, [_I32, _I32]),
             "sat_workspace_adam": (ctypes.c_int64, []),
             "sat_workspace_loss": (ctypes.c_int64, []),
             "sat_decoder_attention_scratch": (ctypes.c_int64, [_I32, _I32, _P, _P, _P]),
-            "sat_decoder_attention_bwd_scratch": (ctypes.c_int64, [_I32, _I32, _P, _P])}
+            "sat_decoder_attention_bwd_scratch": (ctypes.c_int64, [_I32, _I32, _P, _P]),
+            "sat_decoder_lstms_scratch": (ctypes.c_int64, [_I32]),
+            "sat_decoder_lstms_bwd_scratch": (ctypes.c_int64, [_I32])}
 
 _lib: Optional[ctypes.CDLL] = None
 

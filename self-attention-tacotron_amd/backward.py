@@ -246,7 +246,7 @@ def decoder_bwd(P, G, hp, d, dsv, dH2, masks, ws, attn_tile=32, pipe: Pipeline =
         K.decoder_lstms_bwd(
             B=B, T=Tp, U=Dd, zc=zc, zh=zh, W1r=W1[A + M1 + M2:], W2=W2, G1=S["G1"],
             C1S=S["C1S"], G2=S["G2"], C2S=S["C2S"], DH2=dH2, mask1_c=m1c, mask1_h=m1h,
-            mask2_c=m2c, mask2_h=m2h, DG1=DG1, DG2=DG2, ctr=scratch.lstm_ctr[1],
+            mask2_c=m2c, mask2_h=m2h, DG1=DG1, DG2=DG2, ctr=scratch.lstm_ctr,
             err=scratch.lstm_err[1])
         dh0_chunk(0, Tp)
         sb = scratch.bwd

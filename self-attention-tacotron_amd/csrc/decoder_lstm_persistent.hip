@@ -8,40 +8,41 @@
 // a launch-per-step wavefront -- ~740 launches per direction per training step, each paying a
 // kernel boundary plus a cold reload of its recurrent weights from MALL.  Here every workgroup
 // keeps its weight columns in registers for the whole sequence, and one step costs one in-kernel
-// group barrier plus on-chip arithmetic.
+// hand-off plus on-chip arithmetic.
 //
-// Layout (same as the attention chain): 8 groups x 32 workgroups (256, one per CU).  Group
-// g = blockIdx % 8 owns utterances b = g + 8*ub (ub < B/8 <= 4); workgroup j = blockIdx / 8 owns
-// units [8j, 8j+8) of BOTH layers.  The LSTMs couple units, never utterances, so a group's
-// hand-offs never leave the group.
-//   forward, iteration i (0..T'):   LSTM1 step i  and  LSTM2 step i-1  (one barrier)
-//     LSTM1 step i   needs h1_{i-1} (all units)                       -> H1S[i]
-//     LSTM2 step i-1 needs h1'_{i-1} (raw output, its input) and h2_{i-2} -> H1RAW[i-1], H2S[i-1]
-//   backward, iteration j (0..T'):  LSTM2 step T'-1-j  and  LSTM1 step T'-j  (one barrier)
+// Layout: 16 groups x 16 workgroups of 512 threads (256, one per CU).  Group g = blockIdx % 16
+// owns utterances b = g + 16*ub (ub < 2, b < B); workgroup j = blockIdx / 16 owns units
+// [16j, 16j+16) of BOTH layers, wave w of it units 16j + 2w, +1.  The LSTMs couple units, never
+// utterances, so a group's hand-offs never leave the group, and blocks g, g+16, ... share an XCD
+// under the observed round-robin placement (speed only).  A step's hand-off is an all-gather of
+// the group's rows, so two utterances per group (not four over 32 workgroups) halve the bytes
+// every workgroup must pull per step; the weights per workgroup double (96 floats per thread at
+// 512 threads).
+//   forward, iteration i (0..T'):   LSTM1 step i  and  LSTM2 step i-1
+//     LSTM1 step i   needs h1_{i-1} (all units)
+//     LSTM2 step i-1 needs h1'_{i-1} (raw output, its input) and h2_{i-2}
+//   backward, iteration j (0..T'):  LSTM2 step T'-1-j  and  LSTM1 step T'-j
 //     LSTM2 step t   needs dgates2_{t+1} (its recurrent product)
 //     LSTM1 step t+1 needs dgates2_{t+1} (its output gradient through LSTM2's input rows)
 //                    and  dgates1_{t+2} (its recurrent product)
-// Hand-offs: the histories themselves (sc1 stores / sc1 loads, persistent.h); every spin is
-// bounded and a timeout raises err[0] so the grid always drains.
+// Every spin is bounded and a timeout raises err[0] so the grid always drains.
 #include "sat_common.h"
 #include "persistent.h"
 
 namespace sat {
 namespace {
 
-constexpr int kG = 8;              // groups
-constexpr int kGW = 32;            // workgroups per group
+constexpr int kG = 16;             // groups
+constexpr int kGW = 16;            // workgroups per group
 constexpr int kU = 256;            // units per layer
-constexpr int kUW = kU / kGW;      // units per workgroup per layer (8)
-constexpr int kUBmax = 4;          // utterances per group
-constexpr int kC = 4 * kUW;        // gate columns per workgroup per layer (32)
+constexpr int kUW = kU / kGW;      // units per workgroup per layer (16)
+constexpr int kUBmax = 2;          // utterances per group
+constexpr int kThreads = 512;      // 8 waves, 2 units each
 constexpr int kX = 3 * kU;         // forward staging row: [h1_{i-1} | h1'_{i-1} | h2_{i-2}]
-constexpr int kI1 = kU / 32;       // LSTM1 recurrent float4 per thread (8)
-constexpr int kI2 = 2 * kU / 32;   // LSTM2 [input | recurrent] float4 per thread (16)
-constexpr int kIB = 4 * kU / 128;  // backward float4 per thread per weight row (8)
+static_assert(kUW == 2 * (kThreads / 64), "two units per wave");
 
 struct DecLstmFwdP {
-  int B, T, UB;
+  int B, T;
   float zc, zh;
   const float* X1;                                    // [T][B][4U]
   const float* W1r;                                   // [U][U][4]
@@ -50,7 +51,8 @@ struct DecLstmFwdP {
   const float* m1c; const float* m1h; const float* m2c; const float* m2h;   // [T][B][U] | null
   float* H1RAW; float* C1S; float* H1S; float* G1;
   float* H2RAW; float* C2S; float* H2S; float* G2;
-  unsigned* ctr; int* err;
+  float* xch;                                         // hand-off granules (zeroed per call)
+  int* err;
   long long* prof;                                    // [256][4] segment clocks (nullable)
 };
 
@@ -61,52 +63,150 @@ __device__ __forceinline__ float dot4(float4 a, float4 b, float acc) {
   return fmaf(a.w, b.w, acc);
 }
 
-// Forward.  Dot role: thread = (gate column c = unit_local*4 + gate, k-slice ks of 8); its
-// weights are the float4 runs k = 32i + 4ks .. +3 of column c (LSTM1: 8 runs of the recurrent
-// kernel, LSTM2: 16 runs of [input | recurrent]), loaded once into registers.  Pointwise role:
-// threads 0..63 = (layer, ub, unit); each keeps its unit's (c, h) state in registers.
-__global__ void __launch_bounds__(256) dec_lstm_fwd_kernel(DecLstmFwdP p) {
+// Transpose-reduce across the 64 lanes of a wave: v[0..N-1] are per-lane partial sums of N
+// different outputs; each halving exchange pairs (v[i], v[i + n/2]) over one lane bit, after
+// which every lane keeps the half its bit selects, summed with its partner's.  All VALU, no
+// LDS: the 32- and 16-lane exchanges are gfx950 v_permlane32_swap / v_permlane16_swap (after
+// the swap x' + y' is already the kept half's sum), the 8/4-lane ones DPP row shifts (lane l
+// adds lane l+H where bit H of l is clear, lane l-H where it is set).  Lane bits left over when
+// the values run out are plain butterflies, so every lane of a 64/N block ends with the total.
+__device__ __forceinline__ float fsum_swap32(float x, float y) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(y), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float fsum_swap16(float x, float y) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(y), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float x) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, true));
+}
+template <int H, int HALF>
+__device__ __forceinline__ void tr_dpp(float* v, int lane) {
+  const bool hi = (lane & H) != 0;
+#pragma unroll
+  for (int i = 0; i < HALF; ++i) {
+    const float sa = v[i] + dpp_mov<0x100 + H>(v[i]);                // row_shl:H (lane l+H)
+    const float sb = v[i + HALF] + dpp_mov<0x110 + H>(v[i + HALF]);  // row_shr:H (lane l-H)
+    v[i] = hi ? sb : sa;
+  }
+}
+// 32 outputs: lanes 2m, 2m+1 hold output m
+__device__ __forceinline__ void transpose_reduce32(float* v, int lane) {
+#pragma unroll
+  for (int i = 0; i < 16; ++i) v[i] = fsum_swap32(v[i], v[i + 16]);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = fsum_swap16(v[i], v[i + 8]);
+  tr_dpp<8, 4>(v, lane);
+  tr_dpp<4, 2>(v, lane);
+  tr_dpp<2, 1>(v, lane);
+  v[0] += dpp_mov<0xB1>(v[0]);   // quad_perm [1,0,3,2]: lane l ^ 1
+}
+// 16 outputs: lanes 4m..4m+3 hold output m
+__device__ __forceinline__ void transpose_reduce16(float* v, int lane) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = fsum_swap32(v[i], v[i + 8]);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) v[i] = fsum_swap16(v[i], v[i + 4]);
+  tr_dpp<8, 2>(v, lane);
+  tr_dpp<4, 1>(v, lane);
+  v[0] += dpp_mov<0xB1>(v[0]);   // lane l ^ 1
+  v[0] += dpp_mov<0x4E>(v[0]);   // quad_perm [2,3,0,1]: lane l ^ 2
+}
+
+__device__ __forceinline__ unsigned tag_of(float x) { return __float_as_uint(x); }
+
+// Forward.  Dot role: wave w owns units 2w, 2w+1 of the workgroup in both layers (8 gate
+// columns each), lane = k-slice ks: LSTM1's recurrent rows 4ks..4ks+3 and LSTM2's [input |
+// recurrent] rows 8ks..8ks+7 of those 8 columns live in registers (96 floats), so each staged
+// float4 of the input rows feeds 8 columns.  The 32 partial sums per lane (layer x utterance x
+// column) are transpose-reduced across the wave; the 4 gate sums of a (layer, utterance, unit)
+// then sit in lanes l, l+2, l+4, l+6 and lane l runs the cell with its (c, h) state in registers.
+// Hand-off (MI355X_MICROARCH.md / cdna_hip_programming.md Guideline 16, R2: the data IS the
+// flag): every published value travels in an 8-byte {value, tag} granule, two per 16-byte sc1
+// store; a consumer re-loads (sc1) the granules whose tag is not yet the step's epoch.  No group
+// barrier, no drain.  Slots alternate by step parity: a producer can only reach step i+2 after
+// every workgroup of its group has consumed step i.
+//   XA[par][b][u]     = {h1_i, tag, h1'_i, tag}                  (LSTM1 step i)
+//   XB[par][b][u/2]   = {h2_{i-1}[u], tag, h2_{i-1}[u+1], tag}   (LSTM2 step i-1)
+// both published at iteration i with tag i+1 and consumed at iteration i+1.
+__global__ void __launch_bounds__(kThreads) dec_lstm_fwd_kernel(DecLstmFwdP p) {
   __shared__ __attribute__((aligned(16))) float xs[kUBmax][kX];
-  __shared__ float gs[2][kUBmax][kC];
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int g = blockIdx.x % kG, j = blockIdx.x / kG;
   const int u0 = j * kUW;
-  const int B = p.B, T = p.T, UB = p.UB;
-  unsigned* ctr = p.ctr + 64 * g;
+  const int B = p.B, T = p.T;
 
-  const int c = tid >> 3, ks = tid & 7;
-  const int ucol = u0 + (c >> 2), gcol = c & 3;
-  float4 w1[kI1], w2[kI2];
+  // ---- weights: 8 columns (units u0+2w, u0+2w+1, gates i j f o) x my k rows
+  float w1[4][8], w2[8][8];
+  {
+    const int ucol = u0 + 2 * w;
 #pragma unroll
-  for (int i = 0; i < kI1; ++i) {
-    const int k = 32 * i + 4 * ks;
-    const float* src = p.W1r + ((int64_t)k * kU + ucol) * 4 + gcol;
-    w1[i] = make_float4(src[0], src[4 * kU], src[8 * kU], src[12 * kU]);
-  }
+    for (int q = 0; q < 4; ++q) {
+      const float4* src = reinterpret_cast<const float4*>(p.W1r + ((int64_t)(4 * lane + q) * kU + ucol) * 4);
+      const float4 a = src[0], b = src[1];
+      w1[q][0] = a.x; w1[q][1] = a.y; w1[q][2] = a.z; w1[q][3] = a.w;
+      w1[q][4] = b.x; w1[q][5] = b.y; w1[q][6] = b.z; w1[q][7] = b.w;
+    }
 #pragma unroll
-  for (int i = 0; i < kI2; ++i) {
-    const int k = 32 * i + 4 * ks;
-    const float* src = p.W2 + ((int64_t)k * kU + ucol) * 4 + gcol;
-    w2[i] = make_float4(src[0], src[4 * kU], src[8 * kU], src[12 * kU]);
+    for (int q = 0; q < 8; ++q) {
+      const float4* src = reinterpret_cast<const float4*>(p.W2 + ((int64_t)(8 * lane + q) * kU + ucol) * 4);
+      const float4 a = src[0], b = src[1];
+      w2[q][0] = a.x; w2[q][1] = a.y; w2[q][2] = a.z; w2[q][3] = a.w;
+      w2[q][4] = b.x; w2[q][5] = b.y; w2[q][6] = b.z; w2[q][7] = b.w;
+    }
   }
-
-  // pointwise role
-  const bool pw = tid < 64;
-  const int layer = (tid >> 5) & 1, pub = (tid >> 3) & 3, pul = tid & 7;
-  const bool pw_on = pw && pub < UB;
-  const int pb = g + kG * pub, pu = u0 + pul;
+  bool uvalid[kUBmax];
+#pragma unroll
+  for (int ub = 0; ub < kUBmax; ++ub) uvalid[ub] = g + kG * ub < B;
+  // ---- cell role: output m = lane >> 1 = layer*16 + ub*8 + uu*4 + gate; lanes with gate 0
+  const int m = lane >> 1;
+  const int layer = m >> 4, pub = (m >> 3) & 1, puu = (m >> 2) & 1;
+  const int pu = u0 + 2 * w + puu;
+  const int pb = g + kG * pub;
+  const bool cell = (lane & 7) == 0 && pb < B;
   float cst = 0.f, hst = 0.f;
   float4 bias2 = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (pw_on) {
+  if (cell) {
     const int64_t i0 = (int64_t)pb * kU + pu;
     cst = layer == 0 ? p.C1S[i0] : p.C2S[i0];
     hst = layer == 0 ? p.H1S[i0] : p.H2S[i0];
     if (layer == 1) bias2 = reinterpret_cast<const float4*>(p.b2)[pu];
   }
   const bool masked = p.m1c != nullptr;
-  const auto rH1S = rsrc(p.H1S), rH1R = rsrc(p.H1RAW), rH2S = rsrc(p.H2S);
+  float* XA = p.xch;                                   // [2][B][U] x 4
+  float* XBb = p.xch + (size_t)8 * B * kU;              // [2][B][U/2] x 4
+  const auto rXA = rsrc(XA), rXB = rsrc(XBb);
+  // hand-off granules this thread consumes: XA (ub = tid / 256, u = tid % 256), XB (tid < 256)
+  const int aub = tid >> 8, au = tid & (kU - 1);
+  const int ab = g + kG * aub;
+  const bool a_on = ab < B;
+  const int bub = tid >> 7, bu2 = tid & (kU / 2 - 1);
+  const int bb = g + kG * bub;
+  const bool b_on = tid < kUBmax * (kU / 2) && bb < B;
 
-  // optional segment clocks (thread 0): barrier wait, staging loads, dots, pointwise
+  // cell operands of iteration ii (forward inputs, plain loads), prefetched one iteration
+  // ahead so their HBM latency hides behind the hand-off wait
+  auto load_ops = [&](int ii, float4& xp_, float& mc_, float& mh_) {
+    const int tt = layer == 0 ? ii : ii - 1;
+    xp_ = bias2;
+    mc_ = 1.f - p.zc;
+    mh_ = 1.f - p.zh;
+    if (cell && tt >= 0 && tt < T) {
+      const int64_t bu = ((int64_t)tt * B + pb) * kU + pu;
+      if (layer == 0) xp_ = reinterpret_cast<const float4*>(p.X1)[bu];
+      if (masked) {
+        mc_ = layer == 0 ? p.m1c[bu] : p.m2c[bu];
+        mh_ = layer == 0 ? p.m1h[bu] : p.m2h[bu];
+      }
+    }
+  };
+  float4 xpn;
+  float mcn, mhn;
+  load_ops(0, xpn, mcn, mhn);
+
+  // optional segment clocks (thread 0): hand-off wait, staging, dots, cell + publish
   long long tp[4] = {0, 0, 0, 0};
   long long t0 = wall_clock64();
   auto tick = [&](int seg) {
@@ -116,105 +216,135 @@ __global__ void __launch_bounds__(256) dec_lstm_fwd_kernel(DecLstmFwdP p) {
       t0 = t1;
     }
   };
+
   for (int i = 0; i <= T; ++i) {
     const bool do1 = i < T, do2 = i >= 1;
     const int t = layer == 0 ? i : i - 1;
-    const bool pw_step = pw_on && (layer == 0 ? do1 : do2);
-    // pointwise operands of this step (forward inputs: plain loads, issued first)
-    float4 xp = bias2;
-    float mc = 1.f - p.zc, mh = 1.f - p.zh;
-    if (pw_step) {
-      const int64_t bu = ((int64_t)t * B + pb) * kU + pu;
-      if (layer == 0) xp = reinterpret_cast<const float4*>(p.X1)[bu];
-      if (masked) {
-        mc = layer == 0 ? p.m1c[bu] : p.m2c[bu];
-        mh = layer == 0 ? p.m1h[bu] : p.m2h[bu];
+    const bool cell_step = cell && (layer == 0 ? do1 : do2);
+    const float4 xp = xpn;
+    const float mc = mcn, mh = mhn;
+    // ---- consume: h1_{i-1}, h1'_{i-1} (XA) and h2_{i-2} (XB) of the group's utterances
+    if (i == 0) {
+      xs[aub][au] = a_on ? p.H1S[(int64_t)ab * kU + au] : 0.f;
+    } else {
+      const unsigned ep = (unsigned)i;
+      const int par = i & 1;
+      float4 ga = make_float4(0.f, 0.f, 0.f, 0.f), gb = ga;
+      bool oka = !a_on, okb = !b_on;
+      for (unsigned spins = 0;; ++spins) {
+        if (!oka) {
+          ga = ldc4(rXA, (par * B + ab) * kU + au);
+          oka = tag_of(ga.y) == ep && tag_of(ga.w) == ep;
+        }
+        if (!okb) {
+          gb = ldc4(rXB, (par * B + bb) * (kU / 2) + bu2);
+          okb = tag_of(gb.y) == ep && tag_of(gb.w) == ep;
+        }
+        if (oka && okb) break;
+        if ((spins & 255u) == 255u) {
+          if (__hip_atomic_load(p.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) break;
+          if (spins > (1u << 20)) {   // a producer never published (not co-resident?)
+            __hip_atomic_store(p.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+          }
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      tick(0);
+      xs[aub][au] = ga.x;
+      xs[aub][kU + au] = ga.z;
+      if (tid < kUBmax * (kU / 2)) {
+        xs[bub][2 * kU + 2 * bu2] = gb.x;
+        xs[bub][2 * kU + 2 * bu2 + 1] = gb.z;
       }
     }
-    // stage the group's recurrent/input rows (other workgroups' outputs: sc1 loads)
-    for (int idx = tid; idx < UB * (kX / 4); idx += 256) {
-      const int ub = idx / (kX / 4), q = idx - ub * (kX / 4);
-      const int b = g + kG * ub;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (q < kU / 4) {
-        if (do1) v = ldc4(rH1S, ((i * B + b) * kU) / 4 + q);
-      } else if (do2) {
-        if (q < kU / 2) v = ldc4(rH1R, (((i - 1) * B + b) * kU) / 4 + q - kU / 4);
-        else v = ldc4(rH2S, (((i - 1) * B + b) * kU) / 4 + q - kU / 2);
-      }
-      *reinterpret_cast<float4*>(&xs[ub][4 * q]) = v;
-    }
+    if (i < T) load_ops(i + 1, xpn, mcn, mhn);
     __syncthreads();
     tick(1);
-    float a1[kUBmax], a2[kUBmax];
+    // ---- dots: v[layer*16 + ub*8 + column]
+    float v[32];
 #pragma unroll
     for (int ub = 0; ub < kUBmax; ++ub) {
-      a1[ub] = 0.f;
-      a2[ub] = 0.f;
-      if (ub < UB) {
+      float a1[8], a2[8];
+#pragma unroll
+      for (int cc = 0; cc < 8; ++cc) { a1[cc] = 0.f; a2[cc] = 0.f; }
+      if (uvalid[ub]) {
         const float4* x4 = reinterpret_cast<const float4*>(xs[ub]);
         if (do1) {
+          const float4 x = x4[lane];
+          const float xv[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
-          for (int q = 0; q < kI1; ++q) a1[ub] = dot4(x4[8 * q + ks], w1[q], a1[ub]);
+          for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int cc = 0; cc < 8; ++cc) a1[cc] = fmaf(xv[q], w1[q][cc], a1[cc]);
         }
         if (do2) {
+          const float4 xa = x4[kU / 4 + 2 * lane], xb = x4[kU / 4 + 2 * lane + 1];
+          const float xv[8] = {xa.x, xa.y, xa.z, xa.w, xb.x, xb.y, xb.z, xb.w};
 #pragma unroll
-          for (int q = 0; q < kI2; ++q) a2[ub] = dot4(x4[kU / 4 + 8 * q + ks], w2[q], a2[ub]);
+          for (int q = 0; q < 8; ++q)
+#pragma unroll
+            for (int cc = 0; cc < 8; ++cc) a2[cc] = fmaf(xv[q], w2[q][cc], a2[cc]);
         }
       }
-    }
 #pragma unroll
-    for (int o = 1; o < 8; o <<= 1)
-#pragma unroll
-      for (int ub = 0; ub < kUBmax; ++ub) {
-        a1[ub] += __shfl_xor(a1[ub], o, 64);
-        a2[ub] += __shfl_xor(a2[ub], o, 64);
-      }
-    if (ks == 0) {
-#pragma unroll
-      for (int ub = 0; ub < kUBmax; ++ub) {
-        gs[0][ub][c] = a1[ub];
-        gs[1][ub][c] = a2[ub];
+      for (int cc = 0; cc < 8; ++cc) {
+        v[ub * 8 + cc] = a1[cc];
+        v[16 + ub * 8 + cc] = a2[cc];
       }
     }
-    __syncthreads();
+    transpose_reduce32(v, lane);
+    // gates of (layer, ub, unit): i at lane l, j at l+2, f at l+4, o at l+6 (l % 8 == 0)
+    const float gj_ = dpp_mov<0x102>(v[0]);
+    const float gf_ = dpp_mov<0x104>(v[0]);
+    const float go_ = dpp_mov<0x106>(v[0]);
     tick(2);
-    if (pw_step) {
-      const float* gg = gs[layer][pub] + 4 * pul;
-      const float gi = sigmf(gg[0] + xp.x);
-      const float gj = tanhf(gg[1] + xp.y);
-      const float gf = sigmf(gg[2] + xp.z + 1.0f);   // forget_bias = 1.0
-      const float go = sigmf(gg[3] + xp.w);
+    float hpub = hst;                                   // value published by LSTM2 lanes
+    if (cell_step) {
+      const float gi = sigmf(v[0] + xp.x);
+      const float gj = tanhf(gj_ + xp.y);
+      const float gf = sigmf(gf_ + xp.z + 1.0f);   // forget_bias = 1.0
+      const float go = sigmf(go_ + xp.w);
       const float cn = gf * cst + gi * gj;
       const float hn = go * tanhf(cn);
       const float c2 = mc * cn + (1.f - mc) * cst;
       const float h2 = mh * hn + (1.f - mh) * hst;
       cst = c2;
       hst = h2;
+      hpub = h2;
       const int64_t bu = ((int64_t)t * B + pb) * kU + pu;
       const int64_t bn = bu + (int64_t)B * kU;       // [t + 1]
       if (layer == 0) {
-        stc(rH1R, (int)bu, hn);
-        stc(rH1S, (int)bn, h2);
+        if (i < T) {
+          const float tg = __uint_as_float((unsigned)(i + 1));
+          stc4(rXA, ((((i + 1) & 1) * B + pb) * kU + pu), make_float4(h2, tg, hn, tg));
+        }
+        p.H1RAW[bu] = hn;
+        p.H1S[bn] = h2;
         p.C1S[bn] = c2;
         reinterpret_cast<float4*>(p.G1)[bu] = make_float4(gi, gj, gf, go);
       } else {
         p.H2RAW[bu] = hn;
-        stc(rH2S, (int)bn, h2);
+        p.H2S[bn] = h2;
         p.C2S[bn] = c2;
         reinterpret_cast<float4*>(p.G2)[bu] = make_float4(gi, gj, gf, go);
       }
     }
+    // LSTM2 lanes publish h2 (at i == 0: the initial state) in unit pairs: the uu = 1 partner
+    // sits 8 lanes up
+    const float hpart = dpp_mov<0x108>(hpub);
+    if (cell && layer == 1 && puu == 0 && i < T) {
+      const float tg = __uint_as_float((unsigned)(i + 1));
+      stc4(rXB, ((((i + 1) & 1) * B + pb) * (kU / 2) + (pu >> 1)), make_float4(hpub, tg, hpart, tg));
+    }
     tick(3);
-    if (i < T) group_barrier(ctr, (unsigned)(i + 1) * kGW, p.err);
-    tick(0);
   }
   if (p.prof && tid == 0)
     for (int i = 0; i < 4; ++i) p.prof[blockIdx.x * 4 + i] = tp[i];
 }
 
 struct DecLstmBwdP {
-  int B, T, UB;
+  int B, T;
   float zc, zh;
   const float* W1r;                                   // [U][U][4]
   const float* W2;                                    // [2U][U][4]
@@ -246,63 +376,58 @@ __device__ __forceinline__ float4 lstm_cell_bwd(float4 g4, float cp, float dy, f
   return make_float4(d_i, d_j, d_f, d_o);
 }
 
-// Backward.  Dot role: thread = (own unit ul = tid/32, k-slice ks = tid%32); its weights are the
-// float4 runs 4ks + 128i of three 4U-long rows of unit u: LSTM2's recurrent row W2[U+u],
-// LSTM2's input row W2[u] (LSTM1's output gradient) and LSTM1's recurrent row W1r[u].
-// Pointwise role: lanes ks < 8 of each unit's 32 lanes = (layer, ub); carries in registers.
-__global__ void __launch_bounds__(256) dec_lstm_bwd_kernel(DecLstmBwdP p) {
+// Backward.  Dot role: wave w owns units u = 2w, 2w+1 of the workgroup; lane = k-slice of 16 of
+// the 4U-long gate-gradient rows.  Its weights are those 16 entries of three rows per unit:
+// LSTM2's recurrent row W2[U+u], LSTM2's input row W2[u] (LSTM1's output gradient) and LSTM1's
+// recurrent row W1r[u] (96 floats).  The 16 partial sums per lane (utterance x unit x
+// {r2, y1, r1, pad}) are transpose-reduced across the wave (permlane swaps + DPP), after which
+// lanes 4m..4m+3 hold output m.  Cells: the lane holding r2 runs LSTM2's cell, the lane holding
+// r1 LSTM1's (y1 comes from 4 lanes below by DPP); carries stay in their registers.  Hand-off:
+// the gate-gradient histories themselves (sc1 stores, drained, one group barrier per step, sc1
+// loads; persistent.h).  Cell operands (forward histories, the head's gradient) are prefetched
+// one iteration ahead so their HBM latency hides behind the barrier.
+__global__ void __launch_bounds__(kThreads) dec_lstm_bwd_kernel(DecLstmBwdP p) {
   __shared__ __attribute__((aligned(16))) float dg2s[kUBmax][4 * kU];
   __shared__ __attribute__((aligned(16))) float dg1s[kUBmax][4 * kU];
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int g = blockIdx.x % kG, j = blockIdx.x / kG;
   const int u0 = j * kUW;
-  const int B = p.B, T = p.T, UB = p.UB;
+  const int B = p.B, T = p.T;
   unsigned* ctr = p.ctr + 64 * g;
 
-  const int ul = tid >> 5, ks = tid & 31;
-  const int u = u0 + ul;
-  float4 wa[kIB], wb[kIB], wc[kIB];
-  {
-    const float4* ra = reinterpret_cast<const float4*>(p.W2 + (int64_t)(kU + u) * 4 * kU);
-    const float4* rb = reinterpret_cast<const float4*>(p.W2 + (int64_t)u * 4 * kU);
-    const float4* rc = reinterpret_cast<const float4*>(p.W1r + (int64_t)u * 4 * kU);
+  float4 wa[2][4], wb[2][4], wc[2][4];
 #pragma unroll
-    for (int i = 0; i < kIB; ++i) {
-      wa[i] = ra[ks + 32 * i];
-      wb[i] = rb[ks + 32 * i];
-      wc[i] = rc[ks + 32 * i];
+  for (int uu = 0; uu < 2; ++uu) {
+    const int u = u0 + 2 * w + uu;
+    const float4* ra = reinterpret_cast<const float4*>(p.W2 + (int64_t)(kU + u) * 4 * kU) + 4 * lane;
+    const float4* rb = reinterpret_cast<const float4*>(p.W2 + (int64_t)u * 4 * kU) + 4 * lane;
+    const float4* rc = reinterpret_cast<const float4*>(p.W1r + (int64_t)u * 4 * kU) + 4 * lane;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      wa[uu][q] = ra[q];
+      wb[uu][q] = rb[q];
+      wc[uu][q] = rc[q];
     }
   }
-  // pointwise role: lanes 0..3 -> LSTM2 of utterance ub = ks, lanes 4..7 -> LSTM1 of ub = ks-4
-  const bool pw = ks < 8;
-  const int layer = ks < 4 ? 2 : 1, pub = ks & 3;
-  const bool pw_on = pw && pub < UB;
-  const int pb = g + kG * pub;
+  bool uvalid[kUBmax];
+#pragma unroll
+  for (int ub = 0; ub < kUBmax; ++ub) uvalid[ub] = g + kG * ub < B;
+  // cell role: output m = lane >> 2 = ub*8 + uu*4 + prod (prod 0: r2 -> LSTM2, 2: r1 -> LSTM1)
+  const int m = lane >> 2, prod = m & 3, puu = (m >> 2) & 1, pub = m >> 3;
+  const int pu = u0 + 2 * w + puu, pb = g + kG * pub;
+  const bool cell = (lane & 3) == 0 && (prod == 0 || prod == 2) && pb < B;
+  const int layer = prod == 0 ? 2 : 1;
   float dhc = 0.f, dcc = 0.f;
   const bool masked = p.m1c != nullptr;
   const auto rDG1 = rsrc(p.DG1), rDG2 = rsrc(p.DG2);
 
-  // optional segment clocks (thread 0): barrier wait, staging loads, dots, pointwise
-  long long tp[4] = {0, 0, 0, 0};
-  long long t0 = wall_clock64();
-  auto tick = [&](int seg) {
-    if (p.prof) {
-      const long long t1 = wall_clock64();
-      tp[seg] += t1 - t0;
-      t0 = t1;
-    }
-  };
-  for (int jj = 0; jj <= T; ++jj) {
-    const int t2 = T - 1 - jj, t1 = T - jj;
-    const bool has2 = t2 >= 0, has1 = jj >= 1;
-    const bool stage2 = jj >= 1, stage1 = jj >= 2;   // DG2[t2+1] and DG1[t1+1] exist
-    const int t = layer == 2 ? t2 : t1;
-    const bool pw_step = pw_on && (layer == 2 ? has2 : has1);
-    // pointwise operands (forward histories and the head's gradient: plain loads, issued first)
-    float4 g4 = make_float4(0.f, 0.f, 0.f, 0.f);
-    float cp = 0.f, dyv = 0.f, mc = 1.f - p.zc, mh = 1.f - p.zh;
-    if (pw_step) {
-      const int64_t bu = ((int64_t)t * B + pb) * kU + u;
+  // cell operands of iteration jj (plain loads of read-only inputs)
+  auto load_ops = [&](int jj, float4& g4, float& cp, float& dyv, float& mc, float& mh) {
+    const int t = layer == 2 ? T - 1 - jj : T - jj;
+    g4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    cp = 0.f; dyv = 0.f; mc = 1.f - p.zc; mh = 1.f - p.zh;
+    if (cell && t >= 0 && t < T) {
+      const int64_t bu = ((int64_t)t * B + pb) * kU + pu;
       if (layer == 2) {
         g4 = reinterpret_cast<const float4*>(p.G2)[bu];
         cp = p.C2S[bu];
@@ -316,68 +441,93 @@ __global__ void __launch_bounds__(256) dec_lstm_bwd_kernel(DecLstmBwdP p) {
         mh = layer == 2 ? p.m2h[bu] : p.m1h[bu];
       }
     }
+  };
+  float4 g4n;
+  float cpn, dyn, mcn, mhn;
+  load_ops(0, g4n, cpn, dyn, mcn, mhn);
+
+  // optional segment clocks (thread 0): barrier wait, staging loads, dots, cells + stores
+  long long tp[4] = {0, 0, 0, 0};
+  long long t0 = wall_clock64();
+  auto tick = [&](int seg) {
+    if (p.prof) {
+      const long long t1 = wall_clock64();
+      tp[seg] += t1 - t0;
+      t0 = t1;
+    }
+  };
+
+  for (int jj = 0; jj <= T; ++jj) {
+    const int t2 = T - 1 - jj, t1 = T - jj;
+    const bool has2 = t2 >= 0, has1 = jj >= 1;
+    const bool stage2 = jj >= 1, stage1 = jj >= 2;   // DG2[t2+1] and DG1[t1+1] exist
+    const int t = layer == 2 ? t2 : t1;
+    const bool cell_step = cell && (layer == 2 ? has2 : has1);
+    const float4 g4 = g4n;
+    const float cp = cpn, dyv = dyn, mc = mcn, mh = mhn;
     // stage dgates2_{t2+1} and dgates1_{t1+1} of the group's utterances (sc1 loads)
-    for (int idx = tid; idx < UB * 2 * kU; idx += 256) {
+    for (int idx = tid; idx < kUBmax * 2 * kU; idx += kThreads) {
       const int ub = idx / (2 * kU), q = idx - ub * (2 * kU);
       const int b = g + kG * ub;
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
       if (q < kU) {
-        if (stage2) v = ldc4(rDG2, (((t2 + 1) * B + b) * 4 * kU) / 4 + q);
+        if (stage2 && b < B) v = ldc4(rDG2, (((t2 + 1) * B + b) * 4 * kU) / 4 + q);
         *reinterpret_cast<float4*>(&dg2s[ub][4 * q]) = v;
       } else {
-        if (stage1) v = ldc4(rDG1, (((t1 + 1) * B + b) * 4 * kU) / 4 + q - kU);
+        if (stage1 && b < B) v = ldc4(rDG1, (((t1 + 1) * B + b) * 4 * kU) / 4 + q - kU);
         *reinterpret_cast<float4*>(&dg1s[ub][4 * (q - kU)]) = v;
       }
     }
+    if (jj < T) load_ops(jj + 1, g4n, cpn, dyn, mcn, mhn);   // in flight across the barrier
     __syncthreads();
     tick(1);
-    float r2[kUBmax], y1[kUBmax], r1[kUBmax];
+    float v[16];
 #pragma unroll
     for (int ub = 0; ub < kUBmax; ++ub) {
-      r2[ub] = 0.f;
-      y1[ub] = 0.f;
-      r1[ub] = 0.f;
-      if (ub < UB) {
-        const float4* d2 = reinterpret_cast<const float4*>(dg2s[ub]);
-        const float4* d1 = reinterpret_cast<const float4*>(dg1s[ub]);
+      float r2[2] = {0.f, 0.f}, y1[2] = {0.f, 0.f}, r1[2] = {0.f, 0.f};
+      if (uvalid[ub]) {
+        const float4* d2 = reinterpret_cast<const float4*>(dg2s[ub]) + 4 * lane;
+        const float4* d1 = reinterpret_cast<const float4*>(dg1s[ub]) + 4 * lane;
         if (stage2) {
 #pragma unroll
-          for (int q = 0; q < kIB; ++q) {
-            const float4 x = d2[ks + 32 * q];
-            r2[ub] = dot4(x, wa[q], r2[ub]);
-            y1[ub] = dot4(x, wb[q], y1[ub]);
+          for (int q = 0; q < 4; ++q) {
+            const float4 x = d2[q];
+#pragma unroll
+            for (int uu = 0; uu < 2; ++uu) {
+              r2[uu] = dot4(x, wa[uu][q], r2[uu]);
+              y1[uu] = dot4(x, wb[uu][q], y1[uu]);
+            }
           }
         }
         if (stage1) {
 #pragma unroll
-          for (int q = 0; q < kIB; ++q) r1[ub] = dot4(d1[ks + 32 * q], wc[q], r1[ub]);
+          for (int q = 0; q < 4; ++q) {
+            const float4 x = d1[q];
+#pragma unroll
+            for (int uu = 0; uu < 2; ++uu) r1[uu] = dot4(x, wc[uu][q], r1[uu]);
+          }
         }
+      }
+#pragma unroll
+      for (int uu = 0; uu < 2; ++uu) {
+        v[ub * 8 + uu * 4 + 0] = r2[uu];
+        v[ub * 8 + uu * 4 + 1] = y1[uu];
+        v[ub * 8 + uu * 4 + 2] = r1[uu];
+        v[ub * 8 + uu * 4 + 3] = 0.f;
       }
     }
-#pragma unroll
-    for (int o = 1; o < 32; o <<= 1)
-#pragma unroll
-      for (int ub = 0; ub < kUBmax; ++ub) {
-        r2[ub] += __shfl_xor(r2[ub], o, 64);
-        y1[ub] += __shfl_xor(y1[ub], o, 64);
-        r1[ub] += __shfl_xor(r1[ub], o, 64);
-      }
+    transpose_reduce16(v, lane);
+    const float y1v = dpp_mov<0x114>(v[0]);     // row_shr:4: y1 sits one output (4 lanes) below
     tick(2);
-    if (pw_step) {
-      float rec = 0.f, dy = dyv;
-#pragma unroll
-      for (int ub = 0; ub < kUBmax; ++ub)
-        if (ub == pub) {
-          if (layer == 2) rec = r2[ub];
-          else { rec = r1[ub]; dy = y1[ub]; }
-        }
+    if (cell_step) {
+      const float rec = layer == 2 ? (stage2 ? v[0] : 0.f) : (stage1 ? v[0] : 0.f);
+      const float dy = layer == 2 ? dyv : y1v;
       const float4 dg = lstm_cell_bwd(g4, cp, dy, rec, mc, mh, dhc, dcc);
-      const int64_t bu = ((int64_t)t * B + pb) * kU + u;
+      const int64_t bu = ((int64_t)t * B + pb) * kU + pu;
       stc4(layer == 2 ? rDG2 : rDG1, (int)bu, dg);
     }
     tick(3);
     if (jj < T) group_barrier(ctr, (unsigned)(jj + 1) * kGW, p.err);
-    else __syncthreads();
     tick(0);
   }
   if (p.prof && tid == 0)
@@ -388,7 +538,7 @@ int check_coresident(const void* kernel, const char* name) {
   int dev = 0, cus = 0, per_cu = 0;
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, 0) != hipSuccess) {
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kThreads, 0) != hipSuccess) {
     set_error("%s: device query failed", name);
     return SAT_ERR_HIP;
   }
@@ -397,49 +547,52 @@ int check_coresident(const void* kernel, const char* name) {
   return SAT_OK;
 }
 
-int reset_sync(uint32_t* ctr, int32_t* err, hipStream_t s, const char* name) {
-  if (hipMemsetAsync(ctr, 0, kG * 64 * sizeof(unsigned), s) != hipSuccess ||
-      hipMemsetAsync(err, 0, 2 * sizeof(int), s) != hipSuccess) {
-    set_error("%s: memset failed", name);
-    return SAT_ERR_HIP;
-  }
-  return SAT_OK;
-}
-
 }  // namespace
 }  // namespace sat
 
 using namespace sat;
 
+extern "C" int64_t sat_decoder_lstms_scratch(int32_t B) {
+  return (int64_t)12 * B * kU;       // XA [2][B][U] + XB [2][B][U/2] 16-byte granule pairs
+}
+
+extern "C" int64_t sat_decoder_lstms_bwd_scratch(int32_t B) {
+  (void)B;
+  return kG * 64;                    // group counter words
+}
+
 extern "C" int sat_decoder_lstms_fwd(const SatDecLstmFwd* a, void* stream) {
   const char* nm = "sat_decoder_lstms_fwd";
   SAT_CHECK_ARG(a && a->B > 0 && a->T > 0, "%s: bad sizes", nm);
   SAT_CHECK_ARG(a->U == kU, "%s: compiled for U=256 (the self-attention-tacotron configs)", nm);
-  SAT_CHECK_ARG(a->B % kG == 0 && a->B / kG <= kUBmax, "%s: B in {8,16,24,32}", nm);
+  SAT_CHECK_ARG(a->B <= kG * kUBmax, "%s: B <= 32", nm);
   SAT_CHECK_ARG(a->X1 && a->W1r && a->W2 && a->b2 && a->H1RAW && a->C1S && a->H1S && a->G1 &&
-                a->H2RAW && a->C2S && a->H2S && a->G2 && a->ctr && a->err, "%s: null pointer", nm);
+                a->H2RAW && a->C2S && a->H2S && a->G2 && a->xch && a->err, "%s: null pointer", nm);
   SAT_CHECK_ARG((a->mask1_c == nullptr) == (a->mask1_h == nullptr) &&
                 (a->mask1_c == nullptr) == (a->mask2_c == nullptr) &&
                 (a->mask2_c == nullptr) == (a->mask2_h == nullptr),
                 "%s: the four zoneout masks are all given or all NULL", nm);
   SAT_CHECK_ARG(aligned16(a->X1) && aligned16(a->b2) && aligned16(a->G1) && aligned16(a->G2) &&
-                aligned16(a->H1S) && aligned16(a->H1RAW) && aligned16(a->H2S),
+                aligned16(a->W1r) && aligned16(a->W2) && aligned16(a->xch),
                 "%s: 16-byte aligned operands", nm);
   SAT_CHECK_ARG((int64_t)(a->T + 1) * a->B * 4 * kU < (1ll << 29), "%s: histories too long", nm);
   int rc = check_coresident(reinterpret_cast<const void*>(dec_lstm_fwd_kernel), nm);
   if (rc != SAT_OK) return rc;
   DecLstmFwdP p;
-  p.B = a->B; p.T = a->T; p.UB = a->B / kG; p.zc = a->zc; p.zh = a->zh;
+  p.B = a->B; p.T = a->T; p.zc = a->zc; p.zh = a->zh;
   p.X1 = a->X1; p.W1r = a->W1r; p.W2 = a->W2; p.b2 = a->b2;
   p.m1c = a->mask1_c; p.m1h = a->mask1_h; p.m2c = a->mask2_c; p.m2h = a->mask2_h;
   p.H1RAW = a->H1RAW; p.C1S = a->C1S; p.H1S = a->H1S; p.G1 = a->G1;
   p.H2RAW = a->H2RAW; p.C2S = a->C2S; p.H2S = a->H2S; p.G2 = a->G2;
-  p.ctr = a->ctr; p.err = a->err;
+  p.xch = a->xch; p.err = a->err;
   p.prof = reinterpret_cast<long long*>(a->prof);
   hipStream_t s = as_stream(stream);
-  rc = reset_sync(a->ctr, a->err, s, nm);
-  if (rc != SAT_OK) return rc;
-  hipLaunchKernelGGL(dec_lstm_fwd_kernel, dim3(kG * kGW), dim3(256), 0, s, p);
+  if (hipMemsetAsync(a->xch, 0, sat_decoder_lstms_scratch(a->B) * sizeof(float), s) != hipSuccess ||
+      hipMemsetAsync(a->err, 0, 2 * sizeof(int), s) != hipSuccess) {
+    set_error("%s: memset failed", nm);
+    return SAT_ERR_HIP;
+  }
+  hipLaunchKernelGGL(dec_lstm_fwd_kernel, dim3(kG * kGW), dim3(kThreads), 0, s, p);
   SAT_LAUNCH_CHECK(nm);
   return SAT_OK;
 }
@@ -448,7 +601,7 @@ extern "C" int sat_decoder_lstms_bwd(const SatDecLstmBwd* a, void* stream) {
   const char* nm = "sat_decoder_lstms_bwd";
   SAT_CHECK_ARG(a && a->B > 0 && a->T > 0, "%s: bad sizes", nm);
   SAT_CHECK_ARG(a->U == kU, "%s: compiled for U=256 (the self-attention-tacotron configs)", nm);
-  SAT_CHECK_ARG(a->B % kG == 0 && a->B / kG <= kUBmax, "%s: B in {8,16,24,32}", nm);
+  SAT_CHECK_ARG(a->B <= kG * kUBmax, "%s: B <= 32", nm);
   SAT_CHECK_ARG(a->W1r && a->W2 && a->G1 && a->C1S && a->G2 && a->C2S && a->DH2 && a->DG1 &&
                 a->DG2 && a->ctr && a->err, "%s: null pointer", nm);
   SAT_CHECK_ARG((a->mask1_c == nullptr) == (a->mask1_h == nullptr) &&
@@ -461,16 +614,19 @@ extern "C" int sat_decoder_lstms_bwd(const SatDecLstmBwd* a, void* stream) {
   int rc = check_coresident(reinterpret_cast<const void*>(dec_lstm_bwd_kernel), nm);
   if (rc != SAT_OK) return rc;
   DecLstmBwdP p;
-  p.B = a->B; p.T = a->T; p.UB = a->B / kG; p.zc = a->zc; p.zh = a->zh;
+  p.B = a->B; p.T = a->T; p.zc = a->zc; p.zh = a->zh;
   p.W1r = a->W1r; p.W2 = a->W2; p.G1 = a->G1; p.C1S = a->C1S; p.G2 = a->G2; p.C2S = a->C2S;
   p.DH2 = a->DH2;
   p.m1c = a->mask1_c; p.m1h = a->mask1_h; p.m2c = a->mask2_c; p.m2h = a->mask2_h;
   p.DG1 = a->DG1; p.DG2 = a->DG2; p.ctr = a->ctr; p.err = a->err;
   p.prof = reinterpret_cast<long long*>(a->prof);
   hipStream_t s = as_stream(stream);
-  rc = reset_sync(a->ctr, a->err, s, nm);
-  if (rc != SAT_OK) return rc;
-  hipLaunchKernelGGL(dec_lstm_bwd_kernel, dim3(kG * kGW), dim3(256), 0, s, p);
+  if (hipMemsetAsync(a->ctr, 0, kG * 64 * sizeof(unsigned), s) != hipSuccess ||
+      hipMemsetAsync(a->err, 0, 2 * sizeof(int), s) != hipSuccess) {
+    set_error("%s: memset failed", nm);
+    return SAT_ERR_HIP;
+  }
+  hipLaunchKernelGGL(dec_lstm_bwd_kernel, dim3(kG * kGW), dim3(kThreads), 0, s, p);
   SAT_LAUNCH_CHECK(nm);
   return SAT_OK;
 }

@@ -232,7 +232,7 @@ def decoder_forward(P: Dict[str, torch.Tensor], hp, d: Dims, m1: torch.Tensor, m
             B=B, T=Tp, U=Dd, zc=zc, zh=zh, X1=X1, W1r=W1[A + M1 + M2:], W2=W2,
             b2=P["decoder/lstm2/bias"], mask1_c=m1c, mask1_h=m1h, mask2_c=m2c, mask2_h=m2h,
             H1RAW=L1[0], C1S=L1[1], H1S=L1[2], G1=L1[3], H2RAW=L2[0], C2S=L2[1], H2S=L2[2],
-            G2=L2[3], ctr=scratch.lstm_ctr[0], err=scratch.lstm_err[0])
+            G2=L2[3], xch=scratch.lstm_xch, err=scratch.lstm_err[0])
     elif not pipe.enabled:          # layer by layer
         for t in range(Tp):
             K.lstm_step_fwd(**lstm0_desc(t))

@@ -339,8 +339,10 @@ class DecoderAttentionScratch:
         self.bwd = DecoderAttentionBwdScratch(B, N, device)   # the persistent BPTT's own
 
         # the persistent decoder LSTM stack's own counters / error words (fwd, bwd)
-        self.lstm_ctr = torch.zeros(2, words, dtype=torch.int32, device=device)
-        self.lstm_err = torch.zeros(2, 2, dtype=torch.int32, device=device)
+        self.lstm_xch = torch.zeros(int(_lib.load().sat_decoder_lstms_scratch(B)), device=device)
+        self.lstm_ctr = torch.zeros(int(_lib.load().sat_decoder_lstms_bwd_scratch(B)),
+                                    dtype=torch.int32, device=device)
+        self.lstm_err = torch.zeros(2, 2, dtype=torch.int32, device=device)   # fwd, bwd
 
     def check(self):
         """Host check of the in-kernel barrier timeout flags (synchronises)."""

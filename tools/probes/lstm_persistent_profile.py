@@ -39,10 +39,12 @@ for _ in range(2):
 torch.cuda.synchronize()
 sv["dec"].tensors["attn_scratch"].check()
 Tp = 501
+SEGS = {"decoder_lstms_fwd": ["hand-off wait", "LDS staging", "dots + reduce", "cell + publish"],
+        "decoder_lstms_bwd": ["barrier wait", "staging loads", "dots + reduce", "cells + stores"]}
 for name in ("decoder_lstms_fwd", "decoder_lstms_bwd"):
     pr = PROF[name].view(256, 4).cpu().double() / 100.0   # us
     print(name)
-    for i, n in enumerate(["barrier wait", "staging loads", "dots", "pointwise + stores"]):
+    for i, n in enumerate(SEGS[name]):
         col = pr[:, i]
         print(f"  {n:22s} mean {col.mean() / Tp:6.2f} us/step  min {col.min() / Tp:6.2f}  "
               f"max {col.max() / Tp:6.2f}")

@@ -56,65 +56,6 @@ struct DecLstmFwdP {
   long long* prof;                                    // [256][4] segment clocks (nullable)
 };
 
-__device__ __forceinline__ float dot4(float4 a, float4 b, float acc) {
-  acc = fmaf(a.x, b.x, acc);
-  acc = fmaf(a.y, b.y, acc);
-  acc = fmaf(a.z, b.z, acc);
-  return fmaf(a.w, b.w, acc);
-}
-
-// Transpose-reduce across the 64 lanes of a wave: v[0..N-1] are per-lane partial sums of N
-// different outputs; each halving exchange pairs (v[i], v[i + n/2]) over one lane bit, after
-// which every lane keeps the half its bit selects, summed with its partner's.  All VALU, no
-// LDS: the 32- and 16-lane exchanges are gfx950 v_permlane32_swap / v_permlane16_swap (after
-// the swap x' + y' is already the kept half's sum), the 8/4-lane ones DPP row shifts (lane l
-// adds lane l+H where bit H of l is clear, lane l-H where it is set).  Lane bits left over when
-// the values run out are plain butterflies, so every lane of a 64/N block ends with the total.
-__device__ __forceinline__ float fsum_swap32(float x, float y) {
-  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(y), false, false);
-  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
-}
-__device__ __forceinline__ float fsum_swap16(float x, float y) {
-  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(y), false, false);
-  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
-}
-template <int CTRL>
-__device__ __forceinline__ float dpp_mov(float x) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, true));
-}
-template <int H, int HALF>
-__device__ __forceinline__ void tr_dpp(float* v, int lane) {
-  const bool hi = (lane & H) != 0;
-#pragma unroll
-  for (int i = 0; i < HALF; ++i) {
-    const float sa = v[i] + dpp_mov<0x100 + H>(v[i]);                // row_shl:H (lane l+H)
-    const float sb = v[i + HALF] + dpp_mov<0x110 + H>(v[i + HALF]);  // row_shr:H (lane l-H)
-    v[i] = hi ? sb : sa;
-  }
-}
-// 32 outputs: lanes 2m, 2m+1 hold output m
-__device__ __forceinline__ void transpose_reduce32(float* v, int lane) {
-#pragma unroll
-  for (int i = 0; i < 16; ++i) v[i] = fsum_swap32(v[i], v[i + 16]);
-#pragma unroll
-  for (int i = 0; i < 8; ++i) v[i] = fsum_swap16(v[i], v[i + 8]);
-  tr_dpp<8, 4>(v, lane);
-  tr_dpp<4, 2>(v, lane);
-  tr_dpp<2, 1>(v, lane);
-  v[0] += dpp_mov<0xB1>(v[0]);   // quad_perm [1,0,3,2]: lane l ^ 1
-}
-// 16 outputs: lanes 4m..4m+3 hold output m
-__device__ __forceinline__ void transpose_reduce16(float* v, int lane) {
-#pragma unroll
-  for (int i = 0; i < 8; ++i) v[i] = fsum_swap32(v[i], v[i + 8]);
-#pragma unroll
-  for (int i = 0; i < 4; ++i) v[i] = fsum_swap16(v[i], v[i + 4]);
-  tr_dpp<8, 2>(v, lane);
-  tr_dpp<4, 1>(v, lane);
-  v[0] += dpp_mov<0xB1>(v[0]);   // lane l ^ 1
-  v[0] += dpp_mov<0x4E>(v[0]);   // quad_perm [2,3,0,1]: lane l ^ 2
-}
-
 __device__ __forceinline__ unsigned tag_of(float x) { return __float_as_uint(x); }
 
 // Forward.  Dot role: wave w owns units 2w, 2w+1 of the workgroup in both layers (8 gate

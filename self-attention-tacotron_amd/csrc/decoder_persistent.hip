@@ -8,28 +8,30 @@
 // kernel, combine), each paying a ~1.5 us boundary plus a cold reload of its operands (the L2
 // does not survive a boundary): K1/V1 (14 MB) and the LSTM weights (2.2 MB) stream from
 // MALL/HBM 500 times.  Here each (utterance, 32-position tile) K1/V1/K2/V2 slice (68 KB) lives
-// in one workgroup's LDS and each workgroup's 32 LSTM gate columns (68 floats per lane) and
-// query rows live in registers for the whole decode; a step costs two in-kernel group barriers
-// (~1.3-1.8 us each, measured by tools/probes/handoff_probe) plus on-chip arithmetic.
+// in one workgroup's LDS and each workgroup's 32 LSTM gate columns (72 floats per lane) and
+// query rows (32 floats per lane) live in registers for the whole decode.
 //
 // Layout: 8 groups x 32 workgroups (256, one per CU).  Group g = blockIdx % 8 owns utterances
 // b = g + 8*ub (ub < B/8 <= 4) -- workgroups b, b+8, ... share an XCD under the observed
-// round-robin placement, so a group's hand-offs stay in one L2 (speed only; correctness never
-// depends on placement).  Workgroup j = blockIdx / 8 of the group owns LSTM units [8j, 8j+8)
-// and, if j < UB*ntiles, tile (ub = j / ntiles, tile = j % ntiles).  Per step t:
-//   A: combine step t-1's tile partials (every workgroup, redundantly: the context is the LSTM
-//      input); tile workgroups normalise step t-1 on their window (s_{t-1}, alpha_{t-1} from the
-//      raw energies and the combine statistics); LSTM0 step t for the 8 units x UB utterances;
-//      the units' query contribution q_part[j] = h0'_t[8 units] [Wq1 | Wq2][8 units, :]
-//   C: tile workgroups sum the 32 query partials of their utterance, location features,
-//      energies from LDS K1/K2, tile statistics and unnormalised partial contexts
-// Every cross-workgroup operand of a phase is loaded in one batch at the phase start.
-// Hand-offs (guide: MI355X_MICROARCH.md inter-workgroup visibility, "sc1 loads in place of the
-// acquire" table row 1): producers store with sc1 and drain (s_waitcnt vmcnt(0)) before the
-// workgroup barrier; one lane arrives on the group counter (agent-scope atomic) and polls it
-// with sc1 loads; every load of another workgroup's bytes is an sc1 load.  Every spin is
-// bounded: a timeout raises err[0] and all later barriers fall through, so the grid always
-// drains.  All histories the backward needs are written exactly as the launch-based path.
+// round-robin placement (speed only; correctness never depends on placement).  Workgroup
+// j = blockIdx / 8 of the group owns LSTM units [8j, 8j+8) and, if j < UB*ntiles, tile
+// (ub = j / ntiles, tile = j % ntiles).  Per step t:
+//   A (every workgroup): combine step t-1's tile partial records (redundantly: the context is
+//      the LSTM input); LSTM0 step t for its 8 units x UB utterances; publish its units' h_t
+//      and its query contribution q_part[j] = h0'_t[8 units] [Wq1 | Wq2][8 units, :];
+//      tile workgroups then normalise step t-1 on their window (s_{t-1}, alpha_{t-1}).
+//   C (tile workgroups): sum the 32 query partials of their utterance, location features,
+//      energies from LDS K1/K2, tile statistics and the unnormalised partial context.
+// Hand-offs (MI355X_MICROARCH.md price list "handoff-1to1": the data IS the flag): no group
+// barrier, no drain, no counter.  Bulk payloads (partial records, query partials, h) carry the
+// step parity in every float's mantissa LSB (persistent.h lsb_tag); energy and alignment halos
+// travel as 8-byte {value, step+1} granules.  Producers store sc1, consumers load sc1 and
+// re-load only the words whose tag is stale.  Slots alternate by step parity; a producer can
+// reach step t+2 only after every consumer of its step-t slot has consumed it (each step needs
+// every workgroup's query partial and every tile's record), so slots are never overwritten
+// early.  Every spin is bounded: a timeout raises err[0] and all later polls give up, so the
+// grid always drains.  All histories the backward needs are written exactly as the launch-based
+// path writes them (the tagged values where a tagged value was consumed).
 #include "sat_common.h"
 #include "persistent.h"
 
@@ -42,11 +44,17 @@ constexpr int kPN = 32;        // tile positions
 constexpr int kUBmax = 4;      // utterances per group
 constexpr int kU = 256, kM1 = 256, kM2 = 32, kD1 = 224, kD2 = 32, kF = 5, kKW = 10;
 constexpr int kK0 = kM1 + kM2 + kU;            // attention-RNN recurrent input [c1 | c2 | h0]
-constexpr int kPST = 8 + kM1 + kM2;            // partial record stride (floats, 16-B multiple)
-constexpr int kW0 = kK0 / 8;                   // recurrent weights per lane (k-slice of 8)
+constexpr int kKP = 576;                       // kK0 padded to 9 x 64 (zero tail)
+constexpr int kPST = 8 + kM1 + kM2;            // partial record: 8 statistics + 288 context
+constexpr int kP4 = kPST / 4;                  // float4 per record (74)
 constexpr int kQ = kD1 + kD2;                  // query width (= U here)
 constexpr int kUW = kU / kGW;                  // units per workgroup (8)
-static_assert(kK0 % 8 == 0 && kU % kGW == 0 && kQ == 256 && kPST % 4 == 0, "layout");
+constexpr int kPadL = (kKW - 1) / 2;           // 4: SAME padding of the location convolution
+constexpr int kPadR = kKW - 1 - kPadL;         // 5
+constexpr int kEH = 16;                        // energy-halo granules per tile record (9 used)
+constexpr int kAH = 2;                         // alignment-halo granules per tile record
+static_assert(kK0 <= kKP && kKP == 9 * 64 && kU % kGW == 0 && kQ == 256 && kPST % 4 == 0 &&
+              kD1 % 4 == 0, "layout");
 
 struct DecAttnP {
   int B, N, T, ntiles, UB;
@@ -62,30 +70,26 @@ struct DecAttnP {
   float* REC0; float* C0; float* H0RAW; float* G0; float* Q;
   float* S1; float* AL1; float* S2; float* ST; float* LOC;
   float* ZH;                                         // [T][B][N][D1+D2] energy tanh (nullable)
-  float* E;                                          // [2][B][2][N] raw energies
-  float* PART;                                       // [2][B][ntiles][kPST]
-  float* QP;                                         // [2][B][kGW][kQ] query partials
-  unsigned* ctr;                                     // [kG * 64], zero at launch
+  float* HX;                                         // [2][B][U]            tagged h
+  float* EH;                                         // [2][B][ntiles][kEH]  granules
+  float* AH;                                         // [2][B][ntiles][kAH]  granules
+  float* PART;                                       // [2][B][ntiles][kPST] tagged
+  float* QP;                                         // [2][B][kGW][kQ]      tagged
   int* err;                                          // [2]
   long long* prof;                                   // [256][8] segment clocks (nullable)
 };
 
 __device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + __expf(-x)); }
+__device__ __forceinline__ bool any_lane(bool v) { return __builtin_amdgcn_ballot_w64(v) != 0; }
 
-// Per step t, two phases separated by group barriers:
-//   A: every workgroup combines step t-1's tile partials (the context is the LSTM input), tile
-//      workgroups normalise step t-1 on their window, then the LSTM0 step for the workgroup's
-//      8 units and their query contribution q_part[j] = h0'[8 units] Wq[8 units, :];
-//   C: tile workgroups sum the 32 query partials of their utterance and run the tile.
-// Every cross-workgroup operand of a phase is loaded in one batch at the phase start.
 __global__ void __launch_bounds__(256) dec_attn_fwd_kernel(DecAttnP p) {
   __shared__ __attribute__((aligned(16))) float k1s[kPN][kD1];
   __shared__ __attribute__((aligned(16))) float v1s[kPN][kM1];
   __shared__ __attribute__((aligned(16))) float k2s[kPN][kD2];
   __shared__ __attribute__((aligned(16))) float v2s[kPN][kM2];
-  __shared__ __attribute__((aligned(16))) float rin[kUBmax][kK0];
-  __shared__ float gsh[kUBmax][32];
-  __shared__ float hown[kUBmax][kUW];
+  __shared__ __attribute__((aligned(16))) float rin[kUBmax][kKP];
+  __shared__ __attribute__((aligned(16))) float hown[kUBmax][kUW];   // raw outputs (query input)
+  __shared__ __attribute__((aligned(16))) float hst[kUBmax][kUW];    // zoneout states (tagged)
   __shared__ float stat[kUBmax][8];
   __shared__ __attribute__((aligned(16))) float4 qred[4][64];
   // tile phase
@@ -97,7 +101,8 @@ __global__ void __launch_bounds__(256) dec_attn_fwd_kernel(DecAttnP p) {
   __shared__ float cw[kKW * kF + kF];
   __shared__ float fs[kPN][kF];
   __shared__ float sp[kPN + kKW], ap[kPN + 1];
-  __shared__ float ew[kPN + kKW], e2w[kPN], aw[kPN + 2];
+  __shared__ float ew[kPN + kKW], halo[kPadL + kPadR + kAH];
+  __shared__ float aown[kPN];                        // alpha_{t-2} on the own positions
   __shared__ float e1s[kPN], e2s[kPN], w1s[kPN], w2s[kPN];
   __shared__ __attribute__((aligned(16))) float4 cred[4][64];
   __shared__ __attribute__((aligned(16))) float4 c2red[kPN][8];
@@ -106,33 +111,47 @@ __global__ void __launch_bounds__(256) dec_attn_fwd_kernel(DecAttnP p) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = blockIdx.x % kG, j = blockIdx.x / kG;
   const int B = p.B, N = p.N, T = p.T, UB = p.UB, ntiles = p.ntiles;
-  unsigned* ctr = p.ctr + 64 * g;
-  unsigned phase = 0;
   const bool tile_wg = j < UB * ntiles;
   const int tub = tile_wg ? j / ntiles : 0, tile = tile_wg ? j % ntiles : 0;
   const int tb = g + kG * tub;                      // utterance of this workgroup's tile
   const int n0 = tile * kPN, nt = tile_wg ? min(kPN, N - n0) : 0;
   const int64_t trb = (int64_t)tb * N;
-  const int padl = (kKW - 1) / 2;
   const int span = nt + kKW - 1;
+  const bool has_left = tile_wg && tile > 0, has_right = tile_wg && tile + 1 < ntiles;
   const float u = p.u;
-  const auto rREC = rsrc(p.REC0), rAL = rsrc(p.AL1), rE = rsrc(p.E), rPT = rsrc(p.PART);
-  const auto rQP = rsrc(p.QP);
+  const auto rPT = rsrc(p.PART), rQP = rsrc(p.QP), rHX = rsrc(p.HX);
+  const auto rEH = rsrc(p.EH), rAH = rsrc(p.AH);
 
   // ---------------- prologue: resident operands
-  // LSTM: lane (column c = tid >> 3, k-block ks = tid & 7) holds W0r[68 ks + kk][32j + c], so
-  // its recurrent inputs are 17 contiguous float4 of rin (conflict-free: 68 % 32 = 4 banks apart)
-  const int cc = tid >> 3, ks = tid & 7;
-  float w0[kW0];
+  // LSTM (wave-transposed dot): wave w owns local gate columns 8w..8w+7 (units 8j+2w, +1, gates
+  // i j f o), lane owns input rows k = lane + 64 i (i < 9; rows >= 544 are zero)
+  float w0[9][8];
 #pragma unroll
-  for (int kk = 0; kk < kW0; ++kk) w0[kk] = p.W0r[(int64_t)(kW0 * ks + kk) * (4 * kU) + 32 * j + cc];
-  // query partial: lane = output column, holds Wq[8j + uu][col] for its 8 units
-  float wq[kUW];
+  for (int i = 0; i < 9; ++i) {
+    const int k = lane + 64 * i;
+    if (k < kK0) {
+      const float4* src = reinterpret_cast<const float4*>(p.W0r + (int64_t)k * (4 * kU) + 32 * j + 8 * wave);
+      const float4 a = src[0], b = src[1];
+      w0[i][0] = a.x; w0[i][1] = a.y; w0[i][2] = a.z; w0[i][3] = a.w;
+      w0[i][4] = b.x; w0[i][5] = b.y; w0[i][6] = b.z; w0[i][7] = b.w;
+    } else {
 #pragma unroll
-  for (int uu = 0; uu < kUW; ++uu) {
-    const int k = kUW * j + uu;
-    wq[uu] = tid < kD1 ? p.Wq1[k * kD1 + tid] : p.Wq2[k * kD2 + (tid - kD1)];
+      for (int c = 0; c < 8; ++c) w0[i][c] = 0.f;
+    }
   }
+  // query partial: wave = utterance, lane = 4 output columns, 8 unit rows
+  float4 wq[kUW];
+  {
+    const int c = 4 * lane;
+#pragma unroll
+    for (int uu = 0; uu < kUW; ++uu) {
+      const int k = kUW * j + uu;
+      wq[uu] = c < kD1 ? *reinterpret_cast<const float4*>(p.Wq1 + k * kD1 + c)
+                       : *reinterpret_cast<const float4*>(p.Wq2 + k * kD2 + (c - kD1));
+    }
+  }
+  for (int i = tid; i < kUBmax * (kKP - kK0); i += 256)
+    rin[i / (kKP - kK0)][kK0 + i % (kKP - kK0)] = 0.f;
   if (tile_wg) {
     for (int i = tid; i < kPN * kD1 / 4; i += 256) {
       const int r = i / (kD1 / 4), c4 = i - r * (kD1 / 4);
@@ -160,11 +179,29 @@ __global__ void __launch_bounds__(256) dec_attn_fwd_kernel(DecAttnP p) {
     if (tid < kKW * kF) cw[tid] = p.convW[tid];
     if (tid < kF) cw[kKW * kF + tid] = p.convb[tid];
   }
-  float c_own = 0.f, h_own = 0.f;   // lane tid < UB*8: (ub = tid >> 3, unit 8j + (tid & 7))
+  // cell role: after the transpose-reduce the 4 gate sums of (utterance cub, unit cu) sit in
+  // lanes L, L+2, L+4, L+6 with L = 16 cub + 8 cu; lane L runs the cell, its state in registers
+  const int cub = lane >> 4, cu = (lane >> 3) & 1;
+  const int cunit = kUW * j + 2 * wave + cu, cb = g + kG * cub;
+  const bool cell = (lane & 7) == 0 && cub < UB;
+  float c_own = 0.f, h_own = 0.f;
+  const bool masked = p.mask_c != nullptr;
+  auto load_ops = [&](int tt, float4& xp_, float& mc_, float& mh_) {
+    xp_ = make_float4(0.f, 0.f, 0.f, 0.f);
+    mc_ = 1.f - p.zc;
+    mh_ = 1.f - p.zh;
+    if (cell && tt < T) {
+      const int64_t bu = ((int64_t)tt * B + cb) * kU + cunit;
+      xp_ = reinterpret_cast<const float4*>(p.X0)[bu];
+      if (masked) { mc_ = p.mask_c[bu]; mh_ = p.mask_h[bu]; }
+    }
+  };
+  float4 xpn;
+  float mcn, mhn;
+  load_ops(0, xpn, mcn, mhn);
   const int len = tile_wg ? (int)p.lengths[tb] : 0;
   __syncthreads();
 
-  // ---- phase A of step t (combining step s = t - 1); t == T is the epilogue (no LSTM)
   long long tp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   long long t0 = wall_clock64();
   auto tick = [&](int seg) {
@@ -174,63 +211,65 @@ __global__ void __launch_bounds__(256) dec_attn_fwd_kernel(DecAttnP p) {
       t0 = t1;
     }
   };
-  auto phase_a = [&](int t) {
+  bool gave_up = false;   // a poll timed out (err raised): stop waiting, drain the grid
+
+  for (int t = 0; t <= T; ++t) {
     const int s = t - 1;
-    // ======== batch of loads: partials of step s (wave ub), h0_{t-1}, tile windows, X0/masks
-    float4 ph[2][8];
-    float hd[5];
-    const int pbase = ((s & 1) * B + g + kG * wave) * ntiles * kPST;   // floats
+    // ======== A1: step s's partial records (wave = utterance) and h_s; halo granules
+    v2u hg = {0u, 0u};      // tile workgroups, wave 0 lanes < 11: energy / alignment halo
+    if (t > 0 && tile_wg && wave == 0) {
+      const int sl = s & 1;
+      if (lane < kPadL && has_left)
+        hg = ldg(rEH, ((sl * B + tb) * ntiles + tile - 1) * kEH + kPadR + lane);
+      else if (lane >= kPadL && lane < kPadL + kPadR && has_right)
+        hg = ldg(rEH, ((sl * B + tb) * ntiles + tile + 1) * kEH + lane - kPadL);
+      else if (lane >= kPadL + kPadR && lane < kPadL + kPadR + kAH && has_left && t >= 2)
+        hg = ldg(rAH, ((sl * B + tb) * ntiles + tile - 1) * kAH + lane - kPadL - kPadR);
+    }
     if (t > 0 && wave < UB) {
+      const unsigned want = lsb_tag(s);
+      const int b = g + kG * wave;
+      const int pb4 = ((s & 1) * B + b) * ntiles * kP4;
+      const int hx4 = (((s & 1) * B + b) * kU) / 4 + lane;
+      const bool need_h = t < T;
+      float4 ph[2][8], hs[2], h4;
+      unsigned bad = 0xFFFFFFFFu;
+      for (unsigned spins = 0;; ++spins) {
 #pragma unroll
-      for (int jt = 0; jt < 8; ++jt) {
-        const int jc = min(jt, ntiles - 1);
+        for (int jt = 0; jt < 8; ++jt)
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int c4 = min(lane + 64 * h, (kM1 + kM2) / 4 - 1);
-          ph[h][jt] = ldc4(rPT, (pbase + jc * kPST + 8) / 4 + c4);
+          for (int h = 0; h < 2; ++h)
+            if (jt < ntiles && lane + 64 * h < (kM1 + kM2) / 4 && ((bad >> (h * 8 + jt)) & 1))
+              ph[h][jt] = ldc4(rPT, pb4 + jt * kP4 + 2 + lane + 64 * h);
+        if (lane < ntiles) {
+          if ((bad >> 16) & 1) hs[0] = ldc4(rPT, pb4 + lane * kP4);
+          if ((bad >> 17) & 1) hs[1] = ldc4(rPT, pb4 + lane * kP4 + 1);
         }
-      }
-      const int jl = min(lane, ntiles - 1);
+        if (need_h && ((bad >> 18) & 1)) h4 = ldc4(rHX, hx4);
+        bad = 0;
 #pragma unroll
-      for (int q = 0; q < 5; ++q) hd[q] = ldc(rPT, pbase + jl * kPST + q);
-    }
-    float4 h4 = make_float4(0.f, 0.f, 0.f, 0.f);
-    const int hub = tid >> 6, hk = 4 * (tid & 63);
-    if (t > 0 && t < p.T + 1 && hub < UB)
-      h4 = ldc4(rREC, ((t * B + g + kG * hub) * kK0 + kM1 + kM2 + hk) / 4);
-    float ewv = 0.f, e2v = 0.f, awv = 0.f;
-    if (tile_wg && t > 0) {
-      const int eb = (((s & 1) * B + tb) * 2) * N;
-      if (tid < span) {
-        const int n = n0 - padl + tid;
-        ewv = (n >= 0 && n < N) ? ldc(rE, eb + n) : -INFINITY;
-      } else if (tid >= 64 && tid < 64 + nt) {
-        e2v = ldc(rE, eb + N + n0 + tid - 64);
-      } else if (tid >= 128 && tid < 128 + nt + 2) {
-        const int n = n0 - 2 + tid - 128;                       // alpha_{t-2} window
-        awv = n >= 0 ? ldc(rAL, ((t - 1) * B + tb) * N + n) : 0.f;
+        for (int jt = 0; jt < 8; ++jt)
+#pragma unroll
+          for (int h = 0; h < 2; ++h)
+            if (jt < ntiles && lane + 64 * h < (kM1 + kM2) / 4 && !tag_ok4(ph[h][jt], want))
+              bad |= 1u << (h * 8 + jt);
+        if (lane < ntiles) {
+          if (!tag_ok4(hs[0], want)) bad |= 1u << 16;
+          if (!tag_ok4(hs[1], want)) bad |= 1u << 17;
+        }
+        if (need_h && !tag_ok4(h4, want)) bad |= 1u << 18;
+        if (!any_lane(bad != 0) || gave_up) break;
+        if (poll_give_up(spins, p.err)) { gave_up = true; break; }
+        __builtin_amdgcn_s_sleep(1);
       }
-    }
-    float4 xp = make_float4(0.f, 0.f, 0.f, 0.f);
-    float mcv = 1.f - p.zc, mhv = 1.f - p.zh;
-    const int pub = tid >> 3, puu = tid & 7, punit = kUW * j + puu, pb = g + kG * pub;
-    const bool pw = t < T && tid < UB * 8;
-    if (pw) {
-      xp = reinterpret_cast<const float4*>(p.X0 + ((int64_t)t * B + pb) * 4 * kU)[punit];
-      if (p.mask_c) {
-        mcv = p.mask_c[((int64_t)t * B + pb) * kU + punit];
-        mhv = p.mask_h[((int64_t)t * B + pb) * kU + punit];
-      }
-    }
-    // ======== combine step s (one wave per utterance)
-    if (t > 0 && wave < UB) {
-      const int ub = wave, b = g + kG * ub;
+      tick(0);
+      // ---- combine step s (wave = utterance)
       const bool on = lane < ntiles;
-      const float hm1 = on ? hd[0] : -INFINITY, hz1 = on ? hd[1] : 0.f, ha1 = on ? hd[2] : 0.f;
-      const float hm2 = on ? hd[3] : -INFINITY, hz2 = on ? hd[4] : 0.f;
+      const float hm1 = on ? hs[0].x : -INFINITY, hz1 = on ? hs[0].y : 0.f, ha1 = on ? hs[0].z : 0.f;
+      const float hm2 = on ? hs[0].w : -INFINITY, hz2 = on ? hs[1].x : 0.f;
       const float M1 = wave_max(hm1), M2 = wave_max(hm2);
-      const float s1 = (hm1 == -INFINITY) ? 0.f : __expf(hm1 - M1);
-      const float s2 = (hm2 == -INFINITY) ? 0.f : __expf(hm2 - M2);
+      const float s1 = on ? __expf(hm1 - M1) : 0.f;   // an empty tile's max is -FLT_MAX: 0
+      const float s2 = on ? __expf(hm2 - M2) : 0.f;
       const float Z1 = wave_sum(hz1 * s1), A1 = wave_sum(ha1 * s1), Z2 = wave_sum(hz2 * s2);
       const float inv1 = 1.f / A1, inv2 = 1.f / Z2;
 #pragma unroll
@@ -241,148 +280,203 @@ __global__ void __launch_bounds__(256) dec_attn_fwd_kernel(DecAttnP p) {
         float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
         for (int jt = 0; jt < 8; ++jt) {          // lane jt's scale, broadcast by readlane
+          if (jt >= ntiles) break;
           const float w1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(s1), jt));
           const float w2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(s2), jt));
-          const float w = jt < ntiles ? (first ? w1 : w2) : 0.f;
+          const float w = first ? w1 : w2;
           acc.x = fmaf(ph[h][jt].x, w, acc.x); acc.y = fmaf(ph[h][jt].y, w, acc.y);
           acc.z = fmaf(ph[h][jt].z, w, acc.z); acc.w = fmaf(ph[h][jt].w, w, acc.w);
         }
         const float inv = first ? inv1 : inv2;
         acc.x *= inv; acc.y *= inv; acc.z *= inv; acc.w *= inv;
-        reinterpret_cast<float4*>(&rin[ub][0])[c4] = acc;
+        reinterpret_cast<float4*>(&rin[wave][0])[c4] = acc;
         if (j == 0) reinterpret_cast<float4*>(p.REC0 + ((int64_t)t * B + b) * kK0)[c4] = acc;
       }
+      if (need_h) reinterpret_cast<float4*>(&rin[wave][kM1 + kM2])[lane] = h4;
       if (lane == 0) {
-        stat[ub][0] = M1; stat[ub][1] = Z1; stat[ub][2] = A1; stat[ub][3] = M2; stat[ub][4] = Z2;
+        stat[wave][0] = M1; stat[wave][1] = Z1; stat[wave][2] = A1; stat[wave][3] = M2;
+        stat[wave][4] = Z2;
         if (j == 0) {
           float* st = p.ST + ((int64_t)s * B + b) * 4;
           st[0] = M1; st[1] = Z1; st[2] = A1 / Z1; st[3] = Z2;
         }
       }
     } else if (t == 0 && wave < UB) {
-      for (int d = lane; d < kM1 + kM2; d += 64) rin[wave][d] = 0.f;
-    }
-    if (hub < UB) *reinterpret_cast<float4*>(&rin[hub][kM1 + kM2 + hk]) = h4;
-    tick(4);
-    if (tile_wg) {
-      if (tid < span) ew[tid] = ewv;
-      else if (tid >= 64 && tid < 64 + nt) e2w[tid - 64] = e2v;
-      else if (tid >= 128 && tid < 128 + nt + 2) aw[tid - 128] = awv;
+      for (int d = lane; d < kK0; d += 64) rin[wave][d] = 0.f;   // zero initial state
+    } else {
+      tick(0);
     }
     __syncthreads();
-    // ======== tile workgroups: s_{t-1} on the conv window, alpha_{t-1} on [n0-1, n0+nt)
+    tick(1);
+
+    if (t < T) {
+      // ======== A2: LSTM0 step t, 8 gate columns x UB utterances per wave
+      float v[32];
+#pragma unroll
+      for (int q = 0; q < 32; ++q) v[q] = 0.f;
+#pragma unroll
+      for (int i = 0; i < 9; ++i) {
+        float x[kUBmax];
+#pragma unroll
+        for (int ub = 0; ub < kUBmax; ++ub) x[ub] = ub < UB ? rin[ub][lane + 64 * i] : 0.f;
+#pragma unroll
+        for (int ub = 0; ub < kUBmax; ++ub)
+#pragma unroll
+          for (int c = 0; c < 8; ++c) v[ub * 8 + c] = fmaf(x[ub], w0[i][c], v[ub * 8 + c]);
+      }
+      transpose_reduce32(v, lane);
+      const float gj_ = dpp_mov<0x102>(v[0]);
+      const float gf_ = dpp_mov<0x104>(v[0]);
+      const float go_ = dpp_mov<0x106>(v[0]);
+      tick(2);
+      const float4 xp = xpn;
+      const float mc = mcn, mh = mhn;
+      const unsigned bit = lsb_tag(t);
+      if (cell) {
+        const float gi = sigm(v[0] + xp.x);
+        const float gj = tanhf(gj_ + xp.y);
+        const float gf = sigm(gf_ + xp.z + 1.0f);   // forget_bias = 1.0
+        const float go = sigm(go_ + xp.w);
+        const float cn = gf * c_own + gi * gj;
+        const float hn = go * tanhf(cn);
+        const float c2 = mc * cn + (1.f - mc) * c_own;
+        const float h2 = tagf(mh * hn + (1.f - mh) * h_own, bit);   // the value every reader sees
+        c_own = c2; h_own = h2;
+        hown[cub][2 * wave + cu] = hn;
+        hst[cub][2 * wave + cu] = h2;
+        const int64_t tbu = ((int64_t)t * B + cb) * kU + cunit;
+        p.C0[((int64_t)(t + 1) * B + cb) * kU + cunit] = c2;
+        p.REC0[((int64_t)(t + 1) * B + cb) * kK0 + kM1 + kM2 + cunit] = h2;
+        p.H0RAW[tbu] = hn;
+        reinterpret_cast<float4*>(p.G0)[tbu] = make_float4(gi, gj, gf, go);
+      }
+      load_ops(t + 1, xpn, mcn, mhn);
+      __syncthreads();
+      // ======== publish h_t (own units' zoneout states) and the query contribution of the own
+      //          units' raw outputs
+      if (tid < 2 * UB) {
+        const int ub = tid >> 1, hf = tid & 1;
+        stc4(rHX, (((t & 1) * B + g + kG * ub) * kU + kUW * j) / 4 + hf,
+             *reinterpret_cast<const float4*>(&hst[ub][4 * hf]));
+      }
+      if (wave < UB) {
+        float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int uu = 0; uu < kUW; ++uu) {
+          const float h = hown[wave][uu];
+          a.x = fmaf(h, wq[uu].x, a.x); a.y = fmaf(h, wq[uu].y, a.y);
+          a.z = fmaf(h, wq[uu].z, a.z); a.w = fmaf(h, wq[uu].w, a.w);
+        }
+        stc4(rQP, ((((t & 1) * B + g + kG * wave) * kGW + j) * kQ) / 4 + lane, tagf4(a, bit));
+      }
+      tick(3);
+    }
+
+    // ======== A3 (tile workgroups): s_{t-1} on the conv window, alpha_{t-1} on [n0-1, n0+nt)
     if (tile_wg) {
       if (t == 0) {
         if (tid < span) {
-          const int n = n0 - padl + tid;
+          const int n = n0 - kPadL + tid;
           sp[tid] = (n >= 0 && n < N) ? p.S1[trb + n] : 0.f;          // host rows
         }
         if (tid <= nt) ap[tid] = (n0 - 1 + tid >= 0) ? p.AL1[trb + n0 - 1 + tid] : 0.f;
+        if (tid < nt) aown[tid] = p.AL1[trb + n0 + tid];
+        if (tid < kAH) halo[kPadL + kPadR + tid] = n0 - kAH + tid >= 0 ? p.AL1[trb + n0 - kAH + tid] : 0.f;
       } else {
+        if (wave == 0 && lane < kPadL + kPadR + kAH) {   // halo granules: check, re-poll stale
+          const int sl = s & 1;
+          const bool is_el = lane < kPadL, is_er = lane >= kPadL && lane < kPadL + kPadR;
+          const bool src = is_el ? has_left : is_er ? has_right : (has_left && t >= 2);
+          const unsigned want = (unsigned)t;   // step t-1's granules carry tag t
+          bool ok = !src || hg[1] == want;
+          for (unsigned spins = 0; !ok && !gave_up; ++spins) {
+            if (poll_give_up(spins, p.err)) { gave_up = true; break; }
+            __builtin_amdgcn_s_sleep(1);
+            if (is_el) hg = ldg(rEH, ((sl * B + tb) * ntiles + tile - 1) * kEH + kPadR + lane);
+            else if (is_er) hg = ldg(rEH, ((sl * B + tb) * ntiles + tile + 1) * kEH + lane - kPadL);
+            else hg = ldg(rAH, ((sl * B + tb) * ntiles + tile - 1) * kAH + lane - kPadL - kPadR);
+            ok = hg[1] == want;
+          }
+          if (src) halo[lane] = __uint_as_float(hg[0]);
+          else if (is_el || is_er) halo[lane] = -INFINITY;
+          else if (t >= 2) halo[lane] = 0.f;   // alpha left of position 0 (t == 1: host rows)
+        }
+        __syncthreads();
         const float M1 = stat[tub][0], Z1 = stat[tub][1], A1 = stat[tub][2];
         const float M2 = stat[tub][3], Z2 = stat[tub][4];
-        if (tid < span) {
-          const float e = ew[tid];
+        if (tid < span) {   // e_{t-1} on [n0-4, n0+nt+5): halos and the own energies
+          const float e = tid < kPadL ? halo[tid] : tid < kPadL + nt ? e1s[tid - kPadL]
+                                                                     : halo[tid - nt];
+          ew[tid] = e;
           sp[tid] = e == -INFINITY ? 0.f : __expf(e - M1) / Z1;
         }
+        __syncthreads();
         if (tid <= nt) {
           const int n = n0 - 1 + tid;
           float av = 0.f;
           if (n >= 0) {
-            const float e = ew[tid + padl - 1];
+            // alpha_{t-2} at n (and n-1): own positions from aown, the left two from the halo
+            const float a_n = tid >= 1 ? aown[tid - 1] : halo[kPadL + kPadR + 1];
+            const float a_m = tid >= 2 ? aown[tid - 2] : halo[kPadL + kPadR + tid];
+            const float e = ew[tid + kPadL - 1];
             const float pe = e == -INFINITY ? 0.f : __expf(e - M1);
-            av = ((1.f - u) * aw[tid + 1] + u * aw[tid] + 1e-7f) * pe / A1;
+            av = ((1.f - u) * a_n + u * a_m + 1e-7f) * pe / A1;
           }
           ap[tid] = av;
         }
         __syncthreads();
         if (tid < nt) {   // own positions of the history rows s_{t-1}, alpha_{t-1}, s2_{t-1}
           const int n = n0 + tid;
-          p.S1[((int64_t)t * B + tb) * N + n] = sp[tid + padl];
-          stc(rAL, (t * B + tb) * N + n, ap[tid + 1]);
-          const float e = e2w[tid];
+          p.S1[((int64_t)t * B + tb) * N + n] = sp[tid + kPadL];
+          p.AL1[((int64_t)t * B + tb) * N + n] = ap[tid + 1];
+          aown[tid] = ap[tid + 1];
+          const float e = e2s[tid];
           p.S2[((int64_t)s * B + tb) * N + n] = e == -INFINITY ? 0.f : __expf(e - M2) / Z2;
         }
+        if (tid < kAH && t < T)   // alpha_{t-1} at the last two own positions, for the right tile
+          stg(rAH, ((t & 1) * B + tb) * ntiles * kAH + tile * kAH + tid, ap[nt - 1 + tid],
+              (unsigned)(t + 1));
       }
     }
-    if (t == T) return;
+    if (t == T) break;
     __syncthreads();
-    tick(5);
-    // ======== LSTM0 step t: gates for 32 columns x UB utterances
-    {
-      float acc[kUBmax] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 1
-      for (int ub = 0; ub < kUBmax; ++ub) {        // not unrolled: 17 float4 of rin in flight
-        if (ub >= UB) break;
-        const float4* r4 = reinterpret_cast<const float4*>(&rin[ub][kW0 * ks]);
-        float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;   // four independent FMA chains
-#pragma unroll
-        for (int k4 = 0; k4 < kW0 / 4; ++k4) {      // fully unrolled: w0 stays in registers
-          const float4 x = r4[k4];
-          a0 = fmaf(x.x, w0[4 * k4], a0);
-          a1 = fmaf(x.y, w0[4 * k4 + 1], a1);
-          a2 = fmaf(x.z, w0[4 * k4 + 2], a2);
-          a3 = fmaf(x.w, w0[4 * k4 + 3], a3);
-        }
-        acc[ub] = (a0 + a1) + (a2 + a3);
-      }
-#pragma unroll
-      for (int ub = 0; ub < kUBmax; ++ub) {
-        float a = acc[ub];
-        a += __shfl_xor(a, 1, 64);
-        a += __shfl_xor(a, 2, 64);
-        a += __shfl_xor(a, 4, 64);
-        if (ks == 0 && ub < UB) gsh[ub][cc] = a;
-      }
-    }
-    __syncthreads();
-    tick(6);
-    if (pw) {
-      const int64_t tbu = ((int64_t)t * B + pb) * kU + punit;
-      const float gi = sigm(gsh[pub][4 * puu] + xp.x);
-      const float gj = tanhf(gsh[pub][4 * puu + 1] + xp.y);
-      const float gf = sigm(gsh[pub][4 * puu + 2] + xp.z + 1.0f);   // forget_bias = 1.0
-      const float go = sigm(gsh[pub][4 * puu + 3] + xp.w);
-      const float cn = gf * c_own + gi * gj;
-      const float hn = go * tanhf(cn);
-      const float c2 = mcv * cn + (1.f - mcv) * c_own;
-      const float h2 = mhv * hn + (1.f - mhv) * h_own;
-      c_own = c2; h_own = h2;
-      hown[pub][puu] = hn;
-      p.C0[((int64_t)(t + 1) * B + pb) * kU + punit] = c2;
-      stc(rREC, ((t + 1) * B + pb) * kK0 + kM1 + kM2 + punit, h2);
-      p.H0RAW[tbu] = hn;
-      reinterpret_cast<float4*>(p.G0 + ((int64_t)t * B + pb) * 4 * kU)[punit] = make_float4(gi, gj, gf, go);
-    }
-    __syncthreads();
-    tick(7);
-    // ======== query contribution of the workgroup's units: lane = output column
-#pragma unroll
-    for (int ub = 0; ub < kUBmax; ++ub) {
-      if (ub >= UB) break;
-      float a = 0.f;
-#pragma unroll
-      for (int uu = 0; uu < kUW; ++uu) a = fmaf(hown[ub][uu], wq[uu], a);
-      stc(rQP, (((t & 1) * B + g + kG * ub) * kGW + j) * kQ + tid, a);
-    }
-  };
-
-  for (int t = 0; t < T; ++t) {
-    phase_a(t);
-    tick(0);
-    group_barrier(ctr, (++phase) * kGW, p.err);
-    tick(1);
+    tick(4);
 
     // ===================== phase C: attention tile (energies from LDS-resident K1/K2)
     if (tile_wg) {
-      {   // q_t = sum of the 32 query partials of this utterance: 8 float4 loads per lane
-        const int base4 = (((t & 1) * B + tb) * kGW) * (kQ / 4);
+      const unsigned want = lsb_tag(t);
+      const int base4 = (((t & 1) * B + tb) * kGW + wave * 8) * (kQ / 4) + lane;
+      float4 qv8[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) qv8[i] = ldc4(rQP, base4 + i * (kQ / 4));
+      // location features f = Conv1D_SAME(s_{t-1}) + bias (no dependence on the query)
+      float locv = 0.f;
+      if (tid < kPN * kF) {
+        const int i = tid / kF, f = tid - i * kF;
+        float acc = cw[kKW * kF + f];
+#pragma unroll
+        for (int jj = 0; jj < kKW; ++jj) acc = fmaf(sp[i + jj], cw[jj * kF + f], acc);
+        fs[i][f] = acc;
+        locv = acc;
+      }
+      unsigned bad = 0;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) bad |= tag_ok4(qv8[i], want) ? 0u : 1u << i;
+      for (unsigned spins = 0; any_lane(bad != 0) && !gave_up; ++spins) {
+        if (poll_give_up(spins, p.err)) { gave_up = true; break; }
+        __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          if ((bad >> i) & 1) qv8[i] = ldc4(rQP, base4 + i * (kQ / 4));
+        bad = 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) bad |= tag_ok4(qv8[i], want) ? 0u : 1u << i;
+      }
+      tick(5);
+      {
         float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
-        float4 v[8];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) v[i] = ldc4(rQP, base4 + (wave * 8 + i) * (kQ / 4) + lane);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) { a.x += v[i].x; a.y += v[i].y; a.z += v[i].z; a.w += v[i].w; }
+        for (int i = 0; i < 8; ++i) { a.x += qv8[i].x; a.y += qv8[i].y; a.z += qv8[i].z; a.w += qv8[i].w; }
         qred[wave][lane] = a;
       }
       __syncthreads();
@@ -399,19 +493,11 @@ __global__ void __launch_bounds__(256) dec_attn_fwd_kernel(DecAttnP p) {
           q2s[d - kD1] = qv.x; q2s[d - kD1 + 1] = qv.y; q2s[d - kD1 + 2] = qv.z; q2s[d - kD1 + 3] = qv.w;
         }
       }
-      if (tid < kPN * kF) {       // location features f = Conv1D_SAME(s_{t-1}) + bias
-        const int i = tid / kF, f = tid - i * kF;
-        float acc = cw[kKW * kF + f];
-#pragma unroll
-        for (int jj = 0; jj < kKW; ++jj) acc = fmaf(sp[i + jj], cw[jj * kF + f], acc);
-        fs[i][f] = acc;
-        if (p.LOC && i < nt) p.LOC[(((int64_t)t * B + tb) * N + n0 + i) * kF + f] = acc;
-      }
       __syncthreads();
-      // energies: 8 lanes per position, 28 dims (7 float4) of K1 per lane, 4 dims of K2
+      // energies: 8 lanes per position, 28 dims (7 float4) of K1 per lane, 4 dims of K2; the
+      // tanh values are kept for the BPTT (stored after the hand-off is published)
       const int nl = tid >> 3, part = tid & 7;
-      // the tanh values are kept for the BPTT (decoder_persistent_bwd.hip recomputes nothing)
-      float* zrow = (p.ZH && nl < nt) ? p.ZH + ((((int64_t)t * B + tb) * N) + n0 + nl) * kQ : nullptr;
+      float4 zk[kD1 / 32 + 1];
       float acc = 0.f;
       {
         float fl[kF];
@@ -432,7 +518,7 @@ __global__ void __launch_bounds__(256) dec_attn_fwd_kernel(DecAttnP p) {
           }
           const float4 z = make_float4(tanh_fast(pre.x), tanh_fast(pre.y), tanh_fast(pre.z),
                                        tanh_fast(pre.w));
-          if (zrow) *reinterpret_cast<float4*>(zrow + d) = z;
+          zk[jj] = z;
           acc = fmaf(vw.x, z.x, acc);
           acc = fmaf(vw.y, z.y, acc);
           acc = fmaf(vw.z, z.z, acc);
@@ -447,7 +533,7 @@ __global__ void __launch_bounds__(256) dec_attn_fwd_kernel(DecAttnP p) {
         const float4 vw = *reinterpret_cast<const float4*>(&vv2[d]);
         const float4 z = make_float4(tanh_fast(kv.x + qv.x), tanh_fast(kv.y + qv.y),
                                      tanh_fast(kv.z + qv.z), tanh_fast(kv.w + qv.w));
-        if (zrow) *reinterpret_cast<float4*>(zrow + kD1 + d) = z;
+        zk[kD1 / 32] = z;
         acc2 = vw.x * z.x;
         acc2 = fmaf(vw.y, z.y, acc2);
         acc2 = fmaf(vw.z, z.z, acc2);
@@ -455,30 +541,28 @@ __global__ void __launch_bounds__(256) dec_attn_fwd_kernel(DecAttnP p) {
       }
       acc = group8_sum(acc);
       acc2 = group8_sum(acc2);
-      const int eb = (((t & 1) * B + tb) * 2) * N;
-      if (part == 0 && nl < nt) {
-        const bool valid = n0 + nl < len;
-        const float ev1 = valid ? acc : -INFINITY, ev2 = valid ? acc2 : -INFINITY;
-        e1s[nl] = ev1;
-        e2s[nl] = ev2;
-        stc(rE, eb + n0 + nl, ev1);
-        stc(rE, eb + N + n0 + nl, ev2);
+      if (part == 0) {
+        const bool valid = nl < nt && n0 + nl < len;
+        e1s[nl] = valid ? acc : -INFINITY;
+        e2s[nl] = valid ? acc2 : -INFINITY;
       }
       __syncthreads();
       if (wave == 0) {            // tile statistics
-        const float e1v = lane < nt ? e1s[lane] : -INFINITY;
-        const float e2v = lane < nt ? e2s[lane] : -INFINITY;
+        const float e1v = lane < kPN ? e1s[lane] : -INFINITY;
+        const float e2v = lane < kPN ? e2s[lane] : -INFINITY;
         const float m1 = wave_max(e1v), m2 = wave_max(e2v);
         const float pe = (e1v == -INFINITY) ? 0.f : __expf(e1v - m1);
         const float pe2 = (e2v == -INFINITY) ? 0.f : __expf(e2v - m2);
         const float w = lane < nt ? ((1.f - u) * ap[lane + 1] + u * ap[lane] + 1e-7f) * pe : 0.f;
         if (lane < kPN) { w1s[lane] = w; w2s[lane] = lane < nt ? pe2 : 0.f; }
         const float z1 = wave_sum_dpp(pe), a1 = wave_sum_dpp(w), z2 = wave_sum_dpp(pe2);
-        if (lane == 0) { red[0] = m1; red[1] = z1; red[2] = a1; red[3] = m2; red[4] = z2; }
+        if (lane == 0) {   // an empty tile's maxima are -inf: published as -FLT_MAX (finite)
+          red[0] = fmaxf(m1, -3.402823466e38f); red[1] = z1; red[2] = a1;
+          red[3] = fmaxf(m2, -3.402823466e38f); red[4] = z2;
+          red[5] = 0.f; red[6] = 0.f; red[7] = 0.f;
+        }
       }
       __syncthreads();
-      const int pout = (((t & 1) * B + tb) * ntiles + tile) * kPST;
-      if (tid < 5) stc(rPT, pout + tid, red[tid]);
       {   // unnormalised partial contexts: wave owns 8 positions, lane a float4 column
         float4 c = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
@@ -497,11 +581,13 @@ __global__ void __launch_bounds__(256) dec_attn_fwd_kernel(DecAttnP p) {
         }
       }
       __syncthreads();
+      // ---- publish the tile record (tagged) and the energy halo granules
+      const int pout4 = (((t & 1) * B + tb) * ntiles + tile) * kP4;
       if (tid < kM1 / 4) {
         const float4 a0 = cred[0][tid], a1 = cred[1][tid], a2 = cred[2][tid], a3 = cred[3][tid];
-        stc4(rPT, (pout + 8) / 4 + tid,
-             make_float4((a0.x + a1.x) + (a2.x + a3.x), (a0.y + a1.y) + (a2.y + a3.y),
-                         (a0.z + a1.z) + (a2.z + a3.z), (a0.w + a1.w) + (a2.w + a3.w)));
+        stc4(rPT, pout4 + 2 + tid,
+             tagf4(make_float4((a0.x + a1.x) + (a2.x + a3.x), (a0.y + a1.y) + (a2.y + a3.y),
+                               (a0.z + a1.z) + (a2.z + a3.z), (a0.w + a1.w) + (a2.w + a3.w)), want));
       } else if (tid >= 64 && tid < 64 + kM2 / 4) {
         const int jj = tid - 64;
         float4 sm = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -510,23 +596,42 @@ __global__ void __launch_bounds__(256) dec_attn_fwd_kernel(DecAttnP p) {
           const float4 v = c2red[i][jj];
           sm.x += v.x; sm.y += v.y; sm.z += v.z; sm.w += v.w;
         }
-        stc4(rPT, (pout + 8 + kM1) / 4 + jj, sm);
+        stc4(rPT, pout4 + 2 + kM1 / 4 + jj, tagf4(sm, want));
+      } else if (tid >= 128 && tid < 130) {
+        const int q = tid - 128;
+        stc4(rPT, pout4 + q, tagf4(make_float4(red[4 * q], red[4 * q + 1], red[4 * q + 2],
+                                               red[4 * q + 3]), want));
+      } else if (tid >= 192 && tid < 192 + kPadR + kPadL) {   // first 5, last 4 energies
+        const int q = tid - 192;
+        stg(rEH, ((t & 1) * B + tb) * ntiles * kEH + tile * kEH + q,
+            e1s[q < kPadR ? q : kPN - kPadL + (q - kPadR)], (unsigned)(t + 1));
       }
+      tick(6);
+      // ---- histories nobody waits for: energy tanh (for the BPTT), location features
+      if (p.ZH && nl < nt) {
+        float* zrow = p.ZH + ((((int64_t)t * B + tb) * N) + n0 + nl) * kQ;
+#pragma unroll
+        for (int jj = 0; jj < kD1 / 32; ++jj)
+          *reinterpret_cast<float4*>(zrow + part * (kD1 / 8) + 4 * jj) = zk[jj];
+        *reinterpret_cast<float4*>(zrow + kD1 + 4 * part) = zk[kD1 / 32];
+      }
+      if (p.LOC && tid < kPN * kF && tid / kF < nt)
+        p.LOC[(((int64_t)t * B + tb) * N + n0) * kF + tid] = locv;
+      tick(7);
     }
-    tick(2);
-    group_barrier(ctr, (++phase) * kGW, p.err);
-    tick(3);
   }
   if (p.prof && tid == 0)
     for (int i = 0; i < 8; ++i) p.prof[blockIdx.x * 8 + i] = tp[i];
-  // ===================== epilogue: step T-1's context, statistics and normalised rows
-  phase_a(T);
 }
 
 }  // namespace
 }  // namespace sat
 
 using namespace sat;
+
+static int64_t hx_floats(int B) { return (int64_t)2 * B * kU; }
+static int64_t eh_floats(int B, int ntiles) { return (int64_t)2 * B * ntiles * kEH * 2; }
+static int64_t ah_floats(int B, int ntiles) { return (int64_t)2 * B * ntiles * kAH * 2; }
 
 extern "C" int sat_decoder_attention_fwd(const SatDecAttnFwd* a, void* stream) {
   SAT_CHECK_ARG(a && a->B > 0 && a->N > 0 && a->T > 0, "sat_decoder_attention_fwd: bad sizes");
@@ -541,10 +646,12 @@ extern "C" int sat_decoder_attention_fwd(const SatDecAttnFwd* a, void* stream) {
   SAT_CHECK_ARG(a->X0 && a->W0r && a->Wq1 && a->Wq2 && a->K1 && a->V1 && a->K2 && a->V2 &&
                 a->lengths && a->v1 && a->b1 && a->convW && a->convb && a->locW && a->v2 &&
                 a->REC0 && a->C0 && a->H0RAW && a->G0 && a->Q && a->S1 && a->AL1 && a->S2 &&
-                a->ST && a->E && a->PART && a->QP && a->ctr && a->err,
+                a->ST && a->E && a->PART && a->QP && a->err,
                 "sat_decoder_attention_fwd: null pointer");
   SAT_CHECK_ARG((a->mask_c == nullptr) == (a->mask_h == nullptr), "sat_decoder_attention_fwd: masks come in pairs");
-  SAT_CHECK_ARG(aligned16(a->X0) && aligned16(a->G0) && aligned16(a->K1) && aligned16(a->V1),
+  SAT_CHECK_ARG(aligned16(a->X0) && aligned16(a->G0) && aligned16(a->K1) && aligned16(a->V1) &&
+                aligned16(a->W0r) && aligned16(a->Wq1) && aligned16(a->Wq2) && aligned16(a->REC0) &&
+                aligned16(a->Q) && aligned16(a->E) && aligned16(a->PART) && aligned16(a->QP),
                 "sat_decoder_attention_fwd: 16-byte aligned operands");
   // the grid must be co-resident (one workgroup per CU): refuse rather than hang
   int dev = 0, cus = 0, per_cu = 0;
@@ -565,11 +672,18 @@ extern "C" int sat_decoder_attention_fwd(const SatDecAttnFwd* a, void* stream) {
   p.v2 = a->v2; p.mask_c = a->mask_c; p.mask_h = a->mask_h;
   p.REC0 = a->REC0; p.C0 = a->C0; p.H0RAW = a->H0RAW; p.G0 = a->G0; p.Q = a->Q;
   p.S1 = a->S1; p.AL1 = a->AL1; p.S2 = a->S2; p.ST = a->ST; p.LOC = a->LOC;
-  p.E = a->E; p.PART = a->PART; p.QP = a->QP; p.ctr = a->ctr; p.err = a->err;
+  p.HX = a->E;
+  p.EH = a->E + hx_floats(a->B);
+  p.AH = p.EH + eh_floats(a->B, ntiles);
+  p.PART = a->PART; p.QP = a->QP; p.err = a->err;
   p.prof = reinterpret_cast<long long*>(a->prof);
   p.ZH = a->ZH;
   hipStream_t s = as_stream(stream);
-  if (hipMemsetAsync(a->ctr, 0, kG * 64 * sizeof(unsigned), s) != hipSuccess ||
+  // every hand-off slot starts zeroed (tag 0 / LSB 0 never matches steps 0 and 1)
+  const int64_t e_total = hx_floats(a->B) + eh_floats(a->B, ntiles) + ah_floats(a->B, ntiles);
+  if (hipMemsetAsync(a->E, 0, e_total * sizeof(float), s) != hipSuccess ||
+      hipMemsetAsync(a->PART, 0, (size_t)2 * a->B * ntiles * kPST * sizeof(float), s) != hipSuccess ||
+      hipMemsetAsync(a->QP, 0, (size_t)2 * a->B * kGW * kQ * sizeof(float), s) != hipSuccess ||
       hipMemsetAsync(a->err, 0, 2 * sizeof(int), s) != hipSuccess) {
     set_error("sat_decoder_attention_fwd: memset failed");
     return SAT_ERR_HIP;
@@ -582,8 +696,8 @@ extern "C" int sat_decoder_attention_fwd(const SatDecAttnFwd* a, void* stream) {
 extern "C" int64_t sat_decoder_attention_scratch(int32_t B, int32_t N, int64_t* e_floats,
                                                  int64_t* part_floats, int64_t* qp_floats) {
   const int ntiles = ceil_div(N, kPN);
-  if (e_floats) *e_floats = (int64_t)2 * B * 2 * N;
+  if (e_floats) *e_floats = hx_floats(B) + eh_floats(B, ntiles) + ah_floats(B, ntiles);
   if (part_floats) *part_floats = (int64_t)2 * B * ntiles * kPST;
   if (qp_floats) *qp_floats = (int64_t)2 * B * kGW * kQ;
-  return kG * 64;   // counter words
+  return kG * 64;   // counter words (unused by the tagged hand-offs; kept for the ABI)
 }

@@ -54,6 +54,110 @@ __device__ __forceinline__ void group_barrier(unsigned* ctr, unsigned target, in
   __syncthreads();
 }
 
+// ---- data-tagged hand-offs (MI355X_MICROARCH.md "handoff-1to1": the data IS the flag)
+// (1) 8-byte granules {value, tag}: one sc1 dwordx2 store, untorn; used where a value may be
+//     non-finite (raw energies: -inf at padded positions).
+typedef unsigned v2u __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void stg(__amdgpu_buffer_rsrc_t r, int granule, float v, unsigned tag) {
+  const v2u w = {__float_as_uint(v), tag};
+  __builtin_amdgcn_raw_buffer_store_b64(w, r, granule * 8, 0, 16);
+}
+__device__ __forceinline__ v2u ldg(__amdgpu_buffer_rsrc_t r, int granule) {
+  return __builtin_amdgcn_raw_buffer_load_b64(r, granule * 8, 0, 16);
+}
+// (2) step parity in the mantissa LSB of every handed-off float (bulk payloads: contexts,
+//     query partials, states).  A 4-byte word is never torn, so each word carries its own
+//     validity and a 16-byte sc1 store needs no flag, no drain and no barrier.  Slots alternate
+//     by step parity (slot s & 1); the bit for step s is ((s >> 1) + 1) & 1, so a slot's
+//     previous occupant (step s - 2) always carries the other bit and zeroed scratch (LSB 0)
+//     never matches steps 0 and 1.  Cost: <= 1 ulp (6e-8 relative) on the tagged values, which
+//     every consumer reads identically.  Only finite values are tagged.
+__device__ __forceinline__ unsigned lsb_tag(int s) { return (unsigned)(((s >> 1) + 1) & 1); }
+__device__ __forceinline__ float tagf(float x, unsigned bit) {
+  return __uint_as_float((__float_as_uint(x) & ~1u) | bit);
+}
+__device__ __forceinline__ float4 tagf4(float4 v, unsigned bit) {
+  return make_float4(tagf(v.x, bit), tagf(v.y, bit), tagf(v.z, bit), tagf(v.w, bit));
+}
+__device__ __forceinline__ bool tag_ok(float x, unsigned bit) {
+  return ((__float_as_uint(x) ^ bit) & 1u) == 0;
+}
+__device__ __forceinline__ bool tag_ok4(float4 v, unsigned bit) {
+  return (((__float_as_uint(v.x) ^ bit) | (__float_as_uint(v.y) ^ bit) |
+           (__float_as_uint(v.z) ^ bit) | (__float_as_uint(v.w) ^ bit)) & 1u) == 0;
+}
+// bounded-spin bookkeeping of a poll loop: every 256 spins look at the error word; after
+// ~2^20 spins (a producer never published: grid not co-resident) raise it.  Returns true when
+// the loop must give up (the grid then drains with garbage and the host reports err).
+__device__ __forceinline__ bool poll_give_up(unsigned spins, int* err) {
+  if ((spins & 255u) != 255u) return false;
+  if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return true;
+  if (spins > (1u << 20)) {
+    __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return true;
+  }
+  return false;
+}
+
+// ---- wave-level dot helpers shared by the persistent kernels
+__device__ __forceinline__ float dot4(float4 a, float4 b, float acc) {
+  acc = fmaf(a.x, b.x, acc);
+  acc = fmaf(a.y, b.y, acc);
+  acc = fmaf(a.z, b.z, acc);
+  return fmaf(a.w, b.w, acc);
+}
+
+// Transpose-reduce across the 64 lanes of a wave: v[0..N-1] are per-lane partial sums of N
+// different outputs; each halving exchange pairs (v[i], v[i + n/2]) over one lane bit, after
+// which every lane keeps the half its bit selects, summed with its partner's.  All VALU, no
+// LDS: the 32- and 16-lane exchanges are gfx950 v_permlane32_swap / v_permlane16_swap (after
+// the swap x' + y' is already the kept half's sum), the 8/4-lane ones DPP row shifts (lane l
+// adds lane l+H where bit H of l is clear, lane l-H where it is set).  Lane bits left over when
+// the values run out are plain butterflies, so every lane of a 64/N block ends with the total.
+__device__ __forceinline__ float fsum_swap32(float x, float y) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(y), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float fsum_swap16(float x, float y) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(y), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float x) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, true));
+}
+template <int H, int HALF>
+__device__ __forceinline__ void tr_dpp(float* v, int lane) {
+  const bool hi = (lane & H) != 0;
+#pragma unroll
+  for (int i = 0; i < HALF; ++i) {
+    const float sa = v[i] + dpp_mov<0x100 + H>(v[i]);                // row_shl:H (lane l+H)
+    const float sb = v[i + HALF] + dpp_mov<0x110 + H>(v[i + HALF]);  // row_shr:H (lane l-H)
+    v[i] = hi ? sb : sa;
+  }
+}
+// 32 outputs: lanes 2m, 2m+1 hold output m
+__device__ __forceinline__ void transpose_reduce32(float* v, int lane) {
+#pragma unroll
+  for (int i = 0; i < 16; ++i) v[i] = fsum_swap32(v[i], v[i + 16]);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = fsum_swap16(v[i], v[i + 8]);
+  tr_dpp<8, 4>(v, lane);
+  tr_dpp<4, 2>(v, lane);
+  tr_dpp<2, 1>(v, lane);
+  v[0] += dpp_mov<0xB1>(v[0]);   // quad_perm [1,0,3,2]: lane l ^ 1
+}
+// 16 outputs: lanes 4m..4m+3 hold output m
+__device__ __forceinline__ void transpose_reduce16(float* v, int lane) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = fsum_swap32(v[i], v[i + 8]);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) v[i] = fsum_swap16(v[i], v[i + 4]);
+  tr_dpp<8, 2>(v, lane);
+  tr_dpp<4, 1>(v, lane);
+  v[0] += dpp_mov<0xB1>(v[0]);   // lane l ^ 1
+  v[0] += dpp_mov<0x4E>(v[0]);   // quad_perm [2,3,0,1]: lane l ^ 2
+}
 
 }  // namespace
 }  // namespace sat

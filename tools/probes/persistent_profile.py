@@ -1,5 +1,6 @@
 """Segment clocks of the persistent decoder-attention kernel (tools only): per workgroup, the
-wall-clock (100 MHz) time spent in phase A, barrier A, phase C, barrier C over a full decode."""
+wall-clock (100 MHz) time spent in each segment of a step (poll waits, combine, LSTM dot,
+cell + publish, normalise, tile) over a full decode."""
 import os
 import sys
 
@@ -34,11 +35,12 @@ for _ in range(2):
 torch.cuda.synchronize()
 pr = PROF["buf"].view(256, 8).cpu().double() / 100.0   # us
 Tp = 500
-names = ["phase A tail (query partial)", "barrier A", "phase C", "barrier C",
-         "A: loads + combine", "A: tile normalise", "A: LSTM dot", "A: pointwise"]
+names = ["A: poll partials + h", "A: combine", "A: LSTM dot + reduce", "A: cell + publish",
+         "A: tile normalise", "C: poll query partials", "C: tile to publish", "C: tanh/loc stores"]
 for i, n in enumerate(names):
     col = pr[:, i]
     print(f"{n:28s} mean {col.mean() / Tp:7.2f} us/step  min {col.min() / Tp:7.2f}  "
           f"max {col.max() / Tp:7.2f}")
+print(f"total us/step {float(pr.sum(1).mean()) / Tp:.2f}")
 tile = pr[[g + 8 * j for g in range(8) for j in range(28)]]
-print("tile WGs  phase C mean", float(tile[:, 2].mean() / Tp), "us/step")
+print("tile WGs:", " ".join(f"{float(tile[:, i].mean() / Tp):.2f}" for i in range(8)))

@@ -296,7 +296,8 @@ typedef struct SatDecAttnFwd {
   float* REC0; float* C0; float* H0RAW; float* G0; float* Q;
   float* S1; float* AL1; float* S2; float* ST; float* LOC;
   float* E; float* PART; float* QP; uint32_t* ctr; int32_t* err;
-  int64_t* prof;   /* optional [256][8] per-workgroup segment clocks (100 MHz), NULL = off */
+  int64_t* prof;   /* optional [256][16] per-workgroup segment clocks (100 MHz) followed by a
+                      [T][256][4] event trace, NULL = off */
   float* ZH;       /* optional [T][B][N][D1+D2]: tanh of every energy pre-activation, kept for
                       sat_decoder_attention_bwd (which then recomputes no transcendental) */
 } SatDecAttnFwd;

@@ -76,8 +76,10 @@ struct DecAttnP {
   float* PART;                                       // [2][B][ntiles][kPST] tagged
   float* QP;                                         // [2][B][kGW][kQ]      tagged
   int* err;                                          // [2]
-  long long* prof;                                   // [256][8] segment clocks (nullable)
+  long long* prof;                                   // [256][16] segment clocks + [T][256][4] trace (nullable)
 };
+
+typedef float f2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + __expf(-x)); }
 __device__ __forceinline__ bool any_lane(bool v) { return __builtin_amdgcn_ballot_w64(v) != 0; }
@@ -125,18 +127,17 @@ __global__ void __launch_bounds__(256) dec_attn_fwd_kernel(DecAttnP p) {
   // ---------------- prologue: resident operands
   // LSTM (wave-transposed dot): wave w owns local gate columns 8w..8w+7 (units 8j+2w, +1, gates
   // i j f o), lane owns input rows k = lane + 64 i (i < 9; rows >= 544 are zero)
-  float w0[9][8];
+  f2 w0[9][4];
 #pragma unroll
   for (int i = 0; i < 9; ++i) {
     const int k = lane + 64 * i;
     if (k < kK0) {
       const float4* src = reinterpret_cast<const float4*>(p.W0r + (int64_t)k * (4 * kU) + 32 * j + 8 * wave);
       const float4 a = src[0], b = src[1];
-      w0[i][0] = a.x; w0[i][1] = a.y; w0[i][2] = a.z; w0[i][3] = a.w;
-      w0[i][4] = b.x; w0[i][5] = b.y; w0[i][6] = b.z; w0[i][7] = b.w;
+      w0[i][0] = f2{a.x, a.y}; w0[i][1] = f2{a.z, a.w}; w0[i][2] = f2{b.x, b.y}; w0[i][3] = f2{b.z, b.w};
     } else {
 #pragma unroll
-      for (int c = 0; c < 8; ++c) w0[i][c] = 0.f;
+      for (int c = 0; c < 4; ++c) w0[i][c] = f2{0.f, 0.f};
     }
   }
   // query partial: wave = utterance, lane = 4 output columns, 8 unit rows
@@ -150,8 +151,7 @@ __global__ void __launch_bounds__(256) dec_attn_fwd_kernel(DecAttnP p) {
                        : *reinterpret_cast<const float4*>(p.Wq2 + k * kD2 + (c - kD1));
     }
   }
-  for (int i = tid; i < kUBmax * (kKP - kK0); i += 256)
-    rin[i / (kKP - kK0)][kK0 + i % (kKP - kK0)] = 0.f;
+  for (int i = tid; i < kUBmax * kKP; i += 256) rin[i / kKP][i % kKP] = 0.f;   // pad, rows >= UB
   if (tile_wg) {
     for (int i = tid; i < kPN * kD1 / 4; i += 256) {
       const int r = i / (kD1 / 4), c4 = i - r * (kD1 / 4);
@@ -200,10 +200,20 @@ __global__ void __launch_bounds__(256) dec_attn_fwd_kernel(DecAttnP p) {
   float mcn, mhn;
   load_ops(0, xpn, mcn, mhn);
   const int len = tile_wg ? (int)p.lengths[tb] : 0;
+  const float4 b1r = tile_wg && tid < kD1 / 4 ? reinterpret_cast<const float4*>(p.b1)[tid]
+                                                : make_float4(0.f, 0.f, 0.f, 0.f);
   __syncthreads();
 
-  long long tp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  long long tp[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) tp[i] = 0;
   long long t0 = wall_clock64();
+  // optional event trace behind the segment sums: [T][256][4] clocks of thread 0 (A-poll
+  // done for utterance 0, query partial published, query partials received, record published)
+  long long* trace = p.prof ? p.prof + 256 * 16 : nullptr;
+  auto ev = [&](int t, int k) {
+    if (trace && tid == 0 && t < T) trace[((int64_t)t * 256 + blockIdx.x) * 8 + k] = wall_clock64();
+  };
   auto tick = [&](int seg) {
     if (p.prof) {
       const long long t1 = wall_clock64();
@@ -216,6 +226,7 @@ __global__ void __launch_bounds__(256) dec_attn_fwd_kernel(DecAttnP p) {
   for (int t = 0; t <= T; ++t) {
     const int s = t - 1;
     // ======== A1: step s's partial records (wave = utterance) and h_s; halo granules
+    ev(t, 6);
     v2u hg = {0u, 0u};      // tile workgroups, wave 0 lanes < 11: energy / alignment halo
     if (t > 0 && tile_wg && wave == 0) {
       const int sl = s & 1;
@@ -233,19 +244,23 @@ __global__ void __launch_bounds__(256) dec_attn_fwd_kernel(DecAttnP p) {
       const int hx4 = (((s & 1) * B + b) * kU) / 4 + lane;
       const bool need_h = t < T;
       float4 ph[2][8], hs[2], h4;
+      // optimistic full load; while any tile's statistics are stale only those are re-polled
+      // (the producer stores them after its context), then the stale payload words are reloaded
       unsigned bad = 0xFFFFFFFFu;
+      bool light = false;
       for (unsigned spins = 0;; ++spins) {
+        const unsigned ld = light ? (bad & (3u << 16)) : bad;
 #pragma unroll
         for (int jt = 0; jt < 8; ++jt)
 #pragma unroll
           for (int h = 0; h < 2; ++h)
-            if (jt < ntiles && lane + 64 * h < (kM1 + kM2) / 4 && ((bad >> (h * 8 + jt)) & 1))
+            if (jt < ntiles && lane + 64 * h < (kM1 + kM2) / 4 && ((ld >> (h * 8 + jt)) & 1))
               ph[h][jt] = ldc4(rPT, pb4 + jt * kP4 + 2 + lane + 64 * h);
         if (lane < ntiles) {
-          if ((bad >> 16) & 1) hs[0] = ldc4(rPT, pb4 + lane * kP4);
-          if ((bad >> 17) & 1) hs[1] = ldc4(rPT, pb4 + lane * kP4 + 1);
+          if ((ld >> 16) & 1) hs[0] = ldc4(rPT, pb4 + lane * kP4);
+          if ((ld >> 17) & 1) hs[1] = ldc4(rPT, pb4 + lane * kP4 + 1);
         }
-        if (need_h && ((bad >> 18) & 1)) h4 = ldc4(rHX, hx4);
+        if (need_h && ((ld >> 18) & 1)) h4 = ldc4(rHX, hx4);
         bad = 0;
 #pragma unroll
         for (int jt = 0; jt < 8; ++jt)
@@ -259,18 +274,23 @@ __global__ void __launch_bounds__(256) dec_attn_fwd_kernel(DecAttnP p) {
         }
         if (need_h && !tag_ok4(h4, want)) bad |= 1u << 18;
         if (!any_lane(bad != 0) || gave_up) break;
+        const bool was_light = light;
+        light = any_lane((bad & (3u << 16)) != 0);
+        if (was_light && !light) ev(t, 4);
         if (poll_give_up(spins, p.err)) { gave_up = true; break; }
         __builtin_amdgcn_s_sleep(1);
       }
       tick(0);
+      ev(t, 0);
       // ---- combine step s (wave = utterance)
       const bool on = lane < ntiles;
       const float hm1 = on ? hs[0].x : -INFINITY, hz1 = on ? hs[0].y : 0.f, ha1 = on ? hs[0].z : 0.f;
       const float hm2 = on ? hs[0].w : -INFINITY, hz2 = on ? hs[1].x : 0.f;
-      const float M1 = wave_max(hm1), M2 = wave_max(hm2);
+      // ntiles <= 8: the tile statistics sit in lanes 0..7 (DPP reductions, no LDS crossbar)
+      const float M1 = lanes8_max(hm1), M2 = lanes8_max(hm2);
       const float s1 = on ? __expf(hm1 - M1) : 0.f;   // an empty tile's max is -FLT_MAX: 0
       const float s2 = on ? __expf(hm2 - M2) : 0.f;
-      const float Z1 = wave_sum(hz1 * s1), A1 = wave_sum(ha1 * s1), Z2 = wave_sum(hz2 * s2);
+      const float Z1 = lanes8_sum(hz1 * s1), A1 = lanes8_sum(ha1 * s1), Z2 = lanes8_sum(hz2 * s2);
       const float inv1 = 1.f / A1, inv2 = 1.f / Z2;
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
@@ -311,19 +331,25 @@ __global__ void __launch_bounds__(256) dec_attn_fwd_kernel(DecAttnP p) {
 
     if (t < T) {
       // ======== A2: LSTM0 step t, 8 gate columns x UB utterances per wave
-      float v[32];
+      f2 v2[16];
 #pragma unroll
-      for (int q = 0; q < 32; ++q) v[q] = 0.f;
+      for (int q = 0; q < 16; ++q) v2[q] = f2{0.f, 0.f};
 #pragma unroll
       for (int i = 0; i < 9; ++i) {
         float x[kUBmax];
 #pragma unroll
-        for (int ub = 0; ub < kUBmax; ++ub) x[ub] = ub < UB ? rin[ub][lane + 64 * i] : 0.f;
+        for (int ub = 0; ub < kUBmax; ++ub) x[ub] = rin[ub][lane + 64 * i];
 #pragma unroll
-        for (int ub = 0; ub < kUBmax; ++ub)
+        for (int ub = 0; ub < kUBmax; ++ub) {
+          const f2 xx = {x[ub], x[ub]};
 #pragma unroll
-          for (int c = 0; c < 8; ++c) v[ub * 8 + c] = fmaf(x[ub], w0[i][c], v[ub * 8 + c]);
+          for (int cp = 0; cp < 4; ++cp)
+            v2[ub * 4 + cp] = __builtin_elementwise_fma(xx, w0[i][cp], v2[ub * 4 + cp]);
+        }
       }
+      float v[32];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) { v[2 * q] = v2[q].x; v[2 * q + 1] = v2[q].y; }
       transpose_reduce32(v, lane);
       const float gj_ = dpp_mov<0x102>(v[0]);
       const float gf_ = dpp_mov<0x104>(v[0]);
@@ -351,7 +377,9 @@ __global__ void __launch_bounds__(256) dec_attn_fwd_kernel(DecAttnP p) {
         reinterpret_cast<float4*>(p.G0)[tbu] = make_float4(gi, gj, gf, go);
       }
       load_ops(t + 1, xpn, mcn, mhn);
+      tick(12);
       __syncthreads();
+      tick(13);
       // ======== publish h_t (own units' zoneout states) and the query contribution of the own
       //          units' raw outputs
       if (tid < 2 * UB) {
@@ -370,6 +398,7 @@ __global__ void __launch_bounds__(256) dec_attn_fwd_kernel(DecAttnP p) {
         stc4(rQP, ((((t & 1) * B + g + kG * wave) * kGW + j) * kQ) / 4 + lane, tagf4(a, bit));
       }
       tick(3);
+      ev(t, 1);
     }
 
     // ======== A3 (tile workgroups): s_{t-1} on the conv window, alpha_{t-1} on [n0-1, n0+nt)
@@ -446,6 +475,7 @@ __global__ void __launch_bounds__(256) dec_attn_fwd_kernel(DecAttnP p) {
     if (tile_wg) {
       const unsigned want = lsb_tag(t);
       const int base4 = (((t & 1) * B + tb) * kGW + wave * 8) * (kQ / 4) + lane;
+      ev(t, 7);
       float4 qv8[8];
 #pragma unroll
       for (int i = 0; i < 8; ++i) qv8[i] = ldc4(rQP, base4 + i * (kQ / 4));
@@ -459,20 +489,25 @@ __global__ void __launch_bounds__(256) dec_attn_fwd_kernel(DecAttnP p) {
         fs[i][f] = acc;
         locv = acc;
       }
+      // optimistic full load; while any of the wave's 8 rows is stale, lane i < 8 re-polls one
+      // word of row i only, then the stale words are reloaded
       unsigned bad = 0;
 #pragma unroll
       for (int i = 0; i < 8; ++i) bad |= tag_ok4(qv8[i], want) ? 0u : 1u << i;
       for (unsigned spins = 0; any_lane(bad != 0) && !gave_up; ++spins) {
         if (poll_give_up(spins, p.err)) { gave_up = true; break; }
         __builtin_amdgcn_s_sleep(1);
+        const bool light = any_lane(lane < 8 && ((bad >> lane) & 1));
+        if (!light) ev(t, 5);
 #pragma unroll
         for (int i = 0; i < 8; ++i)
-          if ((bad >> i) & 1) qv8[i] = ldc4(rQP, base4 + i * (kQ / 4));
+          if (((bad >> i) & 1) && (!light || lane == i)) qv8[i] = ldc4(rQP, base4 + i * (kQ / 4));
         bad = 0;
 #pragma unroll
         for (int i = 0; i < 8; ++i) bad |= tag_ok4(qv8[i], want) ? 0u : 1u << i;
       }
       tick(5);
+      ev(t, 2);
       {
         float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
@@ -480,6 +515,7 @@ __global__ void __launch_bounds__(256) dec_attn_fwd_kernel(DecAttnP p) {
         qred[wave][lane] = a;
       }
       __syncthreads();
+      tick(14);
       if (tid < kQ / 4) {
         const float4 a0 = qred[0][tid], a1 = qred[1][tid], a2 = qred[2][tid], a3 = qred[3][tid];
         const float4 qv = make_float4((a0.x + a1.x) + (a2.x + a3.x), (a0.y + a1.y) + (a2.y + a3.y),
@@ -487,8 +523,8 @@ __global__ void __launch_bounds__(256) dec_attn_fwd_kernel(DecAttnP p) {
         if (tile == 0) reinterpret_cast<float4*>(p.Q + ((int64_t)t * B + tb) * kQ)[tid] = qv;
         const int d = 4 * tid;
         if (d < kD1) {
-          qb[d] = qv.x + p.b1[d]; qb[d + 1] = qv.y + p.b1[d + 1];
-          qb[d + 2] = qv.z + p.b1[d + 2]; qb[d + 3] = qv.w + p.b1[d + 3];
+          qb[d] = qv.x + b1r.x; qb[d + 1] = qv.y + b1r.y;
+          qb[d + 2] = qv.z + b1r.z; qb[d + 3] = qv.w + b1r.w;
         } else {
           q2s[d - kD1] = qv.x; q2s[d - kD1 + 1] = qv.y; q2s[d - kD1 + 2] = qv.z; q2s[d - kD1 + 3] = qv.w;
         }
@@ -541,6 +577,7 @@ __global__ void __launch_bounds__(256) dec_attn_fwd_kernel(DecAttnP p) {
       }
       acc = group8_sum(acc);
       acc2 = group8_sum(acc2);
+      tick(6);
       if (part == 0) {
         const bool valid = nl < nt && n0 + nl < len;
         e1s[nl] = valid ? acc : -INFINITY;
@@ -550,7 +587,7 @@ __global__ void __launch_bounds__(256) dec_attn_fwd_kernel(DecAttnP p) {
       if (wave == 0) {            // tile statistics
         const float e1v = lane < kPN ? e1s[lane] : -INFINITY;
         const float e2v = lane < kPN ? e2s[lane] : -INFINITY;
-        const float m1 = wave_max(e1v), m2 = wave_max(e2v);
+        const float m1 = wave_max_dpp(e1v), m2 = wave_max_dpp(e2v);
         const float pe = (e1v == -INFINITY) ? 0.f : __expf(e1v - m1);
         const float pe2 = (e2v == -INFINITY) ? 0.f : __expf(e2v - m2);
         const float w = lane < nt ? ((1.f - u) * ap[lane + 1] + u * ap[lane] + 1e-7f) * pe : 0.f;
@@ -563,6 +600,7 @@ __global__ void __launch_bounds__(256) dec_attn_fwd_kernel(DecAttnP p) {
         }
       }
       __syncthreads();
+      tick(8);
       {   // unnormalised partial contexts: wave owns 8 positions, lane a float4 column
         float4 c = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
@@ -581,6 +619,7 @@ __global__ void __launch_bounds__(256) dec_attn_fwd_kernel(DecAttnP p) {
         }
       }
       __syncthreads();
+      tick(9);
       // ---- publish the tile record (tagged) and the energy halo granules
       const int pout4 = (((t & 1) * B + tb) * ntiles + tile) * kP4;
       if (tid < kM1 / 4) {
@@ -588,6 +627,9 @@ __global__ void __launch_bounds__(256) dec_attn_fwd_kernel(DecAttnP p) {
         stc4(rPT, pout4 + 2 + tid,
              tagf4(make_float4((a0.x + a1.x) + (a2.x + a3.x), (a0.y + a1.y) + (a2.y + a3.y),
                                (a0.z + a1.z) + (a2.z + a3.z), (a0.w + a1.w) + (a2.w + a3.w)), want));
+        if (tid < 2)   // statistics last: consumers poll them before the context words
+          stc4(rPT, pout4 + tid, tagf4(make_float4(red[4 * tid], red[4 * tid + 1], red[4 * tid + 2],
+                                                   red[4 * tid + 3]), want));
       } else if (tid >= 64 && tid < 64 + kM2 / 4) {
         const int jj = tid - 64;
         float4 sm = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -597,16 +639,13 @@ __global__ void __launch_bounds__(256) dec_attn_fwd_kernel(DecAttnP p) {
           sm.x += v.x; sm.y += v.y; sm.z += v.z; sm.w += v.w;
         }
         stc4(rPT, pout4 + 2 + kM1 / 4 + jj, tagf4(sm, want));
-      } else if (tid >= 128 && tid < 130) {
-        const int q = tid - 128;
-        stc4(rPT, pout4 + q, tagf4(make_float4(red[4 * q], red[4 * q + 1], red[4 * q + 2],
-                                               red[4 * q + 3]), want));
       } else if (tid >= 192 && tid < 192 + kPadR + kPadL) {   // first 5, last 4 energies
         const int q = tid - 192;
         stg(rEH, ((t & 1) * B + tb) * ntiles * kEH + tile * kEH + q,
             e1s[q < kPadR ? q : kPN - kPadL + (q - kPadR)], (unsigned)(t + 1));
       }
-      tick(6);
+      tick(10);
+      ev(t, 3);
       // ---- histories nobody waits for: energy tanh (for the BPTT), location features
       if (p.ZH && nl < nt) {
         float* zrow = p.ZH + ((((int64_t)t * B + tb) * N) + n0 + nl) * kQ;
@@ -617,11 +656,11 @@ __global__ void __launch_bounds__(256) dec_attn_fwd_kernel(DecAttnP p) {
       }
       if (p.LOC && tid < kPN * kF && tid / kF < nt)
         p.LOC[(((int64_t)t * B + tb) * N + n0) * kF + tid] = locv;
-      tick(7);
+      tick(11);
     }
   }
   if (p.prof && tid == 0)
-    for (int i = 0; i < 8; ++i) p.prof[blockIdx.x * 8 + i] = tp[i];
+    for (int i = 0; i < 16; ++i) p.prof[blockIdx.x * 16 + i] = tp[i];
 }
 
 }  // namespace
@@ -651,7 +690,8 @@ extern "C" int sat_decoder_attention_fwd(const SatDecAttnFwd* a, void* stream) {
   SAT_CHECK_ARG((a->mask_c == nullptr) == (a->mask_h == nullptr), "sat_decoder_attention_fwd: masks come in pairs");
   SAT_CHECK_ARG(aligned16(a->X0) && aligned16(a->G0) && aligned16(a->K1) && aligned16(a->V1) &&
                 aligned16(a->W0r) && aligned16(a->Wq1) && aligned16(a->Wq2) && aligned16(a->REC0) &&
-                aligned16(a->Q) && aligned16(a->E) && aligned16(a->PART) && aligned16(a->QP),
+                aligned16(a->Q) && aligned16(a->E) && aligned16(a->PART) && aligned16(a->QP) &&
+                aligned16(a->b1),
                 "sat_decoder_attention_fwd: 16-byte aligned operands");
   // the grid must be co-resident (one workgroup per CU): refuse rather than hang
   int dev = 0, cus = 0, per_cu = 0;

@@ -112,6 +112,24 @@ __device__ __forceinline__ float wave_sum_dpp(float v) {
   return (a + b) + (c + d);
 }
 
+// full-wave max: DPP within rows of 16, then 4 readlanes (uniform result)
+__device__ __forceinline__ float wave_max_dpp(float v) {
+  v = group8_max(v);
+  v = fmaxf(v, dpp<0x140>(v));
+  const float a = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
+  const float b = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16));
+  const float c = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
+  const float d = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
+  return fmaxf(fmaxf(a, b), fmaxf(c, d));
+}
+// reductions over lanes 0..7 only (DPP, no LDS crossbar), broadcast as a uniform value
+__device__ __forceinline__ float lanes8_sum(float v) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(group8_sum(v)), 0));
+}
+__device__ __forceinline__ float lanes8_max(float v) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(group8_max(v)), 0));
+}
+
 // tanh via one v_exp_f32 and one reciprocal: |error| ~2e-7 absolute, saturates correctly
 // (exp overflow -> +1, underflow -> -1).  Used for the attention energies (1.4 M per step).
 __device__ __forceinline__ float tanh_fast(float x) {

@@ -74,7 +74,30 @@ __global__ void colreduce_kernel(const float* __restrict__ x, int64_t ldx, const
   if (c < C) {
     float mu = 0.f, rs = 0.f;
     if (mode == 1) { mu = mean[c]; rs = rsqrtf(var[c] + eps); }
-    for (int m = r0 + grp; m < r1; m += 4) {
+    // 4 rows per trip, their loads issued together (the trip is latency-bound otherwise)
+    int m = r0 + grp;
+    for (; m + 12 < r1; m += 16) {
+      float v[4], w[4], gv[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int64_t mm = m + 4 * q;
+        v[q] = x[mm * ldx + c];
+        w[q] = (mode == 1 || (mode == 2 && y)) ? y[mm * ldy + c] : 0.f;
+        gv[q] = (mode == 1 && gate) ? gate[mm * ldg + c] : 1.f;
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (mode == 0) { a1 += v[q]; a2 += (double)v[q] * v[q]; }
+        else if (mode == 1) {
+          const float g = gv[q] <= 0.f ? 0.f : v[q];
+          a1 += g; a2 += (double)g * ((w[q] - mu) * rs);
+        } else {
+          a1 += v[q];
+          if (y) a2 += (double)v[q] * w[q];
+        }
+      }
+    }
+    for (; m < r1; m += 4) {
       float v = x[(int64_t)m * ldx + c];
       if (mode == 0) { a1 += v; a2 += (double)v * v; }
       else if (mode == 1) {
@@ -96,13 +119,32 @@ __global__ void colreduce_kernel(const float* __restrict__ x, int64_t ldx, const
   }
 }
 
+// sum of the RB row-block partials of column c: block = 64 columns x 4 row slices, every
+// thread's loads issued together, the 4 slices combined in a fixed order (deterministic)
+__device__ __forceinline__ void sum_partials(const double* part1, const double* part2, int RB, int C,
+                                             int c, double& s, double& q) {
+  __shared__ double r1[4][64], r2[4][64];
+  const int lane = threadIdx.x & 63, sl = threadIdx.x >> 6;
+  double a = 0.0, b = 0.0;
+  if (c < C) {
+#pragma unroll 16
+    for (int r = sl; r < RB; r += 4) { a += part1[(int64_t)r * C + c]; b += part2[(int64_t)r * C + c]; }
+  }
+  r1[sl][lane] = a;
+  r2[sl][lane] = b;
+  __syncthreads();
+  s = (r1[0][lane] + r1[1][lane]) + (r1[2][lane] + r1[3][lane]);
+  q = (r2[0][lane] + r2[1][lane]) + (r2[2][lane] + r2[3][lane]);
+}
+
 // BN statistics finish: mean, biased var; moving averages (momentum, Bessel-corrected var).
 __global__ void bn_stats_finish_kernel(const double* part1, const double* part2, int RB, int M, int C,
                                        float* mean, float* var, float* mov_mean, float* mov_var,
                                        float momentum) {
-  GRID_STRIDE(c, (int64_t)C) {
-    double s = 0.0, q = 0.0;
-    for (int r = 0; r < RB; ++r) { s += part1[(int64_t)r * C + c]; q += part2[(int64_t)r * C + c]; }
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  double s, q;
+  sum_partials(part1, part2, RB, C, c, s, q);
+  if (threadIdx.x < 64 && c < C) {
     const double mu = s / M;
     const double v = fmax(q / M - mu * mu, 0.0);
     mean[c] = (float)mu;
@@ -120,9 +162,10 @@ __global__ void bn_stats_finish_kernel(const double* part1, const double* part2,
 __global__ void colreduce_finish_kernel(const double* part1, const double* part2, int RB, int C,
                                         float* out1, float* out2, float beta, float* acc1,
                                         float* acc2) {
-  GRID_STRIDE(c, (int64_t)C) {
-    double s = 0.0, q = 0.0;
-    for (int r = 0; r < RB; ++r) { s += part1[(int64_t)r * C + c]; q += part2[(int64_t)r * C + c]; }
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  double s, q;
+  sum_partials(part1, part2, RB, C, c, s, q);
+  if (threadIdx.x < 64 && c < C) {
     if (out1) out1[c] = beta != 0.f ? (float)(beta * out1[c] + s) : (float)s;
     if (out2) out2[c] = beta != 0.f ? (float)(beta * out2[c] + q) : (float)q;
     if (acc1) acc1[c] += (float)s;
@@ -471,7 +514,7 @@ extern "C" int sat_bn_stats(const float* x, int64_t ldx, int32_t M, int32_t C, f
   hipLaunchKernelGGL(colreduce_kernel, dim3(ceil_div(C, 64), RB), dim3(256), 0, s, x, ldx,
                      (const float*)nullptr, (int64_t)0, M, C, p1, p2, 0, (const float*)nullptr,
                      (const float*)nullptr, 0.f, (const float*)nullptr, (int64_t)0);
-  hipLaunchKernelGGL(bn_stats_finish_kernel, dim3(grid_for(C)), dim3(256), 0, s, p1, p2, RB, M, C,
+  hipLaunchKernelGGL(bn_stats_finish_kernel, dim3(ceil_div(C, 64)), dim3(256), 0, s, p1, p2, RB, M, C,
                      mean, var, mov_mean, mov_var, momentum);
   SAT_LAUNCH_CHECK("sat_bn_stats");
   return SAT_OK;
@@ -505,7 +548,7 @@ extern "C" int sat_bn_bwd(const float* dy, int64_t lddy, const float* x, int64_t
   hipLaunchKernelGGL(colreduce_kernel, dim3(ceil_div(C, 64), RB), dim3(256), 0, s, dy, lddy, x,
                      ldx, M, C, p1, p2, 1, mean, var, eps, gate, ldg);
   // dbeta += sum(g), dgamma += sum(g * xhat)  (gradients accumulate into the grad arena)
-  hipLaunchKernelGGL(colreduce_finish_kernel, dim3(grid_for(C)), dim3(256), 0, s, p1, p2, RB, C,
+  hipLaunchKernelGGL(colreduce_finish_kernel, dim3(ceil_div(C, 64)), dim3(256), 0, s, p1, p2, RB, C,
                      sum1, sum2, 0.f, dbeta, dgamma);
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_for((int64_t)M * C)), dim3(256), 0, s, dy,
                      lddy, x, ldx, gate, ldg, dx, lddx, M, C, mean, var, eps, gamma, sum1, sum2,
@@ -525,7 +568,7 @@ extern "C" int sat_colsum(const float* x, int64_t ldx, int32_t M, int32_t C, flo
   hipLaunchKernelGGL(colreduce_kernel, dim3(ceil_div(C, 64), RB), dim3(256), 0, s, x, ldx,
                      (const float*)nullptr, (int64_t)0, M, C, p1, p2, 2, (const float*)nullptr,
                      (const float*)nullptr, 0.f, (const float*)nullptr, (int64_t)0);
-  hipLaunchKernelGGL(colreduce_finish_kernel, dim3(grid_for(C)), dim3(256), 0, s, p1, p2, RB, C,
+  hipLaunchKernelGGL(colreduce_finish_kernel, dim3(ceil_div(C, 64)), dim3(256), 0, s, p1, p2, RB, C,
                      out, (float*)nullptr, beta, (float*)nullptr, (float*)nullptr);
   SAT_LAUNCH_CHECK("sat_colsum");
   return SAT_OK;

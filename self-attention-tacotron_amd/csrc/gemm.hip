@@ -261,13 +261,21 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmP p) {
     }
   };
 
-  f32x16 acc[SM][SN];
+  // NC independent accumulator chains per sub-tile (k-steps round-robin): a wave with a single
+  // 32x32 sub-tile would otherwise issue a chain of dependent MFMAs (measured: MFMA pipe 44 %
+  // busy, 69 % of wave cycles issue-stalled); the copies are summed before the epilogue
+  constexpr int NC = (SM * SN >= 4) ? 1 : 4 / (SM * SN);
+  f32x16 acc[SM][SN], accx[NC > 1 ? NC - 1 : 1][SM][SN];
 #pragma unroll
   for (int i = 0; i < SM; ++i)
 #pragma unroll
     for (int j = 0; j < SN; ++j)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+      for (int r = 0; r < 16; ++r) {
+        acc[i][j][r] = 0.f;
+#pragma unroll
+        for (int c = 0; c < (NC > 1 ? NC - 1 : 1); ++c) accx[c][i][j][r] = 0.f;
+      }
 
   const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
   const int li = lane & 31, lk = lane >> 5;
@@ -280,22 +288,43 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmP p) {
   for (int kt = 0; kt < nk; ++kt) {
     const bool more = kt + 1 < nk;
     if (more) fetch(kbeg + (kt + 1) * BK);
+    // every operand of the K-tile goes to registers first (distinct registers per k-step, so
+    // the LDS round trip is paid once per tile, not once per MFMA group); the next tile's LDS
+    // stash is issued halfway through the MFMA stream
+    float a[BK / 2][SM], b[BK / 2][SN];
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 2) {
-      float a[SM], b[SN];
 #pragma unroll
-      for (int i = 0; i < SM; ++i) a[i] = As[cur][kk + lk][wm + i * 32 + li];
+      for (int i = 0; i < SM; ++i) a[kk / 2][i] = As[cur][kk + lk][wm + i * 32 + li];
 #pragma unroll
-      for (int j = 0; j < SN; ++j) b[j] = Bs[cur][kk + lk][wn + j * 32 + li];
+      for (int j = 0; j < SN; ++j) b[kk / 2][j] = Bs[cur][kk + lk][wn + j * 32 + li];
+    }
+    __builtin_amdgcn_sched_barrier(0);   // keep the reads ahead of the MFMA stream
+#pragma unroll
+    for (int kk = 0; kk < BK / 2; ++kk) {
 #pragma unroll
       for (int i = 0; i < SM; ++i)
 #pragma unroll
-        for (int j = 0; j < SN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < SN; ++j) {
+          if (NC == 1 || kk % NC == 0)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[kk][i], b[kk][j], acc[i][j], 0, 0, 0);
+          else
+            accx[kk % NC - 1][i][j] =
+                __builtin_amdgcn_mfma_f32_32x32x2f32(a[kk][i], b[kk][j], accx[kk % NC - 1][i][j], 0, 0, 0);
+        }
+      if (kk == BK / 4 - 1 && more) stash(cur ^ 1);
     }
-    if (more) stash(cur ^ 1);
     __syncthreads();
     cur ^= 1;
+  }
+
+  if constexpr (NC > 1) {
+#pragma unroll
+    for (int i = 0; i < SM; ++i)
+#pragma unroll
+      for (int j = 0; j < SN; ++j)
+#pragma unroll
+        for (int c = 0; c < NC - 1; ++c) acc[i][j] += accx[c][i][j];
   }
 
   // epilogue: C/D map of 32x32 f32 MFMA: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)

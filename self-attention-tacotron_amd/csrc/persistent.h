@@ -70,7 +70,8 @@ __device__ __forceinline__ v2u ldg(__amdgpu_buffer_rsrc_t r, int granule) {
 //     validity and a 16-byte sc1 store needs no flag, no drain and no barrier.  Slots alternate
 //     by step parity (slot s & 1); the bit for step s is ((s >> 1) + 1) & 1, so a slot's
 //     previous occupant (step s - 2) always carries the other bit and zeroed scratch (LSB 0)
-//     never matches steps 0 and 1.  Cost: <= 1 ulp (6e-8 relative) on the tagged values, which
+//     never matches steps 0 and 1 -- provided every slot's first occupant is written at sequence
+//     number 0 or 1 (a slot first written at 2 would match its zeroes).  Cost: <= 1 ulp (6e-8 relative) on the tagged values, which
 //     every consumer reads identically.  Only finite values are tagged.
 __device__ __forceinline__ unsigned lsb_tag(int s) { return (unsigned)(((s >> 1) + 1) & 1); }
 __device__ __forceinline__ float tagf(float x, unsigned bit) {

@@ -347,7 +347,7 @@ class DecoderAttentionScratch:
     def check(self):
         """Host check of the in-kernel barrier timeout flags (synchronises)."""
         if int(self.err[0].item()) != 0:
-            raise _lib.SatLibraryError("sat_decoder_attention_fwd: a group barrier timed out "
+            raise _lib.SatLibraryError("sat_decoder_attention_fwd: an in-kernel hand-off timed out "
                                        "(workgroups not co-resident?)")
         for i, nm in enumerate(("sat_decoder_lstms_fwd", "sat_decoder_lstms_bwd")):
             if int(self.lstm_err[i, 0].item()) != 0:
@@ -379,7 +379,7 @@ class DecoderAttentionBwdScratch:
 
     def check(self):
         if int(self.err[0].item()) != 0:
-            raise _lib.SatLibraryError("sat_decoder_attention_bwd: a group barrier timed out "
+            raise _lib.SatLibraryError("sat_decoder_attention_bwd: an in-kernel hand-off timed out "
                                        "(workgroups not co-resident?)")
 
 

@@ -374,6 +374,47 @@ typedef struct SatDecLstmBwd {
   int64_t* prof;   /* optional [256][4] per-workgroup segment clocks (100 MHz), NULL = off */
 } SatDecLstmBwd;
 
+/* Persistent encoder BiLSTM: all N steps of both directions of ZoneoutCBHG's bidirectional
+ * ZoneoutLSTM (modules/module.py:93-110, TF bidirectional_dynamic_rnn with sequence_length;
+ * zoneout LSTM cell of ext tacotron2) in ONE launch each way.  Replaces the per-step
+ * sat_lstm_steps_fwd / sat_lstm_steps_bwd launches of model.py encoder_fwd and backward.py
+ * (same arithmetic: TF LSTMCell gate order i j f o, forget_bias 1.0, steps at or beyond the
+ * utterance length copy the state and output 0).  One workgroup per (direction, utterance)
+ * holds the whole recurrent matrix in registers, so a step needs no inter-workgroup hand-off.
+ * U = 128.  X_fw, X_bw = the hoisted input projections + bias, element (b, n, c) at
+ * X + b*x_sb + n*x_sn + c; W_fw, W_bw = recurrent kernel rows [U][U][4]; masks [N][B][U] (all
+ * four or none: eval blend); H = raw outputs, direction d at H + b*h_sb + n*h_sn + d*U + u;
+ * CS and HS [N+1][B][U] states (forward direction: row 0 read as the initial state, row n+1
+ * written at step n; backward direction: row N read, row n written at step n); G [N][B][4U]
+ * activated gates. */
+typedef struct SatEncLstmFwd {
+  int32_t B, N, U;
+  float zc, zh;
+  const float* X_fw; const float* X_bw; int64_t x_sb, x_sn;
+  const float* W_fw; const float* W_bw;
+  const float* mc_fw; const float* mh_fw; const float* mc_bw; const float* mh_bw;
+  const int64_t* lengths;
+  float* H; int64_t h_sb, h_sn;
+  float* CS_fw; float* HS_fw; float* CS_bw; float* HS_bw;
+  float* G_fw; float* G_bw;
+} SatEncLstmFwd;
+
+/* Its BPTT: DY = dL/dH (same layout as H) -> DG_fw, DG_bw [N][B][4U] gate gradients (the input and
+ * weight gradients are whole-sequence GEMMs on the host side). */
+typedef struct SatEncLstmBwd {
+  int32_t B, N, U;
+  float zc, zh;
+  const float* W_fw; const float* W_bw;
+  const float* G_fw; const float* G_bw; const float* CS_fw; const float* CS_bw;
+  const float* mc_fw; const float* mh_fw; const float* mc_bw; const float* mh_bw;
+  const int64_t* lengths;
+  const float* DY; int64_t dy_sb, dy_sn;
+  float* DG_fw; float* DG_bw;
+} SatEncLstmBwd;
+
+int sat_encoder_lstm_fwd(const SatEncLstmFwd* args, void* stream);
+int sat_encoder_lstm_bwd(const SatEncLstmBwd* args, void* stream);
+
 int sat_decoder_lstms_fwd(const SatDecLstmFwd* args, void* stream);
 int64_t sat_decoder_lstms_scratch(int32_t B);
 int64_t sat_decoder_lstms_bwd_scratch(int32_t B);

@@ -104,6 +104,16 @@ SatDecLstmBwd = _struct("SatDecLstmBwd", """
     i32:B i32:T i32:U f32:zc f32:zh ptr:W1r ptr:W2 ptr:G1 ptr:C1S ptr:G2 ptr:C2S ptr:DH2
     ptr:mask1_c ptr:mask1_h ptr:mask2_c ptr:mask2_h ptr:DG1 ptr:DG2 ptr:ctr ptr:err ptr:prof""")
 
+SatEncLstmFwd = _struct("SatEncLstmFwd", """
+    i32:B i32:N i32:U f32:zc f32:zh ptr:X_fw ptr:X_bw i64:x_sb i64:x_sn ptr:W_fw ptr:W_bw
+    ptr:mc_fw ptr:mh_fw ptr:mc_bw ptr:mh_bw ptr:lengths ptr:H i64:h_sb i64:h_sn
+    ptr:CS_fw ptr:HS_fw ptr:CS_bw ptr:HS_bw ptr:G_fw ptr:G_bw""")
+
+SatEncLstmBwd = _struct("SatEncLstmBwd", """
+    i32:B i32:N i32:U f32:zc f32:zh ptr:W_fw ptr:W_bw ptr:G_fw ptr:G_bw ptr:CS_fw ptr:CS_bw
+    ptr:mc_fw ptr:mh_fw ptr:mc_bw ptr:mh_bw ptr:lengths ptr:DY i64:dy_sb i64:dy_sn
+    ptr:DG_fw ptr:DG_bw""")
+
 SatAttnStep = _struct("SatAttnStep", """
     i32:B i32:N i32:D1 i32:M1 i32:D2 i32:M2 i32:F i32:KW i32:NT i32:ntiles i32:att1_forward
     f32:u ptr:q i64:q_sb ptr:K1 ptr:V1 ptr:K2 ptr:V2 ptr:lengths ptr:s_prev ptr:a_prev
@@ -130,6 +140,8 @@ SIGNATURES = {
     "sat_decoder_attention_fwd": [ctypes.POINTER(SatDecAttnFwd), _P],
     "sat_decoder_attention_bwd": [ctypes.POINTER(SatDecAttnBwd), _P],
     "sat_decoder_lstms_fwd": [ctypes.POINTER(SatDecLstmFwd), _P],
+    "sat_encoder_lstm_fwd": [ctypes.POINTER(SatEncLstmFwd), _P],
+    "sat_encoder_lstm_bwd": [ctypes.POINTER(SatEncLstmBwd), _P],
     "sat_decoder_lstms_bwd": [ctypes.POINTER(SatDecLstmBwd), _P],
     "sat_attn_param_grad_rows": [_I32, _I32],
     "sat_attn_param_grads": [ctypes.POINTER(SatAttnParamGrad), _P],

@@ -432,8 +432,20 @@ def encoder_bwd(P, G, hp, d, sv, dm1, dm2, lengths, masks, ws):
             mask_c=None if mc is None else mc[n], mask_h=None if mh is None else mh[n],
             zc=zc, zh=zh, dgates=DGs[dr][n], lengths=lengths)
 
-    for i in range(N):
-        K.lstm_steps_bwd([enc_bwd_desc("fw", False, N - 1 - i), enc_bwd_desc("bw", True, i)])
+    if sv.get("enc_persistent"):
+        # both directions' reverse recurrences in ONE launch (encoder_lstm.hip)
+        mcs = {dr: (mk(f"enc/lstm_{dr}/zc"), mk(f"enc/lstm_{dr}/zh")) for dr, _ in dirs}
+        K.encoder_lstm_bwd(
+            B=B, N=N, U=U, zc=zc, zh=zh,
+            W_fw=P["encoder/cbhg/lstm_fw/kernel"][Win:], W_bw=P["encoder/cbhg/lstm_bw/kernel"][Win:],
+            G_fw=sv["enc_lstm"]["fw"]["G"], G_bw=sv["enc_lstm"]["bw"]["G"],
+            CS_fw=sv["enc_lstm"]["fw"]["CS"], CS_bw=sv["enc_lstm"]["bw"]["CS"],
+            mc_fw=mcs["fw"][0], mh_fw=mcs["fw"][1], mc_bw=mcs["bw"][0], mh_bw=mcs["bw"][1],
+            lengths=lengths, DY=dm1, dy_sb=dm1.stride(0), dy_sn=dm1.stride(1),
+            DG_fw=DGs["fw"], DG_bw=DGs["bw"])
+    else:
+        for i in range(N):
+            K.lstm_steps_bwd([enc_bwd_desc("fw", False, N - 1 - i), enc_bwd_desc("bw", True, i)])
     for i, (dr, rev) in enumerate(dirs):
         st = sv["enc_lstm"][dr]
         Wk = P[f"encoder/cbhg/lstm_{dr}/kernel"]

@@ -1,0 +1,282 @@
+// Persistent encoder BiLSTM: ALL N steps of both directions of ZoneoutCBHG's bidirectional
+// ZoneoutLSTM (modules/module.py:93-110: bidirectional_dynamic_rnn(ZoneoutLSTMCell fw, bw,
+// sequence_length=input_lengths); zoneout cell of ext tacotron2) in ONE launch forward and
+// ONE launch backward.  The arithmetic is lstm.hip's per-step kernels' restated (TF LSTMCell
+// gate order i j f o, forget_bias 1.0, zoneout masks as inputs or the eval blend, steps at or
+// beyond the utterance length copy the state and emit 0); only the schedule differs.
+//
+// Why: the per-step path is N = 200 launches each way (fw step n and bw step N-1-n share one
+// multi-problem launch), each paying a kernel boundary and a cold reload of the recurrent
+// weights.  The recurrent matrix of one direction is U x 4U = 128 x 512 floats = exactly 64
+// floats per thread of a 1024-thread workgroup, so ONE workgroup per (direction, utterance)
+// keeps it in registers for the whole sequence and a step needs no inter-workgroup hand-off at
+// all: two LDS barriers (forward) or one (backward) per step.  2B workgroups, no co-residency
+// requirement.
+#include "sat_common.h"
+#include "persistent.h"
+
+namespace sat {
+namespace {
+
+constexpr int kU = 128;            // units per direction
+constexpr int kG4 = 4 * kU;        // gate columns (512)
+constexpr int kTh = 1024;
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+struct EncFwdP {
+  int B, N;
+  float zc, zh;
+  const float* X[2]; int64_t x_sb, x_sn;
+  const float* W[2];
+  const float* mc[2]; const float* mh[2];
+  const int64_t* lengths;
+  float* H; int64_t h_sb, h_sn;
+  float* CS[2]; float* HS[2]; float* G[2];
+};
+
+struct EncBwdP {
+  int B, N;
+  float zc, zh;
+  const float* W[2]; const float* G[2]; const float* CS[2];
+  const float* mc[2]; const float* mh[2];
+  const int64_t* lengths;
+  const float* DY; int64_t dy_sb, dy_sn;
+  float* DG[2];
+};
+
+// Forward.  Dot role: thread t owns gate column c = t >> 1 and recurrent rows
+// k = 64 (t & 1) .. +64 of it (64 weights in registers); the pair's partial sums meet by DPP.
+// Cell role: threads u < 128 own unit u's (c, h) state in registers.
+__global__ void __launch_bounds__(kTh) enc_lstm_fwd_kernel(EncFwdP p) {
+  __shared__ __attribute__((aligned(16))) float hs[kU];
+  __shared__ __attribute__((aligned(16))) float gp[kG4];
+  const int tid = threadIdx.x;
+  const int d = blockIdx.x & 1, b = blockIdx.x >> 1;
+  const int N = p.N, B = p.B;
+  const int c = tid >> 1, hf = tid & 1;
+  f2 w[32];
+  {
+    const float* W = p.W[d];
+#pragma unroll
+    for (int i = 0; i < 32; ++i)
+      w[i] = f2{W[(int64_t)(64 * hf + 2 * i) * kG4 + c], W[(int64_t)(64 * hf + 2 * i + 1) * kG4 + c]};
+  }
+  const int len = (int)p.lengths[b];
+  const bool cell = tid < kU;
+  const int u = tid;
+  const int r0 = d ? N : 0;                 // initial state row
+  float cst = 0.f, hst = 0.f;
+  if (cell) {
+    cst = p.CS[d][((int64_t)r0 * B + b) * kU + u];
+    hst = p.HS[d][((int64_t)r0 * B + b) * kU + u];
+    hs[u] = hst;
+  }
+  const bool masked = p.mc[0] != nullptr;
+  // operands of processing step i (plain loads), prefetched one step ahead
+  auto load_x = [&](int i) {
+    const int n = d ? N - 1 - i : i;
+    return (hf == 0 && i < N) ? p.X[d][(int64_t)b * p.x_sb + (int64_t)n * p.x_sn + c] : 0.f;
+  };
+  auto load_m = [&](int i, float& mc_, float& mh_) {
+    mc_ = 1.f - p.zc;
+    mh_ = 1.f - p.zh;
+    if (cell && masked && i < N) {
+      const int n = d ? N - 1 - i : i;
+      const int64_t r = ((int64_t)n * B + b) * kU + u;
+      mc_ = p.mc[d][r];
+      mh_ = p.mh[d][r];
+    }
+  };
+  float xn = load_x(0), mcn, mhn;
+  load_m(0, mcn, mhn);
+  __syncthreads();
+  for (int i = 0; i < N; ++i) {
+    const int n = d ? N - 1 - i : i;
+    const int nx = d ? n : n + 1;           // state row written
+    const float xv = xn, mc = mcn, mh = mhn;
+    xn = load_x(i + 1);
+    load_m(i + 1, mcn, mhn);
+    // ---- gate pre-activations: column c, rows 64 hf .. 64 hf + 63
+    {
+      const float4* h4 = reinterpret_cast<const float4*>(&hs[64 * hf]);
+      f2 a0 = {0.f, 0.f}, a1 = {0.f, 0.f};
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const float4 h = h4[q];
+        a0 = __builtin_elementwise_fma(f2{h.x, h.y}, w[2 * q], a0);
+        a1 = __builtin_elementwise_fma(f2{h.z, h.w}, w[2 * q + 1], a1);
+      }
+      float acc = (a0.x + a0.y) + (a1.x + a1.y);
+      acc += dpp<0xB1>(acc);                // the pair (lanes t, t ^ 1) of column c
+      if (hf == 0) gp[c] = acc + xv;
+    }
+    __syncthreads();
+    // ---- cell
+    if (cell) {
+      const float4 g = *reinterpret_cast<const float4*>(&gp[4 * u]);
+      const int64_t bu = (int64_t)b * kU + u;
+      float* Hd = p.H + (int64_t)b * p.h_sb + (int64_t)n * p.h_sn + d * kU + u;
+      if (n < len) {
+        const float gi = sigmf(g.x);
+        const float gj = tanhf(g.y);
+        const float gf = sigmf(g.z + 1.0f);   // forget_bias = 1.0
+        const float go = sigmf(g.w);
+        const float cn = gf * cst + gi * gj;
+        const float hn = go * tanhf(cn);
+        cst = mc * cn + (1.f - mc) * cst;
+        hst = mh * hn + (1.f - mh) * hst;
+        *Hd = hn;
+        reinterpret_cast<float4*>(p.G[d])[(int64_t)n * B * kU + bu] = make_float4(gi, gj, gf, go);
+      } else {   // bidirectional_dynamic_rnn(sequence_length): state copied, output 0
+        *Hd = 0.f;
+        reinterpret_cast<float4*>(p.G[d])[(int64_t)n * B * kU + bu] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+      p.CS[d][(int64_t)nx * B * kU + bu] = cst;
+      p.HS[d][(int64_t)nx * B * kU + bu] = hst;
+      hs[u] = hst;
+    }
+    __syncthreads();
+  }
+}
+
+// Backward.  Recurrent-product role: thread t owns row k = t >> 3 (= unit k) and gate columns
+// 64 (t & 7) .. +64 of it; dL/dh_k = sum over the 8 lanes of the row (DPP).  Pointwise role:
+// lane t = 8u runs unit u's reverse step with its carries in registers.  The gate gradients of
+// the previously processed step sit in LDS (double buffer: one barrier per step).
+__global__ void __launch_bounds__(kTh) enc_lstm_bwd_kernel(EncBwdP p) {
+  __shared__ __attribute__((aligned(16))) float dgn[2][kG4];
+  const int tid = threadIdx.x;
+  const int d = blockIdx.x & 1, b = blockIdx.x >> 1;
+  const int N = p.N, B = p.B;
+  const int k = tid >> 3, sl = tid & 7;
+  f2 w[32];
+  {
+    const float4* W4 = reinterpret_cast<const float4*>(p.W[d] + (int64_t)k * kG4 + 64 * sl);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const float4 v = W4[q];
+      w[2 * q] = f2{v.x, v.y};
+      w[2 * q + 1] = f2{v.z, v.w};
+    }
+  }
+  for (int i = tid; i < kG4; i += kTh) dgn[0][i] = 0.f;
+  const int len = (int)p.lengths[b];
+  const bool lead = sl == 0;
+  const int u = k;
+  const bool masked = p.mc[0] != nullptr;
+  struct Ops { float4 g; float cp, dy, mc, mh; };
+  auto load_ops = [&](int i) {
+    Ops o{make_float4(0.f, 0.f, 0.f, 0.f), 0.f, 0.f, 1.f - p.zc, 1.f - p.zh};
+    if (lead && i < N) {
+      const int n = d ? i : N - 1 - i;
+      const int cprow = d ? n + 1 : n;      // c_{t-1} in processing order of the direction
+      const int64_t bu = (int64_t)b * kU + u;
+      o.g = reinterpret_cast<const float4*>(p.G[d])[(int64_t)n * B * kU + bu];
+      o.cp = p.CS[d][(int64_t)cprow * B * kU + bu];
+      o.dy = p.DY[(int64_t)b * p.dy_sb + (int64_t)n * p.dy_sn + d * kU + u];
+      if (masked) {
+        const int64_t r = ((int64_t)n * B + b) * kU + u;
+        o.mc = p.mc[d][r];
+        o.mh = p.mh[d][r];
+      }
+    }
+    return o;
+  };
+  Ops nxt = load_ops(0);
+  float dh_c = 0.f, dc_c = 0.f;
+  __syncthreads();
+  for (int i = 0; i < N; ++i) {
+    const int n = d ? i : N - 1 - i;
+    const Ops o = nxt;
+    nxt = load_ops(i + 1);
+    // ---- recurrent product of the previously processed step's gate gradients
+    float rec;
+    {
+      const float4* g4 = reinterpret_cast<const float4*>(&dgn[i & 1][64 * sl]);
+      f2 a0 = {0.f, 0.f}, a1 = {0.f, 0.f};
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const float4 g = g4[q];
+        a0 = __builtin_elementwise_fma(f2{g.x, g.y}, w[2 * q], a0);
+        a1 = __builtin_elementwise_fma(f2{g.z, g.w}, w[2 * q + 1], a1);
+      }
+      rec = group8_sum((a0.x + a0.y) + (a1.x + a1.y));
+    }
+    if (lead) {
+      const float dh_t = rec + dh_c;
+      const float dc_t = dc_c;
+      const int64_t bu = (int64_t)b * kU + u;
+      float4 dg = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (n < len) {
+        const float gi = o.g.x, gj = o.g.y, gf = o.g.z, go = o.g.w;
+        const float cn = gf * o.cp + gi * gj;
+        const float tc = tanhf(cn);
+        const float dhn = o.dy + o.mh * dh_t;               // dL/dh'
+        const float dcn = o.mc * dc_t + dhn * go * (1.f - tc * tc);
+        dg = make_float4(dcn * gj * gi * (1.f - gi), dcn * gi * (1.f - gj * gj),
+                         dcn * o.cp * gf * (1.f - gf), dhn * tc * go * (1.f - go));
+        dc_c = dcn * gf + (1.f - o.mc) * dc_t;
+        dh_c = (1.f - o.mh) * dh_t;
+      } else {   // beyond the length: the carries pass through unchanged
+        dh_c = dh_t;
+        dc_c = dc_t;
+      }
+      reinterpret_cast<float4*>(p.DG[d])[(int64_t)n * B * kU + bu] = dg;
+      *reinterpret_cast<float4*>(&dgn[(i + 1) & 1][4 * u]) = dg;
+    }
+    __syncthreads();
+  }
+}
+
+}  // namespace
+}  // namespace sat
+
+using namespace sat;
+
+extern "C" int sat_encoder_lstm_fwd(const SatEncLstmFwd* a, void* stream) {
+  SAT_CHECK_ARG(a && a->B > 0 && a->N > 0, "sat_encoder_lstm_fwd: bad sizes");
+  SAT_CHECK_ARG(a->U == kU, "sat_encoder_lstm_fwd: compiled for U = 128 (cbhg_out_units 256)");
+  SAT_CHECK_ARG(a->X_fw && a->X_bw && a->W_fw && a->W_bw && a->lengths && a->H && a->CS_fw &&
+                a->HS_fw && a->CS_bw && a->HS_bw && a->G_fw && a->G_bw,
+                "sat_encoder_lstm_fwd: null pointer");
+  const bool m0 = a->mc_fw != nullptr;
+  SAT_CHECK_ARG((a->mh_fw != nullptr) == m0 && (a->mc_bw != nullptr) == m0 && (a->mh_bw != nullptr) == m0,
+                "sat_encoder_lstm_fwd: zoneout masks come all four or none");
+  SAT_CHECK_ARG(aligned16(a->G_fw) && aligned16(a->G_bw), "sat_encoder_lstm_fwd: 16-byte aligned gates");
+  EncFwdP p;
+  p.B = a->B; p.N = a->N; p.zc = a->zc; p.zh = a->zh;
+  p.X[0] = a->X_fw; p.X[1] = a->X_bw; p.x_sb = a->x_sb; p.x_sn = a->x_sn;
+  p.W[0] = a->W_fw; p.W[1] = a->W_bw;
+  p.mc[0] = a->mc_fw; p.mh[0] = a->mh_fw; p.mc[1] = a->mc_bw; p.mh[1] = a->mh_bw;
+  p.lengths = a->lengths;
+  p.H = a->H; p.h_sb = a->h_sb; p.h_sn = a->h_sn;
+  p.CS[0] = a->CS_fw; p.HS[0] = a->HS_fw; p.CS[1] = a->CS_bw; p.HS[1] = a->HS_bw;
+  p.G[0] = a->G_fw; p.G[1] = a->G_bw;
+  hipLaunchKernelGGL(enc_lstm_fwd_kernel, dim3(2 * a->B), dim3(kTh), 0, as_stream(stream), p);
+  SAT_LAUNCH_CHECK("sat_encoder_lstm_fwd");
+  return SAT_OK;
+}
+
+extern "C" int sat_encoder_lstm_bwd(const SatEncLstmBwd* a, void* stream) {
+  SAT_CHECK_ARG(a && a->B > 0 && a->N > 0, "sat_encoder_lstm_bwd: bad sizes");
+  SAT_CHECK_ARG(a->U == kU, "sat_encoder_lstm_bwd: compiled for U = 128 (cbhg_out_units 256)");
+  SAT_CHECK_ARG(a->W_fw && a->W_bw && a->G_fw && a->G_bw && a->CS_fw && a->CS_bw && a->lengths &&
+                a->DY && a->DG_fw && a->DG_bw, "sat_encoder_lstm_bwd: null pointer");
+  const bool m0 = a->mc_fw != nullptr;
+  SAT_CHECK_ARG((a->mh_fw != nullptr) == m0 && (a->mc_bw != nullptr) == m0 && (a->mh_bw != nullptr) == m0,
+                "sat_encoder_lstm_bwd: zoneout masks come all four or none");
+  SAT_CHECK_ARG(aligned16(a->W_fw) && aligned16(a->W_bw) && aligned16(a->G_fw) && aligned16(a->G_bw) &&
+                aligned16(a->DG_fw) && aligned16(a->DG_bw),
+                "sat_encoder_lstm_bwd: 16-byte aligned operands");
+  EncBwdP p;
+  p.B = a->B; p.N = a->N; p.zc = a->zc; p.zh = a->zh;
+  p.W[0] = a->W_fw; p.W[1] = a->W_bw; p.G[0] = a->G_fw; p.G[1] = a->G_bw;
+  p.CS[0] = a->CS_fw; p.CS[1] = a->CS_bw;
+  p.mc[0] = a->mc_fw; p.mh[0] = a->mh_fw; p.mc[1] = a->mc_bw; p.mh[1] = a->mh_bw;
+  p.lengths = a->lengths;
+  p.DY = a->DY; p.dy_sb = a->dy_sb; p.dy_sn = a->dy_sn;
+  p.DG[0] = a->DG_fw; p.DG[1] = a->DG_bw;
+  hipLaunchKernelGGL(enc_lstm_bwd_kernel, dim3(2 * a->B), dim3(kTh), 0, as_stream(stream), p);
+  SAT_LAUNCH_CHECK("sat_encoder_lstm_bwd");
+  return SAT_OK;
+}

@@ -391,6 +391,24 @@ def decoder_attention_bwd(**kw):
                "sat_decoder_attention_bwd")
 
 
+def encoder_lstm_fwd(**kw):
+    """sat_encoder_lstm_fwd: all steps of both encoder BiLSTM directions in one launch."""
+    a = _lib.SatEncLstmFwd()
+    for k, v in kw.items():
+        setattr(a, k, _p(v) if isinstance(v, torch.Tensor) else v)
+    _lib.check(_lib.load().sat_encoder_lstm_fwd(ctypes.byref(a), _stream()),
+               "sat_encoder_lstm_fwd")
+
+
+def encoder_lstm_bwd(**kw):
+    """sat_encoder_lstm_bwd: the BPTT of both encoder BiLSTM directions in one launch."""
+    a = _lib.SatEncLstmBwd()
+    for k, v in kw.items():
+        setattr(a, k, _p(v) if isinstance(v, torch.Tensor) else v)
+    _lib.check(_lib.load().sat_encoder_lstm_bwd(ctypes.byref(a), _stream()),
+               "sat_encoder_lstm_bwd")
+
+
 def decoder_lstms_fwd(**kw):
     a = _lib.SatDecLstmFwd()
     for k, v in kw.items():

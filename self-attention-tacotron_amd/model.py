@@ -91,7 +91,8 @@ def sa_transformer_fwd(x, P, scope, heads, causal, probs_mask, sv, key):
     return z
 
 
-def encoder_fwd(P, bn: BNState, hp, d: PR.Dims, ids, lengths, masks, training, ws, sv):
+def encoder_fwd(P, bn: BNState, hp, d: PR.Dims, ids, lengths, masks, training, ws, sv,
+                persistent: bool = False):
     """SelfAttentionCBHGEncoder.call (modules/module.py:425-438) -> (M1, M2)."""
     dev = ids.device
     B, N = ids.shape
@@ -174,8 +175,24 @@ def encoder_fwd(P, bn: BNState, hp, d: PR.Dims, ids, lengths, masks, training, w
                     zc=zc, zh=zh, h_raw=out[:, n], c_out=st["CS"][nxt], h_out=st["HS"][nxt],
                     gates=st["G"][n], lengths=lengths)
 
-    for n in range(N):
-        K.lstm_steps_fwd([enc_step("fw", False, n), enc_step("bw", True, N - 1 - n)])
+    sv["enc_persistent"] = persistent and U == 128
+    if sv["enc_persistent"]:
+        # all N steps of both directions in ONE launch (encoder_lstm.hip: one workgroup per
+        # (direction, utterance) keeps the recurrent matrix in registers)
+        mcs = {dr: (mk(f"enc/lstm_{dr}/zc"), mk(f"enc/lstm_{dr}/zh")) for dr in ("fw", "bw")}
+        X = lstm["fw"]["X"]
+        K.encoder_lstm_fwd(
+            B=B, N=N, U=U, zc=zc, zh=zh, X_fw=lstm["fw"]["X"], X_bw=lstm["bw"]["X"],
+            x_sb=X.stride(0), x_sn=X.stride(1),
+            W_fw=P["encoder/cbhg/lstm_fw/kernel"][hw.shape[-1]:],
+            W_bw=P["encoder/cbhg/lstm_bw/kernel"][hw.shape[-1]:],
+            mc_fw=mcs["fw"][0], mh_fw=mcs["fw"][1], mc_bw=mcs["bw"][0], mh_bw=mcs["bw"][1],
+            lengths=lengths, H=m1, h_sb=m1.stride(0), h_sn=m1.stride(1),
+            CS_fw=lstm["fw"]["CS"], HS_fw=lstm["fw"]["HS"], CS_bw=lstm["bw"]["CS"],
+            HS_bw=lstm["bw"]["HS"], G_fw=lstm["fw"]["G"], G_bw=lstm["bw"]["G"])
+    else:
+        for n in range(N):
+            K.lstm_steps_fwd([enc_step("fw", False, n), enc_step("bw", True, N - 1 - n)])
     sv["enc_lstm"] = lstm
     sv["m1"] = m1
     s0 = K.linear(m1, P["encoder/self_attention_projection/kernel"],
@@ -228,7 +245,8 @@ def model_forward(P, bn: BNState, hp, d: PR.Dims, batch: Dict[str, torch.Tensor]
     """model_fn forward + loss.  Returns (outputs dict, Saved)."""
     sv = Saved()
     ids, lengths = batch["source"], batch["source_length"]
-    m1, m2 = encoder_fwd(P, bn, hp, d, ids, lengths, masks, training, ws, sv)
+    m1, m2 = encoder_fwd(P, bn, hp, d, ids, lengths, masks, training, ws, sv,
+                         persistent=persistent)
     spk = None
     if d.multi_speaker:                                               # models/models.py:43-46,69
         ids_s = batch["speaker_id"]

@@ -53,7 +53,7 @@ def _c_sizeof(struct):
 
 STRUCTS = ["SatGemmDesc", "SatLstmFwd", "SatLstmBwd", "SatAttnStep", "SatAttnStepBwd",
            "SatAttnParamGrad", "SatDecAttnFwd", "SatDecAttnBwd", "SatDecLstmFwd",
-           "SatDecLstmBwd", "SatAdamConfig"]
+           "SatDecLstmBwd", "SatEncLstmFwd", "SatEncLstmBwd", "SatAdamConfig"]
 
 
 def _c_offsets(struct, fields):

@@ -10,7 +10,7 @@
 // weights.  The recurrent matrix of one direction is U x 4U = 128 x 512 floats = exactly 64
 // floats per thread of a 1024-thread workgroup, so ONE workgroup per (direction, utterance)
 // keeps it in registers for the whole sequence and a step needs no inter-workgroup hand-off at
-// all: two LDS barriers (forward) or one (backward) per step.  2B workgroups, no co-residency
+// all: two LDS barriers per step forward, one backward.  2B workgroups, no co-residency
 // requirement.
 #include "sat_common.h"
 #include "persistent.h"
@@ -139,30 +139,30 @@ __global__ void __launch_bounds__(kTh) enc_lstm_fwd_kernel(EncFwdP p) {
   }
 }
 
-// Backward.  Recurrent-product role: thread t owns row k = t >> 3 (= unit k) and gate columns
-// 64 (t & 7) .. +64 of it; dL/dh_k = sum over the 8 lanes of the row (DPP).  Pointwise role:
-// lane t = 8u runs unit u's reverse step with its carries in registers.  The gate gradients of
-// the previously processed step sit in LDS (double buffer: one barrier per step).
+// Backward.  Recurrent product, wave-transposed: wave w owns rows 8w .. 8w+7 (units), lane l
+// gate columns 8l .. 8l+7 of them (64 weights in registers), so a step reads 8 floats of the
+// previous step's gate gradients per lane; the 8 partial row sums are transpose-reduced across
+// the wave and lane 8m runs unit 8w+m's reverse step with its carries in registers.  The gate
+// gradients of the previously processed step sit in LDS (double buffer: one barrier per step).
 __global__ void __launch_bounds__(kTh) enc_lstm_bwd_kernel(EncBwdP p) {
   __shared__ __attribute__((aligned(16))) float dgn[2][kG4];
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int d = blockIdx.x & 1, b = blockIdx.x >> 1;
   const int N = p.N, B = p.B;
-  const int k = tid >> 3, sl = tid & 7;
-  f2 w[32];
+  f2 w[8][4];                              // row 8w + r, column pairs 8l + 2cp, +1
   {
-    const float4* W4 = reinterpret_cast<const float4*>(p.W[d] + (int64_t)k * kG4 + 64 * sl);
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const float4 v = W4[q];
-      w[2 * q] = f2{v.x, v.y};
-      w[2 * q + 1] = f2{v.z, v.w};
+    for (int r = 0; r < 8; ++r) {
+      const float4* src = reinterpret_cast<const float4*>(p.W[d] + (int64_t)(8 * wave + r) * kG4 + 8 * lane);
+      const float4 a0 = src[0], a1 = src[1];
+      w[r][0] = f2{a0.x, a0.y}; w[r][1] = f2{a0.z, a0.w};
+      w[r][2] = f2{a1.x, a1.y}; w[r][3] = f2{a1.z, a1.w};
     }
   }
   for (int i = tid; i < kG4; i += kTh) dgn[0][i] = 0.f;
   const int len = (int)p.lengths[b];
-  const bool lead = sl == 0;
-  const int u = k;
+  const bool lead = (lane & 7) == 0;
+  const int u = 8 * wave + (lane >> 3);
   const bool masked = p.mc[0] != nullptr;
   struct Ops { float4 g; float cp, dy, mc, mh; };
   auto load_ops = [&](int i) {
@@ -190,20 +190,23 @@ __global__ void __launch_bounds__(kTh) enc_lstm_bwd_kernel(EncBwdP p) {
     const Ops o = nxt;
     nxt = load_ops(i + 1);
     // ---- recurrent product of the previously processed step's gate gradients
-    float rec;
+    float v[8];
     {
-      const float4* g4 = reinterpret_cast<const float4*>(&dgn[i & 1][64 * sl]);
-      f2 a0 = {0.f, 0.f}, a1 = {0.f, 0.f};
+      const float4* g4 = reinterpret_cast<const float4*>(&dgn[i & 1][8 * lane]);
+      const float4 ga = g4[0], gb = g4[1];
+      const f2 g[4] = {f2{ga.x, ga.y}, f2{ga.z, ga.w}, f2{gb.x, gb.y}, f2{gb.z, gb.w}};
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const float4 g = g4[q];
-        a0 = __builtin_elementwise_fma(f2{g.x, g.y}, w[2 * q], a0);
-        a1 = __builtin_elementwise_fma(f2{g.z, g.w}, w[2 * q + 1], a1);
+      for (int r = 0; r < 8; ++r) {
+        f2 a = g[0] * w[r][0];
+        a = __builtin_elementwise_fma(g[1], w[r][1], a);
+        a = __builtin_elementwise_fma(g[2], w[r][2], a);
+        a = __builtin_elementwise_fma(g[3], w[r][3], a);
+        v[r] = a.x + a.y;
       }
-      rec = group8_sum((a0.x + a0.y) + (a1.x + a1.y));
     }
+    transpose_reduce8(v, lane);
     if (lead) {
-      const float dh_t = rec + dh_c;
+      const float dh_t = v[0] + dh_c;
       const float dc_t = dc_c;
       const int64_t bu = (int64_t)b * kU + u;
       float4 dg = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -242,7 +245,9 @@ extern "C" int sat_encoder_lstm_fwd(const SatEncLstmFwd* a, void* stream) {
   const bool m0 = a->mc_fw != nullptr;
   SAT_CHECK_ARG((a->mh_fw != nullptr) == m0 && (a->mc_bw != nullptr) == m0 && (a->mh_bw != nullptr) == m0,
                 "sat_encoder_lstm_fwd: zoneout masks come all four or none");
-  SAT_CHECK_ARG(aligned16(a->G_fw) && aligned16(a->G_bw), "sat_encoder_lstm_fwd: 16-byte aligned gates");
+  SAT_CHECK_ARG(aligned16(a->G_fw) && aligned16(a->G_bw) && aligned16(a->W_fw) && aligned16(a->W_bw) &&
+                aligned16(a->X_fw) && aligned16(a->X_bw) && a->x_sb % 4 == 0 && a->x_sn % 4 == 0,
+                "sat_encoder_lstm_fwd: 16-byte aligned operands");
   EncFwdP p;
   p.B = a->B; p.N = a->N; p.zc = a->zc; p.zh = a->zh;
   p.X[0] = a->X_fw; p.X[1] = a->X_bw; p.x_sb = a->x_sb; p.x_sn = a->x_sn;

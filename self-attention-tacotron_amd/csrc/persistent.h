@@ -148,6 +148,20 @@ __device__ __forceinline__ void transpose_reduce32(float* v, int lane) {
   tr_dpp<2, 1>(v, lane);
   v[0] += dpp_mov<0xB1>(v[0]);   // quad_perm [1,0,3,2]: lane l ^ 1
 }
+// 8 outputs: lanes 8m..8m+7 hold output m
+__device__ __forceinline__ void transpose_reduce8(float* v, int lane) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) v[i] = fsum_swap32(v[i], v[i + 4]);
+#pragma unroll
+  for (int i = 0; i < 2; ++i) v[i] = fsum_swap16(v[i], v[i + 2]);
+  tr_dpp<8, 1>(v, lane);
+  {   // lane bit 2: partner l ^ 4 via row shifts
+    const float up = dpp_mov<0x104>(v[0]), dn = dpp_mov<0x114>(v[0]);
+    v[0] += (lane & 4) ? dn : up;
+  }
+  v[0] += dpp_mov<0x4E>(v[0]);   // lane l ^ 2
+  v[0] += dpp_mov<0xB1>(v[0]);   // lane l ^ 1
+}
 // 16 outputs: lanes 4m..4m+3 hold output m
 __device__ __forceinline__ void transpose_reduce16(float* v, int lane) {
 #pragma unroll

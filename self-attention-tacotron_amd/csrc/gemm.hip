@@ -4,7 +4,7 @@
 // products, the Conv1D(SAME) of the CBHG (implicit im2col in the A loader -- no im2col buffer
 // in HBM) and all their gradients (transposes are strides; conv dX / dW are A/B modes).
 //
-// Tile: BM x BN x 32, 256 threads = 4 waves in a 2x2 grid, each wave (BM/2)x(BN/2) made of
+// Tile: BM x BN x 32, GM x GN waves (default 2x2 = 256 threads), each wave (BM/GM)x(BN/GN) of
 // 32x32 MFMA sub-tiles.  Global -> registers (tile k+1 prefetched while tile k is multiplied,
 // 16-byte loads whenever the contiguous dimension allows) -> double-buffered LDS ([k][m] /
 // [k][n] images) -> one f32 per lane per MFMA operand; one barrier per K-tile.
@@ -12,6 +12,8 @@
 // tiles to fill 256 CUs: they run split-K into an fp32 workspace slab [S][M][N] and a second
 // launch sums the slabs in a fixed order and applies the epilogue (deterministic, no atomics).
 #include "sat_common.h"
+
+#include <cstdlib>
 
 namespace sat {
 namespace {
@@ -85,20 +87,21 @@ __device__ __forceinline__ float apply_act(float v, int act) {
 
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 
-template <int BM, int BN, int AM, int BMD>
-__global__ void __launch_bounds__(256) gemm_kernel(GemmP p) {
-  constexpr int WM = BM / 2, WN = BN / 2;
+template <int BM, int BN, int AM, int BMD, int GM = 2, int GN = 2>
+__global__ void __launch_bounds__(64 * GM * GN) gemm_kernel(GemmP p) {
+  constexpr int NT = 64 * GM * GN;                               // GM x GN waves
+  constexpr int WM = BM / GM, WN = BN / GN;
   constexpr int SM = WM / 32, SN = WN / 32;
   constexpr bool A_MC = (AM == A_M || AM == A_IM2COLT);        // loads run along m
   constexpr bool B_NC = (BMD == B_N);                          // loads run along n
   constexpr int PA = A_MC ? 4 : 1, PB = B_NC ? 4 : 1;          // LDS row padding
-  constexpr int NA = (AM == A_GEN) ? BM * BK / 256 : BM * BK / 1024;   // per thread
-  constexpr int NB = (BMD == B_GEN) ? BN * BK / 256 : BN * BK / 1024;
+  constexpr int NA = (AM == A_GEN) ? BM * BK / NT : BM * BK / (4 * NT);   // per thread
+  constexpr int NB = (BMD == B_GEN) ? BN * BK / NT : BN * BK / (4 * NT);
   __shared__ __attribute__((aligned(16))) float As[2][BK][BM + PA];
   __shared__ __attribute__((aligned(16))) float Bs[2][BK][BN + PB];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = (wave >> 1) * WM, wn = (wave & 1) * WN;
+  const int wm = (wave / GN) * WM, wn = (wave % GN) * WN;
   int tx = blockIdx.x, ty = blockIdx.y;
   if (p.remap) {   // bijective XCD swizzle: consecutive tiles (one A row panel) share an L2
     const int nwg = gridDim.x * gridDim.y, orig = blockIdx.y * gridDim.x + blockIdx.x;
@@ -123,7 +126,7 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmP p) {
   if constexpr (AM == A_IM2COL) {
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
-      const int gm = m0 + ((tid + i * 256) >> 3);
+      const int gm = m0 + ((tid + i * NT) >> 3);
       const int s = gm / p.a_L, n = gm - s * p.a_L;
       arow[i] = A + (int64_t)s * p.a_L * p.a_sm;
       an[i] = gm < p.M ? n : -(1 << 28);
@@ -132,7 +135,7 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmP p) {
   if constexpr (AM == A_IM2COLT) {
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
-      const int pos = kbeg + (tid + i * 256) / (BM / 4);
+      const int pos = kbeg + (tid + i * NT) / (BM / 4);
       aps[i] = pos / p.a_L;
       apn[i] = pos - aps[i] * p.a_L;
     }
@@ -150,14 +153,14 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmP p) {
     if constexpr (AM == A_K) {
 #pragma unroll
       for (int i = 0; i < NA; ++i) {
-        const int e = tid + i * 256, m = e >> 3, kq = (e & 7) * 4;
+        const int e = tid + i * NT, m = e >> 3, kq = (e & 7) * 4;
         const int gm = m0 + m, gk = k0 + kq;
         ra4[i] = (gm < p.M && gk < kend) ? ld4(A + (int64_t)gm * p.a_sm + gk) : z4;
       }
     } else if constexpr (AM == A_M) {
 #pragma unroll
       for (int i = 0; i < NA; ++i) {
-        const int e = tid + i * 256, k = e / (BM / 4), mq = (e % (BM / 4)) * 4;
+        const int e = tid + i * NT, k = e / (BM / 4), mq = (e % (BM / 4)) * 4;
         const int gm = m0 + mq, gk = k0 + k;
         ra4[i] = (gm < p.M && gk < kend) ? ld4(A + (int64_t)gk * p.a_sk + gm) : z4;
       }
@@ -165,7 +168,7 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmP p) {
       const int tap = k0 / p.a_C, c0 = k0 - tap * p.a_C;
 #pragma unroll
       for (int i = 0; i < NA; ++i) {
-        const int kq = ((tid + i * 256) & 7) * 4;
+        const int kq = ((tid + i * NT) & 7) * 4;
         const int row = an[i] + tap - p.a_shift;
         const bool ok = row >= 0 && row < p.a_L && k0 + kq < kend;
         ra4[i] = ok ? ld4(arow[i] + (int64_t)row * p.a_sm + c0 + kq) : z4;
@@ -173,7 +176,7 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmP p) {
     } else if constexpr (AM == A_IM2COLT) {
 #pragma unroll
       for (int i = 0; i < NA; ++i) {
-        const int e = tid + i * 256, k = e / (BM / 4), mq = (e % (BM / 4)) * 4;
+        const int e = tid + i * NT, k = e / (BM / 4), mq = (e % (BM / 4)) * 4;
         const int row = apn[i] + atap - p.a_shift;
         const bool ok = (k0 + k < kend) && row >= 0 && row < p.a_L && (m0 + mq < p.M);
         ra4[i] = ok ? ld4(A + (int64_t)(aps[i] * p.a_L + row) * p.a_sm + ac0 + mq) : z4;
@@ -183,21 +186,21 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmP p) {
     } else {
 #pragma unroll
       for (int i = 0; i < NA; ++i) {
-        const int e = tid + i * 256, m = e / BK, k = e % BK;
+        const int e = tid + i * NT, m = e / BK, k = e % BK;
         ras[i] = (k0 + k < kend) ? load_a(p, A, m0 + m, k0 + k) : 0.f;
       }
     }
     if constexpr (BMD == B_N) {
 #pragma unroll
       for (int i = 0; i < NB; ++i) {
-        const int e = tid + i * 256, k = e / (BN / 4), nq = (e % (BN / 4)) * 4;
+        const int e = tid + i * NT, k = e / (BN / 4), nq = (e % (BN / 4)) * 4;
         const int gk = k0 + k, gn = n0 + nq;
         rb4[i] = (gk < kend && gn < p.N) ? ld4(B + (int64_t)gk * p.b_sk + gn) : z4;
       }
     } else if constexpr (BMD == B_K) {
 #pragma unroll
       for (int i = 0; i < NB; ++i) {
-        const int e = tid + i * 256, n = e >> 3, kq = (e & 7) * 4;
+        const int e = tid + i * NT, n = e >> 3, kq = (e & 7) * 4;
         const int gk = k0 + kq, gn = n0 + n;
         rb4[i] = (gk < kend && gn < p.N) ? ld4(B + (int64_t)gn * p.b_sn + gk) : z4;
       }
@@ -206,14 +209,14 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmP p) {
       const float* Wt = B + (int64_t)(p.b_taps - 1 - tap) * p.N * p.b_C + o0;
 #pragma unroll
       for (int i = 0; i < NB; ++i) {
-        const int e = tid + i * 256, n = e >> 3, kq = (e & 7) * 4;
+        const int e = tid + i * NT, n = e >> 3, kq = (e & 7) * 4;
         const int gn = n0 + n;
         rb4[i] = (gn < p.N && k0 + kq < kend) ? ld4(Wt + (int64_t)gn * p.b_C + kq) : z4;
       }
     } else {
 #pragma unroll
       for (int i = 0; i < NB; ++i) {
-        const int e = tid + i * 256, n = e / BK, k = e % BK;
+        const int e = tid + i * NT, n = e / BK, k = e % BK;
         rbs[i] = (k0 + k < kend) ? load_b(p, B, k0 + k, n0 + n) : 0.f;
       }
     }
@@ -222,40 +225,40 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmP p) {
     if constexpr (AM == A_K || AM == A_IM2COL) {
 #pragma unroll
       for (int i = 0; i < NA; ++i) {
-        const int e = tid + i * 256, m = e >> 3, kq = (e & 7) * 4;
+        const int e = tid + i * NT, m = e >> 3, kq = (e & 7) * 4;
         As[buf][kq + 0][m] = ra4[i].x; As[buf][kq + 1][m] = ra4[i].y;
         As[buf][kq + 2][m] = ra4[i].z; As[buf][kq + 3][m] = ra4[i].w;
       }
     } else if constexpr (AM == A_M || AM == A_IM2COLT) {
 #pragma unroll
       for (int i = 0; i < NA; ++i) {
-        const int e = tid + i * 256, k = e / (BM / 4), mq = (e % (BM / 4)) * 4;
+        const int e = tid + i * NT, k = e / (BM / 4), mq = (e % (BM / 4)) * 4;
         *reinterpret_cast<float4*>(&As[buf][k][mq]) = ra4[i];
       }
     } else {
 #pragma unroll
       for (int i = 0; i < NA; ++i) {
-        const int e = tid + i * 256, m = e / BK, k = e % BK;
+        const int e = tid + i * NT, m = e / BK, k = e % BK;
         As[buf][k][m] = ras[i];
       }
     }
     if constexpr (BMD == B_N) {
 #pragma unroll
       for (int i = 0; i < NB; ++i) {
-        const int e = tid + i * 256, k = e / (BN / 4), nq = (e % (BN / 4)) * 4;
+        const int e = tid + i * NT, k = e / (BN / 4), nq = (e % (BN / 4)) * 4;
         *reinterpret_cast<float4*>(&Bs[buf][k][nq]) = rb4[i];
       }
     } else if constexpr (BMD == B_K || BMD == B_FLIP) {
 #pragma unroll
       for (int i = 0; i < NB; ++i) {
-        const int e = tid + i * 256, n = e >> 3, kq = (e & 7) * 4;
+        const int e = tid + i * NT, n = e >> 3, kq = (e & 7) * 4;
         Bs[buf][kq + 0][n] = rb4[i].x; Bs[buf][kq + 1][n] = rb4[i].y;
         Bs[buf][kq + 2][n] = rb4[i].z; Bs[buf][kq + 3][n] = rb4[i].w;
       }
     } else {
 #pragma unroll
       for (int i = 0; i < NB; ++i) {
-        const int e = tid + i * 256, n = e / BK, k = e % BK;
+        const int e = tid + i * NT, n = e / BK, k = e % BK;
         Bs[buf][k][n] = rbs[i];
       }
     }
@@ -438,11 +441,11 @@ extern "C" int sat_gemm_rowdot(int32_t M, int32_t N, int32_t K, const float* A, 
 
 using namespace sat;
 
-template <int BM, int BN>
+template <int BM, int BN, int GM = 2, int GN = 2>
 static hipError_t launch_tiles(int am, int bm, dim3 grid, hipStream_t s, const GemmP& p) {
 #define SAT_GEMM_CASE(A_, B_)                                                               \
   if (am == A_ && bm == B_) {                                                               \
-    hipLaunchKernelGGL((gemm_kernel<BM, BN, A_, B_>), grid, dim3(256), 0, s, p);            \
+    hipLaunchKernelGGL((gemm_kernel<BM, BN, A_, B_, GM, GN>), grid, dim3(64 * GM * GN), 0, s, p);            \
     return hipGetLastError();                                                               \
   }
   SAT_GEMM_CASE(A_K, B_N)
@@ -453,7 +456,7 @@ static hipError_t launch_tiles(int am, int bm, dim3 grid, hipStream_t s, const G
   SAT_GEMM_CASE(A_IM2COL, B_FLIP)
   SAT_GEMM_CASE(A_IM2COLT, B_N)
 #undef SAT_GEMM_CASE
-  hipLaunchKernelGGL((gemm_kernel<BM, BN, A_GEN, B_GEN>), grid, dim3(256), 0, s, p);
+  hipLaunchKernelGGL((gemm_kernel<BM, BN, A_GEN, B_GEN, GM, GN>), grid, dim3(64 * GM * GN), 0, s, p);
   return hipGetLastError();
 }
 
@@ -485,7 +488,14 @@ extern "C" int sat_gemm(const SatGemmDesc* d, void* stream) {
   p.add = d->add; p.add_sm = d->add_sm; p.add_sbatch = d->add_sbatch;
   hipStream_t s = as_stream(stream);
   const int nb = d->batch * p.batch2;
-  const bool big = (int64_t)d->M * d->N * nb >= (int64_t)256 * 128 * 128 && d->N >= 96 && d->M >= 96;
+  // 128x128 tiles when the output is large, and for long-K weight-gradient products whose
+  // output is wide enough (split-K then supplies the workgroups; measured per shape with
+  // tools/gemm_census.py: 544x1024x16000 354 -> 262 us, 6144x128x6400 191 -> 136 us, while
+  // 256x256 / 128x512 outputs are faster on 64x64 tiles)
+  const bool wide_dw = nb == 1 && d->K >= 4096 && d->ws != nullptr &&
+                       ((d->M >= 256 && d->N >= 512) || d->M >= 2048);
+  const bool big = ((int64_t)d->M * d->N * nb >= (int64_t)256 * 128 * 128 || wide_dw) &&
+                   d->N >= 96 && d->M >= 96;
   const int BMs = big ? 128 : 64;
   // ---- operand loader variants (vector paths need 16-B aligned rows / batch strides)
   const bool astr = (p.a_sbatch % 4 == 0) && (p.a_sbatch2 % 4 == 0) && aligned16(d->A);
@@ -525,6 +535,8 @@ extern "C" int sat_gemm(const SatGemmDesc* d, void* stream) {
   p.remap = (gx * gy >= 16) ? 1 : 0;
   const int gz = p.splits > 1 ? p.splits : nb;
   const dim3 grid(gx, gy, gz);
+  // (a 4x2-wave 128x128 variant, gemm_kernel<128, 128, ., ., 4, 2>, measured 2-15 % slower on
+  // the step's shapes: tile and wave shape are not what limits this kernel)
   const hipError_t e = big ? launch_tiles<128, 128>(am, bm, grid, s, p)
                            : launch_tiles<64, 64>(am, bm, grid, s, p);
   if (e != hipSuccess) {

@@ -373,21 +373,53 @@ __global__ void __launch_bounds__(64 * GM * GN) gemm_kernel(GemmP p) {
     }
 }
 
-// split-K finish: sum S slabs in order, then the same epilogue as gemm_kernel (batch == 1)
+// split-K finish: sum S slabs in order, then the same epilogue as gemm_kernel (batch == 1).
+// Four consecutive outputs per thread (16-byte slab loads when N % 4 == 0) and four slab loads
+// in flight per trip: the pass is latency-bound, not bandwidth-bound, at these sizes.
+__device__ __forceinline__ float splitk_epilogue(const GemmP& p, int row, int col, float s) {
+  float* dst = p.C + (int64_t)row * p.c_sm + col;
+  float v = p.alpha * s;
+  if (p.beta != 0.f) v += p.beta * (*dst);
+  v = apply_act(v + (p.bias ? p.bias[col] : 0.f), p.act);
+  if (p.mul) v *= p.mul[(int64_t)row * p.mul_sm + col];
+  if (p.add) v += p.add[(int64_t)row * p.add_sm + col];
+  return v;
+}
 __global__ void __launch_bounds__(256) gemm_splitk_reduce(GemmP p) {
   const int64_t total = (int64_t)p.M * p.N;
+  if ((p.N & 3) == 0) {
+    const int64_t total4 = total >> 2;
+    const float4* ws4 = reinterpret_cast<const float4*>(p.ws);
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total4;
+         i += (int64_t)gridDim.x * blockDim.x) {
+      float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+      int k = 0;
+      for (; k + 4 <= p.splits; k += 4) {
+        float4 v[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = ws4[(int64_t)(k + q) * total4 + i];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) { a.x += v[q].x; a.y += v[q].y; a.z += v[q].z; a.w += v[q].w; }
+      }
+      for (; k < p.splits; ++k) {
+        const float4 v = ws4[(int64_t)k * total4 + i];
+        a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+      }
+      const int row = (int)((4 * i) / p.N), col = (int)(4 * i - (int64_t)row * p.N);
+      float* dst = p.C + (int64_t)row * p.c_sm + col;
+      dst[0] = splitk_epilogue(p, row, col, a.x);
+      dst[1] = splitk_epilogue(p, row, col + 1, a.y);
+      dst[2] = splitk_epilogue(p, row, col + 2, a.z);
+      dst[3] = splitk_epilogue(p, row, col + 3, a.w);
+    }
+    return;
+  }
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * blockDim.x) {
     const int row = (int)(i / p.N), col = (int)(i - (int64_t)row * p.N);
     float s = 0.f;
     for (int k = 0; k < p.splits; ++k) s += p.ws[(int64_t)k * total + i];
-    float* dst = p.C + (int64_t)row * p.c_sm + col;
-    float v = p.alpha * s;
-    if (p.beta != 0.f) v += p.beta * (*dst);
-    v = apply_act(v + (p.bias ? p.bias[col] : 0.f), p.act);
-    if (p.mul) v *= p.mul[(int64_t)row * p.mul_sm + col];
-    if (p.add) v += p.add[(int64_t)row * p.add_sm + col];
-    *dst = v;
+    p.C[(int64_t)row * p.c_sm + col] = splitk_epilogue(p, row, col, s);
   }
 }
 
@@ -545,7 +577,8 @@ extern "C" int sat_gemm(const SatGemmDesc* d, void* stream) {
   }
   if (p.splits > 1) {
     const int64_t total = (int64_t)d->M * d->N;
-    const int blocks = (int)std::min<int64_t>((total + 255) / 256, 2048);
+    const int64_t work = (d->N % 4 == 0) ? total / 4 : total;
+    const int blocks = (int)std::min<int64_t>((work + 255) / 256, 2048);
     hipLaunchKernelGGL(gemm_splitk_reduce, dim3(blocks), dim3(256), 0, s, p);
     SAT_LAUNCH_CHECK("sat_gemm(split-k reduce)");
   }

@@ -42,7 +42,7 @@ constexpr int kX = 3 * kU;         // forward staging row: [h1_{i-1} | h1'_{i-1}
 static_assert(kUW == 2 * (kThreads / 64), "two units per wave");
 
 struct DecLstmFwdP {
-  int B, T;
+  int B, T, flags;
   float zc, zh;
   const float* X1;                                    // [T][B][4U]
   const float* W1r;                                   // [U][U][4]
@@ -148,6 +148,8 @@ __global__ void __launch_bounds__(kThreads) dec_lstm_fwd_kernel(DecLstmFwdP p) {
   load_ops(0, xpn, mcn, mhn);
 
   // optional segment clocks (thread 0): hand-off wait, staging, dots, cell + publish
+  // hand-off store policy (persistent.h xcd_local_group): plain stores iff the group is on one XCD
+  const bool xl = (p.flags & 1) ? xcd_local_group(reinterpret_cast<unsigned*>(p.xch + (size_t)12 * B * kU), g, kG, kGW, p.err) : false;
   long long tp[4] = {0, 0, 0, 0};
   long long t0 = wall_clock64();
   auto tick = [&](int seg) {
@@ -258,7 +260,7 @@ __global__ void __launch_bounds__(kThreads) dec_lstm_fwd_kernel(DecLstmFwdP p) {
       if (layer == 0) {
         if (i < T) {
           const float tg = __uint_as_float((unsigned)(i + 1));
-          stc4(rXA, ((((i + 1) & 1) * B + pb) * kU + pu), make_float4(h2, tg, hn, tg));
+          stc4x(xl, rXA, ((((i + 1) & 1) * B + pb) * kU + pu), make_float4(h2, tg, hn, tg));
         }
         p.H1RAW[bu] = hn;
         p.H1S[bn] = h2;
@@ -276,7 +278,7 @@ __global__ void __launch_bounds__(kThreads) dec_lstm_fwd_kernel(DecLstmFwdP p) {
     const float hpart = dpp_mov<0x108>(hpub);
     if (cell && layer == 1 && puu == 0 && i < T) {
       const float tg = __uint_as_float((unsigned)(i + 1));
-      stc4(rXB, ((((i + 1) & 1) * B + pb) * (kU / 2) + (pu >> 1)), make_float4(hpub, tg, hpart, tg));
+      stc4x(xl, rXB, ((((i + 1) & 1) * B + pb) * (kU / 2) + (pu >> 1)), make_float4(hpub, tg, hpart, tg));
     }
     tick(3);
   }
@@ -285,7 +287,7 @@ __global__ void __launch_bounds__(kThreads) dec_lstm_fwd_kernel(DecLstmFwdP p) {
 }
 
 struct DecLstmBwdP {
-  int B, T;
+  int B, T, flags;
   float zc, zh;
   const float* W1r;                                   // [U][U][4]
   const float* W2;                                    // [2U][U][4]
@@ -388,6 +390,8 @@ __global__ void __launch_bounds__(kThreads) dec_lstm_bwd_kernel(DecLstmBwdP p) {
   load_ops(0, g4n, cpn, dyn, mcn, mhn);
 
   // optional segment clocks (thread 0): barrier wait, staging loads, dots, cells + stores
+  // hand-off store policy (persistent.h xcd_local_group): plain stores iff the group is on one XCD
+  const bool xl = (p.flags & 1) ? xcd_local_group(p.ctr + kG * 64, g, kG, kGW, p.err) : false;
   long long tp[4] = {0, 0, 0, 0};
   long long t0 = wall_clock64();
   auto tick = [&](int seg) {
@@ -465,7 +469,7 @@ __global__ void __launch_bounds__(kThreads) dec_lstm_bwd_kernel(DecLstmBwdP p) {
       const float dy = layer == 2 ? dyv : y1v;
       const float4 dg = lstm_cell_bwd(g4, cp, dy, rec, mc, mh, dhc, dcc);
       const int64_t bu = ((int64_t)t * B + pb) * kU + pu;
-      stc4(layer == 2 ? rDG2 : rDG1, (int)bu, dg);
+      stc4x(xl, layer == 2 ? rDG2 : rDG1, (int)bu, dg);
     }
     tick(3);
     if (jj < T) group_barrier(ctr, (unsigned)(jj + 1) * kGW, p.err);
@@ -494,12 +498,12 @@ int check_coresident(const void* kernel, const char* name) {
 using namespace sat;
 
 extern "C" int64_t sat_decoder_lstms_scratch(int32_t B) {
-  return (int64_t)12 * B * kU;       // XA [2][B][U] + XB [2][B][U/2] 16-byte granule pairs
+  return (int64_t)12 * B * kU + kG * kGW;   // XA [2][B][U] + XB [2][B][U/2] granule pairs + XID
 }
 
 extern "C" int64_t sat_decoder_lstms_bwd_scratch(int32_t B) {
   (void)B;
-  return kG * 64;                    // group counter words
+  return kG * 64 + kG * kGW;         // group counter words + XID
 }
 
 extern "C" int sat_decoder_lstms_fwd(const SatDecLstmFwd* a, void* stream) {
@@ -525,7 +529,7 @@ extern "C" int sat_decoder_lstms_fwd(const SatDecLstmFwd* a, void* stream) {
   p.m1c = a->mask1_c; p.m1h = a->mask1_h; p.m2c = a->mask2_c; p.m2h = a->mask2_h;
   p.H1RAW = a->H1RAW; p.C1S = a->C1S; p.H1S = a->H1S; p.G1 = a->G1;
   p.H2RAW = a->H2RAW; p.C2S = a->C2S; p.H2S = a->H2S; p.G2 = a->G2;
-  p.xch = a->xch; p.err = a->err;
+  p.xch = a->xch; p.err = a->err; p.flags = xcd_local_env();
   p.prof = reinterpret_cast<long long*>(a->prof);
   hipStream_t s = as_stream(stream);
   if (hipMemsetAsync(a->xch, 0, sat_decoder_lstms_scratch(a->B) * sizeof(float), s) != hipSuccess ||
@@ -559,10 +563,10 @@ extern "C" int sat_decoder_lstms_bwd(const SatDecLstmBwd* a, void* stream) {
   p.W1r = a->W1r; p.W2 = a->W2; p.G1 = a->G1; p.C1S = a->C1S; p.G2 = a->G2; p.C2S = a->C2S;
   p.DH2 = a->DH2;
   p.m1c = a->mask1_c; p.m1h = a->mask1_h; p.m2c = a->mask2_c; p.m2h = a->mask2_h;
-  p.DG1 = a->DG1; p.DG2 = a->DG2; p.ctr = a->ctr; p.err = a->err;
+  p.DG1 = a->DG1; p.DG2 = a->DG2; p.ctr = a->ctr; p.err = a->err; p.flags = xcd_local_env();
   p.prof = reinterpret_cast<long long*>(a->prof);
   hipStream_t s = as_stream(stream);
-  if (hipMemsetAsync(a->ctr, 0, kG * 64 * sizeof(unsigned), s) != hipSuccess ||
+  if (hipMemsetAsync(a->ctr, 0, (kG * 64 + kG * kGW) * sizeof(unsigned), s) != hipSuccess ||
       hipMemsetAsync(a->err, 0, 2 * sizeof(int), s) != hipSuccess) {
     set_error("%s: memset failed", nm);
     return SAT_ERR_HIP;

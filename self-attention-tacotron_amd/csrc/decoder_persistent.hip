@@ -57,7 +57,7 @@ static_assert(kK0 <= kKP && kKP == 9 * 64 && kU % kGW == 0 && kQ == 256 && kPST 
               kD1 % 4 == 0, "layout");
 
 struct DecAttnP {
-  int B, N, T, ntiles, UB;
+  int B, N, T, ntiles, UB, flags;
   float u, zc, zh;
   const float* X0;                                   // [T][B][4U] prenet part + bias
   const float* W0r;                                  // [K0][U][4]
@@ -75,6 +75,7 @@ struct DecAttnP {
   float* AH;                                         // [2][B][ntiles][kAH]  granules
   float* PART;                                       // [2][B][ntiles][kPST] tagged
   float* QP;                                         // [2][B][kGW][kQ]      tagged
+  unsigned* XID;                                     // [256] XCC_ID + 1 per workgroup (zeroed)
   int* err;                                          // [2]
   long long* prof;                                   // [256][16] segment clocks + [T][256][4] trace (nullable)
 };
@@ -203,6 +204,10 @@ __global__ void __launch_bounds__(256) dec_attn_fwd_kernel(DecAttnP p) {
   const float4 b1r = tile_wg && tid < kD1 / 4 ? reinterpret_cast<const float4*>(p.b1)[tid]
                                                 : make_float4(0.f, 0.f, 0.f, 0.f);
   __syncthreads();
+
+  // hand-off store policy: plain stores (lines kept in the XCD's L2) iff the whole group was
+  // found on one XCD, else sc1 (persistent.h xcd_local_group; placement is observed, not promised)
+  const bool xl = (p.flags & 1) ? xcd_local_group(p.XID, g, kG, kGW, p.err) : false;
 
   long long tp[16];
 #pragma unroll
@@ -384,7 +389,7 @@ __global__ void __launch_bounds__(256) dec_attn_fwd_kernel(DecAttnP p) {
       //          units' raw outputs
       if (tid < 2 * UB) {
         const int ub = tid >> 1, hf = tid & 1;
-        stc4(rHX, (((t & 1) * B + g + kG * ub) * kU + kUW * j) / 4 + hf,
+        stc4x(xl, rHX, (((t & 1) * B + g + kG * ub) * kU + kUW * j) / 4 + hf,
              *reinterpret_cast<const float4*>(&hst[ub][4 * hf]));
       }
       if (wave < UB) {
@@ -395,7 +400,7 @@ __global__ void __launch_bounds__(256) dec_attn_fwd_kernel(DecAttnP p) {
           a.x = fmaf(h, wq[uu].x, a.x); a.y = fmaf(h, wq[uu].y, a.y);
           a.z = fmaf(h, wq[uu].z, a.z); a.w = fmaf(h, wq[uu].w, a.w);
         }
-        stc4(rQP, ((((t & 1) * B + g + kG * wave) * kGW + j) * kQ) / 4 + lane, tagf4(a, bit));
+        stc4x(xl, rQP, ((((t & 1) * B + g + kG * wave) * kGW + j) * kQ) / 4 + lane, tagf4(a, bit));
       }
       tick(3);
       ev(t, 1);
@@ -463,7 +468,7 @@ __global__ void __launch_bounds__(256) dec_attn_fwd_kernel(DecAttnP p) {
           p.S2[((int64_t)s * B + tb) * N + n] = e == -INFINITY ? 0.f : __expf(e - M2) / Z2;
         }
         if (tid < kAH && t < T)   // alpha_{t-1} at the last two own positions, for the right tile
-          stg(rAH, ((t & 1) * B + tb) * ntiles * kAH + tile * kAH + tid, ap[nt - 1 + tid],
+          stgx(xl, rAH, ((t & 1) * B + tb) * ntiles * kAH + tile * kAH + tid, ap[nt - 1 + tid],
               (unsigned)(t + 1));
       }
     }
@@ -624,11 +629,11 @@ __global__ void __launch_bounds__(256) dec_attn_fwd_kernel(DecAttnP p) {
       const int pout4 = (((t & 1) * B + tb) * ntiles + tile) * kP4;
       if (tid < kM1 / 4) {
         const float4 a0 = cred[0][tid], a1 = cred[1][tid], a2 = cred[2][tid], a3 = cred[3][tid];
-        stc4(rPT, pout4 + 2 + tid,
+        stc4x(xl, rPT, pout4 + 2 + tid,
              tagf4(make_float4((a0.x + a1.x) + (a2.x + a3.x), (a0.y + a1.y) + (a2.y + a3.y),
                                (a0.z + a1.z) + (a2.z + a3.z), (a0.w + a1.w) + (a2.w + a3.w)), want));
         if (tid < 2)   // statistics last: consumers poll them before the context words
-          stc4(rPT, pout4 + tid, tagf4(make_float4(red[4 * tid], red[4 * tid + 1], red[4 * tid + 2],
+          stc4x(xl, rPT, pout4 + tid, tagf4(make_float4(red[4 * tid], red[4 * tid + 1], red[4 * tid + 2],
                                                    red[4 * tid + 3]), want));
       } else if (tid >= 64 && tid < 64 + kM2 / 4) {
         const int jj = tid - 64;
@@ -638,10 +643,10 @@ __global__ void __launch_bounds__(256) dec_attn_fwd_kernel(DecAttnP p) {
           const float4 v = c2red[i][jj];
           sm.x += v.x; sm.y += v.y; sm.z += v.z; sm.w += v.w;
         }
-        stc4(rPT, pout4 + 2 + kM1 / 4 + jj, tagf4(sm, want));
+        stc4x(xl, rPT, pout4 + 2 + kM1 / 4 + jj, tagf4(sm, want));
       } else if (tid >= 192 && tid < 192 + kPadR + kPadL) {   // first 5, last 4 energies
         const int q = tid - 192;
-        stg(rEH, ((t & 1) * B + tb) * ntiles * kEH + tile * kEH + q,
+        stgx(xl, rEH, ((t & 1) * B + tb) * ntiles * kEH + tile * kEH + q,
             e1s[q < kPadR ? q : kPN - kPadL + (q - kPadR)], (unsigned)(t + 1));
       }
       tick(10);
@@ -671,6 +676,7 @@ using namespace sat;
 static int64_t hx_floats(int B) { return (int64_t)2 * B * kU; }
 static int64_t eh_floats(int B, int ntiles) { return (int64_t)2 * B * ntiles * kEH * 2; }
 static int64_t ah_floats(int B, int ntiles) { return (int64_t)2 * B * ntiles * kAH * 2; }
+static constexpr int64_t kXidWords = kG * kGW;
 
 extern "C" int sat_decoder_attention_fwd(const SatDecAttnFwd* a, void* stream) {
   SAT_CHECK_ARG(a && a->B > 0 && a->N > 0 && a->T > 0, "sat_decoder_attention_fwd: bad sizes");
@@ -715,12 +721,15 @@ extern "C" int sat_decoder_attention_fwd(const SatDecAttnFwd* a, void* stream) {
   p.HX = a->E;
   p.EH = a->E + hx_floats(a->B);
   p.AH = p.EH + eh_floats(a->B, ntiles);
+  p.XID = reinterpret_cast<unsigned*>(p.AH + ah_floats(a->B, ntiles));
   p.PART = a->PART; p.QP = a->QP; p.err = a->err;
+  p.flags = xcd_local_env();
   p.prof = reinterpret_cast<long long*>(a->prof);
   p.ZH = a->ZH;
   hipStream_t s = as_stream(stream);
   // every hand-off slot starts zeroed (tag 0 / LSB 0 never matches steps 0 and 1)
-  const int64_t e_total = hx_floats(a->B) + eh_floats(a->B, ntiles) + ah_floats(a->B, ntiles);
+  const int64_t e_total = hx_floats(a->B) + eh_floats(a->B, ntiles) + ah_floats(a->B, ntiles) +
+                        kXidWords;
   if (hipMemsetAsync(a->E, 0, e_total * sizeof(float), s) != hipSuccess ||
       hipMemsetAsync(a->PART, 0, (size_t)2 * a->B * ntiles * kPST * sizeof(float), s) != hipSuccess ||
       hipMemsetAsync(a->QP, 0, (size_t)2 * a->B * kGW * kQ * sizeof(float), s) != hipSuccess ||
@@ -736,7 +745,7 @@ extern "C" int sat_decoder_attention_fwd(const SatDecAttnFwd* a, void* stream) {
 extern "C" int64_t sat_decoder_attention_scratch(int32_t B, int32_t N, int64_t* e_floats,
                                                  int64_t* part_floats, int64_t* qp_floats) {
   const int ntiles = ceil_div(N, kPN);
-  if (e_floats) *e_floats = hx_floats(B) + eh_floats(B, ntiles) + ah_floats(B, ntiles);
+  if (e_floats) *e_floats = hx_floats(B) + eh_floats(B, ntiles) + ah_floats(B, ntiles) + kXidWords;
   if (part_floats) *part_floats = (int64_t)2 * B * ntiles * kPST;
   if (qp_floats) *qp_floats = (int64_t)2 * B * kGW * kQ;
   return kG * 64;   // counter words (unused by the tagged hand-offs; kept for the ABI)

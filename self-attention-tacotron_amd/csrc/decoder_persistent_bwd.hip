@@ -38,7 +38,7 @@ constexpr int kHalo = kPN + kKW - 1;         // 41 positions of dL/df_{t+1} a ti
 constexpr int kJF = kKW * kF;                // 50 taps of the location convolution
 
 struct DecAttnBwdP {
-  int B, N, T, ntiles, UB;
+  int B, N, T, ntiles, UB, flags;
   float u, zc, zh;
   const float* REC0; const float* C0; const float* G0;
   const float* S1; const float* AL1; const float* S2; const float* ST; const float* LOC;
@@ -102,6 +102,8 @@ __global__ void __launch_bounds__(kTh) dec_attn_bwd_kernel(DecAttnBwdP p) {
   float* PS = p.YA + 2 * B * N;              // [2][B][8][2] tile sums (s1, s2 of step t-1)
   const auto rRDP = rsrc(p.RDP), rYA = rsrc(p.YA), rPS = rsrc(PS), rDF = rsrc(p.DFH),
              rDQ = rsrc(p.DQP);
+  // hand-off store policy (persistent.h xcd_local_group): plain stores iff the group is on one XCD
+  const bool xl = (p.flags & 1) ? xcd_local_group(p.ctr + kG * 64, g, kG, kGW, p.err) : false;
   // LPP-16 layout of the tile work: 16 lanes per memory position
   const int pl = tid >> 4, part = tid & 15;
   // unit layout of phase Z: (utterance zu, unit 8j + zuu, 16-lane part)
@@ -206,7 +208,7 @@ __global__ void __launch_bounds__(kTh) dec_attn_bwd_kernel(DecAttnBwdP p) {
       acc[r] += dpp<0xB1>(acc[r]);
       acc[r] += dpp<0x4E>(acc[r]);
     }
-    if (cg == (ub & 3)) stc4(rRDP, (base + wrow) / 4, make_float4(acc[0], acc[1], acc[2], acc[3]));
+    if (cg == (ub & 3)) stc4x(xl, rRDP, (base + wrow) / 4, make_float4(acc[0], acc[1], acc[2], acc[3]));
   };
   // part B: the recurrent-product rows (k >= 288) of DG0[t+1] (still in dgs) for step t
   auto rowdot_b = [&](int t) {
@@ -346,7 +348,7 @@ __global__ void __launch_bounds__(kTh) dec_attn_bwd_kernel(DecAttnBwdP p) {
       const float e1v = st * (ds - s2), e2v = s2v[pl] * (c2 - s3);
       if (valid) {
         const int64_t o = ((int64_t)t * B + tb) * N + n0 + pl;
-        if (part == 0) stc(rYA, (slot * B + tb) * N + n0 + pl, yv);
+        if (part == 0) stcx(xl, rYA, (slot * B + tb) * N + n0 + pl, yv);
         else if (part == 1) p.DE1[o] = e1v;
         else if (part == 2) p.DE2[o] = e2v;
       }
@@ -386,7 +388,7 @@ __global__ void __launch_bounds__(kTh) dec_attn_bwd_kernel(DecAttnBwdP p) {
 #pragma unroll
       for (int f = 0; f < kF; ++f) {
         const float v = group16_sum(dfp[f]);
-        if (valid && part == f) stc(rDF, (((t * B + tb) * N) + n0 + pl) * kF + f, v);
+        if (valid && part == f) stcx(xl, rDF, (((t * B + tb) * N) + n0 + pl) * kF + f, v);
         p2 = fmaf(v, fl[f] - cb[f], p2);
       }
       float p1 = valid ? yv * prior : 0.f;
@@ -419,13 +421,13 @@ __global__ void __launch_bounds__(kTh) dec_attn_bwd_kernel(DecAttnBwdP p) {
           const float4 v = *reinterpret_cast<const float4*>(&dqred[w][4 * tid]);
           acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
         }
-        stc4(rDQ, ((t * B + tb) * ntiles + tile) * (kQ / 4) + tid, acc);
+        stc4x(xl, rDQ, ((t * B + tb) * ntiles + tile) * (kQ / 4) + tid, acc);
       } else if (tid >= kQ && tid < kQ + 2) {
         const int i = tid - kQ;
         float acc = 0.f;
 #pragma unroll
         for (int w = 0; w < kWv; ++w) acc += red2[w][i];
-        stc(rPS, ((slot * B + tb) * 8 + tile) * 2 + i, acc);
+        stcx(xl, rPS, ((slot * B + tb) * 8 + tile) * 2 + i, acc);
       }
       tick(3);
     } else {
@@ -513,7 +515,7 @@ __global__ void __launch_bounds__(kTh) dec_attn_bwd_kernel(DecAttnBwdP p) {
             float a = x.x * wt[0];
             a = fmaf(x.y, wt[1], a); a = fmaf(x.z, wt[2], a); a = fmaf(x.w, wt[3], a);
             a = group8_sum(a);
-            if (c8 == 0) stc(rRDP, base + 256 + tr, a);
+            if (c8 == 0) stcx(xl, rRDP, base + 256 + tr, a);
           }
         }
       }
@@ -565,10 +567,10 @@ extern "C" int sat_decoder_attention_bwd(const SatDecAttnBwd* a, void* stream) {
   p.v2 = a->v2;
   p.W0r = a->W0r; p.Wq1 = a->Wq1; p.Wq2 = a->Wq2; p.mask_c = a->mask_c; p.mask_h = a->mask_h;
   p.DH0 = a->DH0; p.ZH = a->ZH; p.RD = a->RD; p.DG0 = a->DG0; p.DE1 = a->DE1; p.DE2 = a->DE2;
-  p.DFH = a->DFH; p.DQP = a->DQP; p.RDP = a->RDP; p.YA = a->YA; p.ctr = a->ctr; p.err = a->err;
+  p.DFH = a->DFH; p.DQP = a->DQP; p.RDP = a->RDP; p.YA = a->YA; p.ctr = a->ctr; p.err = a->err; p.flags = xcd_local_env();
   p.prof = reinterpret_cast<long long*>(a->prof);
   hipStream_t s = as_stream(stream);
-  if (hipMemsetAsync(a->ctr, 0, kG * 64 * sizeof(unsigned), s) != hipSuccess ||
+  if (hipMemsetAsync(a->ctr, 0, (kG * 64 + kG * kGW) * sizeof(unsigned), s) != hipSuccess ||
       hipMemsetAsync(a->err, 0, 2 * sizeof(int), s) != hipSuccess) {
     set_error("sat_decoder_attention_bwd: memset failed");
     return SAT_ERR_HIP;
@@ -582,5 +584,5 @@ extern "C" int64_t sat_decoder_attention_bwd_scratch(int32_t B, int32_t N, int64
                                                      int64_t* ya_floats) {
   if (rdp_floats) *rdp_floats = (int64_t)2 * B * kGW * kK0;
   if (ya_floats) *ya_floats = (int64_t)2 * B * N + (int64_t)2 * B * 8 * 2;
-  return kG * 64;
+  return kG * 64 + kG * kGW;   // group counters + XID
 }

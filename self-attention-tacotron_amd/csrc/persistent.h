@@ -6,6 +6,7 @@
 // of another workgroup's bytes is an sc1 load.
 #pragma once
 #include "sat_common.h"
+#include <cstdlib>
 
 namespace sat {
 namespace {
@@ -87,6 +88,76 @@ __device__ __forceinline__ bool tag_ok4(float4 v, unsigned bit) {
   return (((__float_as_uint(v.x) ^ bit) | (__float_as_uint(v.y) ^ bit) |
            (__float_as_uint(v.z) ^ bit) | (__float_as_uint(v.w) ^ bit)) & 1u) == 0;
 }
+// ---- XCD-local store policy of a hand-off group.  A plain (aux 0) buffer store is written
+//      through the CU's L1 into its XCD's L2 and the line STAYS there, where an sc1 load from
+//      any CU of the same XCD finds it; an sc1 store drops the line (MI355X_MICROARCH.md,
+//      stores row), so a same-XCD consumer then reads at the cross-XCD rate.  The plain form is
+//      used only when the group has CHECKED at run time (xcd_local_group) that every producer
+//      and consumer of its hand-offs sits on one XCD; otherwise every store stays sc1.
+__device__ __forceinline__ void stc4x(bool xl, __amdgpu_buffer_rsrc_t r, int idx4, float4 v) {
+  const v4u w = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z),
+                 __float_as_uint(v.w)};
+  if (xl) __builtin_amdgcn_raw_buffer_store_b128(w, r, idx4 * 16, 0, 0);
+  else __builtin_amdgcn_raw_buffer_store_b128(w, r, idx4 * 16, 0, 16);
+}
+__device__ __forceinline__ void stgx(bool xl, __amdgpu_buffer_rsrc_t r, int granule, float v,
+                                     unsigned tag) {
+  const v2u w = {__float_as_uint(v), tag};
+  if (xl) __builtin_amdgcn_raw_buffer_store_b64(w, r, granule * 8, 0, 0);
+  else __builtin_amdgcn_raw_buffer_store_b64(w, r, granule * 8, 0, 16);
+}
+__device__ __forceinline__ void stcx(bool xl, __amdgpu_buffer_rsrc_t r, int idx, float v) {
+  if (xl) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, idx * 4, 0, 0);
+  else __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, idx * 4, 0, 16);
+}
+// host: SAT_XCD_LOCAL=0 forces sc1 stores everywhere (A/B switch of the store policy)
+static inline int xcd_local_env() {
+  const char* e = getenv("SAT_XCD_LOCAL");
+  return (e && e[0] == '0') ? 0 : 1;
+}
+__device__ __forceinline__ unsigned xcc_id() {
+  unsigned x;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(x));
+  return x;
+}
+// Placement check of one hand-off group (members blockIdx = g + stride * i, i < n <= 64): every
+// member publishes XCC_ID + 1 (sc1) into its word of `ids` (zeroed scratch), wave 0 polls the
+// group's words (sc1, bounded) and the group is XCD-local iff all ids agree.  Every member reads
+// the same words, so every member reaches the same verdict.  A timeout raises err and returns
+// false (sc1 everywhere).  Call from all threads of the workgroup (it ends in a barrier).
+__device__ __forceinline__ bool xcd_local_group(unsigned* ids, int g, int stride, int n,
+                                                int* err) {
+  __shared__ int verdict;
+  __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(ids, 0, 0x7fffffff, 0x00020000);
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_raw_buffer_store_b32(xcc_id() + 1u, r, blockIdx.x * 4, 0, 16);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    unsigned v = 0, spins = 0;
+    bool ok = true;
+    for (;;) {
+      v = lane < n ? __builtin_amdgcn_raw_buffer_load_b32(r, (g + stride * lane) * 4, 0, 16) : 1u;
+      if (__builtin_amdgcn_ballot_w64(v == 0u) == 0) break;
+      __builtin_amdgcn_s_sleep(1);
+      if ((++spins & 255u) == 255u) {
+        if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0 ||
+            spins > (1u << 20)) {
+          if (spins > (1u << 20)) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          ok = false;
+          break;
+        }
+      }
+    }
+    const unsigned first = __builtin_amdgcn_readfirstlane(v);
+    const bool same = __builtin_amdgcn_ballot_w64(lane < n && v != first) == 0;
+    if (lane == 0) verdict = (ok && same) ? 1 : 0;
+  }
+  __syncthreads();
+  return verdict != 0;
+}
+
 // bounded-spin bookkeeping of a poll loop: every 256 spins look at the error word; after
 // ~2^20 spins (a producer never published: grid not co-resident) raise it.  Returns true when
 // the loop must give up (the grid then drains with garbage and the host reports err).

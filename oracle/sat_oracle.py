@@ -435,7 +435,8 @@ def model_forward(p: Dict[str, Tensor], bufs, hp, batch: Dict[str, Tensor],
 
 
 def infer_free_running(p: Dict[str, Tensor], bufs, hp, batch: Dict[str, Tensor],
-                       max_iters: Optional[int] = None, min_iters: int = 10):
+                       max_iters: Optional[int] = None, min_iters: int = 10,
+                       forced: Optional[tuple] = None, feed: str = "mel"):
     """PREDICT branch of model_fn (models/models.py:84-97, 252-277) with the inference decoder
     of RNNTransformer (modules/module.py:766-784): dynamic_decode over
     OutputAndStopTokenTransparentWrapper(TransformerWrapper(RNNStateHistoryWrapper(DecoderRNNV2)))
@@ -450,8 +451,17 @@ def infer_free_running(p: Dict[str, Tensor], bufs, hp, batch: Dict[str, Tensor],
     Eval semantics throughout: no dropout (apply_dropout_on_inference=False, hparams.py:105),
     zoneout blend, BatchNorm moving statistics.  Returns mel [B, T_out*r, mels], stop
     [B, T_out], alignments, the decoder-self-attention probabilities of the last step and
-    T_out (the number of decoder steps run)."""
+    T_out (the number of decoder steps run).
+
+    ``forced=(A1, A2)`` ([B, T', N] each) restates the forced-alignment second pass
+    (models/models.py:118-148): the mechanisms are TeacherForcing{Forward,Additive}Attention
+    (modules/teacher_forcing_attention.py:30-35: step t returns A[:, t], the query is unused),
+    the helper OneHotValidationHelper(teacher_forcing=False) (modules/helpers.py:96-108): exactly
+    T' steps, no stop-token termination, and with ``feed="softmax"`` step t+1 is fed the softmax
+    over the feature bins of each frame of step t's output, last n_feed frames (:100-104)."""
     max_iters = hp.max_iters if max_iters is None else max_iters
+    if forced is not None:
+        max_iters = forced[0].shape[1]
     m1, m2, enc_al = encoder(batch["source"], batch["source_length"], p, bufs, hp, None, False)
     spk = None
     if hp.use_speaker_embedding and hp.speaker_embedd_to_prenet:
@@ -479,8 +489,11 @@ def infer_free_running(p: Dict[str, Tensor], bufs, hp, batch: Dict[str, Tensor],
         cell_in = torch.cat([pre, c1, c2], dim=-1)
         h0_out, c0, h0 = zoneout_lstm_step(cell_in, c0, h0, p["decoder/attention_lstm/kernel"],
                                            p["decoder/attention_lstm/bias"], zc, zh, None, None)
-        a1, st1 = att1(h0_out, st1)
-        a2, st2 = att2(h0_out, st2)
+        if forced is not None:
+            a1, a2 = forced[0][:, t], forced[1][:, t]
+        else:
+            a1, st1 = att1(h0_out, st1)
+            a2, st2 = att2(h0_out, st2)
         c1 = (a1.unsqueeze(1) @ att1.values).squeeze(1)
         c2 = (a2.unsqueeze(1) @ att2.values).squeeze(1)
         o = torch.cat([h0_out, c1, c2], dim=-1)
@@ -502,8 +515,11 @@ def infer_free_running(p: Dict[str, Tensor], bufs, hp, batch: Dict[str, Tensor],
         stops.append(stop_t)
         al1.append(a1)
         al2.append(a2)
-        x = mel_t[:, -M * nf:]
-        if t > min_iters and bool((torch.sigmoid(stop_t) > 0.5).all()):
+        if feed == "softmax":
+            x = torch.softmax(mel_t.view(B, r, M), dim=-1).reshape(B, r * M)[:, -M * nf:]
+        else:
+            x = mel_t[:, -M * nf:]
+        if forced is None and t > min_iters and bool((torch.sigmoid(stop_t) > 0.5).all()):
             break
     T_out = len(mels)
     mel = torch.stack(mels, dim=1).reshape(B, T_out * r, M)

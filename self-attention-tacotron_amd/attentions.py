@@ -14,11 +14,13 @@ dual-source tile kernel, with this mechanism as source 1).  Inside the decoder t
 mechanisms of ``dual_source_attention_factory`` are fused into ONE kernel per step; the
 per-mechanism call here is the plugin-level entry for stepping a single mechanism.
 
-Supported kinds on this path: ``"forward"`` (ForwardAttention) and ``"additive"``
-(BahdanauAttention).  ``"location_sensitive"``, ``"teacher_forcing_forward"`` and
-``"teacher_forcing_additive"`` are reference kinds outside the LJSpeech/VCTK self-attention
-configs: they raise ``NotImplementedError``; unknown kinds raise ``ValueError`` like the
-reference.
+Supported kinds on this path: ``"forward"`` (ForwardAttention), ``"additive"``
+(BahdanauAttention) and the forced-alignment kinds ``"teacher_forcing_forward"`` /
+``"teacher_forcing_additive"`` (modules/teacher_forcing_attention.py:13-78: step ``index``
+returns ``teacher_alignments[:, index]``; used by ``force_alignment_*_factory`` and the
+``use_forced_alignment_mode`` pass of model_fn).  ``"location_sensitive"`` is a reference kind
+outside the LJSpeech/VCTK self-attention configs: it raises ``NotImplementedError``; unknown
+kinds raise ``ValueError`` like the reference.
 """
 
 from __future__ import annotations
@@ -42,7 +44,7 @@ class AttentionOptions(namedtuple("AttentionOptions", ["attention",
     pass
 
 
-_OUT_OF_SCOPE = ("location_sensitive", "teacher_forcing_forward", "teacher_forcing_additive")
+_OUT_OF_SCOPE = ("location_sensitive",)
 _DUMMY_D2, _DUMMY_M2 = 32, 4     # inert second source when a single mechanism is stepped
 
 
@@ -160,6 +162,53 @@ class BahdanauAttention(_HipAttention):
         return s, s
 
 
+class TeacherForcingAttention:
+    """TeacherForcingForwardAttention / TeacherForcingAdditiveAttention
+    (modules/teacher_forcing_attention.py:13-78).  Memory preparation is TF BahdanauAttention's
+    (values = memory masked past memory_sequence_length, on libsat_hip); the memory layer's keys
+    are never read by ``__call__`` and are not formed.  State = (previous alignments, index),
+    initial index -1 (:38-41); ``__call__`` ignores the query and returns
+    ``teacher_alignments[:, index + 1]`` as both the alignments and the next state's alignments
+    (:30-35).  ``teacher_alignments``: [B, T', N] device tensor."""
+
+    def __init__(self, kind: str, options: AttentionOptions, memory: torch.Tensor,
+                 memory_sequence_length: torch.Tensor, teacher_alignments: torch.Tensor):
+        if memory.dtype != torch.float32 or not memory.is_cuda:
+            raise TypeError("memory must be a float32 device tensor [B, N, M]")
+        if teacher_alignments is None:
+            raise ValueError(f"{kind} attention needs teacher_alignments [B, T', N]")
+        B, N, _ = memory.shape
+        if (teacher_alignments.dim() != 3 or teacher_alignments.shape[0] != B
+                or teacher_alignments.shape[2] != N):
+            raise ValueError(f"teacher_alignments must be [B={B}, T', N={N}], got "
+                             f"{tuple(teacher_alignments.shape)}")
+        self.kind = kind
+        self.options = options
+        self.batch_size, self.N = B, N
+        self.values = K.seq_mask(memory.contiguous(), memory_sequence_length)
+        self.teacher_alignments = teacher_alignments
+
+    @property
+    def alignments_size(self) -> int:
+        return self.N
+
+    @property
+    def state_size(self):
+        return self.N, 1
+
+    def initial_alignments(self, batch_size: int, dtype=torch.float32) -> torch.Tensor:
+        return torch.zeros(batch_size, self.N, device=self.values.device, dtype=dtype)
+
+    def initial_state(self, batch_size: int, dtype=torch.float32):
+        return self.initial_alignments(batch_size, dtype), -1
+
+    def __call__(self, query, state):
+        _, prev_index = state
+        index = int(prev_index) + 1
+        alignments = self.teacher_alignments[:, index]
+        return alignments, (alignments, index)
+
+
 def attention_mechanism_factory(options: AttentionOptions):
     """modules/attentions.py:25-62."""
     def attention_fn(memory, memory_sequence_length, teacher_alignments=None, variables=None,
@@ -168,6 +217,9 @@ def attention_mechanism_factory(options: AttentionOptions):
             cls = ForwardAttention
         elif options.attention == "additive":
             cls = BahdanauAttention
+        elif options.attention in ("teacher_forcing_forward", "teacher_forcing_additive"):
+            return TeacherForcingAttention(options.attention, options, memory,
+                                           memory_sequence_length, teacher_alignments)
         elif options.attention in _OUT_OF_SCOPE:
             raise NotImplementedError(
                 f"attention mechanism {options.attention!r} is outside the hot path "
@@ -203,6 +255,28 @@ def dual_source_attention_factory(params):
     return attention_mechanism_factory(o1), attention_mechanism_factory(o2)
 
 
+def force_alignment_attention_factory(params):
+    """models/attention_factories.py:40-48."""
+    return attention_mechanism_factory(AttentionOptions(
+        attention=params.forced_alignment_attention, num_units=params.attention_out_units,
+        attention_kernel=params.attention_kernel, attention_filters=params.attention_filters,
+        smoothing=False, cumulative_weights=params.cumulative_weights,
+        use_transition_agent=params.use_forward_attention_transition_agent))
+
+
+def force_alignment_dual_source_attention_factory(params):
+    """models/attention_factories.py:51-66."""
+    common = dict(attention_kernel=params.attention_kernel,
+                  attention_filters=params.attention_filters, smoothing=False,
+                  cumulative_weights=params.cumulative_weights,
+                  use_transition_agent=params.use_forward_attention_transition_agent)
+    o1 = AttentionOptions(attention=params.forced_alignment_attention,
+                          num_units=params.attention1_out_units, **common)
+    o2 = AttentionOptions(attention=params.forced_alignment_attention2,
+                          num_units=params.attention2_out_units, **common)
+    return attention_mechanism_factory(o1), attention_mechanism_factory(o2)
+
+
 def mechanism_variables(P: Dict[str, torch.Tensor], scope: str) -> Dict[str, torch.Tensor]:
     """The scope-relative variables of one mechanism from the model's parameter views."""
     pre = scope.rstrip("/") + "/"
@@ -210,5 +284,7 @@ def mechanism_variables(P: Dict[str, torch.Tensor], scope: str) -> Dict[str, tor
 
 
 __all__ = ["AttentionOptions", "attention_mechanism_factory", "attention_factory",
-           "dual_source_attention_factory", "ForwardAttention", "BahdanauAttention",
+           "dual_source_attention_factory", "force_alignment_attention_factory",
+           "force_alignment_dual_source_attention_factory", "TeacherForcingAttention",
+           "ForwardAttention", "BahdanauAttention",
            "mechanism_variables"]

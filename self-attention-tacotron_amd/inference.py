@@ -19,6 +19,15 @@ tacotron2 ``StopTokenBasedInferenceHelper`` (analog modules/helpers.py:111-160):
   of steps, the outputs are then cut at the first finished step (the steps computed past it
   never feed anything the reference returns).
 
+Forced-alignment mode (``forced_alignments=(A1, A2)``, the second decoder pass of model_fn
+under ``use_forced_alignment_mode``, models/models.py:118-148): the mechanisms are
+``TeacherForcing{Forward,Additive}Attention`` (modules/teacher_forcing_attention.py:13-78), so
+step t's alignments are the given ``A[:, t]`` and the contexts are ``A[:, t] . values``; the
+helper is ``OneHotValidationHelper(teacher_forcing=False)`` (modules/helpers.py:61-108): step
+t+1 is fed the per-frame softmax over the feature bins of step t's output (``feed="softmax"``,
+the fork's code-prediction feedback, :100-104) and the loop runs exactly T' = A.shape[1] steps
+(``finished = time + 1 >= num_steps``, :101), with no stop-token termination.
+
 Every arithmetic op is a libsat_hip kernel; torch allocates, views and copies.
 """
 
@@ -39,13 +48,23 @@ class FreeRunningDecoder:
     between host reads of the device-side finished flag."""
 
     def __init__(self, model, max_iters: Optional[int] = None, min_iters: int = 10,
-                 check_every: int = 25):
+                 check_every: int = 25, forced_alignments=None, feed: str = "mel"):
         self.m = model
         self.hp = model.hp
         self.d: Dims = model.d
         self.max_iters = int(self.hp.max_iters if max_iters is None else max_iters)
         self.min_iters = int(min_iters)
         self.check_every = max(1, int(check_every))
+        if feed not in ("mel", "softmax"):
+            raise ValueError(f"feed must be 'mel' or 'softmax', got {feed!r}")
+        self.feed = feed
+        self.forced = None
+        if forced_alignments is not None:
+            a1, a2 = forced_alignments
+            if a1.shape != a2.shape or a1.dim() != 3:
+                raise ValueError("forced alignments must be two [B, T', N] tensors")
+            self.forced = (a1.contiguous(), a2.contiguous())
+            self.max_iters = int(a1.shape[1])
 
     # ------------------------------------------------------------------ one decode
     @torch.no_grad()
@@ -63,6 +82,10 @@ class FreeRunningDecoder:
             K.embedding_fwd(P["speaker_embedding"], batch["speaker_id"], spk, d.spk_offset, err)
         Tm = self.max_iters
         f32 = dict(device=dev, dtype=torch.float32)
+        forced = self.forced
+        if forced is not None and tuple(forced[0].shape) != (B, Tm, N):
+            raise ValueError(f"forced alignments must be [B={B}, T', N={N}], got "
+                             f"{tuple(forced[0].shape)}")
         M, r, nf = d.num_mels, d.r, hp.n_feed_frame
         A, Dd, M1, M2, D1, D2 = d.att_rnn, d.dec, d.m1, d.m2, d.d1, d.d2
         R0 = M1 + M2 + A
@@ -81,6 +104,7 @@ class FreeRunningDecoder:
         MEL = torch.zeros(Tm, B, M * r, **f32)
         STOP = torch.zeros(Tm, B, 1, **f32)
         GO = torch.zeros(B, M * nf, **f32)
+        SMX = torch.empty(B, M * r, **f32)                # softmax feedback (feed="softmax")
         REC0 = torch.zeros(Tm + 1, B, R0, **f32)          # [c1 | c2 | h0] per step
         C0 = torch.zeros(2, B, A, **f32)
         H0RAW = torch.empty(B, A, **f32)
@@ -169,13 +193,38 @@ class FreeRunningDecoder:
 
         def step(t):
             cur, nxt = t % 2, (t + 1) % 2
-            x = GO if t == 0 else MEL[t - 1][:, M * (r - nf):]
+            if t == 0:
+                x = GO
+            elif self.feed == "softmax":                  # OneHotValidationHelper :100-104
+                K.softmax_fwd(MEL[t - 1].view(B * r, M), SMX.view(B * r, M), causal=False)
+                x = SMX[:, M * (r - nf):]
+            else:
+                x = MEL[t - 1][:, M * (r - nf):]
             pre = prenets(x)
             K.linear(pre, W0[:p_w], P["decoder/attention_lstm/bias"], out=X0)
             K.lstm_step_fwd(B=B, U=A, K=R0, t=t, xproj=X0, rin=REC0[t], W=W0[p_w:],
                             c_prev=C0[cur], h_prev=REC0[t, :, M1 + M2:], mask_c=None,
                             mask_h=None, zc=zc, zh=zh, h_raw=H0RAW, c_out=C0[nxt],
                             h_out=REC0[t + 1, :, M1 + M2:], gates=GA)
+            if forced is not None:
+                forced_step(t)
+            else:
+                attention_step(t)
+            # LSTM1 on o_t = [h0'_t | c1_t | c2_t] (ConcatOutputAndAttentionWrapper)
+            lstm_stack(t, cur, nxt)
+            head_step(H2RAW, t)
+            if forced is None:
+                K.stop_check(STOP[t], t, self.min_iters, state)
+
+        def forced_step(t):
+            """TeacherForcing*Attention: alignments = A[:, t]; contexts = A[:, t] . values."""
+            a1t, a2t = forced[0][:, t], forced[1][:, t]
+            AL1[t + 1].copy_(a1t)
+            S2[t].copy_(a2t)
+            K.gemm(a1t.unsqueeze(1), V1, REC0[t + 1][:, :M1].unsqueeze(1))
+            K.gemm(a2t.unsqueeze(1), V2, REC0[t + 1][:, M1:M1 + M2].unsqueeze(1))
+
+        def attention_step(t):
             K.rowdot(H0RAW, QT, Q)
             K.attn_step_fwd(
                 B=B, N=N, D1=D1, M1=M1, D2=D2, M2=M2, F=d.loc_f, KW=d.loc_k, NT=32,
@@ -189,7 +238,8 @@ class FreeRunningDecoder:
                 v2=P[f"{a2}/attention_v"], e1=E1, e2=E2, part=PART, part_stride=pst,
                 s_out=S1[t + 1], a_out=AL1[t + 1], s2_out=S2[t], ctx=REC0[t + 1], ctx_sb=R0,
                 stats=None, loc_out=None)
-            # LSTM1 on o_t = [h0'_t | c1_t | c2_t] (ConcatOutputAndAttentionWrapper)
+
+        def lstm_stack(t, cur, nxt):
             K.linear(H0RAW, W1[:A], P["decoder/lstm1/bias"], out=X1)
             K.gemm(REC0[t + 1][:, :M1 + M2], W1[A:A + M1 + M2], X1, beta=1.0)
             K.lstm_step_fwd(B=B, U=Dd, K=Dd, t=t, xproj=X1, rin=L1[1][cur],
@@ -201,12 +251,12 @@ class FreeRunningDecoder:
                             c_prev=L2[0][cur], h_prev=L2[1][cur], mask_c=None, mask_h=None,
                             zc=zc, zh=zh, h_raw=H2RAW, c_out=L2[0][nxt], h_out=L2[1][nxt],
                             gates=GD)
-            head_step(H2RAW, t)
-            K.stop_check(STOP[t], t, self.min_iters, state)
 
         steps = Tm
         for t in range(Tm):
             step(t)
+            if forced is not None:
+                continue
             if (t + 1) % self.check_every == 0 or t + 1 == Tm:
                 first = int(state.item())
                 if first >= 0:

@@ -212,10 +212,51 @@ class DualSourceSelfAttentionTacotronModel:
         return EstimatorSpec(ModeKeys.PREDICT, loss=None, train_op=None, predictions=preds,
                              eval_metric_ops=None)
 
+    def forced_alignment_pass(self, batch) -> Dict[str, object]:
+        """``use_forced_alignment_mode`` (models/models.py:84-97, 118-148): a teacher-forced
+        validation pass (eval semantics; equal to the training-branch decoder by
+        modules/transformer_test.py:44-90) yields the alignment histories, then a second pass
+        decodes with ``force_alignment_dual_source_attention_factory`` mechanisms
+        (TeacherForcing*Attention replaying those alignments) under
+        ``OneHotValidationHelper(teacher_forcing=False)`` (softmax feedback, exactly T' steps).
+        Returns the second pass's outputs (the ones the reference's loss and predictions use)
+        with its alignment histories [B, N, T'] and the teacher-forced first pass's."""
+        from .attentions import force_alignment_dual_source_attention_factory
+        from .inference import FreeRunningDecoder
+        hp = self.params
+        kinds = (hp.forced_alignment_attention, hp.forced_alignment_attention2)
+        for k in kinds:
+            if k not in ("teacher_forcing_forward", "teacher_forcing_additive"):
+                raise ValueError(f"forced_alignment_attention must be a teacher_forcing kind: {k}")
+        force_alignment_dual_source_attention_factory(hp)          # option checks
+        with torch.no_grad():
+            first, _ = self.engine.forward(batch, None, training=False, need_grad=False)
+            a1 = first["alignment1"].permute(1, 0, 2).contiguous()    # [B, T', N]
+            a2 = first["alignment2"].permute(1, 0, 2).contiguous()
+            dec = FreeRunningDecoder(self.engine, forced_alignments=(a1, a2), feed="softmax")
+            out = dec.run(batch)
+        out["teacher_alignment1"] = a1.transpose(1, 2)
+        out["teacher_alignment2"] = a2.transpose(1, 2)
+        return out
+
+    def _forced_eval(self, batch) -> EstimatorSpec:
+        from . import kernels as K
+        out = self.forced_alignment_pass(batch)
+        mel, stop = out["mel"], out["stop"]
+        loss = torch.zeros(8, device=mel.device)
+        K.loss_fwd_bwd(mel, batch["mel"], batch["mel_mask"], stop.contiguous(), batch["done"],
+                       batch["done_mask"], loss)
+        metrics = {"loss": loss[0:1], "code_loss": 0.1 * loss[1:2], "done_loss": loss[2:3],
+                   "alignment1": out["alignment1"], "alignment2": out["alignment2"]}
+        return EstimatorSpec(ModeKeys.EVAL, loss=loss[0:1], train_op=None,
+                             predictions={"mel": mel, "stop_token": stop}, eval_metric_ops=metrics)
+
     def model_fn(self, features, labels, mode, params=None) -> EstimatorSpec:
         if mode == ModeKeys.PREDICT:
             return self._predict(features)
         batch = self._batch(features, labels)
+        if mode == ModeKeys.EVAL and getattr(self.params, "use_forced_alignment_mode", False):
+            return self._forced_eval(batch)
         if mode == ModeKeys.TRAIN:
             tr = self._trainer(batch)
             out = tr.step(batch)

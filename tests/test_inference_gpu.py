@@ -57,3 +57,73 @@ def test_stop_token_termination(cuda, bias):
     assert out["steps"] == ref["steps"] == (12 if bias > 0 else 30)
     assert out["mel"].shape[1] == out["steps"] * hp.outputs_per_step
     np.testing.assert_allclose(out["mel"].cpu().numpy(), ref["mel"].numpy(), atol=2e-4)
+
+
+def test_teacher_forcing_mechanism_replays_alignments(cuda):
+    """TeacherForcing*Attention (modules/teacher_forcing_attention.py:30-41): state (alignments,
+    index) starts at index -1; call k returns teacher_alignments[:, k], whatever the query."""
+    from sat_amd import attentions as A
+    from sat_amd import hparams
+    hp = hparams.ljspeech_hparams()
+    fn1, fn2 = A.force_alignment_dual_source_attention_factory(hp)
+    g = torch.Generator().manual_seed(0)
+    mem = torch.randn(2, 7, 32, generator=g).to(cuda)
+    lens = torch.tensor([7, 4], dtype=torch.int64, device=cuda)
+    ta = torch.softmax(torch.randn(2, 5, 7, generator=g), -1).to(cuda)
+    mech = fn2(mem, lens, ta)
+    assert mech.alignments_size == 7
+    np.testing.assert_array_equal(mech.values[1, 4:].cpu().numpy(), 0.0)   # masked memory
+    state = mech.initial_state(2)
+    assert state[1] == -1
+    for k in range(5):
+        al, state = mech(torch.randn(2, 256, device=cuda), state)
+        assert state[1] == k
+        assert torch.equal(al, ta[:, k])
+    with pytest.raises(ValueError, match="teacher_alignments"):
+        fn1(mem, lens, None)
+
+
+@pytest.mark.parametrize("preset", ["ljspeech", "vctk"])
+def test_forced_alignment_pass_matches_oracle(cuda, preset):
+    """use_forced_alignment_mode second pass (models/models.py:118-148): forced alignments from
+    the teacher-forced pass, softmax feedback, exactly T' steps; HIP vs the oracle's
+    restatement (infer_free_running(forced=..., feed='softmax'))."""
+    from sat_amd.inference import FreeRunningDecoder
+    hp, m, b, gb, p64, bufs, O = _setup(cuda, preset, scale_stop=9.0)
+    tf = O.model_forward(p64, bufs, hp, O.to_torch(b), None, training=False)
+    a1, a2 = tf["alignment1"], tf["alignment2"]                      # [B, T', N] float64
+    fa = (a1.float().to(cuda), a2.float().to(cuda))
+    out = FreeRunningDecoder(m, forced_alignments=fa, feed="softmax").run(gb)
+    ref = O.infer_free_running(p64, bufs, hp, O.to_torch(b), forced=(a1, a2), feed="softmax")
+    assert out["steps"] == ref["steps"] == a1.shape[1]
+    np.testing.assert_allclose(out["mel"].cpu().numpy(), ref["mel"].numpy(), atol=2e-5)
+    np.testing.assert_allclose(out["stop"].cpu().numpy(), ref["stop"].numpy(), atol=2e-5)
+    np.testing.assert_allclose(out["alignment1"].cpu().numpy(),
+                               a1.permute(0, 2, 1).numpy(), atol=1e-7)
+
+
+def test_model_fn_eval_forced_alignment_mode(cuda):
+    """model_fn EVAL with use_forced_alignment_mode: the loss of the forced pass's outputs
+    (0.1 * L1 + BCE, models/models.py:159-173) equals the oracle's on its restatement."""
+    from sat_amd import hparams, models as MD, params
+    from sat_amd.models import PreprocessedSourceData, PreprocessedTargetData
+    from oracle import sat_oracle as O
+    from sat_amd import data
+    hp = hparams.ljspeech_hparams()
+    hp.set_hparam("use_forced_alignment_mode", True)
+    vals = params.init_params(hp, seed=5)
+    model = MD.DualSourceSelfAttentionTacotronModel(hp, device=cuda, init_values=vals)
+    b = data.synthetic_batch(hp, 2, N=11, T=16, shape="ljs", seed=4)
+    ids = np.arange(2)
+    feats = PreprocessedSourceData(ids, ids, b["source"], b["source_length"], None)
+    labels = PreprocessedTargetData(ids, ids, b["mel"], b["target_length"], b["done"],
+                                    b["mel_mask"], b["done_mask"])
+    spec = model.model_fn(feats, labels, MD.ModeKeys.EVAL, hp)
+    p64, bufs, tb = O.to_torch(vals), O.to_torch(params.init_bn_buffers(hp)), O.to_torch(b)
+    tf = O.model_forward(p64, bufs, hp, tb, None, training=False)
+    ref = O.infer_free_running(p64, bufs, hp, tb, forced=(tf["alignment1"], tf["alignment2"]),
+                               feed="softmax")
+    l = O.losses(ref["mel"], ref["stop"].unsqueeze(-1), tb["mel"], tb["mel_mask"], tb["done"],
+                 tb["done_mask"])
+    ref_loss = float(l["loss"]) if isinstance(l, dict) else float(l[0])
+    assert abs(float(spec.loss.item()) - ref_loss) < 1e-5 * max(1.0, abs(ref_loss))

@@ -216,3 +216,41 @@ def test_free_running_stop_rule():
         vals["decoder/stop_token_projection/bias"] = np.full((1,), bias, np.float32)
         out = O.infer_free_running(O.to_torch(vals), bufs, hp, b, max_iters=15, min_iters=4)
         assert out["steps"] == steps
+
+
+def test_forced_alignment_replay_equals_free_running():
+    """Forced-alignment pass (TeacherForcing*Attention, modules/teacher_forcing_attention.py:
+    30-35) replaying the alignments a free-running decode computed, with the same feedback,
+    reproduces that decode: the teacher mechanisms return exactly what the real ones did."""
+    from sat_amd import data, hparams, params
+    hp = hparams.ljspeech_hparams()
+    p = O.to_torch(params.init_params(hp, seed=5))
+    bufs = O.to_torch(params.init_bn_buffers(hp))
+    b = O.to_torch(data.synthetic_batch(hp, 2, N=9, T=16, shape="ljs", seed=3))
+    inf = O.infer_free_running(p, bufs, hp, b, max_iters=8, min_iters=100)
+    fa = O.infer_free_running(p, bufs, hp, b, forced=(inf["alignment1"], inf["alignment2"]))
+    assert fa["steps"] == 8
+    np.testing.assert_allclose(fa["mel"].numpy(), inf["mel"].numpy(), rtol=1e-12, atol=1e-12)
+    np.testing.assert_allclose(fa["stop"].numpy(), inf["stop"].numpy(), rtol=1e-12, atol=1e-12)
+
+
+def test_forced_alignment_softmax_feedback():
+    """OneHotValidationHelper(teacher_forcing=False) (modules/helpers.py:96-108): step t+1 is fed
+    softmax over the bins of step t's last frame, T' steps exactly, stop tokens ignored."""
+    from sat_amd import data, hparams, params
+    hp = hparams.ljspeech_hparams()
+    vals = params.init_params(hp, seed=5)
+    vals["decoder/stop_token_projection/bias"] = np.full((1,), 9.0, np.float32)  # would stop
+    p = O.to_torch(vals)
+    bufs = O.to_torch(params.init_bn_buffers(hp))
+    b = O.to_torch(data.synthetic_batch(hp, 2, N=9, T=16, shape="ljs", seed=3))
+    tf = O.model_forward(p, bufs, hp, b, None, training=False)
+    a1, a2 = tf["alignment1"], tf["alignment2"]
+    fa = O.infer_free_running(p, bufs, hp, b, forced=(a1, a2), feed="softmax", min_iters=0)
+    assert fa["steps"] == a1.shape[1] == 8
+    M, r = hp.num_mels, hp.outputs_per_step
+    # step 0 sees the go frame and the teacher-forced alpha_0: identical to the teacher-forced
+    # pass; from step 1 the fed frames differ (softmax vs target)
+    np.testing.assert_allclose(fa["mel"][:, :r].numpy(), tf["mel"][:, :r].numpy(), atol=1e-12)
+    assert not np.allclose(fa["mel"][:, r:2 * r].numpy(), tf["mel"][:, r:2 * r].numpy())
+    assert torch.isfinite(fa["mel"]).all() and fa["mel"].shape == (2, 16, M)

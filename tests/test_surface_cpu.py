@@ -1,6 +1,7 @@
 """Plugin surface without a GPU: AttentionOptions / factory dispatch and error behaviour
 (modules/attentions.py:15-62, models/attention_factories.py:11-37, models/models.py:325-378)."""
 import pytest
+import torch
 
 import _sat_path
 
@@ -28,10 +29,26 @@ def test_mechanism_dispatch_errors():
     unknown = A.attention_mechanism_factory(A.AttentionOptions("nope", 8, 3, 2, False, False, False))
     with pytest.raises(ValueError, match="Unknown attention mechanism"):
         unknown(None, None)
-    for kind in ("location_sensitive", "teacher_forcing_forward", "teacher_forcing_additive"):
+    fn = A.attention_mechanism_factory(A.AttentionOptions("location_sensitive", 8, 3, 2, False,
+                                                          False, False))
+    with pytest.raises(NotImplementedError):
+        fn(None, None)
+    for kind in ("teacher_forcing_forward", "teacher_forcing_additive"):
         fn = A.attention_mechanism_factory(A.AttentionOptions(kind, 8, 3, 2, False, False, False))
-        with pytest.raises(NotImplementedError):
-            fn(None, None)
+        with pytest.raises(TypeError, match="device tensor"):     # host memory is refused
+            fn(torch.zeros(1, 2, 3), torch.ones(1, dtype=torch.int64), torch.zeros(1, 1, 2))
+
+
+def test_force_alignment_factories_read_hparams():
+    """models/attention_factories.py:40-66: the forced kinds come from
+    forced_alignment_attention / forced_alignment_attention2 (hparams.py:95,99)."""
+    hp = hparams.ljspeech_hparams()
+    f1, f2 = A.force_alignment_dual_source_attention_factory(hp)
+    assert f1.options == A.AttentionOptions("teacher_forcing_additive", 224, 10, 5, False, False,
+                                            False)
+    assert f2.options == A.AttentionOptions("teacher_forcing_additive", 32, 10, 5, False, False,
+                                            False)
+    assert A.force_alignment_attention_factory(hp).options.num_units == hp.attention_out_units
 
 
 @pytest.mark.parametrize("field,factory", [("encoder", lambda hp: M.encoder_factory(hp, True)),

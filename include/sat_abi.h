@@ -510,6 +510,18 @@ int sat_adam_step(float* params, const float* grads, float* m, float* v, int64_t
                   int64_t* global_step, float* scalars, void* workspace,
                   const SatAdamConfig* cfg, void* stream);
 
+/* ---------------------------------------------------------------- dataset records (host)
+ * TFRecord framing of the dataset path: datasets/ljspeech/dataset.py:96-112 reads
+ * tf.data.TFRecordDataset files written by preprocess/ljspeech.py:23-45 (utils/tfrecord.py:46-49).
+ * Host memory, no device work; used by sat_amd/tfrecord.py. */
+uint32_t sat_crc32c(const void* data, int64_t n, uint32_t crc);      /* CRC-32C, continuable */
+uint32_t sat_tfrecord_masked_crc(const void* data, int64_t n);       /* TF's masked form */
+int64_t sat_tfrecord_frame(const void* data, int64_t n, void* out);  /* out: n + 16 bytes */
+/* (offset, length) of each payload in a buffer of records (up to cap pairs); returns the record
+ * count or a negative SAT_ERR_* on truncation / checksum mismatch (verify != 0) */
+int64_t sat_tfrecord_index(const void* buf, int64_t n, int32_t verify, int64_t* spans,
+                           int64_t cap);
+
 #ifdef __cplusplus
 }
 #endif

@@ -177,7 +177,11 @@ RESTYPES = {"sat_workspace_colreduce": (ctypes.c_int64, [_I32, _I32]),
             "sat_decoder_attention_scratch": (ctypes.c_int64, [_I32, _I32, _P, _P, _P]),
             "sat_decoder_attention_bwd_scratch": (ctypes.c_int64, [_I32, _I32, _P, _P]),
             "sat_decoder_lstms_scratch": (ctypes.c_int64, [_I32]),
-            "sat_decoder_lstms_bwd_scratch": (ctypes.c_int64, [_I32])}
+            "sat_decoder_lstms_bwd_scratch": (ctypes.c_int64, [_I32]),
+            "sat_crc32c": (ctypes.c_uint32, [_P, _I64, ctypes.c_uint32]),
+            "sat_tfrecord_masked_crc": (ctypes.c_uint32, [_P, _I64]),
+            "sat_tfrecord_frame": (ctypes.c_int64, [_P, _I64, _P]),
+            "sat_tfrecord_index": (ctypes.c_int64, [_P, _I64, _I32, _P, _I64])}
 
 _lib: Optional[ctypes.CDLL] = None
 

@@ -128,20 +128,20 @@ __global__ void __launch_bounds__(kThreads) dec_lstm_fwd_kernel(DecLstmFwdP p) {
   const bool b_on = tid < kUBmax * (kU / 2) && bb < B;
 
   // cell operands of iteration ii (forward inputs, plain loads), prefetched one iteration
-  // ahead so their HBM latency hides behind the hand-off wait
+  // ahead so their HBM latency hides behind the hand-off wait.  Branch-free (clamped in-range
+  // address, raw values; defaults applied at the use) so no vmcnt wait lands before the wait.
+  auto ops_on = [&](int ii) {
+    const int tt = layer == 0 ? ii : ii - 1;
+    return cell && tt >= 0 && tt < T;
+  };
   auto load_ops = [&](int ii, float4& xp_, float& mc_, float& mh_) {
     const int tt = layer == 0 ? ii : ii - 1;
-    xp_ = bias2;
-    mc_ = 1.f - p.zc;
-    mh_ = 1.f - p.zh;
-    if (cell && tt >= 0 && tt < T) {
-      const int64_t bu = ((int64_t)tt * B + pb) * kU + pu;
-      if (layer == 0) xp_ = reinterpret_cast<const float4*>(p.X1)[bu];
-      if (masked) {
-        mc_ = layer == 0 ? p.m1c[bu] : p.m2c[bu];
-        mh_ = layer == 0 ? p.m1h[bu] : p.m2h[bu];
-      }
-    }
+    const int64_t bu = ops_on(ii) ? ((int64_t)tt * B + pb) * kU + pu : 0;
+    const float* Mc = masked ? (layer == 0 ? p.m1c : p.m2c) : p.X1;
+    const float* Mh = masked ? (layer == 0 ? p.m1h : p.m2h) : p.X1;
+    xp_ = reinterpret_cast<const float4*>(p.X1)[bu];
+    mc_ = Mc[bu];
+    mh_ = Mh[bu];
   };
   float4 xpn;
   float mcn, mhn;
@@ -164,8 +164,6 @@ __global__ void __launch_bounds__(kThreads) dec_lstm_fwd_kernel(DecLstmFwdP p) {
     const bool do1 = i < T, do2 = i >= 1;
     const int t = layer == 0 ? i : i - 1;
     const bool cell_step = cell && (layer == 0 ? do1 : do2);
-    const float4 xp = xpn;
-    const float mc = mcn, mh = mhn;
     // ---- consume: h1_{i-1}, h1'_{i-1} (XA) and h2_{i-2} (XB) of the group's utterances
     if (i == 0) {
       xs[aub][au] = a_on ? p.H1S[(int64_t)ab * kU + au] : 0.f;
@@ -201,6 +199,12 @@ __global__ void __launch_bounds__(kThreads) dec_lstm_fwd_kernel(DecLstmFwdP p) {
         xs[bub][2 * kU + 2 * bu2 + 1] = gb.z;
       }
     }
+    // this iteration's prefetched operands (waited for only now, after the hand-off), then
+    // the next iteration's prefetch
+    const bool on_i = ops_on(i);
+    const float4 xp = (layer == 0 && on_i) ? xpn : bias2;
+    const float mc = (masked && on_i) ? mcn : 1.f - p.zc;
+    const float mh = (masked && on_i) ? mhn : 1.f - p.zh;
     if (i < T) load_ops(i + 1, xpn, mcn, mhn);
     __syncthreads();
     tick(1);
@@ -364,26 +368,23 @@ __global__ void __launch_bounds__(kThreads) dec_lstm_bwd_kernel(DecLstmBwdP p) {
   const bool masked = p.m1c != nullptr;
   const auto rDG1 = rsrc(p.DG1), rDG2 = rsrc(p.DG2);
 
-  // cell operands of iteration jj (plain loads of read-only inputs)
+  // cell operands of iteration jj (plain loads of read-only inputs).  Branch-free: every lane
+  // loads from a clamped in-range address and only cell lanes of live steps use the values, so
+  // the loads stay in flight across the barrier (a conditional load into a defaulted register
+  // forces a vmcnt(0) at the join).
   auto load_ops = [&](int jj, float4& g4, float& cp, float& dyv, float& mc, float& mh) {
     const int t = layer == 2 ? T - 1 - jj : T - jj;
-    g4 = make_float4(0.f, 0.f, 0.f, 0.f);
-    cp = 0.f; dyv = 0.f; mc = 1.f - p.zc; mh = 1.f - p.zh;
-    if (cell && t >= 0 && t < T) {
-      const int64_t bu = ((int64_t)t * B + pb) * kU + pu;
-      if (layer == 2) {
-        g4 = reinterpret_cast<const float4*>(p.G2)[bu];
-        cp = p.C2S[bu];
-        dyv = p.DH2[bu];
-      } else {
-        g4 = reinterpret_cast<const float4*>(p.G1)[bu];
-        cp = p.C1S[bu];
-      }
-      if (masked) {
-        mc = layer == 2 ? p.m2c[bu] : p.m1c[bu];
-        mh = layer == 2 ? p.m2h[bu] : p.m1h[bu];
-      }
-    }
+    const bool on = cell && t >= 0 && t < T;
+    const int64_t bu = on ? ((int64_t)t * B + pb) * kU + pu : 0;
+    const float* Gp = layer == 2 ? p.G2 : p.G1;
+    const float* Cs = layer == 2 ? p.C2S : p.C1S;
+    const float* Mc = masked ? (layer == 2 ? p.m2c : p.m1c) : Cs;
+    const float* Mh = masked ? (layer == 2 ? p.m2h : p.m1h) : Cs;
+    g4 = reinterpret_cast<const float4*>(Gp)[bu];
+    cp = Cs[bu];
+    dyv = p.DH2[bu];
+    mc = Mc[bu];
+    mh = Mh[bu];
   };
   float4 g4n;
   float cpn, dyn, mcn, mhn;
@@ -409,19 +410,23 @@ __global__ void __launch_bounds__(kThreads) dec_lstm_bwd_kernel(DecLstmBwdP p) {
     const int t = layer == 2 ? t2 : t1;
     const bool cell_step = cell && (layer == 2 ? has2 : has1);
     const float4 g4 = g4n;
-    const float cp = cpn, dyv = dyn, mc = mcn, mh = mhn;
-    // stage dgates2_{t2+1} and dgates1_{t1+1} of the group's utterances (sc1 loads)
-    for (int idx = tid; idx < kUBmax * 2 * kU; idx += kThreads) {
-      const int ub = idx / (2 * kU), q = idx - ub * (2 * kU);
-      const int b = g + kG * ub;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (q < kU) {
-        if (stage2 && b < B) v = ldc4(rDG2, (((t2 + 1) * B + b) * 4 * kU) / 4 + q);
-        *reinterpret_cast<float4*>(&dg2s[ub][4 * q]) = v;
-      } else {
-        if (stage1 && b < B) v = ldc4(rDG1, (((t1 + 1) * B + b) * 4 * kU) / 4 + q - kU);
-        *reinterpret_cast<float4*>(&dg1s[ub][4 * (q - kU)]) = v;
-      }
+    const float cp = cpn, dyv = dyn;
+    const float mc = masked ? mcn : 1.f - p.zc, mh = masked ? mhn : 1.f - p.zh;
+    // stage dgates2_{t2+1} and dgates1_{t1+1} of the group's utterances (sc1 loads): thread =
+    // (utterance slot tid / U, float4 column tid % U); both loads issued before either is used
+    {
+      static_assert(kUBmax * kU == kThreads, "staging map");
+      const int ub = tid / kU, q = tid - ub * kU, b = g + kG * ub;
+      const bool bo = b < B;
+      const int bb = bo ? b : 0;
+      const int ta = stage2 ? t2 + 1 : 0, tc = stage1 ? t1 + 1 : 0;
+      float4 v2 = ldc4(rDG2, (((ta * B + bb) * 4 * kU) / 4) + q);
+      float4 v1 = ldc4(rDG1, (((tc * B + bb) * 4 * kU) / 4) + q);
+      const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (!(stage2 && bo)) v2 = z;
+      if (!(stage1 && bo)) v1 = z;
+      *reinterpret_cast<float4*>(&dg2s[ub][4 * q]) = v2;
+      *reinterpret_cast<float4*>(&dg1s[ub][4 * q]) = v1;
     }
     if (jj < T) load_ops(jj + 1, g4n, cpn, dyn, mcn, mhn);   // in flight across the barrier
     __syncthreads();

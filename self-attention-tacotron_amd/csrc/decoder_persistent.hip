@@ -187,15 +187,15 @@ __global__ void __launch_bounds__(256) dec_attn_fwd_kernel(DecAttnP p) {
   const bool cell = (lane & 7) == 0 && cub < UB;
   float c_own = 0.f, h_own = 0.f;
   const bool masked = p.mask_c != nullptr;
+  // prefetched cell operands: branch-free loads (clamped address, raw values, defaults applied
+  // at the use), so the prefetch stays in flight across the barrier and hand-off waits
   auto load_ops = [&](int tt, float4& xp_, float& mc_, float& mh_) {
-    xp_ = make_float4(0.f, 0.f, 0.f, 0.f);
-    mc_ = 1.f - p.zc;
-    mh_ = 1.f - p.zh;
-    if (cell && tt < T) {
-      const int64_t bu = ((int64_t)tt * B + cb) * kU + cunit;
-      xp_ = reinterpret_cast<const float4*>(p.X0)[bu];
-      if (masked) { mc_ = p.mask_c[bu]; mh_ = p.mask_h[bu]; }
-    }
+    const int64_t bu = (cell && tt < T) ? ((int64_t)tt * B + cb) * kU + cunit : 0;
+    const float* Mc = masked ? p.mask_c : p.X0;
+    const float* Mh = masked ? p.mask_h : p.X0;
+    xp_ = reinterpret_cast<const float4*>(p.X0)[bu];
+    mc_ = Mc[bu];
+    mh_ = Mh[bu];
   };
   float4 xpn;
   float mcn, mhn;
@@ -360,8 +360,8 @@ __global__ void __launch_bounds__(256) dec_attn_fwd_kernel(DecAttnP p) {
       const float gf_ = dpp_mov<0x104>(v[0]);
       const float go_ = dpp_mov<0x106>(v[0]);
       tick(2);
-      const float4 xp = xpn;
-      const float mc = mcn, mh = mhn;
+      const float4 xp = xpn;                       // used by cell lanes only (t < T here)
+      const float mc = masked ? mcn : 1.f - p.zc, mh = masked ? mhn : 1.f - p.zh;
       const unsigned bit = lsb_tag(t);
       if (cell) {
         const float gi = sigm(v[0] + xp.x);

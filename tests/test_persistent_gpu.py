@@ -69,3 +69,34 @@ def test_persistent_gradients_match_oracle(cuda):
         if not err < 2e-4:
             bad.append((name, float(err)))
     assert not bad, bad
+
+
+def test_xcd_store_policy_is_bitwise_neutral(cuda, monkeypatch):
+    """The hand-off store policy (persistent.h xcd_local_group: plain stores when the group
+    is on one XCD, sc1 otherwise; SAT_XCD_LOCAL=0 forces sc1) changes where lines live, never
+    the values: forward outputs and every parameter gradient are bit-identical (the embedding
+    table's atomic scatter-add aside)."""
+    from sat_amd import data, engine, hparams, params
+    hp = hparams.ljspeech_hparams()
+    vals = params.init_params(hp, seed=5)
+    b = data.synthetic_batch(hp, 16, N=60, T=40, shape="ljs", seed=9)
+    Np, Tp = b["source"].shape[1], b["mel"].shape[1] // hp.outputs_per_step
+    mk = data.synthetic_masks(hp, 16, Np, Tp, seed=10)
+    gb = {k: torch.tensor(v).to(cuda) for k, v in b.items()}
+    gm = {k: torch.tensor(v).to(cuda) for k, v in mk.items()}
+    res = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("SAT_XCD_LOCAL", flag)
+        m = engine.Tacotron(hp, cuda, init_values=vals, persistent_decoder=True)
+        out, sv = m.forward(gb, gm, training=True)
+        m.backward(sv)
+        torch.cuda.synchronize()
+        sv["dec"].tensors["attn_scratch"].check()
+        res.append((out["mel"].cpu().numpy(), m.grads_dict()))
+    (mel_a, g_a), (mel_b, g_b) = res
+    np.testing.assert_array_equal(mel_a, mel_b)
+    for k in g_a:
+        if k == "embedding":        # scatter-add with fp32 atomics (elementwise.hip): the order
+            np.testing.assert_allclose(g_a[k], g_b[k], rtol=1e-5, atol=1e-9)   # varies per run
+        else:
+            np.testing.assert_array_equal(g_a[k], g_b[k], err_msg=k)

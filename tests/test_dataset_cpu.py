@@ -236,3 +236,23 @@ def test_dataset_factory_names():
     hp.set_hparam("dataset", "codes.dataset.DatasetSource")
     with pytest.raises(ValueError, match="Unknown dataset"):
         D.dataset_factory([], [], hp)
+
+
+def test_shuffle_repeat_merge(tmp_path):
+    """shuffle (buffer algorithm of tf.data: a permutation, seeded), repeat(count), cache and
+    merge_target_to_source (:306-320: SourceDataForPrediction carries the target mel)."""
+    hp = _hp(max_iters=500)
+    srcs, tgts = _write_corpus(tmp_path, [120, 130, 140, 150, 160], [5, 6, 7, 8, 9])
+    z = D.DatasetSource.create_from_tfrecord_files(srcs, tgts, hp, cycle_length=2).prepare_and_zip()
+    ids = [int(s.id) for s, _ in z]
+    assert sorted(ids) == list(range(5))
+    sh = [int(s.id) for s, _ in z.shuffle(3, seed=1)]
+    assert sorted(sh) == sorted(ids)
+    assert sh == [int(s.id) for s, _ in z.shuffle(3, seed=1)]           # seeded: repeatable
+    assert [int(s.id) for s, _ in z.repeat(2)] == ids + ids
+    c = z.cache()
+    assert [int(s.id) for s, _ in c] == [int(s.id) for s, _ in c] == ids
+    s, t = next(iter(z.group_by_batch(batch_size=5).merge_target_to_source()))
+    assert isinstance(s, D.SourceDataForPrediction)
+    np.testing.assert_array_equal(s.mel, t.mel)
+    np.testing.assert_array_equal(s.target_length, t.target_length)

@@ -497,7 +497,11 @@ int sat_loss_fwd_bwd(const float* mel, const float* tgt, const float* tmask, con
  * models/models.py:175-189 + :283-287 over the whole flat arena in three launches:
  * global norm (fp64 partials), scalar prepare (Noam lr, clip scale, Adam bias correction, reads
  * and increments *global_step on the device), elementwise Adam (TF epsilon-hat form).
- * scalars[4] receives {norm, clip scale, lr, lr_t}.  workspace: sat_workspace_adam() bytes. */
+ * scalars[4] receives {norm, clip scale, lr, lr_t}.  workspace: sat_workspace_adam() bytes.
+ * Health guard: if any of the n_health int32 words at `health` (device; the step's in-kernel
+ * error words) is non-zero the whole update is skipped -- params, moments and *global_step stay
+ * as they were -- and status[2] (device, nullable) becomes {skipped steps + 1, first error code}.
+ * Lets a replayed training graph refuse garbage without a host sync. */
 typedef struct SatAdamConfig {
   float lr0, beta1, beta2, eps, clip_norm;   /* clip_norm <= 0 disables clipping */
   int32_t decay, step_factor;
@@ -508,7 +512,8 @@ int64_t sat_workspace_adam(void);
 int sat_global_norm_sq(const float* g, int64_t n, double* partials, void* stream);
 int sat_adam_step(float* params, const float* grads, float* m, float* v, int64_t n,
                   int64_t* global_step, float* scalars, void* workspace,
-                  const SatAdamConfig* cfg, void* stream);
+                  const SatAdamConfig* cfg, const int32_t* health, int32_t n_health,
+                  int32_t* status, void* stream);
 
 /* ---------------------------------------------------------------- dataset records (host)
  * TFRecord framing of the dataset path: datasets/ljspeech/dataset.py:96-112 reads

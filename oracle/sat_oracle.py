@@ -436,7 +436,8 @@ def model_forward(p: Dict[str, Tensor], bufs, hp, batch: Dict[str, Tensor],
 
 def infer_free_running(p: Dict[str, Tensor], bufs, hp, batch: Dict[str, Tensor],
                        max_iters: Optional[int] = None, min_iters: int = 10,
-                       forced: Optional[tuple] = None, feed: str = "mel"):
+                       forced: Optional[tuple] = None, feed: str = "mel",
+                       helper: Optional[str] = None):
     """PREDICT branch of model_fn (models/models.py:84-97, 252-277) with the inference decoder
     of RNNTransformer (modules/module.py:766-784): dynamic_decode over
     OutputAndStopTokenTransparentWrapper(TransformerWrapper(RNNStateHistoryWrapper(DecoderRNNV2)))
@@ -458,10 +459,26 @@ def infer_free_running(p: Dict[str, Tensor], bufs, hp, batch: Dict[str, Tensor],
     (modules/teacher_forcing_attention.py:30-35: step t returns A[:, t], the query is unused),
     the helper OneHotValidationHelper(teacher_forcing=False) (modules/helpers.py:96-108): exactly
     T' steps, no stop-token termination, and with ``feed="softmax"`` step t+1 is fed the softmax
-    over the feature bins of each frame of step t's output, last n_feed frames (:100-104)."""
+    over the feature bins of each frame of step t's output, last n_feed frames (:100-104).
+
+    ``helper="validation"`` restates OneHotValidationHelper without forced alignments
+    (modules/helpers.py:61-108, RNNTransformer with is_validation, modules/module.py:733-738):
+    exactly T' = batch["mel"].shape[1] / r steps with the real attention mechanisms, no stop
+    termination; ``feed="softmax"`` (teacher_forcing=False, model_fn EVAL's loss) or
+    ``feed="target"`` (teacher_forcing=True: step t+1 is fed targets[:, t, -M*n_feed:], :103 --
+    the incremental branch modules/transformer_test.py:44-90 compares with training)."""
     max_iters = hp.max_iters if max_iters is None else max_iters
     if forced is not None:
         max_iters = forced[0].shape[1]
+        helper = "validation"
+    helper = "stop_token" if helper is None else helper
+    tg = None
+    if helper == "validation" and forced is None:
+        max_iters = batch["mel"].shape[1] // hp.outputs_per_step
+    if feed == "target":
+        assert helper == "validation", "feed='target' is OneHotValidationHelper(teacher_forcing=True)"
+        Bt = batch["mel"].shape[0]
+        tg = batch["mel"].reshape(Bt, max_iters, -1)
     m1, m2, enc_al = encoder(batch["source"], batch["source_length"], p, bufs, hp, None, False)
     spk = None
     if hp.use_speaker_embedding and hp.speaker_embedd_to_prenet:
@@ -517,9 +534,11 @@ def infer_free_running(p: Dict[str, Tensor], bufs, hp, batch: Dict[str, Tensor],
         al2.append(a2)
         if feed == "softmax":
             x = torch.softmax(mel_t.view(B, r, M), dim=-1).reshape(B, r * M)[:, -M * nf:]
+        elif feed == "target":
+            x = tg[:, t, -M * nf:]
         else:
             x = mel_t[:, -M * nf:]
-        if forced is None and t > min_iters and bool((torch.sigmoid(stop_t) > 0.5).all()):
+        if helper == "stop_token" and t > min_iters and bool((torch.sigmoid(stop_t) > 0.5).all()):
             break
     T_out = len(mels)
     mel = torch.stack(mels, dim=1).reshape(B, T_out * r, M)

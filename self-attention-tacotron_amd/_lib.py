@@ -168,7 +168,8 @@ SIGNATURES.update({
     "sat_transpose": [_P, _I64, _P, _I64, _I32, _I32, _P],
     "sat_gemm_rowdot": [_I32, _I32, _I32, _P, _I64, _P, _I64, _P, _I64, _F, _F, _P],
     "sat_global_norm_sq": [_P, _I64, _P, _P],
-    "sat_adam_step": [_P, _P, _P, _P, _I64, _P, _P, _P, ctypes.POINTER(SatAdamConfig), _P],
+    "sat_adam_step": [_P, _P, _P, _P, _I64, _P, _P, _P, ctypes.POINTER(SatAdamConfig), _P, _I32,
+                      _P, _P],
 })
 
 RESTYPES = {"sat_workspace_colreduce": (ctypes.c_int64, [_I32, _I32]),

@@ -537,8 +537,8 @@ extern "C" int sat_decoder_lstms_fwd(const SatDecLstmFwd* a, void* stream) {
   p.xch = a->xch; p.err = a->err; p.flags = xcd_local_env();
   p.prof = reinterpret_cast<long long*>(a->prof);
   hipStream_t s = as_stream(stream);
-  if (hipMemsetAsync(a->xch, 0, sat_decoder_lstms_scratch(a->B) * sizeof(float), s) != hipSuccess ||
-      hipMemsetAsync(a->err, 0, 2 * sizeof(int), s) != hipSuccess) {
+  if (zero_dwords(a->xch, sat_decoder_lstms_scratch(a->B), s) != hipSuccess ||
+      zero_words(a->err, 2, s) != hipSuccess) {
     set_error("%s: memset failed", nm);
     return SAT_ERR_HIP;
   }
@@ -571,8 +571,8 @@ extern "C" int sat_decoder_lstms_bwd(const SatDecLstmBwd* a, void* stream) {
   p.DG1 = a->DG1; p.DG2 = a->DG2; p.ctr = a->ctr; p.err = a->err; p.flags = xcd_local_env();
   p.prof = reinterpret_cast<long long*>(a->prof);
   hipStream_t s = as_stream(stream);
-  if (hipMemsetAsync(a->ctr, 0, (kG * 64 + kG * kGW) * sizeof(unsigned), s) != hipSuccess ||
-      hipMemsetAsync(a->err, 0, 2 * sizeof(int), s) != hipSuccess) {
+  if (zero_dwords(a->ctr, (kG * 64 + kG * kGW), s) != hipSuccess ||
+      zero_words(a->err, 2, s) != hipSuccess) {
     set_error("%s: memset failed", nm);
     return SAT_ERR_HIP;
   }

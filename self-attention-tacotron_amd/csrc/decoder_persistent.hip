@@ -12,7 +12,7 @@
 // query rows (32 floats per lane) live in registers for the whole decode.
 //
 // Layout: 8 groups x 32 workgroups (256, one per CU).  Group g = blockIdx % 8 owns utterances
-// b = g + 8*ub (ub < B/8 <= 4) -- workgroups b, b+8, ... share an XCD under the observed
+// b = g + 8*ub < B (ub < 4) -- workgroups b, b+8, ... share an XCD under the observed
 // round-robin placement (speed only; correctness never depends on placement).  Workgroup
 // j = blockIdx / 8 of the group owns LSTM units [8j, 8j+8) and, if j < UB*ntiles, tile
 // (ub = j / ntiles, tile = j % ntiles).  Per step t:
@@ -113,7 +113,11 @@ __global__ void __launch_bounds__(256) dec_attn_fwd_kernel(DecAttnP p) {
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = blockIdx.x % kG, j = blockIdx.x / kG;
-  const int B = p.B, N = p.N, T = p.T, UB = p.UB, ntiles = p.ntiles;
+  const int B = p.B, N = p.N, T = p.T, ntiles = p.ntiles;
+  // utterances of this group (b = g + 8 ub < B); a group without any has no hand-off partner
+  // outside itself, so it leaves at once
+  const int UB = g < B ? (B - 1 - g) / kG + 1 : 0;
+  if (UB == 0) return;
   const bool tile_wg = j < UB * ntiles;
   const int tub = tile_wg ? j / ntiles : 0, tile = tile_wg ? j % ntiles : 0;
   const int tb = g + kG * tub;                      // utterance of this workgroup's tile
@@ -684,10 +688,10 @@ extern "C" int sat_decoder_attention_fwd(const SatDecAttnFwd* a, void* stream) {
                 a->F == kF && a->KW == kKW,
                 "sat_decoder_attention_fwd: compiled for U=256, M1=256, M2=32, D1=224, D2=32, "
                 "F=5, KW=10 (the self-attention-tacotron configs)");
-  SAT_CHECK_ARG(a->B % kG == 0 && a->B / kG <= kUBmax, "sat_decoder_attention_fwd: B in {8,16,24,32}");
+  SAT_CHECK_ARG(a->B <= kG * kUBmax, "sat_decoder_attention_fwd: B <= 32");
   const int ntiles = ceil_div(a->N, kPN);
-  SAT_CHECK_ARG((a->B / kG) * ntiles <= kGW && ntiles <= 8,
-                "sat_decoder_attention_fwd: (B/8) * ceil(N/32) must be <= 32");
+  SAT_CHECK_ARG(ceil_div(a->B, kG) * ntiles <= kGW && ntiles <= 8,
+                "sat_decoder_attention_fwd: ceil(B/8) * ceil(N/32) must be <= 32");
   SAT_CHECK_ARG(a->X0 && a->W0r && a->Wq1 && a->Wq2 && a->K1 && a->V1 && a->K2 && a->V2 &&
                 a->lengths && a->v1 && a->b1 && a->convW && a->convb && a->locW && a->v2 &&
                 a->REC0 && a->C0 && a->H0RAW && a->G0 && a->Q && a->S1 && a->AL1 && a->S2 &&
@@ -710,7 +714,7 @@ extern "C" int sat_decoder_attention_fwd(const SatDecAttnFwd* a, void* stream) {
   SAT_CHECK_ARG((int64_t)cus * per_cu >= kG * kGW,
                 "sat_decoder_attention_fwd: fewer than 256 co-resident workgroups on this device");
   DecAttnP p;
-  p.B = a->B; p.N = a->N; p.T = a->T; p.ntiles = ntiles; p.UB = a->B / kG;
+  p.B = a->B; p.N = a->N; p.T = a->T; p.ntiles = ntiles; p.UB = ceil_div(a->B, kG);
   p.u = a->u; p.zc = a->zc; p.zh = a->zh;
   p.X0 = a->X0; p.W0r = a->W0r; p.Wq1 = a->Wq1; p.Wq2 = a->Wq2;
   p.K1 = a->K1; p.V1 = a->V1; p.K2 = a->K2; p.V2 = a->V2; p.lengths = a->lengths;
@@ -730,10 +734,10 @@ extern "C" int sat_decoder_attention_fwd(const SatDecAttnFwd* a, void* stream) {
   // every hand-off slot starts zeroed (tag 0 / LSB 0 never matches steps 0 and 1)
   const int64_t e_total = hx_floats(a->B) + eh_floats(a->B, ntiles) + ah_floats(a->B, ntiles) +
                         kXidWords;
-  if (hipMemsetAsync(a->E, 0, e_total * sizeof(float), s) != hipSuccess ||
-      hipMemsetAsync(a->PART, 0, (size_t)2 * a->B * ntiles * kPST * sizeof(float), s) != hipSuccess ||
-      hipMemsetAsync(a->QP, 0, (size_t)2 * a->B * kGW * kQ * sizeof(float), s) != hipSuccess ||
-      hipMemsetAsync(a->err, 0, 2 * sizeof(int), s) != hipSuccess) {
+  if (zero_dwords(a->E, e_total, s) != hipSuccess ||
+      zero_dwords(a->PART, (size_t)2 * a->B * ntiles * kPST, s) != hipSuccess ||
+      zero_dwords(a->QP, (size_t)2 * a->B * kGW * kQ, s) != hipSuccess ||
+      zero_words(a->err, 2, s) != hipSuccess) {
     set_error("sat_decoder_attention_fwd: memset failed");
     return SAT_ERR_HIP;
   }

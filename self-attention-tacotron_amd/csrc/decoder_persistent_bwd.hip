@@ -90,7 +90,11 @@ __global__ void __launch_bounds__(kTh) dec_attn_bwd_kernel(DecAttnBwdP p) {
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = blockIdx.x % kG, j = blockIdx.x / kG;
-  const int B = p.B, N = p.N, T = p.T, UB = p.UB, ntiles = p.ntiles;
+  const int B = p.B, N = p.N, T = p.T, ntiles = p.ntiles;
+  // utterances of this group (b = g + 8 ub < B); a group without any has no hand-off partner
+  // outside itself, so it leaves at once
+  const int UB = g < B ? (B - 1 - g) / kG + 1 : 0;
+  if (UB == 0) return;
   unsigned* ctr = p.ctr + 64 * g;
   unsigned phase = 0;
   const bool tile_wg = j < UB * ntiles;
@@ -538,10 +542,10 @@ extern "C" int sat_decoder_attention_bwd(const SatDecAttnBwd* a, void* stream) {
   SAT_CHECK_ARG(a->U == kU && a->M1 == kM1 && a->M2 == kM2 && a->D1 == kD1 && a->D2 == kD2 &&
                 a->F == kF && a->KW == kKW,
                 "sat_decoder_attention_bwd: compiled for the self-attention-tacotron shapes");
-  SAT_CHECK_ARG(a->B % kG == 0 && a->B / kG <= kUBmax, "sat_decoder_attention_bwd: B in {8,16,24,32}");
+  SAT_CHECK_ARG(a->B <= kG * kUBmax, "sat_decoder_attention_bwd: B <= 32");
   const int ntiles = ceil_div(a->N, kPN);
-  SAT_CHECK_ARG((a->B / kG) * ntiles <= kGW && ntiles <= 8,
-                "sat_decoder_attention_bwd: (B/8) * ceil(N/32) must be <= 32");
+  SAT_CHECK_ARG(ceil_div(a->B, kG) * ntiles <= kGW && ntiles <= 8,
+                "sat_decoder_attention_bwd: ceil(B/8) * ceil(N/32) must be <= 32");
   SAT_CHECK_ARG(a->REC0 && a->C0 && a->G0 && a->S1 && a->AL1 && a->S2 && a->ST &&
                 a->LOC && a->V1 && a->V2 && a->v1 && a->convW && a->convb &&
                 a->locW && a->v2 && a->W0r && a->Wq1 && a->Wq2 && a->DH0 && a->ZH && a->RD && a->DG0 &&
@@ -558,7 +562,7 @@ extern "C" int sat_decoder_attention_bwd(const SatDecAttnBwd* a, void* stream) {
   SAT_CHECK_ARG((int64_t)cus * per_cu >= kG * kGW,
                 "sat_decoder_attention_bwd: fewer than 256 co-resident workgroups on this device");
   DecAttnBwdP p;
-  p.B = a->B; p.N = a->N; p.T = a->T; p.ntiles = ntiles; p.UB = a->B / kG;
+  p.B = a->B; p.N = a->N; p.T = a->T; p.ntiles = ntiles; p.UB = ceil_div(a->B, kG);
   p.u = a->u; p.zc = a->zc; p.zh = a->zh;
   p.REC0 = a->REC0; p.C0 = a->C0; p.G0 = a->G0; p.S1 = a->S1; p.AL1 = a->AL1;
   p.S2 = a->S2; p.ST = a->ST; p.LOC = a->LOC;
@@ -570,8 +574,8 @@ extern "C" int sat_decoder_attention_bwd(const SatDecAttnBwd* a, void* stream) {
   p.DFH = a->DFH; p.DQP = a->DQP; p.RDP = a->RDP; p.YA = a->YA; p.ctr = a->ctr; p.err = a->err; p.flags = xcd_local_env();
   p.prof = reinterpret_cast<long long*>(a->prof);
   hipStream_t s = as_stream(stream);
-  if (hipMemsetAsync(a->ctr, 0, (kG * 64 + kG * kGW) * sizeof(unsigned), s) != hipSuccess ||
-      hipMemsetAsync(a->err, 0, 2 * sizeof(int), s) != hipSuccess) {
+  if (zero_dwords(a->ctr, (kG * 64 + kG * kGW), s) != hipSuccess ||
+      zero_words(a->err, 2, s) != hipSuccess) {
     set_error("sat_decoder_attention_bwd: memset failed");
     return SAT_ERR_HIP;
   }

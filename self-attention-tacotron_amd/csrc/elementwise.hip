@@ -1,7 +1,7 @@
 // Bandwidth-bound kernels of the path: memory masking, embedding, BatchNormalization, max-pool,
 // highway combine, row softmax (self-attention), activation backward, the fused loss.
 // All reductions are deterministic (fixed per-thread order + fixed-shape tree), except the
-// embedding backward scatter-add (fp32 atomics, ~1.6 M adds per step).
+// embedding backward scatter-add (deterministic: one workgroup per table row, ids scanned in order).
 #include "sat_common.h"
 
 namespace sat {
@@ -42,14 +42,38 @@ __global__ void embed_fwd_kernel(const float* __restrict__ table, const int64_t*
   }
 }
 
-__global__ void embed_bwd_kernel(const float* __restrict__ dout, const int64_t* __restrict__ ids,
-                                 float* __restrict__ dtable, int64_t R, int D, int V, int64_t offset) {
-  GRID_STRIDE(i, R * D) {
-    const int64_t r = i / D;
-    const int c = (int)(i - r * D);
-    const int64_t id = ids[r] - offset;
-    if (id >= 0 && id < V) atomicAdd(&dtable[id * D + c], dout[i]);
+// Deterministic scatter-add: one workgroup per (table row v, 256-column block) scans the ids in
+// chunks of 256 and adds the rows that hit v in ascending r -- a fixed summation order, so the
+// gradient is bit-reproducible run to run (fp32 atomics are not: their order follows timing).
+// Per chunk each wave ballots its 64 ids against v; the matches are then walked lowest bit first.
+__global__ void __launch_bounds__(256) embed_bwd_kernel(const float* __restrict__ dout,
+                                                        const int64_t* __restrict__ ids,
+                                                        float* __restrict__ dtable, int64_t R,
+                                                        int D, int V, int64_t offset) {
+  __shared__ unsigned long long hit[4];
+  const int v = blockIdx.x, c = blockIdx.y * 256 + threadIdx.x;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float acc = 0.f;
+  bool any = false;
+  for (int64_t r0 = 0; r0 < R; r0 += 256) {
+    const int64_t r = r0 + threadIdx.x;
+    const bool m = r < R && ids[r] - offset == v;
+    const unsigned long long b = __builtin_amdgcn_ballot_w64(m);
+    if (lane == 0) hit[wave] = b;
+    __syncthreads();
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      unsigned long long bits = hit[w];
+      while (bits) {
+        const int k = __builtin_ctzll(bits);
+        bits &= bits - 1;
+        any = true;
+        if (c < D) acc += dout[(r0 + 64 * w + k) * D + c];
+      }
+    }
+    __syncthreads();
   }
+  if (any && c < D) dtable[(int64_t)v * D + c] += acc;
 }
 
 // ---------------------------------------------------------------- column reductions
@@ -490,7 +514,8 @@ extern "C" int sat_embedding_bwd(const float* dout, const int64_t* ids, float* d
                                  int32_t D, int32_t V, int64_t offset, void* stream) {
   SAT_CHECK_ARG(dout && ids && dtable && R >= 0 && D > 0 && V > 0, "sat_embedding_bwd: bad args");
   if (R == 0) return SAT_OK;
-  hipLaunchKernelGGL(embed_bwd_kernel, dim3(grid_for(R * D)), dim3(256), 0, as_stream(stream),
+  if (R == 0) return SAT_OK;
+  hipLaunchKernelGGL(embed_bwd_kernel, dim3(V, ceil_div(D, 256)), dim3(256), 0, as_stream(stream),
                      dout, ids, dtable, R, D, V, offset);
   SAT_LAUNCH_CHECK("sat_embedding_bwd");
   return SAT_OK;

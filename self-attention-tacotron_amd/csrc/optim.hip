@@ -5,6 +5,10 @@
 //                            p -= lr * sqrt(1-b2^t)/(1-b1^t) * m / (sqrt(v) + eps),  t = step+1
 // Everything that changes per step (global_step, the norm, lr_t) lives in device memory, so the
 // whole training step can be captured once in a hipGraph and replayed.
+// Health guard: the step's error words (the persistent kernels' hand-off timeouts, the embedding
+// id-range flag) are read on the device; if any is set the update is skipped entirely (params,
+// moments and global_step untouched) and status = {skipped steps, first error code seen} records
+// it, so a replayed graph never applies garbage and the host can raise without a sync.
 #include "sat_common.h"
 
 namespace sat {
@@ -37,8 +41,14 @@ __global__ void __launch_bounds__(256) sumsq_kernel(const float* __restrict__ g,
 __global__ void adam_prepare_kernel(const double* __restrict__ part, int nparts,
                                     int64_t* __restrict__ global_step, float* __restrict__ scalars,
                                     double lr0, int decay, int step_factor, double b1, double b2,
-                                    double clip, int do_clip, double gscale) {
+                                    double clip, int do_clip, double gscale,
+                                    const int* __restrict__ health, int n_health,
+                                    int* __restrict__ status, int* __restrict__ skip) {
   __shared__ double sh[256];
+  __shared__ int bad;
+  if (threadIdx.x == 0) bad = 0;
+  __syncthreads();
+  if ((int)threadIdx.x < n_health && health[threadIdx.x] != 0) atomicCAS(&bad, 0, health[threadIdx.x]);
   double acc = 0.0;
   for (int i = threadIdx.x; i < nparts; i += blockDim.x) acc += part[i];
   sh[threadIdx.x] = acc;
@@ -48,6 +58,14 @@ __global__ void adam_prepare_kernel(const double* __restrict__ part, int nparts,
     __syncthreads();
   }
   if (threadIdx.x == 0) {
+    *skip = bad != 0 ? 1 : 0;
+    if (bad != 0) {                       // unhealthy step: no update, no step increment
+      if (status) {
+        status[0] += 1;
+        if (status[1] == 0) status[1] = bad;
+      }
+      return;
+    }
     const double norm = gscale * sqrt(sh[0]);
     const double scale = gscale * (do_clip ? clip / fmax(norm, clip) : 1.0);
     const int64_t gs = *global_step;
@@ -71,7 +89,9 @@ __global__ void __launch_bounds__(256) adam_update_kernel(float* __restrict__ p,
                                                           const float* __restrict__ g,
                                                           float* __restrict__ m, float* __restrict__ v,
                                                           int64_t n, const float* __restrict__ scalars,
-                                                          float b1, float b2, float eps) {
+                                                          float b1, float b2, float eps,
+                                                          const int* __restrict__ skip) {
+  if (*skip) return;
   const float scale = scalars[1], lr_t = scalars[3];
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
@@ -89,7 +109,8 @@ __global__ void __launch_bounds__(256) adam_update_kernel(float* __restrict__ p,
 
 using namespace sat;
 
-extern "C" int64_t sat_workspace_adam(void) { return (int64_t)kNormBlocks * sizeof(double); }
+// workspace: fp64 norm partials, then the skip word of the health guard
+extern "C" int64_t sat_workspace_adam(void) { return (int64_t)kNormBlocks * sizeof(double) + 16; }
 
 extern "C" int sat_global_norm_sq(const float* g, int64_t n, double* part, void* stream) {
   SAT_CHECK_ARG(g && part && n >= 0, "sat_global_norm_sq: bad args");
@@ -100,20 +121,24 @@ extern "C" int sat_global_norm_sq(const float* g, int64_t n, double* part, void*
 
 extern "C" int sat_adam_step(float* params, const float* grads, float* m, float* v, int64_t n,
                              int64_t* global_step, float* scalars, void* workspace,
-                             const SatAdamConfig* cfg, void* stream) {
+                             const SatAdamConfig* cfg, const int32_t* health, int32_t n_health,
+                             int32_t* status, void* stream) {
   SAT_CHECK_ARG(params && grads && m && v && global_step && scalars && workspace && cfg && n >= 0,
                 "sat_adam_step: bad args");
+  SAT_CHECK_ARG(n_health >= 0 && n_health <= 256 && (n_health == 0 || health),
+                "sat_adam_step: health words: 0..256 int32 (pointer needed when n_health > 0)");
   SAT_CHECK_ARG(cfg->grad_scale > 0.f, "sat_adam_step: grad_scale must be > 0");
   hipStream_t s = as_stream(stream);
   double* part = reinterpret_cast<double*>(workspace);
+  int* skip = reinterpret_cast<int*>(part + kNormBlocks);
   hipLaunchKernelGGL(sumsq_kernel, dim3(kNormBlocks), dim3(256), 0, s, grads, n, part);
   hipLaunchKernelGGL(adam_prepare_kernel, dim3(1), dim3(256), 0, s, part, kNormBlocks, global_step,
                      scalars, (double)cfg->lr0, cfg->decay, cfg->step_factor, (double)cfg->beta1,
                      (double)cfg->beta2, (double)cfg->clip_norm, cfg->clip_norm > 0.f ? 1 : 0,
-                     (double)cfg->grad_scale);
+                     (double)cfg->grad_scale, health, n_health, status, skip);
   const int blocks = (int)std::min<int64_t>((n + 255) / 256, 8192);
   hipLaunchKernelGGL(adam_update_kernel, dim3(blocks), dim3(256), 0, s, params, grads, m, v, n,
-                     scalars, cfg->beta1, cfg->beta2, cfg->eps);
+                     scalars, cfg->beta1, cfg->beta2, cfg->eps, skip);
   SAT_LAUNCH_CHECK("sat_adam_step");
   return SAT_OK;
 }

@@ -1,5 +1,6 @@
 // Internal helpers shared by the libsat_hip kernels (gfx950 / CDNA4 only).
 #pragma once
+#include <algorithm>
 
 #include <hip/hip_runtime.h>
 #include <cstdint>
@@ -140,5 +141,23 @@ __device__ __forceinline__ float tanh_fast(float x) {
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 inline int ceil_div(int64_t a, int64_t b) { return static_cast<int>((a + b - 1) / b); }
+
+// Scratch, counters and error words of the persistent launches are cleared by a kernel rather
+// than hipMemsetAsync: under hipGraph replay an 8-byte memset node was seen to write 0x16161616
+// instead of 0 into an error word (tools/probes/graph_vs_eager.py), which made polls give up and
+// the guarded optimiser skip the step.  A kernel node has no such path.
+__global__ static void zero_dwords_kernel(unsigned* __restrict__ p, int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    p[i] = 0u;
+}
+inline hipError_t zero_dwords(void* p, int64_t n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  const int blocks = (int)std::min<int64_t>((n + 255) / 256, 1024);
+  hipLaunchKernelGGL(zero_dwords_kernel, dim3(blocks), dim3(256), 0, s,
+                     reinterpret_cast<unsigned*>(p), n);
+  return hipGetLastError();
+}
+inline hipError_t zero_words(int* p, int n, hipStream_t s) { return zero_dwords(p, n, s); }
 
 }  // namespace sat

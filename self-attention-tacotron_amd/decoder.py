@@ -62,7 +62,7 @@ def persistent_eligible(d: Dims, B: int, N: int, attn_tile: int = 32) -> bool:
     return (d.att1 == "forward" and d.att2 == "additive" and attn_tile == 32 and
             (d.att_rnn, d.m1, d.m2, d.d1, d.d2, d.loc_f, d.loc_k, d.dec) ==
             (256, 256, 32, 224, 32, 5, 10, 256)
-            and B % 8 == 0 and B // 8 <= 4 and (B // 8) * ((N + 31) // 32) <= 32)
+            and 0 < B <= 32 and ((B + 7) // 8) * ((N + 31) // 32) <= 32)
 
 
 def decoder_forward(P: Dict[str, torch.Tensor], hp, d: Dims, m1: torch.Tensor, m2: torch.Tensor,

@@ -44,6 +44,16 @@ def allreduce_grads(flat: torch.Tensor, group=None) -> None:
         tdist.all_reduce(flat, op=tdist.ReduceOp.SUM, group=group)
 
 
+def average_buffer(flat: torch.Tensor, group=None) -> None:
+    """Mean over replicas in place (BatchNorm moving statistics: the replicas' updates are
+    averaged each step so every rank holds the same EVAL / checkpoint state; TF1
+    MirroredStrategy's exact aggregation of BN moving averages is unpinned)."""
+    w = world_size(group)
+    if w > 1:
+        tdist.all_reduce(flat, op=tdist.ReduceOp.SUM, group=group)
+        flat.mul_(1.0 / w)
+
+
 def max_over_ranks(value: float, device, group=None) -> float:
     """The bench's step time: the slowest rank defines the job's throughput."""
     if world_size(group) == 1:

@@ -39,22 +39,46 @@ class Tacotron:
         self.pipe = Pipeline(self.device, pipeline_chunk)
         # attention chain of the decoder forward as one persistent launch (when eligible)
         self.persistent_decoder = persistent_decoder
+        # one persistent-kernel scratch per batch size, sized for the largest N seen (a batch of
+        # a smaller N runs in a prefix of it), so a stream of differently padded batches does
+        # not grow device memory
         self._scratch = {}
+        # health arena: int32 error words of one step -- [0:2] attention chain fwd, [2:4] / [4:6]
+        # decoder LSTM stack fwd / bwd, [6:8] attention chain bwd, [8] embedding id range,
+        # [9] speaker-embedding id range; read on the device by the guarded Adam step
+        self.health = torch.zeros(16, dtype=torch.int32, device=self.device)
+
+    HEALTH_WORDS = {0: "sat_decoder_attention_fwd hand-off timeout",
+                    2: "sat_decoder_lstms_fwd hand-off timeout",
+                    4: "sat_decoder_lstms_bwd group-barrier timeout",
+                    6: "sat_decoder_attention_bwd group-barrier timeout",
+                    8: "embedding id out of range", 9: "speaker id out of range"}
+
+    def scratch(self, B: int, N: int):
+        sc = self._scratch.get(B)
+        if sc is None or sc.N < N:
+            sc = K.DecoderAttentionScratch(B, max(N, 0 if sc is None else sc.N), self.device,
+                                           errs=self.health)
+            self._scratch[B] = sc
+        return sc
 
     # ------------------------------------------------------------------ steps
     def forward(self, batch: Dict[str, torch.Tensor], masks=None, training: bool = True,
                 need_grad: bool = True):
         B, N = batch["source"].shape
-        scratch = None
-        if self.persistent_decoder:
-            key = (B, N)
-            if key not in self._scratch:
-                self._scratch[key] = K.DecoderAttentionScratch(B, N, self.device)
-            scratch = self._scratch[key]
+        scratch = self.scratch(B, N) if self.persistent_decoder else None
         return model_forward(self.P, self.bn, self.hp, self.d, batch, masks, training, self.ws,
                              compute_grad_seeds=need_grad, attn_tile=self.attn_tile,
                              pipe=self.pipe, persistent=self.persistent_decoder,
-                             scratch=scratch)
+                             scratch=scratch, health=self.health)
+
+    def raise_on_health(self, words) -> None:
+        """Raise SatLibraryError naming every set error word (host copy of the arena)."""
+        bad = [f"{self.HEALTH_WORDS.get(i, f'word {i}')} (code {int(v)})"
+               for i, v in enumerate(words) if int(v) != 0]
+        if bad:
+            from ._lib import SatLibraryError
+            raise SatLibraryError("training step unhealthy: " + "; ".join(bad))
 
     def backward(self, saved, zero: bool = True):
         if zero:

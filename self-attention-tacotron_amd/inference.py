@@ -28,6 +28,19 @@ t+1 is fed the per-frame softmax over the feature bins of step t's output (``fee
 the fork's code-prediction feedback, :100-104) and the loop runs exactly T' = A.shape[1] steps
 (``finished = time + 1 >= num_steps``, :101), with no stop-token termination.
 
+Validation decoding (``helper="validation"``: ``OneHotValidationHelper``, modules/helpers.py:61-108,
+built by ``RNNTransformer.__call__`` with ``is_validation=True``, modules/module.py:733-738):
+exactly T' = T/r steps of the batch's targets (``finished = time + 1 >= num_steps``, :101), no
+stop-token termination; step t+1 is fed either the per-frame softmax of step t's output
+(``feed="softmax"``, teacher_forcing=False: model_fn EVAL's ``loss``/``code_loss``/``done_loss``,
+models/models.py:86-97, 159-173) or the target frame ``targets[:, t, -M*n_feed:]``
+(``feed="target"``, teacher_forcing=True: the incremental branch modules/transformer_test.py:44-90
+compares with the training branch).
+
+Schedule: every buffer of a decode lives in a per-shape plan (static addresses), so a decode of
+``check_every`` steps can be captured once as a hipGraph (``graphs=True``) and replayed: the host
+issues one graph launch per chunk instead of ~30 kernel launches per step.
+
 Every arithmetic op is a libsat_hip kernel; torch allocates, views and copies.
 """
 
@@ -43,21 +56,40 @@ from .model import BNState, encoder_fwd
 from .params import Dims
 
 
+class _Plan:
+    """Static buffers of one decode shape (B, N, T_max) plus the per-step launch closures."""
+
+
 class FreeRunningDecoder:
-    """One free-running decode of a batch (eval semantics).  ``check_every`` = decoder steps
-    between host reads of the device-side finished flag."""
+    """Incremental decoding of a batch with eval semantics (no dropout, zoneout blend, BN moving
+    statistics).
+
+    ``helper``: ``"stop_token"`` (PREDICT, StopTokenBasedInferenceHelper: up to ``max_iters``
+    steps, stops once every utterance's stop token fired after ``min_iters``) or
+    ``"validation"`` (OneHotValidationHelper: exactly T' = batch["mel"].shape[1] / r steps).
+    ``feed``: what step t+1 is fed -- ``"mel"`` (the last predicted frame), ``"softmax"`` (its
+    per-frame softmax over the feature bins) or ``"target"`` (the target frame; validation only).
+    ``forced_alignments=(A1, A2)`` replays given alignments (TeacherForcing*Attention) and
+    implies the validation helper with T' = A1.shape[1].
+    ``check_every`` = decoder steps between host reads of the device-side finished flag (and
+    the steps per captured graph when ``graphs=True``)."""
 
     def __init__(self, model, max_iters: Optional[int] = None, min_iters: int = 10,
-                 check_every: int = 25, forced_alignments=None, feed: str = "mel"):
+                 check_every: int = 25, forced_alignments=None, feed: str = "mel",
+                 helper: Optional[str] = None, graphs: bool = False):
         self.m = model
         self.hp = model.hp
         self.d: Dims = model.d
+        if getattr(self.hp, "apply_dropout_on_inference", False):
+            # PreNet(apply_dropout_on_inference=True) keeps prenet dropout at inference
+            # (modules/module.py:1513-1517); this build decodes with eval semantics only
+            raise NotImplementedError("apply_dropout_on_inference=True is not supported: "
+                                      "decoding runs with eval semantics (no prenet dropout)")
         self.max_iters = int(self.hp.max_iters if max_iters is None else max_iters)
         self.min_iters = int(min_iters)
         self.check_every = max(1, int(check_every))
-        if feed not in ("mel", "softmax"):
-            raise ValueError(f"feed must be 'mel' or 'softmax', got {feed!r}")
-        self.feed = feed
+        if feed not in ("mel", "softmax", "target"):
+            raise ValueError(f"feed must be 'mel', 'softmax' or 'target', got {feed!r}")
         self.forced = None
         if forced_alignments is not None:
             a1, a2 = forced_alignments
@@ -65,27 +97,32 @@ class FreeRunningDecoder:
                 raise ValueError("forced alignments must be two [B, T', N] tensors")
             self.forced = (a1.contiguous(), a2.contiguous())
             self.max_iters = int(a1.shape[1])
+            helper = "validation" if helper is None else helper
+        helper = "stop_token" if helper is None else helper
+        if helper not in ("stop_token", "validation"):
+            raise ValueError(f"helper must be 'stop_token' or 'validation', got {helper!r}")
+        if feed == "target" and helper != "validation":
+            raise ValueError("feed='target' (teacher forcing) needs the validation helper")
+        if self.forced is not None and helper != "validation":
+            raise ValueError("forced alignments run under the validation helper")
+        self.helper = helper
+        self.feed = feed
+        self.graphs = bool(graphs)
+        self._plans: Dict[tuple, _Plan] = {}
 
-    # ------------------------------------------------------------------ one decode
-    @torch.no_grad()
-    def run(self, batch: Dict[str, torch.Tensor]) -> Dict[str, object]:
+    # ------------------------------------------------------------------ plan (static buffers)
+    def _plan(self, B: int, N: int, Tm: int) -> _Plan:
+        key = (B, N, Tm)
+        pl = self._plans.get(key)
+        if pl is None:
+            pl = self._build(B, N, Tm)
+            self._plans[key] = pl
+        return pl
+
+    def _build(self, B: int, N: int, Tm: int) -> _Plan:
         m, hp, d = self.m, self.hp, self.d
         P, dev = m.P, m.device
-        ids, lengths = batch["source"], batch["source_length"]
-        B, N = ids.shape
-        sv = {}
-        m1, m2 = encoder_fwd(P, m.bn, hp, d, ids, lengths, None, False, m.ws, sv)
-        spk = None
-        if d.multi_speaker:
-            spk = torch.empty(B, d.spk_dim, device=dev)
-            err = torch.zeros(1, dtype=torch.int32, device=dev)
-            K.embedding_fwd(P["speaker_embedding"], batch["speaker_id"], spk, d.spk_offset, err)
-        Tm = self.max_iters
         f32 = dict(device=dev, dtype=torch.float32)
-        forced = self.forced
-        if forced is not None and tuple(forced[0].shape) != (B, Tm, N):
-            raise ValueError(f"forced alignments must be [B={B}, T', N={N}], got "
-                             f"{tuple(forced[0].shape)}")
         M, r, nf = d.num_mels, d.r, hp.n_feed_frame
         A, Dd, M1, M2, D1, D2 = d.att_rnn, d.dec, d.m1, d.m2, d.d1, d.d2
         R0 = M1 + M2 + A
@@ -94,42 +131,45 @@ class FreeRunningDecoder:
         att1_fwd = 1 if d.att1 == "forward" else 0
         if d.att2 != "additive":
             raise NotImplementedError("attention2 must be 'additive' (hparams.py:98)")
-
-        # ---- memories (TF _prepare_memory + memory_layer)
-        V1 = K.seq_mask(m1, lengths)
-        V2 = K.seq_mask(m2, lengths)
-        K1 = K.linear(V1, P[f"{a1}/memory_layer/kernel"])
-        K2 = K.linear(V2, P[f"{a2}/memory_layer/kernel"])
+        pl = _Plan()
+        pl.B, pl.N, pl.Tm = B, N, Tm
+        # ---- inputs (copied in per run) and memories
+        pl.lengths = torch.zeros(B, dtype=torch.int64, device=dev)
+        pl.V1 = torch.zeros(B, N, M1, **f32)
+        pl.V2 = torch.zeros(B, N, M2, **f32)
+        pl.K1 = torch.zeros(B, N, D1, **f32)
+        pl.K2 = torch.zeros(B, N, D2, **f32)
+        pl.sp = torch.zeros(B, d.dec_prenet[0], **f32) if d.multi_speaker else None
+        pl.XT = torch.zeros(Tm, B, M * nf, **f32) if self.feed == "target" else None
+        pl.FA = ((torch.zeros(B, Tm, N, **f32), torch.zeros(B, Tm, N, **f32))
+                 if self.forced is not None else None)
         # ---- state (step-major histories)
-        MEL = torch.zeros(Tm, B, M * r, **f32)
-        STOP = torch.zeros(Tm, B, 1, **f32)
+        pl.MEL = MEL = torch.zeros(Tm, B, M * r, **f32)
+        pl.STOP = STOP = torch.zeros(Tm, B, 1, **f32)
         GO = torch.zeros(B, M * nf, **f32)
-        SMX = torch.empty(B, M * r, **f32)                # softmax feedback (feed="softmax")
-        REC0 = torch.zeros(Tm + 1, B, R0, **f32)          # [c1 | c2 | h0] per step
+        SMX = torch.empty(B, M * r, **f32)                 # softmax feedback (feed="softmax")
+        pl.REC0 = REC0 = torch.zeros(Tm + 1, B, R0, **f32)  # [c1 | c2 | h0] per step
         C0 = torch.zeros(2, B, A, **f32)
         H0RAW = torch.empty(B, A, **f32)
         L1 = [torch.zeros(2, B, Dd, **f32), torch.zeros(2, B, Dd, **f32)]   # c, h ping-pong
         L2 = [torch.zeros(2, B, Dd, **f32), torch.zeros(2, B, Dd, **f32)]
         H1RAW = torch.empty(B, Dd, **f32)
         H2RAW = torch.empty(B, Dd, **f32)
-        GA = torch.empty(B, 4 * A, **f32)                 # activated gates (unused at inference)
+        GA = torch.empty(B, 4 * A, **f32)                  # activated gates (unused here)
         GD = torch.empty(B, 4 * Dd, **f32)
         X0 = torch.empty(B, 4 * A, **f32)
         X1 = torch.empty(B, 4 * Dd, **f32)
         X2 = torch.empty(B, 4 * Dd, **f32)
         Q = torch.empty(B, D1 + D2, **f32)
-        S1 = torch.zeros(Tm + 1, B, N, **f32)
-        AL1 = torch.zeros(Tm + 1, B, N, **f32)
-        AL1[0, :, 0] = 1.0                                # forward_attention.py:131-133
-        S2 = torch.zeros(Tm, B, N, **f32)
+        pl.S1 = S1 = torch.zeros(Tm + 1, B, N, **f32)
+        pl.AL1 = AL1 = torch.zeros(Tm + 1, B, N, **f32)
+        pl.S2 = S2 = torch.zeros(Tm, B, N, **f32)
         ntiles = (N + 31) // 32
         pst = K.part_stride(M1, M2)
         E1 = torch.empty(B, N, **f32)
         E2 = torch.empty(B, N, **f32)
         PART = torch.empty(B, ntiles, pst, **f32)
-        QT = torch.empty(D1 + D2, A, **f32)
-        K.transpose(P[f"{a1}/query_layer/kernel"], QT[:D1])
-        K.transpose(P[f"{a2}/query_layer/kernel"], QT[D1:])
+        pl.QT = QT = torch.empty(D1 + D2, A, **f32)
         W0 = P["decoder/attention_lstm/kernel"]
         W1 = P["decoder/lstm1/kernel"]
         W2 = P["decoder/lstm2/kernel"]
@@ -140,16 +180,17 @@ class FreeRunningDecoder:
         KC = [torch.zeros(B, Tm, dsa, **f32) for _ in range(d.dec_hops)]
         VC = [torch.zeros(B, Tm, dsa, **f32) for _ in range(d.dec_hops)]
         # row t of each hop's causal probabilities (= the final step's full [T', T'] matrix)
-        SA_P = [torch.zeros(B, H, Tm, Tm, **f32) for _ in range(d.dec_hops)]
-        state = torch.full((1,), -1, dtype=torch.int32, device=dev)
-        sp = None
-        if spk is not None:
-            ms = "decoder/prenet0"
-            sp = K.linear(spk, P[f"{ms}/speaker_projection/kernel"],
-                          P[f"{ms}/speaker_projection/bias"], act="softsign")
+        pl.SA_P = SA_P = [torch.zeros(B, H, Tm, Tm, **f32) for _ in range(d.dec_hops)]
+        pl.state = state = torch.full((1,), -1, dtype=torch.int32, device=dev)
+        pl.zero_each_run = [REC0, C0, L1[0], L1[1], L2[0], L2[1], S1, AL1, S2, MEL, STOP]
+        pl.graphs = {}
+        lengths, V1, V2, K1, K2 = pl.lengths, pl.V1, pl.V2, pl.K1, pl.K2
+        sp, XT, FA = pl.sp, pl.XT, pl.FA
+        feed, forced_mode, stop_mode = self.feed, FA is not None, self.helper == "stop_token"
+        min_iters = self.min_iters
 
         def prenets(x):
-            if sp is not None:                            # multi_speaker_modules.py:27-32
+            if sp is not None:                             # multi_speaker_modules.py:27-32
                 ms = "decoder/prenet0"
                 y = K.gemm(x, P[f"{ms}/dense0/kernel"], bias=P[f"{ms}/dense0/bias"], act="relu",
                            add=sp)
@@ -191,34 +232,9 @@ class FreeRunningDecoder:
             K.linear(z, P["decoder/stop_token_projection/kernel"],
                      P["decoder/stop_token_projection/bias"], out=STOP[t])
 
-        def step(t):
-            cur, nxt = t % 2, (t + 1) % 2
-            if t == 0:
-                x = GO
-            elif self.feed == "softmax":                  # OneHotValidationHelper :100-104
-                K.softmax_fwd(MEL[t - 1].view(B * r, M), SMX.view(B * r, M), causal=False)
-                x = SMX[:, M * (r - nf):]
-            else:
-                x = MEL[t - 1][:, M * (r - nf):]
-            pre = prenets(x)
-            K.linear(pre, W0[:p_w], P["decoder/attention_lstm/bias"], out=X0)
-            K.lstm_step_fwd(B=B, U=A, K=R0, t=t, xproj=X0, rin=REC0[t], W=W0[p_w:],
-                            c_prev=C0[cur], h_prev=REC0[t, :, M1 + M2:], mask_c=None,
-                            mask_h=None, zc=zc, zh=zh, h_raw=H0RAW, c_out=C0[nxt],
-                            h_out=REC0[t + 1, :, M1 + M2:], gates=GA)
-            if forced is not None:
-                forced_step(t)
-            else:
-                attention_step(t)
-            # LSTM1 on o_t = [h0'_t | c1_t | c2_t] (ConcatOutputAndAttentionWrapper)
-            lstm_stack(t, cur, nxt)
-            head_step(H2RAW, t)
-            if forced is None:
-                K.stop_check(STOP[t], t, self.min_iters, state)
-
         def forced_step(t):
             """TeacherForcing*Attention: alignments = A[:, t]; contexts = A[:, t] . values."""
-            a1t, a2t = forced[0][:, t], forced[1][:, t]
+            a1t, a2t = FA[0][:, t], FA[1][:, t]
             AL1[t + 1].copy_(a1t)
             S2[t].copy_(a2t)
             K.gemm(a1t.unsqueeze(1), V1, REC0[t + 1][:, :M1].unsqueeze(1))
@@ -252,22 +268,129 @@ class FreeRunningDecoder:
                             zc=zc, zh=zh, h_raw=H2RAW, c_out=L2[0][nxt], h_out=L2[1][nxt],
                             gates=GD)
 
+        def step(t):
+            cur, nxt = t % 2, (t + 1) % 2
+            if t == 0:
+                x = GO
+            elif feed == "target":                         # OneHotValidationHelper :103
+                x = XT[t]
+            elif feed == "softmax":                        # OneHotValidationHelper :100-104
+                K.softmax_fwd(MEL[t - 1].view(B * r, M), SMX.view(B * r, M), causal=False)
+                x = SMX[:, M * (r - nf):]
+            else:
+                x = MEL[t - 1][:, M * (r - nf):]
+            pre = prenets(x)
+            K.linear(pre, W0[:p_w], P["decoder/attention_lstm/bias"], out=X0)
+            K.lstm_step_fwd(B=B, U=A, K=R0, t=t, xproj=X0, rin=REC0[t], W=W0[p_w:],
+                            c_prev=C0[cur], h_prev=REC0[t, :, M1 + M2:], mask_c=None,
+                            mask_h=None, zc=zc, zh=zh, h_raw=H0RAW, c_out=C0[nxt],
+                            h_out=REC0[t + 1, :, M1 + M2:], gates=GA)
+            if forced_mode:
+                forced_step(t)
+            else:
+                attention_step(t)
+            # LSTM1 on o_t = [h0'_t | c1_t | c2_t] (ConcatOutputAndAttentionWrapper)
+            lstm_stack(t, cur, nxt)
+            head_step(H2RAW, t)
+            if stop_mode:
+                K.stop_check(STOP[t], t, min_iters, state)
+
+        pl.step = step
+        return pl
+
+    # ------------------------------------------------------------------ one decode
+    def _prepare(self, pl: _Plan, batch, spk_rows):
+        """Per-run inputs into the plan's static buffers: memories, feeds, reset state."""
+        m, hp, d = self.m, self.hp, self.d
+        P = m.P
+        B, N, Tm = pl.B, pl.N, pl.Tm
+        for t in pl.zero_each_run:
+            t.zero_()
+        pl.AL1[0, :, 0] = 1.0                                 # forward_attention.py:131-133
+        pl.state.fill_(-1)
+        pl.lengths.copy_(batch["source_length"])
+        K.transpose(P["decoder/attention1/query_layer/kernel"], pl.QT[:d.d1])
+        K.transpose(P["decoder/attention2/query_layer/kernel"], pl.QT[d.d1:])
+        if pl.sp is not None:
+            ms = "decoder/prenet0"
+            K.linear(spk_rows, P[f"{ms}/speaker_projection/kernel"],
+                     P[f"{ms}/speaker_projection/bias"], act="softsign", out=pl.sp)
+        if pl.XT is not None:                                  # OneHotValidationHelper :103
+            M, r, nf = d.num_mels, d.r, hp.n_feed_frame
+            tg = batch["mel"].reshape(B, Tm, M * r)
+            pl.XT[1:].copy_(tg[:, :-1, M * (r - nf):].transpose(0, 1))
+        if pl.FA is not None:
+            pl.FA[0].copy_(self.forced[0])
+            pl.FA[1].copy_(self.forced[1])
+
+    def _steps(self, pl: _Plan, a: int, b: int):
+        if not self.graphs:
+            for t in range(a, b):
+                pl.step(t)
+            return
+        g = pl.graphs.get(a)
+        if g is None:
+            # capture on a side stream (the current stream's pending work is joined first);
+            # the graph's private pool keeps every per-step temporary alive across replays
+            s = torch.cuda.Stream(device=self.m.device)
+            s.wait_stream(torch.cuda.current_stream())
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.stream(s):
+                with torch.cuda.graph(g, stream=s):
+                    for t in range(a, b):
+                        pl.step(t)
+            torch.cuda.current_stream().wait_stream(s)
+            pl.graphs[a] = g
+        g.replay()
+
+    @torch.no_grad()
+    def run(self, batch: Dict[str, torch.Tensor]) -> Dict[str, object]:
+        m, hp, d = self.m, self.hp, self.d
+        P, dev = m.P, m.device
+        ids, lengths = batch["source"], batch["source_length"]
+        B, N = ids.shape
+        if self.helper == "validation" and self.forced is None:
+            if "mel" not in batch:
+                raise ValueError("the validation helper needs the batch's targets (batch['mel'])")
+            Tm = int(batch["mel"].shape[1]) // d.r              # OneHotValidationHelper :69
+        else:
+            Tm = self.max_iters
+        if self.forced is not None and tuple(self.forced[0].shape) != (B, Tm, N):
+            raise ValueError(f"forced alignments must be [B={B}, T', N={N}], got "
+                             f"{tuple(self.forced[0].shape)}")
+        pl = self._plan(B, N, Tm)
+        sv = {}
+        m1, m2 = encoder_fwd(P, m.bn, hp, d, ids, lengths, None, False, m.ws, sv)
+        spk = None
+        if d.multi_speaker:
+            spk = torch.empty(B, d.spk_dim, device=dev)
+            err = torch.zeros(1, dtype=torch.int32, device=dev)
+            K.embedding_fwd(P["speaker_embedding"], batch["speaker_id"], spk, d.spk_offset, err)
+        # ---- memories (TF _prepare_memory + memory_layer) into the plan's buffers
+        self._prepare(pl, batch, spk)
+        K.seq_mask(m1, pl.lengths, out=pl.V1)
+        K.seq_mask(m2, pl.lengths, out=pl.V2)
+        K.linear(pl.V1, P["decoder/attention1/memory_layer/kernel"], out=pl.K1)
+        K.linear(pl.V2, P["decoder/attention2/memory_layer/kernel"], out=pl.K2)
+
+        stop_mode = self.helper == "stop_token"
         steps = Tm
-        for t in range(Tm):
-            step(t)
-            if forced is not None:
-                continue
-            if (t + 1) % self.check_every == 0 or t + 1 == Tm:
-                first = int(state.item())
+        for a in range(0, Tm, self.check_every):
+            b = min(Tm, a + self.check_every)
+            self._steps(pl, a, b)
+            if stop_mode:
+                first = int(pl.state.item())
                 if first >= 0:
                     steps = first + 1
                     break
-        B_, T_ = B, steps
-        mel = MEL[:T_].permute(1, 0, 2).reshape(B_, T_ * r, M)
-        stop = STOP[:T_, :, 0].transpose(0, 1).contiguous()
+        T_ = steps
+        r, M = d.r, d.num_mels
+        mel = pl.MEL[:T_].permute(1, 0, 2).reshape(B, T_ * r, M)
+        stop = pl.STOP[:T_, :, 0].transpose(0, 1).contiguous()
         return {"mel": mel, "stop": stop, "steps": T_,
-                "alignment1": AL1[1:T_ + 1].permute(1, 2, 0).contiguous(),   # [B, N, T']
-                "alignment2": S2[:T_].permute(1, 2, 0).contiguous(),
-                "decoder_self_alignments": [SA_P[h][:, :, :T_, :T_] for h in range(d.dec_hops)],
+                "alignment1": pl.AL1[1:T_ + 1].permute(1, 2, 0).contiguous(),   # [B, N, T']
+                "alignment2": pl.S2[:T_].permute(1, 2, 0).contiguous(),
+                "decoder_self_alignments": [pl.SA_P[h][:, :, :T_, :T_].clone()
+                                            for h in range(d.dec_hops)],
                 "encoder_self_alignments": [sv[f"enc_sa{h}"]["P"] for h in range(d.enc_hops)],
                 "m1": m1, "m2": m2}

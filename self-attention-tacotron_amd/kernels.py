@@ -327,7 +327,12 @@ class DecoderAttentionScratch:
     """Device scratch of sat_decoder_attention_fwd for one (B, N): raw energies, tile partials,
     group counters and the error word (allocated before graph capture)."""
 
-    def __init__(self, B: int, N: int, device):
+    def __init__(self, B: int, N: int, device, errs: torch.Tensor = None):
+        """``errs``: optional int32 device words (>= 8) the four persistent kernels' error pairs
+        are carved from (the engine's health arena, read by the guarded Adam step)."""
+        if errs is None:
+            errs = torch.zeros(8, dtype=torch.int32, device=device)
+        self.B, self.N = B, N
         e, pt, qp = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
         words = int(_lib.load().sat_decoder_attention_scratch(B, N, ctypes.byref(e),
                                                               ctypes.byref(pt), ctypes.byref(qp)))
@@ -335,14 +340,14 @@ class DecoderAttentionScratch:
         self.PART = torch.empty(pt.value, device=device)
         self.QP = torch.empty(qp.value, device=device)
         self.ctr = torch.zeros(words, dtype=torch.int32, device=device)
-        self.err = torch.zeros(2, dtype=torch.int32, device=device)
-        self.bwd = DecoderAttentionBwdScratch(B, N, device)   # the persistent BPTT's own
+        self.err = errs[0:2]
+        self.bwd = DecoderAttentionBwdScratch(B, N, device, errs[6:8])   # the persistent BPTT's own
 
         # the persistent decoder LSTM stack's own counters / error words (fwd, bwd)
         self.lstm_xch = torch.zeros(int(_lib.load().sat_decoder_lstms_scratch(B)), device=device)
         self.lstm_ctr = torch.zeros(int(_lib.load().sat_decoder_lstms_bwd_scratch(B)),
                                     dtype=torch.int32, device=device)
-        self.lstm_err = torch.zeros(2, 2, dtype=torch.int32, device=device)   # fwd, bwd
+        self.lstm_err = errs[2:6].view(2, 2)                                  # fwd, bwd
 
     def check(self):
         """Host check of the in-kernel barrier timeout flags (synchronises)."""
@@ -368,14 +373,14 @@ class DecoderAttentionBwdScratch:
     """Device scratch of sat_decoder_attention_bwd for one (B, N): row-dot partials, the
     alignment-recursion gradient ping-pong, group counters and the error word."""
 
-    def __init__(self, B: int, N: int, device):
+    def __init__(self, B: int, N: int, device, err: torch.Tensor = None):
         rdp, ya = ctypes.c_int64(), ctypes.c_int64()
         words = int(_lib.load().sat_decoder_attention_bwd_scratch(B, N, ctypes.byref(rdp),
                                                                   ctypes.byref(ya)))
         self.RDP = torch.empty(rdp.value, device=device)
         self.YA = torch.empty(ya.value, device=device)
         self.ctr = torch.zeros(words, dtype=torch.int32, device=device)
-        self.err = torch.zeros(2, dtype=torch.int32, device=device)
+        self.err = torch.zeros(2, dtype=torch.int32, device=device) if err is None else err
 
     def check(self):
         if int(self.err[0].item()) != 0:

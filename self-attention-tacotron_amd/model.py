@@ -33,8 +33,11 @@ class BNState:
         for scope, ch in self.names:
             self.offsets[scope] = (off, ch)
             off += ch
-        self.mean = torch.zeros(off, device=device)
-        self.var = torch.ones(off, device=device)
+        # one flat buffer [means | variances]: data-parallel replicas average it in ONE
+        # collective (dp.average_buffer)
+        self.buf = torch.cat([torch.zeros(off), torch.ones(off)]).to(device)
+        self.mean = self.buf[:off]
+        self.var = self.buf[off:]
 
     def span(self, first_scope: str, count_ch: int):
         o, _ = self.offsets[first_scope]
@@ -92,13 +95,17 @@ def sa_transformer_fwd(x, P, scope, heads, causal, probs_mask, sv, key):
 
 
 def encoder_fwd(P, bn: BNState, hp, d: PR.Dims, ids, lengths, masks, training, ws, sv,
-                persistent: bool = False):
-    """SelfAttentionCBHGEncoder.call (modules/module.py:425-438) -> (M1, M2)."""
+                persistent: bool = False, err: Optional[torch.Tensor] = None):
+    """SelfAttentionCBHGEncoder.call (modules/module.py:425-438) -> (M1, M2).  ``err``: the
+    int32 word the embedding's id-range check raises (zeroed here; default a fresh one)."""
     dev = ids.device
     B, N = ids.shape
     mk = (lambda n: masks[n]) if masks is not None else (lambda n: None)
     emb = torch.empty(B, N, d.embed, device=dev)
-    err = torch.zeros(1, dtype=torch.int32, device=dev)
+    if err is None:
+        err = torch.zeros(1, dtype=torch.int32, device=dev)
+    else:
+        err.zero_()
     K.embedding_fwd(P["embedding"], ids, emb, 0, err)
     sv["emb_err"] = err
     x = emb
@@ -241,17 +248,23 @@ class Saved(dict):
 def model_forward(P, bn: BNState, hp, d: PR.Dims, batch: Dict[str, torch.Tensor],
                   masks: Optional[Dict[str, torch.Tensor]], training: bool, ws: K.Workspace,
                   compute_grad_seeds: bool = True, attn_tile: int = 32, pipe=None,
-                  persistent: bool = False, scratch=None):
-    """model_fn forward + loss.  Returns (outputs dict, Saved)."""
+                  persistent: bool = False, scratch=None,
+                  health: Optional[torch.Tensor] = None):
+    """model_fn forward + loss.  Returns (outputs dict, Saved).  ``health``: the engine's int32
+    error arena -- words 8 and 9 take the embedding / speaker-embedding id-range flags."""
     sv = Saved()
     ids, lengths = batch["source"], batch["source_length"]
     m1, m2 = encoder_fwd(P, bn, hp, d, ids, lengths, masks, training, ws, sv,
-                         persistent=persistent)
+                         persistent=persistent, err=None if health is None else health[8:9])
     spk = None
     if d.multi_speaker:                                               # models/models.py:43-46,69
         ids_s = batch["speaker_id"]
         spk = torch.empty(ids_s.shape[0], d.spk_dim, device=m1.device)
-        sv["spk_err"] = torch.zeros(1, dtype=torch.int32, device=m1.device)
+        if health is None:
+            sv["spk_err"] = torch.zeros(1, dtype=torch.int32, device=m1.device)
+        else:
+            sv["spk_err"] = health[9:10]
+            sv["spk_err"].zero_()
         K.embedding_fwd(P["speaker_embedding"], ids_s, spk, d.spk_offset, sv["spk_err"])
     dout, dsv = decoder_forward(P, hp, d, m1, m2, lengths, batch["mel"], masks,
                                 attn_tile=attn_tile, spk=spk, persistent=persistent,

@@ -10,8 +10,10 @@ returns an ``EstimatorSpec``:
 * TRAIN  -- one full training step on libsat_hip (masks drawn on the device, forward, BPTT,
   [RCCL all-reduce], clip_by_global_norm(1.0) + TF Adam + Noam decay), loss = 0.1 L1 + BCE
   (models/models.py:151-189);
-* EVAL   -- the teacher-forced evaluation loss ``loss_with_teacher`` (dropout off, zoneout
-  blend, BatchNorm moving statistics; models/models.py:208-231) and its metric components;
+* EVAL   -- ``loss`` of the validation decode (OneHotValidationHelper: softmax feedback, exactly
+  T' steps with real attention; models/models.py:86-97) plus the teacher-forced
+  ``loss_with_teacher`` metrics (models/models.py:208-235, 305-320); eval semantics (dropout off,
+  zoneout blend, BatchNorm moving statistics);
 * PREDICT -- free-running inference (BASELINE configs[4]; inference.FreeRunningDecoder: the
   stop-token helper + the KV-cached incremental decoder self-attention), returning the
   reference's predictions dict (models/models.py:252-277).
@@ -29,6 +31,7 @@ from typing import Dict, Optional
 import numpy as np
 import torch
 
+from . import dp
 from . import params as PR
 from .engine import Tacotron
 from .train import Trainer
@@ -136,8 +139,13 @@ class DualSourceSelfAttentionTacotronModel:
         if warm_start_from is not None:
             raise NotImplementedError("warm start from TF checkpoints is outside the hot path")
         self.engine = Tacotron(params, device, seed=seed, init_values=init_values)
-        self._trainers: Dict[tuple, Trainer] = {}
-        self._seed = seed
+        # data-parallel replicas start from rank 0's weights and statistics
+        dp.broadcast_params(self.engine.params)
+        dp.broadcast_params(self.engine.bn.buf)
+        self._trainer: Optional[Trainer] = None
+        # dropout / zoneout masks differ per replica (each rank's shard is its own batch)
+        self._seed = seed + 1000003 * dp.rank()
+        self._eval_decoder = None
 
     @staticmethod
     def learning_rate_decay(init_rate, global_step, step_factor):
@@ -164,18 +172,15 @@ class DualSourceSelfAttentionTacotronModel:
             b["speaker_id"] = _to_device(features.speaker_id, dev, torch.int64)
         return b
 
-    def _trainer(self, batch) -> Trainer:
+    def _get_trainer(self, batch) -> Trainer:
+        """ONE trainer (one optimiser state) for every batch shape: its mask views are re-pointed
+        per shape inside one arena (Trainer.reshape), so memory stays flat over a stream of
+        differently padded batches."""
         B, N = batch["source"].shape
         Tp = batch["mel"].shape[1] // self.params.outputs_per_step
-        key = (B, N, Tp)
-        if key not in self._trainers:
-            shared = next(iter(self._trainers.values()), None)
-            tr = Trainer(self.engine, B, N, Tp, seed=self._seed)
-            if shared is not None:          # one optimiser state per model
-                tr.exp_avg, tr.exp_avg_sq = shared.exp_avg, shared.exp_avg_sq
-                tr.global_step, tr.seed = shared.global_step, shared.seed
-            self._trainers[key] = tr
-        return self._trainers[key]
+        if self._trainer is None:
+            self._trainer = Trainer(self.engine, B, N, Tp, seed=self._seed)
+        return self._trainer
 
     def _predict(self, features) -> EstimatorSpec:
         """PREDICT (models/models.py:84-97, 252-277): free-running decode (inference.py) and
@@ -239,36 +244,62 @@ class DualSourceSelfAttentionTacotronModel:
         out["teacher_alignment2"] = a2.transpose(1, 2)
         return out
 
-    def _forced_eval(self, batch) -> EstimatorSpec:
+    def _loss_of(self, mel, stop, batch):
+        """0.1 * codes_loss + binary_loss (models/models.py:159-173) of a decode's outputs."""
         from . import kernels as K
-        out = self.forced_alignment_pass(batch)
-        mel, stop = out["mel"], out["stop"]
         loss = torch.zeros(8, device=mel.device)
-        K.loss_fwd_bwd(mel, batch["mel"], batch["mel_mask"], stop.contiguous(), batch["done"],
-                       batch["done_mask"], loss)
-        metrics = {"loss": loss[0:1], "code_loss": 0.1 * loss[1:2], "done_loss": loss[2:3],
+        K.loss_fwd_bwd(mel.contiguous(), batch["mel"], batch["mel_mask"], stop.contiguous(),
+                       batch["done"], batch["done_mask"], loss)
+        return loss
+
+    def validation_pass(self, batch) -> Dict[str, object]:
+        """EVAL's own decode (models/models.py:86-97 with is_validation=True,
+        teacher_forcing=False): OneHotValidationHelper (modules/helpers.py:61-108) -- exactly
+        T' = T/r steps with real attention, step t+1 fed the per-frame softmax of step t's
+        output."""
+        from .inference import FreeRunningDecoder
+        if self._eval_decoder is None:
+            self._eval_decoder = FreeRunningDecoder(self.engine, helper="validation",
+                                                    feed="softmax")
+        return self._eval_decoder.run(batch)
+
+    def _eval(self, batch) -> EstimatorSpec:
+        """EVAL (models/models.py:84-97, 151-173, 208-235, 305-320):
+        * ``loss`` / ``code_loss`` / ``done_loss`` of the validation decode (softmax feedback,
+          T' steps; under ``use_forced_alignment_mode`` the forced second pass instead);
+        * ``loss_with_teacher`` / ``code_loss_with_teacher`` / ``done_loss_with_teacher`` of the
+          teacher-forced pass (validation with teacher forcing, equal to the training branch
+          in eval mode by modules/transformer_test.py:44-90)."""
+        hp = self.params
+        with torch.no_grad():
+            if getattr(hp, "use_forced_alignment_mode", False):
+                out = self.forced_alignment_pass(batch)
+            else:
+                out = self.validation_pass(batch)
+            l = self._loss_of(out["mel"], out["stop"], batch)
+            teach, _ = self.engine.forward(batch, None, training=False, need_grad=False)
+        code_loss, done_loss = 0.1 * l[1:2], l[2:3]
+        loss = code_loss + done_loss                                  # + regularization (0)
+        metrics = {"code_loss": code_loss, "done_loss": done_loss,
+                   "loss_with_teacher": teach["loss"],
+                   "code_loss_with_teacher": 0.1 * teach["l1"],
+                   "done_loss_with_teacher": teach["bce"],
                    "alignment1": out["alignment1"], "alignment2": out["alignment2"]}
-        return EstimatorSpec(ModeKeys.EVAL, loss=loss[0:1], train_op=None,
-                             predictions={"mel": mel, "stop_token": stop}, eval_metric_ops=metrics)
+        return EstimatorSpec(ModeKeys.EVAL, loss=loss, train_op=None,
+                             predictions={"mel": out["mel"], "stop_token": out["stop"]},
+                             eval_metric_ops=metrics)
 
     def model_fn(self, features, labels, mode, params=None) -> EstimatorSpec:
         if mode == ModeKeys.PREDICT:
             return self._predict(features)
         batch = self._batch(features, labels)
-        if mode == ModeKeys.EVAL and getattr(self.params, "use_forced_alignment_mode", False):
-            return self._forced_eval(batch)
         if mode == ModeKeys.TRAIN:
-            tr = self._trainer(batch)
+            tr = self._get_trainer(batch)
             out = tr.step(batch)
             return EstimatorSpec(mode, loss=out["loss"], train_op=tr.global_step,
                                  predictions=None, eval_metric_ops=None)
         if mode == ModeKeys.EVAL:
-            with torch.no_grad():
-                out, _ = self.engine.forward(batch, None, training=False, need_grad=False)
-            metrics = {"loss_with_teacher": out["loss"], "code_loss_with_teacher": 0.1 * out["l1"],
-                       "done_loss_with_teacher": out["bce"]}
-            return EstimatorSpec(mode, loss=out["loss"], train_op=None, predictions=None,
-                                 eval_metric_ops=metrics)
+            return self._eval(batch)
         raise ValueError(f"Unknown mode: {mode}")
 
     # ---- tf.estimator.Estimator-like drivers

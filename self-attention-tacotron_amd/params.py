@@ -83,6 +83,13 @@ def resolve_dims(hp) -> Dims:
                                   "shipped self-attention configs")
     if hp.use_external_speaker_embedding or hp.use_accent_type:
         raise NotImplementedError("external speaker / accent embeddings are out of scope")
+    if getattr(hp, "code_loss_type", "l1") != "l1":
+        # hparams.py:153 allows 'l1' or 'mse'; the shipped configs use l1 and the loss kernel
+        # (sat_loss_fwd_bwd) computes only that -- refuse rather than silently compute L1
+        raise NotImplementedError(f"code_loss_type={hp.code_loss_type!r}: only 'l1' is built")
+    if getattr(hp, "use_l2_regularization", False):
+        # models/models.py:164-171 (ext l2_regularization_loss with a name blacklist)
+        raise NotImplementedError("use_l2_regularization=True is not built (off in the configs)")
     half = hp.cbhg_out_units // 2
     assert hp.cbhg_out_units % 2 == 0
     if hp.projection2_out_channels != hp.encoder_prenet_out_units[-1]:

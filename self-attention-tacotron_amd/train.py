@@ -20,6 +20,7 @@ from __future__ import annotations
 
 from typing import Dict, Optional
 
+import numpy as np
 import torch
 
 from . import _lib
@@ -40,6 +41,12 @@ class Trainer:
         self.global_step = torch.zeros(1, dtype=torch.int64, device=dev)
         self.seed = torch.tensor([seed], dtype=torch.int64, device=dev)
         self.scalars = torch.zeros(4, dtype=torch.float32, device=dev)
+        # guarded update: {skipped steps, first error code} on the device; a pinned host mirror
+        # refreshed after every step is inspected at the start of the next (no sync)
+        self.status = torch.zeros(2, dtype=torch.int32, device=dev)
+        self._mirror = torch.zeros(2 + model.health.numel(), dtype=torch.int32,
+                                   pin_memory=torch.cuda.is_available())
+        self._mirror_evt = None
         self.adam_ws = torch.empty(int(_lib.load().sat_workspace_adam()), dtype=torch.uint8,
                                    device=dev)
         self.cfg = _lib.SatAdamConfig()
@@ -48,13 +55,32 @@ class Trainer:
         self.cfg.clip_norm = 1.0
         self.cfg.decay = 1 if hp.decay_learning_rate else 0
         self.cfg.step_factor = hp.learning_rate_step_factor
-        self.specs = mask_specs(hp, B, N, Tp)
-        self.masks: Dict[str, torch.Tensor] = {
-            s.name: torch.empty(s.shape, device=dev) for s in self.specs}
+        # every mask is a view of ONE arena, re-viewed when the batch shape changes (grown only
+        # when a larger shape arrives), so a stream of differently padded batches keeps device
+        # memory flat
+        self._mask_arena = torch.empty(0, device=dev)
+        self.shape = None
+        self.reshape(B, N, Tp)
         self.pg = process_group
         self.world = dp.world_size(process_group)
         self.cfg.grad_scale = dp.grad_scale(process_group)
         self.last_loss = None
+
+    def reshape(self, B: int, N: int, Tp: int) -> None:
+        """Point the mask views at a (B, N, T') batch shape."""
+        if self.shape == (B, N, Tp):
+            return
+        self.specs = mask_specs(self.hp, B, N, Tp)
+        need = sum(int(np.prod(s.shape)) for s in self.specs)
+        if need > self._mask_arena.numel():
+            self._mask_arena = torch.empty(need, device=self.m.device)
+        self.masks: Dict[str, torch.Tensor] = {}
+        off = 0
+        for s in self.specs:
+            n = int(np.prod(s.shape))
+            self.masks[s.name] = self._mask_arena[off:off + n].view(s.shape)
+            off += n
+        self.shape = (B, N, Tp)
 
     def draw_masks(self):
         """One Philox launch per mask tensor; stream ids are fixed per mask, the seed advances
@@ -73,21 +99,55 @@ class Trainer:
         return out
 
     def reduce_grads(self):
+        """The step's one gradient exchange (SUM; 1/world folded into Adam) plus the mean of
+        the BatchNorm moving statistics (a few KB) so replicas never drift apart."""
         dp.allreduce_grads(self.m.grads, self.pg)
+        bn = getattr(self.m, "bn", None)
+        if bn is not None and self.world > 1:
+            dp.average_buffer(bn.buf, self.pg)
 
     def apply(self):
+        """Guarded clip + Adam: skipped on the device when any health word of the step is set."""
         m = self.m
         _lib.check(_lib.load().sat_adam_step(
             m.params.data_ptr(), m.grads.data_ptr(), self.exp_avg.data_ptr(),
             self.exp_avg_sq.data_ptr(), m.params.numel(), self.global_step.data_ptr(),
             self.scalars.data_ptr(), self.adam_ws.data_ptr(), _lib.ctypes.byref(self.cfg),
+            m.health.data_ptr(), m.health.numel(), self.status.data_ptr(),
             K._stream()), "sat_adam_step")
         _lib.call("sat_counter_add", self.seed.data_ptr(), 1, K._stream())
 
+    # ---- health: the previous step's verdict, read from pinned memory without a sync
+    def publish_health(self):
+        """Queue the copy of {status, health words} to the pinned mirror (outside graphs)."""
+        self._mirror[:2].copy_(self.status, non_blocking=True)
+        self._mirror[2:].copy_(self.m.health, non_blocking=True)
+        self._mirror_evt = torch.cuda.Event()
+        self._mirror_evt.record()
+
+    def check_health(self, wait: bool = False):
+        """Raise SatLibraryError if a finished step was skipped by the guard (``wait`` blocks
+        until the last published step is done)."""
+        if self._mirror_evt is None:
+            return
+        if wait:
+            self._mirror_evt.synchronize()
+        elif not self._mirror_evt.query():
+            return
+        if int(self._mirror[0]) != 0:
+            self.m.raise_on_health(self._mirror[2:].tolist())
+            raise _lib.SatLibraryError(
+                f"{int(self._mirror[0])} training step(s) skipped by the health guard "
+                f"(first error code {int(self._mirror[1])})")
+
     def step(self, batch):
+        self.check_health()
+        B, N = batch["source"].shape
+        self.reshape(B, N, batch["mel"].shape[1] // self.hp.outputs_per_step)
         out = self.forward_backward(batch)
         self.reduce_grads()
         self.apply()
+        self.publish_health()
         return out
 
 
@@ -95,7 +155,10 @@ class GraphedStep:
     """Capture Trainer.step (or its forward/backward half when an eager collective sits in
     between) into hipGraphs and replay them: kills the ~5k host launches per step."""
 
-    def __init__(self, trainer: Trainer, batch, warmup: int = 1):
+    def __init__(self, trainer: Trainer, batch, warmup: int = 1, split: Optional[bool] = None):
+        """``split`` (default: world > 1) captures forward/backward and clip + Adam as two
+        graphs with ``trainer.reduce_grads`` (the eager RCCL all-reduce) replayed between
+        them."""
         self.t = trainer
         self.batch = batch
         s = torch.cuda.Stream()
@@ -105,7 +168,7 @@ class GraphedStep:
                 trainer.step(batch)
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
-        self.split = trainer.world > 1
+        self.split = trainer.world > 1 if split is None else bool(split)
         self.g_fb = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.g_fb):
             self.out = trainer.forward_backward(batch)
@@ -118,8 +181,10 @@ class GraphedStep:
         torch.cuda.synchronize()
 
     def replay(self):
+        self.t.check_health()
         self.g_fb.replay()
         if self.split:
             self.t.reduce_grads()
             self.g_apply.replay()
+        self.t.publish_health()
         return self.out

@@ -38,6 +38,7 @@ def test_tfrecord_batches_drive_model_fn(cuda, tmp_path):
     ref = O.model_forward(O.to_torch(vals), O.to_torch(params.init_bn_buffers(hp)), hp,
                           O.to_torch(tb), None, training=False)
     ref_loss = float(ref["loss"])
-    assert abs(float(spec.loss.item()) - ref_loss) < 1e-5 * max(1.0, abs(ref_loss))
+    got = float(spec.eval_metric_ops["loss_with_teacher"].item())
+    assert abs(got - ref_loss) < 1e-5 * max(1.0, abs(ref_loss))
     out = model.model_fn(*batches[1], MD.ModeKeys.TRAIN, hp)
     assert np.isfinite(float(out.loss.item()))

@@ -35,15 +35,35 @@ def _worker(rank, world, port, q):
         res["bcast"] = bool(torch.all(p == 1.0))
         # one SUM all-reduce of the flat gradient arena + 1/world folded into Adam's config
         hp = hparams.ljspeech_hparams()
-        model = types.SimpleNamespace(hp=hp, device=torch.device("cpu"),
-                                      params=torch.zeros(4096),
-                                      grads=torch.arange(4096, dtype=torch.float32) * (rank + 1))
+        model = types.SimpleNamespace(
+            hp=hp, device=torch.device("cpu"), params=torch.zeros(4096),
+            grads=torch.arange(4096, dtype=torch.float32) * (rank + 1),
+            health=torch.zeros(16, dtype=torch.int32),
+            bn=types.SimpleNamespace(buf=torch.full((64,), float(rank))))
         tr = train.Trainer(model, B=2, N=8, Tp=4)
         tr.reduce_grads()
         expect = torch.arange(4096, dtype=torch.float32) * sum(r + 1 for r in range(world))
         res["sum"] = bool(torch.equal(model.grads, expect))
         res["scale"] = tr.cfg.grad_scale
         res["world"] = tr.world
+        # BatchNorm moving statistics: averaged over the replicas in the same exchange
+        res["bn"] = bool(torch.allclose(model.bn.buf, torch.full((64,), (world - 1) / 2)))
+        # the optimiser applied on every rank to the reduced arena (a host restatement of the
+        # fused clip + Adam step with grad_scale = 1/world) leaves bit-identical replicas
+        from oracle import sat_oracle as O
+        p = torch.linspace(-1, 1, 4096, dtype=torch.float64)
+        mo = torch.zeros_like(p)
+        vo = torch.zeros_like(p)
+        for step in range(1, 3):
+            g = model.grads.double() * tr.cfg.grad_scale
+            (g,), _ = O.clip_by_global_norm([g], 1.0)
+            p, mo, vo = O.adam_tf(p, g, mo, vo,
+                                  O.learning_rate(hp.initial_learning_rate, step - 1), step)
+        gathered = [torch.empty_like(p) for _ in range(world)]
+        tdist.all_gather(gathered, p)
+        res["replicas_equal"] = all(torch.equal(gathered[0], x) for x in gathered[1:])
+        # masks are drawn per replica: the model_fn seed offset differs by rank
+        res["seed_offset"] = 1000003 * dp.rank()
         # max-over-ranks step time
         res["max"] = dp.max_over_ranks(0.5 + rank, "cpu")
         tdist.barrier()
@@ -66,7 +86,8 @@ def test_dp_world2_gloo():
     for r in range(2):
         res = out[r]
         assert isinstance(res, dict), res
-        assert res["bcast"] and res["sum"]
+        assert res["bcast"] and res["sum"] and res["bn"] and res["replicas_equal"]
+        assert res["seed_offset"] == 1000003 * r
         assert res["scale"] == pytest.approx(0.5) and res["world"] == 2
         assert res["max"] == pytest.approx(1.5)
 

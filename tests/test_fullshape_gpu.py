@@ -1,0 +1,112 @@
+"""The hot path at the configured length against the float64 oracle.
+
+north_star bar: mel frames within 1e-4 mean-L1 of the reference over LJSpeech-shape batches of
+<= 1000 frames, i.e. 500 recurrent decoder steps -- the length where fp32 drift through the
+recurrence and the persistent kernels' <= 1-ulp hand-off tags would
+show.  Every case runs the persistent kernels that the bench times (any B <= 32 is eligible).
+
+* C1 (LJSpeech, B=2, N=200, T=1000): eval mode (dropout off, zoneout blend -- the
+  teacher-forced ``loss_with_teacher`` computation, models/models.py:208-231) and train mode
+  with injected dropout / zoneout masks;
+* gradients at B=8, N=200 (7 attention tiles and their halos), T=1000, ragged lengths;
+* C2 (B=32: 4 utterances per hand-off group) forward in eval mode.
+
+Tolerances (written per assertion): mel mean-L1 <= 1e-4 (north_star); loss within 1e-5
+relative; stop logits mean-abs <= 1e-4; every parameter gradient within 1e-3 of
+max(|g_ref|, 1e-4 max|g|) (fp32 BPTT over 500 steps against float64 autograd).
+Set SAT_PARITY_REPORT=<file> to append the achieved numbers as JSON lines."""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _report(name, **vals):
+    path = os.environ.get("SAT_PARITY_REPORT")
+    if path:
+        with open(path, "a") as f:
+            f.write(json.dumps({"case": name, **vals}) + "\n")
+
+
+def _run(cuda, B, N, T, train, shape="max", seed=11, grads=False):
+    from sat_amd import data, engine, hparams, params
+    from sat_amd.decoder import persistent_eligible
+    from oracle import sat_oracle as O
+    hp = hparams.ljspeech_hparams()
+    vals = params.init_params(hp, seed=5)
+    b = data.synthetic_batch(hp, B, N=N, T=T, shape=shape, seed=seed)
+    Np, Tp = b["source"].shape[1], b["mel"].shape[1] // hp.outputs_per_step
+    mk = data.synthetic_masks(hp, B, Np, Tp, seed=seed + 1) if train else None
+    m = engine.Tacotron(hp, cuda, init_values=vals)
+    assert persistent_eligible(m.d, B, Np)
+    gb = {k: torch.tensor(v).to(cuda) for k, v in b.items()}
+    gm = None if mk is None else {k: torch.tensor(v).to(cuda) for k, v in mk.items()}
+    out, sv = m.forward(gb, gm, training=train, need_grad=grads)
+    assert "attn_scratch" in sv["dec"].tensors          # the persistent kernels ran
+    if grads:
+        m.backward(sv)
+    torch.cuda.synchronize()
+    sv["dec"].tensors["attn_scratch"].check()
+    p64 = {k: v.requires_grad_(grads) for k, v in O.to_torch(vals).items()}
+    with torch.set_grad_enabled(grads):
+        ref = O.model_forward(p64, O.to_torch(params.init_bn_buffers(hp)), hp, O.to_torch(b),
+                              None if mk is None else O.to_torch(mk), training=train)
+        if grads:
+            ref["loss"].backward()
+    return hp, m, out, ref, p64, b
+
+
+def _compare_outputs(name, out, ref, b):
+    mel = out["mel"].double().cpu().numpy()
+    rmel = ref["mel"].detach().numpy()
+    w = b["mel_mask"][..., None].astype(bool) & np.ones_like(rmel, bool)
+    l1 = float(np.abs(mel - rmel)[w].mean())
+    l1_all = float(np.abs(mel - rmel).mean())
+    mx = float(np.abs(mel - rmel).max())
+    stop = out["stop"].double().cpu().numpy().reshape(ref["stop"].shape)
+    st = float(np.abs(stop - ref["stop"].detach().numpy()).mean())
+    loss, rloss = float(out["loss"].item()), float(ref["loss"].detach())
+    _report(name, mel_mean_l1=l1, mel_mean_l1_padded=l1_all, mel_max_abs=mx, stop_mean_abs=st,
+            loss=loss, loss_ref=rloss)
+    assert l1 <= 1e-4, f"{name}: mel mean-L1 {l1:.3e} > 1e-4"
+    assert l1_all <= 1e-4
+    assert st <= 1e-4, f"{name}: stop mean-abs {st:.3e}"
+    assert abs(loss - rloss) <= 1e-5 * max(1.0, abs(rloss)), (loss, rloss)
+
+
+@pytest.mark.parametrize("train", [False, True], ids=["eval", "train_masks"])
+def test_c1_full_length_matches_oracle(cuda, train):
+    """C1: B=2, N=200, T=1000 -> 500 decoder steps (modules/forward_attention.py:88-122,
+    modules/module.py:743-765), persistent kernels vs the float64 oracle."""
+    hp, m, out, ref, _, b = _run(cuda, 2, 200, 1000, train)
+    _compare_outputs(f"c1_{'train' if train else 'eval'}", out, ref, b)
+
+
+def test_c2_full_shape_forward_matches_oracle(cuda):
+    """C2: B=32 (four utterances per hand-off group, 7 tiles each), N=200, T=1000, eval."""
+    hp, m, out, ref, _, b = _run(cuda, 32, 200, 1000, False, seed=21)
+    _compare_outputs("c2_eval", out, ref, b)
+
+
+def test_gradients_full_length_match_oracle(cuda):
+    """BPTT over 500 steps at B=8, N<=200 (ragged; up to 7 tiles with halos), T<=1000, train
+    mode with injected masks: loss and every parameter gradient vs float64 autograd."""
+    hp, m, out, ref, p64, b = _run(cuda, 8, 200, 1000, True, shape="ljs", seed=31, grads=True)
+    assert b["source"].shape[1] > 160 and b["mel"].shape[1] >= 800   # long, ragged batch
+    _compare_outputs("grad_b8_outputs", out, ref, b)
+    grads = m.grads_dict()
+    gmax = max(float(p.grad.abs().max()) for p in p64.values())
+    worst, bad = 0.0, []
+    for name, p in p64.items():
+        g_ref = p.grad.numpy()
+        scale = max(np.abs(g_ref).max(), 1e-4 * gmax)
+        err = float(np.abs(grads[name].astype(np.float64) - g_ref).max() / scale)
+        worst = max(worst, err)
+        if not err <= 1e-3:
+            bad.append((name, err))
+    _report("grad_b8", worst_rel_grad_err=worst, steps=int(b["mel"].shape[1] // 2))
+    assert not bad, bad

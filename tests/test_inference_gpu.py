@@ -5,6 +5,9 @@ modules/rnn_wrappers.py:87-124, 188-214, helpers analog modules/helpers.py:111-1
 
 Tolerances: the decode feeds its own predictions back for up to max_iters steps, so fp32 vs
 float64 drift compounds through the recurrence; mel frames within 2e-4 absolute over 40 steps."""
+import json
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -127,3 +130,113 @@ def test_model_fn_eval_forced_alignment_mode(cuda):
                  tb["done_mask"])
     ref_loss = float(l["loss"]) if isinstance(l, dict) else float(l[0])
     assert abs(float(spec.loss.item()) - ref_loss) < 1e-5 * max(1.0, abs(ref_loss))
+
+
+def _vbatch(cuda, preset="ljspeech", B=3, N=15, T=40, seed=6):
+    from sat_amd import data, engine, hparams, params
+    from oracle import sat_oracle as O
+    hp = getattr(hparams, f"{preset}_hparams")()
+    vals = params.init_params(hp, seed=5)
+    m = engine.Tacotron(hp, cuda, init_values=vals)
+    b = data.synthetic_batch(hp, B, N=N, T=T, shape="ljs", seed=seed)
+    gb = {k: torch.tensor(v).to(cuda) for k, v in b.items()}
+    return hp, vals, m, b, gb, O
+
+
+@pytest.mark.parametrize("feed", ["softmax", "target"])
+@pytest.mark.parametrize("preset", ["ljspeech", "vctk"])
+def test_validation_decode_matches_oracle(cuda, preset, feed):
+    """OneHotValidationHelper (modules/helpers.py:61-108): exactly T' steps with the real
+    attention; feed = softmax of the previous output (teacher_forcing=False, EVAL's loss) or the
+    target frame (teacher_forcing=True).  HIP vs the oracle's restatement."""
+    from sat_amd import params
+    from sat_amd.inference import FreeRunningDecoder
+    hp, vals, m, b, gb, O = _vbatch(cuda, preset)
+    out = FreeRunningDecoder(m, helper="validation", feed=feed).run(gb)
+    ref = O.infer_free_running(O.to_torch(vals), O.to_torch(params.init_bn_buffers(hp)), hp,
+                               O.to_torch(b), helper="validation", feed=feed)
+    Tp = b["mel"].shape[1] // hp.outputs_per_step
+    assert out["steps"] == ref["steps"] == Tp
+    np.testing.assert_allclose(out["mel"].cpu().numpy(), ref["mel"].numpy(), atol=2e-5)
+    np.testing.assert_allclose(out["stop"].cpu().numpy(), ref["stop"].numpy(), atol=2e-5)
+    np.testing.assert_allclose(out["alignment1"].cpu().numpy(),
+                               ref["alignment1"].permute(0, 2, 1).numpy(), atol=2e-6)
+
+
+def test_model_fn_eval_losses_match_oracle(cuda):
+    """model_fn EVAL (models/models.py:84-97, 151-173, 208-235, 305-320): ``loss`` /
+    ``code_loss`` / ``done_loss`` from the softmax-fed validation decode, the ``*_with_teacher``
+    metrics from the teacher-forced pass -- both vs the oracle."""
+    from sat_amd import hparams, models as MD, params
+    from sat_amd.models import PreprocessedSourceData, PreprocessedTargetData
+    hp, vals, m, b, gb, O = _vbatch(cuda, B=2, N=12, T=24, seed=8)
+    model = MD.DualSourceSelfAttentionTacotronModel(hp, device=cuda, init_values=vals)
+    ids = np.arange(2)
+    feats = PreprocessedSourceData(ids, ids, b["source"], b["source_length"], None)
+    labels = PreprocessedTargetData(ids, ids, b["mel"], b["target_length"], b["done"],
+                                    b["mel_mask"], b["done_mask"])
+    spec = model.model_fn(feats, labels, MD.ModeKeys.EVAL, hp)
+    p64, bufs, tb = O.to_torch(vals), O.to_torch(params.init_bn_buffers(hp)), O.to_torch(b)
+    val = O.infer_free_running(p64, bufs, hp, tb, helper="validation", feed="softmax")
+    loss, l1, bce = O.losses(val["mel"], val["stop"].unsqueeze(-1), tb["mel"], tb["mel_mask"],
+                             tb["done"], tb["done_mask"])
+    teach = O.model_forward(p64, bufs, hp, tb, None, training=False)
+    mt = spec.eval_metric_ops
+    close = lambda a, r: abs(float(a.item()) - float(r)) <= 1e-5 * max(1.0, abs(float(r)))  # noqa
+    assert close(spec.loss, loss)
+    assert close(mt["code_loss"], 0.1 * l1) and close(mt["done_loss"], bce)
+    assert close(mt["loss_with_teacher"], teach["loss"])
+    assert close(mt["code_loss_with_teacher"], 0.1 * teach["l1"])
+    assert close(mt["done_loss_with_teacher"], teach["bce"])
+    assert abs(float(spec.loss.item()) - float(mt["loss_with_teacher"].item())) > 1e-6
+
+
+@pytest.mark.parametrize("B,N,T", [(3, 15, 40), (32, 200, 1000)], ids=["small", "c2_full"])
+def test_teacher_forced_incremental_equals_training(cuda, B, N, T):
+    """modules/transformer_test.py:44-90 on the HIP path: the training branch (teacher-forced
+    dynamic_decode + causal self-attention over the whole output, here the persistent kernels
+    and the batched head) equals the incremental branch driven by
+    OneHotValidationHelper(teacher_forcing=True) (per-step kernels + TransformerWrapper's
+    re-run, here the KV-cached head): outputs, stop tokens and argmax samples.  The two paths
+    share no kernel of the decoder loop, so agreement is to fp32 rounding: mel max-abs <= 5e-5
+    and mean-abs <= 2e-6 (the reference asserts rtol = atol = 1e-6 on TF's single path)."""
+    from sat_amd.inference import FreeRunningDecoder
+    hp, vals, m, b, gb, O = _vbatch(cuda, B=B, N=N, T=T, seed=9)
+    with torch.no_grad():
+        tr, _ = m.forward(gb, None, training=False, need_grad=False)
+    inc = FreeRunningDecoder(m, helper="validation", feed="target").run(gb)
+    d_mel = (tr["mel"] - inc["mel"]).abs()
+    d_stop = (tr["stop"].view_as(inc["stop"]) - inc["stop"]).abs()
+    r = hp.outputs_per_step
+    s_tr = tr["mel"].view(B, -1, r, hp.num_mels).argmax(-1)
+    s_in = inc["mel"].view(B, -1, r, hp.num_mels).argmax(-1)
+    agree = float((s_tr == s_in).float().mean())
+    path = os.environ.get("SAT_PARITY_REPORT")
+    if path:
+        with open(path, "a") as f:
+            f.write(json.dumps({"case": f"a17_{B}x{N}x{T}", "mel_max_abs": float(d_mel.max()),
+                                "mel_mean_abs": float(d_mel.mean()),
+                                "stop_max_abs": float(d_stop.max()),
+                                "sample_agreement": agree}) + "\n")
+    assert float(d_mel.max()) <= 5e-5 and float(d_mel.mean()) <= 2e-6
+    assert float(d_stop.max()) <= 5e-5
+    assert agree >= 0.999                     # argmax ties may flip under rounding
+
+
+def test_graph_decode_equals_eager(cuda):
+    """Chunked hipGraph capture of the decode (graphs=True) replays the eager launches:
+    bitwise-equal outputs, early stop included, and a second replay of the same plan."""
+    from sat_amd.inference import FreeRunningDecoder
+    hp, vals, m, b, gb, O = _vbatch(cuda, B=3, N=15, T=20, seed=2)
+    eager = FreeRunningDecoder(m, max_iters=40, check_every=7).run(gb)
+    dec = FreeRunningDecoder(m, max_iters=40, check_every=7, graphs=True)
+    g1 = dec.run(gb)
+    g2 = dec.run(gb)
+    for g in (g1, g2):
+        assert g["steps"] == eager["steps"]
+        assert torch.equal(g["mel"], eager["mel"]) and torch.equal(g["stop"], eager["stop"])
+        assert torch.equal(g["alignment1"], eager["alignment1"])
+    val_e = FreeRunningDecoder(m, helper="validation", feed="softmax").run(gb)
+    val_g = FreeRunningDecoder(m, helper="validation", feed="softmax", graphs=True,
+                               check_every=5).run(gb)
+    assert torch.equal(val_e["mel"], val_g["mel"])

@@ -75,3 +75,31 @@ def test_learning_rate_decay_matches_reference_formula():
     assert f(5e-4, 0, 1) == pytest.approx(5e-4 * 4000 ** 0.5 * 4000 ** -1.5)
     assert f(5e-4, 3999, 1) == pytest.approx(5e-4 * 4000 ** 0.5 * 4000 ** -0.5)
     assert f(5e-4, 15999, 1) == pytest.approx(5e-4 * 4000 ** 0.5 * 16000 ** -0.5)
+
+
+def test_unbuilt_options_raise():
+    """Options the reference accepts but this build does not compute raise instead of being
+    silently ignored."""
+    import types
+    import pytest
+    from sat_amd import hparams, params
+    from sat_amd.inference import FreeRunningDecoder
+    hp = hparams.ljspeech_hparams()
+    hp.set_hparam("code_loss_type", "mse")
+    with pytest.raises(NotImplementedError, match="code_loss_type"):
+        params.resolve_dims(hp)
+    hp = hparams.ljspeech_hparams()
+    hp.set_hparam("use_l2_regularization", True)
+    with pytest.raises(NotImplementedError, match="l2"):
+        params.resolve_dims(hp)
+    hp = hparams.ljspeech_hparams()
+    hp.set_hparam("apply_dropout_on_inference", True)
+    fake = types.SimpleNamespace(hp=hp, d=params.resolve_dims(hp))
+    with pytest.raises(NotImplementedError, match="apply_dropout_on_inference"):
+        FreeRunningDecoder(fake)
+    hp = hparams.ljspeech_hparams()
+    fake = types.SimpleNamespace(hp=hp, d=params.resolve_dims(hp))
+    with pytest.raises(ValueError, match="validation helper"):
+        FreeRunningDecoder(fake, feed="target")
+    dec = FreeRunningDecoder(fake, helper="validation", feed="target")
+    assert dec.helper == "validation" and dec.feed == "target"

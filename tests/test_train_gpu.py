@@ -54,3 +54,73 @@ def test_graph_replay_equals_eager_and_trains(cuda):
     torch.cuda.synchronize()
     assert torch.equal(m.params, m2.params), "graph replay diverged from eager execution"
     assert losses[-1] < losses[0]
+
+
+def test_split_replay_equals_unsplit(cuda):
+    """GraphedStep's data-parallel form (forward/backward graph, eager reduce_grads, clip+Adam
+    graph; train.py) replays bitwise like the single-graph form.  The collective is the one
+    seam: with world 1 it is the identity, so the two must agree exactly."""
+    from sat_amd import engine, train
+    hp, m, batch, tr = _setup(cuda, seed=4)
+    m2 = engine.Tacotron(hp, cuda, seed=42)
+    tr2 = train.Trainer(m2, 2, batch["source"].shape[1], batch["mel"].shape[1] // 2, seed=7)
+    calls = []
+    tr2.reduce_grads = lambda: calls.append(1)          # injected reducer (the RCCL seam)
+    g1 = train.GraphedStep(tr, batch, warmup=1, split=False)
+    g2 = train.GraphedStep(tr2, batch, warmup=1, split=True)
+    assert g2.split and not g1.split
+    for _ in range(3):
+        g1.replay()
+        g2.replay()
+    torch.cuda.synchronize()
+    assert len(calls) == 1 + 3                          # warm-up step + every replay
+    assert torch.equal(m.params, m2.params)
+    assert torch.equal(tr.exp_avg_sq, tr2.exp_avg_sq)
+
+
+def test_health_guard_skips_update_and_raises(cuda):
+    """a set error word of the step (here: the attention chain's hand-off timeout
+    word, forced) makes the guarded Adam step skip the update on the device -- params, moments
+    and global step untouched -- and the trainer raises at its next step without a sync."""
+    from sat_amd import _lib
+    hp, m, batch, tr = _setup(cuda, seed=5)
+    tr.step(batch)
+    torch.cuda.synchronize()
+    tr.check_health(wait=True)                          # healthy step: no raise
+    p0, gs0 = m.params.clone(), int(tr.global_step.item())
+    tr.forward_backward(batch)
+    m.health[0] = 1                                     # as a timed-out poll would leave it
+    tr.apply()
+    tr.publish_health()
+    torch.cuda.synchronize()
+    assert torch.equal(m.params, p0) and int(tr.global_step.item()) == gs0
+    assert int(tr.status[0].item()) == 1 and int(tr.status[1].item()) == 1
+    with pytest.raises(_lib.SatLibraryError, match="hand-off timeout"):
+        tr.check_health(wait=True)
+
+
+def test_model_fn_memory_flat_over_shapes(cuda):
+    """model_fn TRAIN over many distinct padded shapes keeps one trainer (mask views
+    re-pointed inside one arena) and one persistent scratch per batch size sized for the largest
+    N -- device memory stays flat after the largest shape has been seen."""
+    import gc
+    from sat_amd import hparams, models as MD
+    hp = hparams.ljspeech_hparams()
+    model = MD.DualSourceSelfAttentionTacotronModel(hp, device=cuda, seed=1)
+    it = iter(MD.synthetic_input_fn(hp, 4, N=60, T=120, shape="ljs", seed=3)())
+    feats, labels = next(it)
+    big = MD.synthetic_input_fn(hp, 4, N=60, T=120, shape="max", seed=0)
+    model.model_fn(*next(iter(big())), MD.ModeKeys.TRAIN, hp)      # the largest shape first
+    torch.cuda.synchronize()
+    gc.collect()
+    base = torch.cuda.memory_allocated()
+    shapes = set()
+    for _ in range(12):
+        f, l = next(it)
+        shapes.add((f.source.shape[1], l.codes.shape[1]))
+        model.model_fn(f, l, MD.ModeKeys.TRAIN, hp)
+    torch.cuda.synchronize()
+    gc.collect()
+    assert len(shapes) >= 6
+    assert torch.cuda.memory_allocated() <= base + (1 << 20)
+    assert len(model.engine._scratch) == 1

@@ -12,8 +12,10 @@ value  : whole-job frames/s = n_gpus * B * T * steps / max-over-ranks wall time 
 Run:  python bench.py [--gpus N --steps K --warmup W]
       torchrun --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
 Extra objects on the JSON line: ``roofline`` (the persistent decoder attention kernel, the
-step's dominant kernel, timed live with HIP events on the stream it runs on) and
-``cpu_baseline`` (the CPU oracle, bounded sample).
+step's dominant kernel, timed live with HIP events on the stream it runs on), ``cpu_baseline``
+(the CPU oracle, bounded sample), ``median_ms_per_step`` (per-step HIP events) and, at N=1, the
+other single-GPU configs: ``c4_vctk_training`` (configs[3]) and ``c5_free_running``
+(configs[4]).  Any training step skipped by the health guard aborts the run before printing.
 """
 
 from __future__ import annotations
@@ -41,13 +43,17 @@ HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    # median of >= 50 steps after 10 warm-up steps
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--chars", type=int, default=200)
     ap.add_argument("--frames", type=int, default=1000)
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extra", action="store_true",
+                    help="skip the C4 (VCTK training) and C5 (free-running inference) lines")
+    ap.add_argument("--extra-steps", type=int, default=10)
     ap.add_argument("--no-roofline", action="store_true",
                     help="skip the attention-kernel probe (profiling runs of the step alone)")
     ap.add_argument("--cpu-baseline-batch", type=int, default=2)
@@ -77,7 +83,7 @@ def attention_probe(rec, B, N, reps=6):
     steps of attention RNN + query + dual-source attention in one launch), timed with HIP events
     on the stream it is launched on, re-launched on the training step's own buffers after the
     timed region; and its algorithmic bytes per launch (SURVEY.md 8(d) per-step attention bytes
-    plus the attention RNN / query operands, times T')."""
+    times T')."""
     kw = rec.kw
     if kw is None:
         return None
@@ -95,27 +101,25 @@ def attention_probe(rec, B, N, reps=6):
     avg_s = ev0.elapsed_time(ev1) / 1e3 / reps
     D1, M1, D2, M2, F, KW, U = (int(kw[k]) for k in ("D1", "M1", "D2", "M2", "F", "KW", "U"))
     f = 4  # fp32
+    # per decoder step 4 (549 B N + 67,191) bytes = K1/V1/K2/V2 + the two
+    # alignment states of every utterance + the attention's own weights (query, location, v)
     attn_step = f * (B * N * (D1 + M1 + D2 + M2 + 5) + (M1 + M2) * (D1 + D2)
-                     + F * (KW + 1) + F * D1 + 2 * D1 + D2)       # 4(549BN+67191)
-    rnn_step = f * ((M1 + M2 + U) * 4 * U + U * (D1 + D2)      # recurrent + query weights
-                    + B * (4 * U                               # X0 row read
-                           + (M1 + M2 + U) + U + U + 4 * U + (D1 + D2)))   # histories written
-    bytes_launch = T * (attn_step + rnn_step)
+                     + F * (KW + 1) + F * D1 + 2 * D1 + D2)
+    bytes_launch = T * attn_step
     achieved = bytes_launch / avg_s / 1e9
     traffic, pmc_src = _pmc_traffic()
     return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
             "kernel": "dec_attn_fwd_kernel (sat_decoder_attention_fwd, persistent, T' steps)",
             "bytes_per_launch": int(bytes_launch), "attn_bytes_per_step": int(attn_step),
-            "rnn_bytes_per_step": int(rnn_step), "steps_per_launch": T,
-            "avg_launch_us": round(avg_s * 1e6, 1), "us_per_step": round(avg_s * 1e6 / T, 3),
-            "launches_timed": reps,
-            "note": "achieved = ALGORITHMIC bytes (K1/V1/K2/V2 + state + weights streamed every "
-                    "decoder step, as a per-step implementation must) / HIP-event launch time; "
-                    "the kernel keeps K/V slices in LDS and weight columns in registers, so its "
-                    "real memory traffic (traffic, rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, "
-                    f"{pmc_src}) is far lower: it is bound by the in-kernel group barriers and "
-                    "on-chip phase latency, not by HBM"}
+            "steps_per_launch": T, "avg_launch_us": round(avg_s * 1e6, 1),
+            "us_per_step": round(avg_s * 1e6 / T, 3), "launches_timed": reps,
+            "note": "achieved = SURVEY 8(d) ALGORITHMIC attention bytes (4(549 B N + 67191) per "
+                    "decoder step: K1/V1/K2/V2, alignment states, attention weights) x T' / "
+                    "HIP-event launch time on the launching stream; the kernel keeps K/V slices "
+                    "in LDS, so its real memory traffic (traffic = per-launch FETCH_SIZE + "
+                    f"WRITE_SIZE, {pmc_src}) is lower: it is bound by its in-kernel hand-off "
+                    "latency, not by HBM"}
 
 
 def _pmc_traffic():
@@ -173,6 +177,67 @@ def cpu_baseline(hp, args):
                       f"full training step(s) (fwd + BPTT + Adam), {dt:.2f} s/step"}
 
 
+def c4_vctk_training(args):
+    """C4 (BASELINE configs[3]): VCTK multi-speaker self-attention-tacotron.json (speaker
+    embedding 152 x 16 + MultiSpeakerPreNet), batch 32, teacher-forced training step, graphed."""
+    from sat_amd import data, engine, hparams, train
+    hp = hparams.vctk_hparams()
+    B, N, T = args.batch, args.chars, args.frames
+    m = engine.Tacotron(hp, "cuda", seed=4321)
+    b = data.synthetic_batch(hp, B, N=N, T=T, shape="max", seed=77)
+    batch = {k: torch.tensor(v).cuda() for k, v in b.items()}
+    tr = train.Trainer(m, B, N, T // hp.outputs_per_step, seed=99)
+    g = train.GraphedStep(tr, batch, warmup=1)
+    for _ in range(3):
+        g.replay()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.extra_steps):
+        g.replay()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / args.extra_steps
+    tr.check_health(wait=True)
+    out = {"metric": "teacher-forced mel frames/sec, VCTK multi-speaker batch=32, 1 MI355X",
+           "value": round(B * T / dt, 1), "unit": "frames/s", "ms_per_step": round(1e3 * dt, 3),
+           "steps": args.extra_steps, "config": {"workload": "VCTK self-attention-tacotron.json "
+                                                 "teacher-forced training step, configs[3]",
+                                                 "batch": B, "chars": N, "mel_frames": T}}
+    del g, tr, m
+    torch.cuda.empty_cache()
+    return out
+
+
+def c5_free_running(args, B=8, steps=500):
+    """C5 (BASELINE configs[4]): LJSpeech free-running inference, batch 8, 500 decoder steps
+    (no early stop: min_iters = max_iters), the step loop captured as hipGraphs of 25 steps."""
+    from sat_amd import data, engine, hparams
+    from sat_amd.inference import FreeRunningDecoder
+    hp = hparams.ljspeech_hparams()
+    m = engine.Tacotron(hp, "cuda", seed=1234)
+    b = data.synthetic_batch(hp, B, N=args.chars, T=args.frames, shape="max", seed=55)
+    batch = {k: torch.tensor(v).cuda() for k, v in b.items()}
+    dec = FreeRunningDecoder(m, max_iters=steps, min_iters=steps, check_every=25, graphs=True)
+    out = dec.run(batch)                           # builds the plan and captures the graphs
+    assert out["steps"] == steps
+    torch.cuda.synchronize()
+    reps = 3
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        dec.run(batch)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / reps
+    r = hp.outputs_per_step
+    res = {"metric": "free-running mel frames/sec, LJSpeech batch=8, 500 decoder steps, 1 MI355X",
+           "value": round(B * steps * r / dt, 1), "unit": "frames/s",
+           "ms_per_decode": round(1e3 * dt, 2), "us_per_decoder_step": round(1e6 * dt / steps, 1),
+           "config": {"workload": "predict_mel.py path (encoder + stop-token decoder, KV-cached "
+                                  "decoder self-attention), configs[4]", "batch": B,
+                      "chars": args.chars, "decoder_steps": steps, "hip_graph": True}}
+    del dec, m
+    torch.cuda.empty_cache()
+    return res
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -210,18 +275,28 @@ def main():
     if dist:
         torch.distributed.barrier()
     torch.cuda.synchronize()
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    evs[0].record()
+    for i in range(args.steps):
         run()
+        evs[i + 1].record()
     torch.cuda.synchronize()
     if dist:
         torch.distributed.barrier()
     dt = time.perf_counter() - t0
     dt = dp.max_over_ranks(dt, "cuda")
+    step_ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)]
+    # a step the health guard skipped (hand-off timeout, id out of range) voids the number
+    trainer.check_health(wait=True)
     loss1 = float(trainer.last_loss.item())
     frames = world * B * T * args.steps
     value = frames / dt
     roof = None if args.no_roofline else attention_probe(rec, B, N)
+    extra = {}
+    if rank == 0 and world == 1 and not args.no_extra:
+        extra["c4_vctk_training"] = c4_vctk_training(args)
+        extra["c5_free_running"] = c5_free_running(args)
     if rank == 0:
         cpu = None if args.no_cpu_baseline else cpu_baseline(hp, args)
         line = {
@@ -235,7 +310,8 @@ def main():
                        "mel_frames": T, "num_mels": hp.num_mels, "r": hp.outputs_per_step,
                        "decoder_steps": T // hp.outputs_per_step, "parallelism": f"dp{world}",
                        "hip_graph": not args.no_graph, "params": model.num_params},
-            "roofline": roof, "cpu_baseline": cpu,
+            "median_ms_per_step": round(float(np.median(step_ms)), 3),
+            "roofline": roof, "cpu_baseline": cpu, **extra,
             "loss_first_timed": round(loss0, 5), "loss_last": round(loss1, 5),
         }
         print(json.dumps(line), flush=True)

@@ -682,8 +682,28 @@ static int64_t eh_floats(int B, int ntiles) { return (int64_t)2 * B * ntiles * k
 static int64_t ah_floats(int B, int ntiles) { return (int64_t)2 * B * ntiles * kAH * 2; }
 static constexpr int64_t kXidWords = kG * kGW;
 
+// SAT_ATTN_FWD8=0 selects the 8-groups x 32-workgroups layout below even where the
+// one-utterance-per-8-workgroups layout (decoder_persistent8.hip, N <= 256) applies (A/B switch)
+static bool fwd8_enabled() {
+  const char* e = getenv("SAT_ATTN_FWD8");
+  return !(e && e[0] == '0');
+}
+
 extern "C" int sat_decoder_attention_fwd(const SatDecAttnFwd* a, void* stream) {
   SAT_CHECK_ARG(a && a->B > 0 && a->N > 0 && a->T > 0, "sat_decoder_attention_fwd: bad sizes");
+  if (fwd8_enabled() && dec_attn_fwd8_eligible(a)) {
+    SAT_CHECK_ARG(a->X0 && a->W0r && a->Wq1 && a->Wq2 && a->K1 && a->V1 && a->K2 && a->V2 &&
+                  a->lengths && a->v1 && a->b1 && a->convW && a->convb && a->locW && a->v2 &&
+                  a->REC0 && a->C0 && a->H0RAW && a->G0 && a->Q && a->S1 && a->AL1 && a->S2 &&
+                  a->ST && a->QP && a->err,
+                  "sat_decoder_attention_fwd: null pointer");
+    SAT_CHECK_ARG((a->mask_c == nullptr) == (a->mask_h == nullptr), "sat_decoder_attention_fwd: masks come in pairs");
+    SAT_CHECK_ARG(aligned16(a->X0) && aligned16(a->G0) && aligned16(a->K1) && aligned16(a->V1) &&
+                  aligned16(a->W0r) && aligned16(a->REC0) && aligned16(a->Q) && aligned16(a->QP) &&
+                  (a->ZH == nullptr || ((uintptr_t)a->ZH & 7) == 0),
+                  "sat_decoder_attention_fwd: 16-byte aligned operands");
+    return dec_attn_fwd8_launch(a, as_stream(stream));
+  }
   SAT_CHECK_ARG(a->U == kU && a->M1 == kM1 && a->M2 == kM2 && a->D1 == kD1 && a->D2 == kD2 &&
                 a->F == kF && a->KW == kKW,
                 "sat_decoder_attention_fwd: compiled for U=256, M1=256, M2=32, D1=224, D2=32, "

@@ -247,3 +247,9 @@ __device__ __forceinline__ void transpose_reduce16(float* v, int lane) {
 
 }  // namespace
 }  // namespace sat
+
+namespace sat {
+// one-utterance-per-8-workgroups layout of the attention-chain forward (decoder_persistent8.hip)
+bool dec_attn_fwd8_eligible(const SatDecAttnFwd* a);
+int dec_attn_fwd8_launch(const SatDecAttnFwd* a, hipStream_t s);
+}  // namespace sat

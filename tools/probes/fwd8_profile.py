@@ -1,0 +1,73 @@
+"""Attention-chain forward: one-utterance-per-8-workgroups kernel (decoder_persistent8.hip) vs
+the 8 x 32 layout (SAT_ATTN_FWD8=0): HIP-event launch time on the training step's own buffers,
+the new kernel's segment clocks, and bitwise agreement of the histories (tools only)."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+import _sat_path  # noqa: E402
+
+_sat_path.load()
+import torch  # noqa: E402
+
+from sat_amd import data, engine, hparams  # noqa: E402
+from sat_amd import kernels as K  # noqa: E402
+
+orig = K.decoder_attention_fwd
+KW = {}
+
+
+def rec(**kw):
+    KW.update(kw)
+    orig(**kw)
+
+
+K.decoder_attention_fwd = rec
+B = int(sys.argv[1]) if len(sys.argv) > 1 else 32
+hp = hparams.ljspeech_hparams()
+m = engine.Tacotron(hp, "cuda", seed=1)
+b = data.synthetic_batch(hp, B, N=200, T=1000, shape="max", seed=1)
+gb = {k: torch.tensor(v).cuda() for k, v in b.items()}
+m.forward(gb, None, training=False, need_grad=True)
+torch.cuda.synchronize()
+kw = dict(KW)
+Tp = int(kw["T"])
+
+
+def timed(flag, reps=5):
+    os.environ["SAT_ATTN_FWD8"] = flag
+    for _ in range(2):
+        orig(**kw)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        orig(**kw)
+    e1.record()
+    torch.cuda.synchronize()
+    out = {k: kw[k].clone() for k in ("REC0", "C0", "H0RAW", "G0", "Q", "S1", "AL1", "S2", "ST",
+                                      "LOC", "ZH") if kw.get(k) is not None}
+    err = int(kw["err"][0].item())
+    return e0.elapsed_time(e1) * 1e3 / reps, out, err
+
+
+t_new, o_new, e_new = timed("1")
+t_old, o_old, e_old = timed("0")
+print(f"B={B} N=200 T'={Tp}: fwd8 {t_new:.1f} us/launch = {t_new / Tp:.2f} us/step (err {e_new}); "
+      f"8x32 {t_old:.1f} us = {t_old / Tp:.2f} us/step (err {e_old})", flush=True)
+for k in o_new:
+    d = (o_new[k] - o_old[k]).abs()
+    print(f"  {k:6s} max|new-old| {float(d.max()):.3e}  mean {float(d.mean()):.3e}")
+os.environ["SAT_ATTN_FWD8"] = "1"
+prof = torch.zeros(256 * 16, dtype=torch.int64, device="cuda")
+orig(**dict(kw, prof=prof))
+torch.cuda.synchronize()
+pr = prof.view(256, 16).cpu().double() / 100.0
+names = ["wait B records", "sync (staged)", "combine", "sync (c)", "c-dot + cell",
+         "sync (cell)", "q partial + publish A", "normalise", "loc + L", "wait A records",
+         "q sum (2 syncs)", "energies", "sync + stats", "sync + ctx + publish B", "h-dot", "-"]
+rows = [g + 32 * j for g in range(B) for j in range(8)]
+for i, n in enumerate(names[:15]):
+    col = pr[rows, i]
+    print(f"  {n:24s} {float(col.mean()) / Tp:6.3f} us/step (max {float(col.max()) / Tp:6.3f})")
+print(f"  total {float(pr[rows].sum(1).mean()) / Tp:.3f} us/step")

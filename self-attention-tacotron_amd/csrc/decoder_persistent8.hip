@@ -31,6 +31,10 @@
 #include "sat_common.h"
 #include "persistent.h"
 
+#ifndef SAT_FWD8_TRACE
+#define SAT_FWD8_TRACE 0
+#endif
+
 namespace sat {
 namespace {
 
@@ -223,6 +227,11 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
     }
   };
   bool gave_up = false;
+#if SAT_FWD8_TRACE
+  // per-wave event clocks of workgroup 0 over steps 100..107: prof[4096 + ...] (build with
+  // -DSAT_FWD8_TRACE=1; tools/probes/fwd8_profile.py prints them)
+  long long* evt = (p.prof && blockIdx.x == 0) ? p.prof + 256 * 16 : nullptr;
+#endif
 
   for (int t = 0; t <= T; ++t) {
     const int s = t - 1;
@@ -231,7 +240,16 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
     // and spilled the register-resident weights)
     int tid = tid0;
     asm volatile("" : "+v"(tid));
-    const int lane = tid & 63, wave = tid >> 6;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform (scalar)
+    auto ev = [&](int k) {
+#if SAT_FWD8_TRACE
+      if (evt && t >= 100 && t < 108 && lane == 0) evt[((t - 100) * 8 + wave) * 16 + k] = wall_clock64();
+#else
+      (void)k;
+#endif
+    };
+    ev(0);
     // ============ 1. records B_{t-1}: wave jj stages record jj (wave 0 lanes 16..26 the halos)
     if (t > 0) {
       const int rb0 = ((s & 1) * B + b) * kW;
@@ -268,8 +286,10 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
       else if (two) recs[wave][lane - kM2 / 4] = x2;
       if (hl) halo[hq] = hv;
       tick(0);
+    ev(1);
       lds_barrier();
       tick(1);
+    ev(2);
       // combine: thread d < 288 one context dim; the record scales from lanes 0..7 of each
       // wave (DPP, identical arithmetic in every workgroup of the group), broadcast by readlane
       if (wave < (kC + 63) / 64) {
@@ -281,13 +301,13 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
         const float Z1 = lanes8_sum(st.y * sc1), A1 = lanes8_sum(st.z * sc1);
         const float Z2 = lanes8_sum(z2 * sc2);
         if (tid < kC) {
-          const bool first = tid < kM1;
+          const bool first = wave < kM1 / 64;      // wave-uniform: c1 dims (waves 0..3) or c2
+          const float sc = first ? sc1 : sc2;
           const float* rf = reinterpret_cast<const float*>(&recs[0][2]) + tid;
           float a = 0.f;
 #pragma unroll
-          for (int k = 0; k < kW; ++k)
-            a = fmaf(rf[k * kR4 * 4], first ? rdl(sc1, k) : rdl(sc2, k), a);
-          a *= first ? 1.f / A1 : 1.f / Z2;
+          for (int k = 0; k < kW; ++k) a = fmaf(rf[k * kR4 * 4], rdl(sc, k), a);
+          a *= __builtin_amdgcn_rcpf(first ? A1 : Z2);
           cbuf[tid] = a;
           if (j == 0) p.REC0[((int64_t)t * B + b) * kK0 + tid] = a;
         }
@@ -298,8 +318,10 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
       }
     }
     tick(2);
+    ev(3);
     lds_barrier();
     tick(3);
+    ev(4);
 
     // ============ 2. LSTM step t: c part of the dot, gates (one activation per lane), cell;
     //                 publish record A_t
@@ -362,8 +384,10 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
       }
       load_ops(t + 1, lane, wave, xgn, mcn, mhn);
       tick(4);
+    ev(5);
       lds_barrier();
       tick(5);
+    ev(6);
       // query partial over the own 32 units: wave w owns query columns 32w .. 32w+31; lane l
       // column 32w + (l & 31), units 16 (l >> 5) .. + 15; halves folded, quads gathered
       {
@@ -384,6 +408,7 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
           stc4x(xl, rRA, (ra + kQ) / 4 + lane, *reinterpret_cast<const float4*>(&hst[4 * lane]));
       }
       tick(6);
+    ev(7);
     }
 
     // ============ 3. normalise step t-1 on the own positions (alpha tagged for record B_t)
@@ -428,6 +453,7 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
     }
     if (t == T) break;
     tick(7);
+    ev(8);
 
     // ============ 4. location features f_t and the query-independent energy part
     if (tid < nt * kF) {
@@ -441,7 +467,7 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
     lds_barrier();
     // energy role: lane = dim chunk c (4 dims of [D1 | D2]), wave = positions 4w .. 4w+3
     float4 Lr[4];
-    {
+    if (4 * wave < nt) {
       const int c = lane;
       float4 lw[kF];
 #pragma unroll
@@ -462,6 +488,7 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
       }
     }
     tick(8);
+    ev(9);
 
     // ============ 5. records A_t: wave jj stages record jj (query partial, h_t states)
     {
@@ -483,11 +510,13 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
       if (two) reinterpret_cast<float4*>(hbuf)[(kUW / 4) * wave + lane] = x2;   // units 32 jj + 4 lane
     }
     tick(9);
+    ev(10);
     lds_barrier();
     tick(10);
+    ev(11);
 
     // ============ 6. energies: q chunk summed per lane (record order), tanh, dots with v
-    {
+    if (4 * wave < nt) {
       const unsigned bit = lsb_tag(t);
       const int c = lane;
       float4 q = qst[0][c];
@@ -517,10 +546,15 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
         const float ev = valid ? tagf(e[0], bit) : -INFINITY;
         if (m < 4) eown[r] = ev; else e2own[r] = ev;
       }
+    } else if (lane < 8) {                     // idle wave: its positions are padding
+      const int r = 4 * wave + (lane & 3);
+      if (lane < 4) eown[r] = -INFINITY; else e2own[r] = -INFINITY;
     }
     tick(11);
+    ev(12);
     lds_barrier();
     tick(12);
+    ev(13);
     // tile statistics (every wave redundantly, lane = position) and the wave's own copy of
     // the alignment weights; wave 1 publishes the statistics words
     {
@@ -546,6 +580,7 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // own-wave LDS copy is ready
     }
     tick(13);
+    ev(14);
     // partial contexts, published per wave: wave w owns c1 columns 32w .. 32w+31 (lane l:
     // column 32w + (l & 31), positions 16 (l >> 5) .. + 15); wave 0 also the 32 c2 columns;
     // wave 1 the halo words (first 5 / last 4 energies, last 2 alpha_{t-1})
@@ -584,6 +619,7 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
       }
     }
     tick(14);
+    ev(15);
     // ============ 7. h part of step t+1's gate sums (h_t arrived with records A_t)
     if (t + 1 < T) {
       f2 acc[8];

@@ -335,6 +335,10 @@ typedef struct SatDecAttnBwd {
 int sat_decoder_attention_bwd(const SatDecAttnBwd* args, void* stream);
 int64_t sat_decoder_attention_bwd_scratch(int32_t B, int32_t N, int64_t* rdp_floats,
                                           int64_t* ya_floats);
+/* Query-gradient parts per step the BPTT writes into DQP [T][B][parts][D1+D2]: 1 (dq_t
+ * fully reduced) when the one-utterance-per-8-workgroups layout applies (N <= 256;
+ * SAT_ATTN_BWD8=0 disables it), else ceil(N / 32) tile partials. */
+int32_t sat_decoder_attention_bwd_dq_parts(int32_t B, int32_t N);
 
 /* Persistent decoder LSTM stack: all T steps of DecoderRNNV2's two ZoneoutLSTM(U) layers
  * (ext tacotron2 DecoderRNNV2, built at modules/module.py:1531-1540) in ONE launch, LSTM2 one

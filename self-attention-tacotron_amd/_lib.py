@@ -177,6 +177,7 @@ RESTYPES = {"sat_workspace_colreduce": (ctypes.c_int64, [_I32, _I32]),
             "sat_workspace_loss": (ctypes.c_int64, []),
             "sat_decoder_attention_scratch": (ctypes.c_int64, [_I32, _I32, _P, _P, _P]),
             "sat_decoder_attention_bwd_scratch": (ctypes.c_int64, [_I32, _I32, _P, _P]),
+            "sat_decoder_attention_bwd_dq_parts": (ctypes.c_int32, [_I32, _I32]),
             "sat_decoder_lstms_scratch": (ctypes.c_int64, [_I32]),
             "sat_decoder_lstms_bwd_scratch": (ctypes.c_int64, [_I32]),
             "sat_crc32c": (ctypes.c_uint32, [_P, _I64, ctypes.c_uint32]),

@@ -15,6 +15,7 @@ from typing import Dict
 
 import torch
 
+from . import _lib
 from . import kernels as K
 from .model import _contig_span
 from .pipeline import SEQUENTIAL, Pipeline
@@ -184,7 +185,11 @@ def decoder_bwd(P, G, hp, d, dsv, dH2, masks, ws, attn_tile=32, pipe: Pipeline =
     DFH = torch.empty(Tp, B, N, max(d.loc_f, 1), **f32)     # location-feature gradient history
     DE1 = torch.empty(Tp, B, N, **f32)                      # energy-gradient histories
     DE2 = torch.empty(Tp, B, N, **f32)
-    DQP = torch.empty(Tp, B, ntiles, D1 + D2, **f32)   # per-step, per-tile query gradients
+    # per-step query gradients: per-tile partials (launch path, 8 x 32 persistent kernel) or
+    # fully reduced (one part: the one-utterance-per-8-workgroups BPTT)
+    dq_parts = (int(_lib.load().sat_decoder_attention_bwd_dq_parts(B, N))
+                if S.get("attn_scratch") is not None else ntiles)
+    DQP = torch.empty(Tp, B, dq_parts, D1 + D2, **f32)
     hc = [torch.zeros(B, A, **f32), torch.zeros(B, A, **f32)]
     cc = [torch.zeros(B, A, **f32), torch.zeros(B, A, **f32)]
     mc0, mh0 = mk("dec/lstm0/zc"), mk("dec/lstm0/zh")
@@ -354,14 +359,14 @@ def decoder_bwd(P, G, hp, d, dsv, dH2, masks, ws, attn_tile=32, pipe: Pipeline =
         K.axpby(pg_sum[o:o + D1], G[f"{a1}/attention_v"], 1.0, 1.0); o += D1
     K.axpby(pg_sum[o:o + D2], G[f"{a2}/attention_v"], 1.0, 1.0)
     # the per-tile partials of every step sum into the query-layer / bias gradients
-    DQf = DQP.view(Tp * B * ntiles, D1 + D2)
+    DQf = DQP.view(Tp * B * dq_parts, D1 + D2)
     if fwd:
         qsum = torch.zeros(D1 + D2, **f32)
         K.colsum(DQf, qsum, ws, beta=0.0)
         K.axpby(qsum[:D1], G[f"{a1}/attention_bias"], 1.0, 1.0)
     H0f = S["H0RAW"].view(Tp * B, A)
-    DQt = DQP.view(Tp * B, ntiles, D1 + D2)
-    for tile in range(ntiles):
+    DQt = DQP.view(Tp * B, dq_parts, D1 + D2)
+    for tile in range(dq_parts):
         K.gemm(H0f.t(), DQt[:, tile, :D1], G[f"{a1}/query_layer/kernel"], beta=1.0)
         K.gemm(H0f.t(), DQt[:, tile, D1:], G[f"{a2}/query_layer/kernel"], beta=1.0)
     # ---- memories: values via the alignment histories, keys via memory_layer

@@ -539,6 +539,18 @@ using namespace sat;
 
 extern "C" int sat_decoder_attention_bwd(const SatDecAttnBwd* a, void* stream) {
   SAT_CHECK_ARG(a && a->B > 0 && a->N > 0 && a->T > 0, "sat_decoder_attention_bwd: bad sizes");
+  if (dec_attn_bwd8_eligible(a)) {               // one utterance per 8 workgroups (N <= 256)
+    SAT_CHECK_ARG(a->REC0 && a->C0 && a->G0 && a->S1 && a->AL1 && a->S2 && a->ST && a->LOC &&
+                  a->V1 && a->V2 && a->v1 && a->convW && a->convb && a->locW && a->v2 &&
+                  a->W0r && a->Wq1 && a->Wq2 && a->DH0 && a->ZH && a->RD && a->DG0 && a->DE1 &&
+                  a->DE2 && a->DFH && a->DQP && a->RDP && a->err,
+                  "sat_decoder_attention_bwd: null pointer");
+    SAT_CHECK_ARG((a->mask_c == nullptr) == (a->mask_h == nullptr), "sat_decoder_attention_bwd: masks come in pairs");
+    SAT_CHECK_ARG(aligned16(a->W0r) && aligned16(a->G0) && aligned16(a->DG0) && aligned16(a->ZH) &&
+                  aligned16(a->DQP) && aligned16(a->RDP) && aligned16(a->REC0),
+                  "sat_decoder_attention_bwd: 16-byte aligned operands");
+    return dec_attn_bwd8_launch(a, as_stream(stream));
+  }
   SAT_CHECK_ARG(a->U == kU && a->M1 == kM1 && a->M2 == kM2 && a->D1 == kD1 && a->D2 == kD2 &&
                 a->F == kF && a->KW == kKW,
                 "sat_decoder_attention_bwd: compiled for the self-attention-tacotron shapes");

@@ -252,4 +252,6 @@ namespace sat {
 // one-utterance-per-8-workgroups layout of the attention-chain forward (decoder_persistent8.hip)
 bool dec_attn_fwd8_eligible(const SatDecAttnFwd* a);
 int dec_attn_fwd8_launch(const SatDecAttnFwd* a, hipStream_t s);
+bool dec_attn_bwd8_eligible(const SatDecAttnBwd* a);   // decoder_persistent8_bwd.hip
+int dec_attn_bwd8_launch(const SatDecAttnBwd* a, hipStream_t s);
 }  // namespace sat

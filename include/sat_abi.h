@@ -85,6 +85,12 @@ typedef struct SatGemmDesc {
 } SatGemmDesc;
 
 int sat_gemm(const SatGemmDesc* desc, void* stream);
+/* Tuning hook (probes): force the tile (64/128 x 64/128) and split-K factor of the calling
+ * thread's subsequent sat_gemm launches on the LDS-staged kernel; bm = 0 restores the planner. */
+int sat_gemm_force_plan(int32_t bm, int32_t bn, int32_t splits);
+/* Speed-of-light probe (tools/probes/gemm_sol.py): mode bit 0 skips the LDS kernel's operand
+ * DMA, bit 1 its epilogue stores (results are then garbage); 0 = normal.  Calling thread only. */
+int sat_gemm_probe_mode(int32_t mode);
 /* Skinny product C = alpha * A . Bt^T + beta * C, A [M][K], Bt [N][K] rows contiguous in K
  * (16-B aligned, K % 4 == 0): the per-step gradient of the attention contexts through the
  * attention RNN's input weights (M = batch). */

@@ -125,6 +125,8 @@ SIGNATURES = {
     "sat_version": [],
     "sat_device_arch": [ctypes.c_char_p, _I32],
     "sat_gemm": [ctypes.POINTER(SatGemmDesc), _P],
+    "sat_gemm_force_plan": [_I32, _I32, _I32],
+    "sat_gemm_probe_mode": [_I32],
     "sat_rng_fill": [_P, _I64, _P, _U64, _F, _F, _P],
     "sat_counter_add": [_P, _U64, _P],
     "sat_stop_check": [_P, _I64, _I32, _I32, _I32, _P, _P],

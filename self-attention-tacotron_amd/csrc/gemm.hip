@@ -4,10 +4,13 @@
 // products, the Conv1D(SAME) of the CBHG (implicit im2col in the A loader -- no im2col buffer
 // in HBM) and all their gradients (transposes are strides; conv dX / dW are A/B modes).
 //
-// Tile: BM x BN x 32, GM x GN waves (default 2x2 = 256 threads), each wave (BM/GM)x(BN/GN) of
-// 32x32 MFMA sub-tiles.  Global -> registers (tile k+1 prefetched while tile k is multiplied,
-// 16-byte loads whenever the contiguous dimension allows) -> double-buffered LDS ([k][m] /
-// [k][n] images) -> one f32 per lane per MFMA operand; one barrier per K-tile.
+// Two kernels:
+//  * gemm_lds_kernel (default whenever both operands are 16-byte loadable): LDS-DMA
+//    (global_load_lds_dwordx4) into a 3-stage ring, counted waits, one raw barrier per K-tile,
+//    fragments of tile k+1 read into a second register set while tile k's last MFMAs run; tile
+//    64/128 x 64/128 and split-K chosen per launch by a cycle model (launch_lds);
+//  * gemm_kernel (register-staged, any strides / modes): BM x BN x 32 tiles, GM x GN waves,
+//    global -> registers -> double-buffered LDS, one barrier per K-tile.
 // Weight-gradient products (K = T' * B = 16,000 rows, M x N <= 1024 x 1024) have too few output
 // tiles to fill 256 CUs: they run split-K into an fp32 workspace slab [S][M][N] and a second
 // launch sums the slabs in a fixed order and applies the epilogue (deterministic, no atomics).
@@ -44,6 +47,7 @@ struct GemmP {
   int splits, kchunk;          // split-K: grid.z = splits (batch == 1), partial slabs in ws
   float* ws;
   int remap;                   // XCD-aware tile order over the xy plane
+  int probe;                   // sat_gemm_probe_mode: 1 skip DMA, 2 skip epilogue (probes only)
 };
 
 // Operand loader variants, chosen on the host so the main loop carries no mode branches.
@@ -423,6 +427,371 @@ __global__ void __launch_bounds__(256) gemm_splitk_reduce(GemmP p) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// LDS-DMA pipelined variant (the default for every vector-loadable operand mode).
+//
+// Operand tiles go global -> LDS with global_load_lds_dwordx4 (no VGPR staging, no ds_write
+// pass) into a 3-stage ring, so two K-tiles are in flight while one is multiplied; waits are
+// counted (vmcnt(LPT) leaves the newest tile in flight) and the per-K-tile barrier is a raw
+// s_barrier (a __syncthreads would drain every outstanding DMA).  The LDS images are lane-linear
+// copies of the global tile:
+//   * K-major image [rows][32] (operand contiguous along k: A_K, A_IM2COL, B_K, B_FLIP), the
+//     16-byte chunk q of row r stored at slot q ^ ((r >> 1) & 7) (swizzle applied on the SOURCE
+//     address), read back with ds_read_b128: 4 k values per lane -- conflict-free over the four
+//     16-lane groups of ds_read_b128;
+//   * M/N-major image [32][rows] (contiguous along m / n: A_M, A_IM2COLT, B_N), read with
+//     ds_read_b32, 32 consecutive floats per 32-lane group -- conflict-free without a swizzle.
+// The reduction index is permuted inside a K-tile, identically for both operands: MFMA step
+// t = 4 jj + i takes k = 8 jj + 4 h + i in lane half h (h = lane >> 5), so a ds_read_b128 of
+// chunk 2 jj + h feeds four consecutive steps.  Out-of-range chunks (tile edges, conv padding)
+// are read from a zero page, so the loads need no branches and no masks.
+__device__ __attribute__((aligned(16))) float g_gemm_zero[64];
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+__device__ __forceinline__ void raw_barrier() { asm volatile("s_barrier" ::: "memory"); }
+
+// One global_load_lds_dwordx4: 16 bytes per lane into LDS at lds_off + 16 * lane.  Issued from
+// inline asm so the compiler does not track it: its own wait insertion would otherwise put a
+// vmcnt(0) before every ds_read of the ring (it cannot tell the ring's stages apart) and drain
+// the pipeline each K-tile.  Completion is ordered by the explicit counted waits below.
+__device__ __forceinline__ void dma16(const float* src, uint32_t lds_off) {
+  int keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(src), "s"(lds_off)
+      : "memory");
+}
+
+template <int BM, int BN, int AM, int BMD>
+__global__ void __launch_bounds__(256) gemm_lds_kernel(GemmP p) {
+  constexpr int ST = 3;
+  constexpr int WM = BM / 2, WN = BN / 2;             // 2 x 2 waves
+  constexpr int SM = WM / 32, SN = WN / 32;           // 32x32 MFMA sub-tiles per wave
+  constexpr bool AKM = (AM == A_K || AM == A_IM2COL); // A image K-major
+  constexpr bool BKM = (BMD == B_K || BMD == B_FLIP); // B image K-major
+  constexpr int A_SZ = BM * BK, B_SZ = BN * BK, ST_SZ = A_SZ + B_SZ;
+  constexpr int NA = BM / 32, NB = BN / 32;           // 1-KB DMA instructions per wave per tile
+  constexpr int LPT = NA + NB;
+  static_assert(LPT <= 24, "vmcnt budget");
+  __shared__ __attribute__((aligned(16))) float lds[ST * ST_SZ];
+  const uint32_t lds_base = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) float*)lds);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = (w >> 1) * WM, wn = (w & 1) * WN;
+  int tx = blockIdx.x, ty = blockIdx.y;
+  if (p.remap) {   // bijective XCD swizzle: consecutive tiles (one A row panel) share an L2
+    const int nwg = gridDim.x * gridDim.y, orig = blockIdx.y * gridDim.x + blockIdx.x;
+    const int q = nwg >> 3, r = nwg & 7, xcd = orig & 7;
+    const int t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+    ty = t / gridDim.x;
+    tx = t - ty * gridDim.x;
+  }
+  int bz, bz2, split;
+  if (p.splits > 1) { bz = 0; bz2 = 0; split = blockIdx.z; }
+  else { bz = blockIdx.z / p.batch2; bz2 = blockIdx.z - bz * p.batch2; split = 0; }
+  const int m0 = ty * BM, n0 = tx * BN;
+  const float* A = p.A + bz * p.a_sbatch + bz2 * p.a_sbatch2;
+  const float* B = p.B + bz * p.b_sbatch + bz2 * p.b_sbatch2;
+  const int kbeg = split * p.kchunk;
+  const int kend = min(p.K, kbeg + p.kchunk);
+  const float* zero = g_gemm_zero;
+
+  // ---- per-lane loader state, advanced by one K-tile per issue
+  // K-major images: instruction i of wave w covers rows (4 i + w) * 8 + (lane >> 3); the lane's
+  // chunk (after the swizzle) is the same for every instruction
+  const int kq = 4 * ((lane & 7) ^ ((4 * (w & 1) + (lane >> 4)) & 7));
+  // M/N-major images: instruction i covers k rows (4 i + w) * (256 / rows) + lane / (rows / 4)
+  const float* aptr[NA];
+  int ai[NA];
+  const int amq = AKM ? 0 : 4 * (lane % (BM / 4));
+#pragma unroll
+  for (int i = 0; i < NA; ++i) {
+    if constexpr (AM == A_K) {
+      const int gm = m0 + (4 * i + w) * 8 + (lane >> 3);
+      ai[i] = gm < p.M;
+      aptr[i] = A + (int64_t)min(gm, p.M - 1) * p.a_sm + kbeg + kq;
+    } else if constexpr (AM == A_IM2COL) {   // (utterance, position) of the output row
+      const int gm = m0 + (4 * i + w) * 8 + (lane >> 3);
+      const int s = gm / p.a_L, n = gm - s * p.a_L;
+      aptr[i] = A + (int64_t)s * p.a_L * p.a_sm;
+      ai[i] = gm < p.M ? n : -(1 << 28);
+    } else if constexpr (AM == A_M) {
+      ai[i] = kbeg + (4 * i + w) * (256 / BM) + lane / (BM / 4);     // k row
+      aptr[i] = A + (int64_t)ai[i] * p.a_sk + m0 + amq;
+    } else {
+      ai[i] = kbeg + (4 * i + w) * (256 / BM) + lane / (BM / 4);     // k position
+      aptr[i] = nullptr;
+    }
+  }
+  const bool amok = AKM ? true : (m0 + amq < p.M);
+  int atap = 0, ac0 = 0;
+  if constexpr (AM == A_IM2COLT) { atap = m0 / p.a_C; ac0 = m0 - atap * p.a_C; }
+  const float* bptr[NB];
+  int bi[NB];
+  const int bnq = BKM ? 0 : 4 * (lane % (BN / 4));
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    if constexpr (BKM) {
+      const int gn = n0 + (4 * i + w) * 8 + (lane >> 3);
+      bi[i] = gn < p.N;
+      const int gc = min(gn, p.N - 1);
+      bptr[i] = (BMD == B_K) ? B + (int64_t)gc * p.b_sn + kbeg + kq : B + (int64_t)gc * p.b_C + kq;
+    } else {
+      bi[i] = kbeg + (4 * i + w) * (256 / BN) + lane / (BN / 4);
+      bptr[i] = B + (int64_t)bi[i] * p.b_sk + n0 + bnq;
+    }
+  }
+  const bool bnok = BKM ? true : (n0 + bnq < p.N);
+
+  // DMA of K-tile k0 into ring stage `stage`; the running pointers advance by one K-tile
+  auto issue = [&](int stage, int k0) {
+    if (p.probe & 1) return;
+    const uint32_t la = lds_base + (uint32_t)(stage * ST_SZ * 4);
+    const uint32_t lb = la + A_SZ * 4;
+    if constexpr (AM == A_K) {
+      const bool kok = k0 + kq < kend;
+#pragma unroll
+      for (int i = 0; i < NA; ++i) {
+        dma16((ai[i] && kok) ? aptr[i] : zero, la + (4 * i + w) * 1024);
+        aptr[i] += BK;
+      }
+    } else if constexpr (AM == A_IM2COL) {
+      const int tap = k0 / p.a_C, c0 = k0 - tap * p.a_C;
+      const bool kok = k0 + kq < kend;
+#pragma unroll
+      for (int i = 0; i < NA; ++i) {
+        const int row = ai[i] + tap - p.a_shift;
+        const bool ok = kok && row >= 0 && row < p.a_L;
+        dma16(ok ? aptr[i] + (int64_t)row * p.a_sm + c0 + kq : zero, la + (4 * i + w) * 1024);
+      }
+    } else if constexpr (AM == A_M) {
+#pragma unroll
+      for (int i = 0; i < NA; ++i) {
+        dma16((amok && ai[i] < kend) ? aptr[i] : zero, la + (4 * i + w) * 1024);
+        ai[i] += BK;
+        aptr[i] += (int64_t)BK * p.a_sk;
+      }
+    } else {   // A_IM2COLT: m = tap * C + c (one tap per tile), k = (utterance, position)
+#pragma unroll
+      for (int i = 0; i < NA; ++i) {
+        const int pos = ai[i];
+        const int s = pos / p.a_L, n = pos - s * p.a_L;
+        const int row = n + atap - p.a_shift;
+        const bool ok = amok && pos < kend && row >= 0 && row < p.a_L;
+        dma16(ok ? A + (int64_t)(s * p.a_L + row) * p.a_sm + ac0 + amq : zero,
+              la + (4 * i + w) * 1024);
+        ai[i] += BK;
+      }
+    }
+    if constexpr (BMD == B_N) {
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {
+        dma16((bnok && bi[i] < kend) ? bptr[i] : zero, lb + (4 * i + w) * 1024);
+        bi[i] += BK;
+        bptr[i] += (int64_t)BK * p.b_sk;
+      }
+    } else if constexpr (BMD == B_K) {
+      const bool kok = k0 + kq < kend;
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {
+        dma16((bi[i] && kok) ? bptr[i] : zero, lb + (4 * i + w) * 1024);
+        bptr[i] += BK;
+      }
+    } else {   // B_FLIP: W[taps-1-tap][n][o], k = tap * C + o (one tap per tile)
+      const int tap = k0 / p.b_C, o0 = k0 - tap * p.b_C;
+      const int64_t off = (int64_t)(p.b_taps - 1 - tap) * p.N * p.b_C + o0;
+      const bool kok = k0 + kq < kend;
+#pragma unroll
+      for (int i = 0; i < NB; ++i)
+        dma16((bi[i] && kok) ? bptr[i] + off : zero, lb + (4 * i + w) * 1024);
+    }
+  };
+
+  constexpr int NC = (SM * SN >= 4) ? 1 : 4 / (SM * SN);
+  f32x16 acc[NC][SM][SN];
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+#pragma unroll
+    for (int i = 0; i < SM; ++i)
+#pragma unroll
+      for (int j = 0; j < SN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[c][i][j][r] = 0.f;
+
+  const int li = lane & 31, lh = lane >> 5;
+  const int swz = (li >> 1) & 7;     // K-major read swizzle of this lane's rows
+  // fragments of one K-tile: step t = 4 jj + i takes k = 8 jj + 4 h + i (both operands)
+  auto read_frags = [&](int stage, float (&a)[16][SM], float (&b)[16][SN]) {
+    const float* la = lds + stage * ST_SZ;
+    const float* lb = la + A_SZ;
+    if constexpr (AKM) {
+#pragma unroll
+      for (int i = 0; i < SM; ++i)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          const float4 v = *reinterpret_cast<const float4*>(
+              la + (wm + i * 32 + li) * BK + 4 * ((2 * jj + lh) ^ swz));
+          a[4 * jj][i] = v.x; a[4 * jj + 1][i] = v.y; a[4 * jj + 2][i] = v.z; a[4 * jj + 3][i] = v.w;
+        }
+    } else {
+#pragma unroll
+      for (int t = 0; t < 16; ++t)
+#pragma unroll
+        for (int i = 0; i < SM; ++i)
+          a[t][i] = la[(8 * (t >> 2) + 4 * lh + (t & 3)) * BM + wm + i * 32 + li];
+    }
+    if constexpr (BKM) {
+#pragma unroll
+      for (int j = 0; j < SN; ++j)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          const float4 v = *reinterpret_cast<const float4*>(
+              lb + (wn + j * 32 + li) * BK + 4 * ((2 * jj + lh) ^ swz));
+          b[4 * jj][j] = v.x; b[4 * jj + 1][j] = v.y; b[4 * jj + 2][j] = v.z; b[4 * jj + 3][j] = v.w;
+        }
+    } else {
+#pragma unroll
+      for (int t = 0; t < 16; ++t)
+#pragma unroll
+        for (int j = 0; j < SN; ++j)
+          b[t][j] = lb[(8 * (t >> 2) + 4 * lh + (t & 3)) * BN + wn + j * 32 + li];
+    }
+  };
+  auto mfma_steps = [&](int t0, int t1, const float (&a)[16][SM], const float (&b)[16][SN]) {
+#pragma unroll
+    for (int t = t0; t < t1; ++t)
+#pragma unroll
+      for (int i = 0; i < SM; ++i)
+#pragma unroll
+        for (int j = 0; j < SN; ++j)
+          acc[t % NC][i][j] =
+              __builtin_amdgcn_mfma_f32_32x32x2f32(a[t][i], b[t][j], acc[t % NC][i][j], 0, 0, 0);
+  };
+
+  // Schedule per K-tile kt (fragments of kt already in registers): issue the DMA of kt+2 into
+  // the stage read two tiles ago; MFMA steps 0-7; wait for this wave's DMA of kt+1 and barrier
+  // (then every wave's kt+1 tile has landed, and every wave has finished reading the stage
+  // the next issue overwrites); read kt+1's fragments into the other register set while
+  // MFMA steps 8-15 of kt run.  Two register sets alternate, so the loop is unrolled by 2.
+  const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+  float fa0[16][SM], fb0[16][SN], fa1[16][SM], fb1[16][SN];
+  if (nk > 0) {
+    issue(0, kbeg);
+    if (nk > 1) issue(1, kbeg + BK);
+    if (nk > 1) wait_vmcnt<LPT>(); else wait_vmcnt<0>();
+    raw_barrier();
+    read_frags(0, fa0, fb0);
+  }
+  auto tile = [&](int kt, int stage, const float (&ca)[16][SM], const float (&cb)[16][SN],
+                  float (&na)[16][SM], float (&nb)[16][SN]) {
+    const bool more2 = kt + 2 < nk;
+    if (more2) issue(stage == 0 ? 2 : stage - 1, kbeg + (kt + 2) * BK);
+    mfma_steps(0, 8, ca, cb);
+    if (kt + 1 < nk) {
+      if (more2) wait_vmcnt<LPT>(); else wait_vmcnt<0>();
+      raw_barrier();
+      read_frags(stage == 2 ? 0 : stage + 1, na, nb);
+    }
+    mfma_steps(8, 16, ca, cb);
+  };
+  int stage = 0, kt = 0;
+  for (; kt + 1 < nk; kt += 2) {
+    tile(kt, stage, fa0, fb0, fa1, fb1);
+    stage = stage == 2 ? 0 : stage + 1;
+    tile(kt + 1, stage, fa1, fb1, fa0, fb0);
+    stage = stage == 2 ? 0 : stage + 1;
+  }
+  if (kt < nk) tile(kt, stage, fa0, fb0, fa1, fb1);
+
+  if constexpr (NC > 1) {
+#pragma unroll
+    for (int c = 1; c < NC; ++c)
+#pragma unroll
+      for (int i = 0; i < SM; ++i)
+#pragma unroll
+        for (int j = 0; j < SN; ++j) acc[0][i][j] += acc[c][i][j];
+  }
+
+  if (p.probe & 2) {
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < SM; ++i)
+#pragma unroll
+      for (int j = 0; j < SN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) s += acc[0][i][j][r];
+    if (s == 1234.5f) p.C[0] = s;
+    return;
+  }
+  // epilogue: C/D map of 32x32 f32 MFMA: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5).
+  // Whole tiles with a plain epilogue (the common case) take a branch-free store loop.
+  const bool full = (m0 + BM <= p.M) && (n0 + BN <= p.N);
+  if (p.splits > 1) {
+    float* slab = p.ws + (int64_t)split * p.M * p.N;
+#pragma unroll
+    for (int i = 0; i < SM; ++i)
+#pragma unroll
+      for (int j = 0; j < SN; ++j) {
+        const int col = n0 + wn + j * 32 + li;
+        const int row0 = m0 + wm + i * 32 + 4 * lh;
+        float* dst = slab + (int64_t)row0 * p.N + col;
+        if (full) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) dst[((r & 3) + 8 * (r >> 2)) * p.N] = acc[0][i][j][r];
+        } else if (col < p.N) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            if (row0 + (r & 3) + 8 * (r >> 2) < p.M)
+              dst[((r & 3) + 8 * (r >> 2)) * p.N] = acc[0][i][j][r];
+        }
+      }
+    return;
+  }
+  float* C = p.C + bz * p.c_sbatch + bz2 * p.c_sbatch2;
+  const float* bias = p.bias ? p.bias + bz * p.bias_sbatch : nullptr;
+  const float* mul = p.mul ? p.mul + bz * p.mul_sbatch + bz2 * p.mul_sbatch2 : nullptr;
+  const float* add = p.add ? p.add + bz * p.add_sbatch : nullptr;
+  if (full && !mul && !add && p.beta == 0.f && p.act == 0) {
+    const int64_t cs = p.c_sm;
+#pragma unroll
+    for (int i = 0; i < SM; ++i)
+#pragma unroll
+      for (int j = 0; j < SN; ++j) {
+        const int col = n0 + wn + j * 32 + li;
+        const float bv = bias ? bias[col] : 0.f;
+        float* dst = C + (int64_t)(m0 + wm + i * 32 + 4 * lh) * cs + col;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dst[((r & 3) + 8 * (r >> 2)) * cs] = p.alpha * acc[0][i][j][r] + bv;
+      }
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < SM; ++i)
+#pragma unroll
+    for (int j = 0; j < SN; ++j) {
+      const int col = n0 + wn + j * 32 + li;
+      if (col >= p.N) continue;
+      const float bv = bias ? bias[col] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if (row >= p.M) continue;
+        float* dst = C + (int64_t)row * p.c_sm + col;
+        float v = p.alpha * acc[0][i][j][r];
+        if (p.beta != 0.f) v += p.beta * (*dst);
+        v = apply_act(v + bv, p.act);
+        if (mul) v *= mul[(int64_t)row * p.mul_sm + col];
+        if (add) v += add[(int64_t)row * p.add_sm + col];
+        *dst = v;
+      }
+    }
+}
 
 // Skinny product C[M][N] = alpha * A[M][K] . Bt[N][K]^T + beta * C with both operands' rows
 // contiguous in K (a per-decoder-step [B=32] x [4U=1024] x [288] gradient product): 8 lanes
@@ -492,6 +861,141 @@ static hipError_t launch_tiles(int am, int bm, dim3 grid, hipStream_t s, const G
   return hipGetLastError();
 }
 
+// Tuning hook for probes (tools/probes/gemm_sweep.py): a forced tile / split-K plan for the
+// calling thread's next launches on the LDS kernel (bm = 0 restores the cost model).
+static thread_local int t_force_bm = 0, t_force_bn = 0, t_force_s = 0, t_probe = 0;
+extern "C" int sat_gemm_probe_mode(int32_t m) {
+  SAT_CHECK_ARG(m >= 0 && m <= 3, "sat_gemm_probe_mode: bad mode");
+  t_probe = m;
+  return SAT_OK;
+}
+extern "C" int sat_gemm_force_plan(int32_t bm, int32_t bn, int32_t splits) {
+  SAT_CHECK_ARG(bm == 0 || ((bm == 64 || bm == 128) && (bn == 64 || bn == 128) && splits >= 1),
+                "sat_gemm_force_plan: bad plan");
+  t_force_bm = bm; t_force_bn = bn; t_force_s = splits;
+  return SAT_OK;
+}
+
+// SAT_GEMM_LDS=0 selects the register-staged kernel for every product (A/B switch).
+static bool gemm_lds_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("SAT_GEMM_LDS");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+static void launch_splitk_reduce(const SatGemmDesc* d, const GemmP& p, hipStream_t s) {
+  const int64_t total = (int64_t)d->M * d->N;
+  const int64_t work = (d->N % 4 == 0) ? total / 4 : total;
+  const int blocks = (int)std::min<int64_t>((work + 255) / 256, 2048);
+  hipLaunchKernelGGL(gemm_splitk_reduce, dim3(blocks), dim3(256), 0, s, p);
+}
+
+template <int BM, int BN>
+static hipError_t launch_lds_tiles(int am, int bm, dim3 grid, hipStream_t s, const GemmP& p) {
+#define SAT_GEMM_CASE(A_, B_)                                                               \
+  if (am == A_ && bm == B_) {                                                               \
+    hipLaunchKernelGGL((gemm_lds_kernel<BM, BN, A_, B_>), grid, dim3(256), 0, s, p);       \
+    return hipGetLastError();                                                               \
+  }
+  SAT_GEMM_CASE(A_K, B_N)
+  SAT_GEMM_CASE(A_K, B_K)
+  SAT_GEMM_CASE(A_M, B_N)
+  SAT_GEMM_CASE(A_M, B_K)
+  SAT_GEMM_CASE(A_IM2COL, B_N)
+  SAT_GEMM_CASE(A_IM2COL, B_FLIP)
+  SAT_GEMM_CASE(A_IM2COLT, B_N)
+#undef SAT_GEMM_CASE
+  return hipErrorInvalidValue;
+}
+
+// Plan + launch on the LDS-DMA kernel.  Returns 1 (nothing launched) when an operand is not
+// vector-loadable.  The tile shape and split-K factor minimise a cycle model of the launch:
+// MFMA cycles per CU (tiles spread over 256 CUs, BM*BN*kchunk/128 cycles per tile) + an
+// unhidden pipeline fill/drain per residency round (occupancy set by the 3-stage LDS ring) +
+// the split-K reduce (launch + slab traffic).
+static int launch_lds(const SatGemmDesc* d, GemmP& p, int nb, hipStream_t s) {
+  const bool astr = (p.a_sbatch % 4 == 0) && (p.a_sbatch2 % 4 == 0) && aligned16(d->A);
+  const bool bstr = (p.b_sbatch % 4 == 0) && (p.b_sbatch2 % 4 == 0) && aligned16(d->B);
+  int am = -1, bm = -1;
+  if (d->a_mode == 0) {
+    if (astr && d->a_sk == 1 && d->a_sm % 4 == 0 && d->K % 4 == 0) am = A_K;
+    else if (astr && d->a_sm == 1 && d->a_sk % 4 == 0 && d->M % 4 == 0) am = A_M;
+  } else if (d->a_mode == 1) {
+    if (astr && d->a_sk == 1 && d->a_sm % 4 == 0 && d->a_C % BK == 0) am = A_IM2COL;
+  } else {
+    if (astr && d->a_sk == 1 && d->a_sm % 4 == 0 && d->a_C % 64 == 0) am = A_IM2COLT;
+  }
+  if (d->b_mode == 0) {
+    if (bstr && d->b_sn == 1 && d->b_sk % 4 == 0 && d->N % 4 == 0) bm = B_N;
+    else if (bstr && d->b_sk == 1 && d->b_sn % 4 == 0 && d->K % 4 == 0) bm = B_K;
+  } else {
+    if (bstr && d->b_C % BK == 0) bm = B_FLIP;
+  }
+  if (am < 0 || bm < 0) return 1;
+  if ((am == A_IM2COL && bm != B_N && bm != B_FLIP) || (am == A_IM2COLT && bm != B_N) ||
+      (bm == B_FLIP && am != A_IM2COL))
+    return 1;
+  struct Cand { int bm, bn, occ; };
+  // (ties go to the first: two 128x64 workgroups per CU overlap each other's epilogue)
+  static const Cand cands[4] = {{128, 64, 2}, {64, 128, 2}, {128, 128, 1}, {64, 64, 3}};
+  const bool can_split = nb == 1 && d->ws != nullptr && d->K >= 512;
+  double best = 1e30;
+  int bc = 3, bs = 1, bkc = d->K;
+  for (int c = 0; c < 4; ++c) {
+    const Cand& cd = cands[c];
+    if (am == A_IM2COLT && d->a_C % cd.bm != 0) continue;
+    const int gx = ceil_div(d->N, cd.bn), gy = ceil_div(d->M, cd.bm);
+    const int64_t base = (int64_t)gx * gy * nb;
+    const int smax = can_split ? std::min(64, std::max(1, d->K / 256)) : 1;
+    for (int S = 1; S <= smax; S = (S < 4 ? S + 1 : S * 2)) {
+      const int kc = (ceil_div(d->K, S) + BK - 1) / BK * BK;
+      const int Se = ceil_div(d->K, kc);
+      if (Se > 1 && (int64_t)Se * d->M * d->N * 4 > d->ws_bytes) break;
+      const int64_t tiles = base * Se;
+      const int64_t per_cu = (tiles + 255) / 256;
+      // MFMA efficiency vs resident waves x 32x32 sub-tiles per wave (probe: gemm_sweep.py)
+      const int conc = (int)std::min<int64_t>(cd.occ, per_cu);
+      const double eta = std::min(0.85, 0.35 + 0.2 * conc * (cd.bm / 64) * (cd.bn / 64));
+      const double mfma = (double)per_cu * cd.bm * cd.bn * std::max(kc, BK) / 128.0 / eta;
+      const double fill = (double)((per_cu + cd.occ - 1) / cd.occ) * 4000.0;
+      const double red = Se > 1 ? 2400.0 * (2.0 + (double)d->M * d->N * Se * 4 / 3.0e6) : 0.0;
+      const double cost = mfma + fill + red;
+      if (cost < best * 0.97) { best = cost; bc = c; bs = Se; bkc = kc; }
+    }
+  }
+  if (t_force_bm > 0) {
+    for (int c = 0; c < 4; ++c)
+      if (cands[c].bm == t_force_bm && cands[c].bn == t_force_bn) bc = c;
+    if (am == A_IM2COLT && d->a_C % cands[bc].bm != 0) return 1;
+    bs = can_split ? t_force_s : 1;
+    bkc = (ceil_div(d->K, bs) + BK - 1) / BK * BK;
+    bs = ceil_div(d->K, bkc);
+    if (bs > 1 && (int64_t)bs * d->M * d->N * 4 > d->ws_bytes) return 1;
+  }
+  const Cand& cd = cands[bc];
+  const int gx = ceil_div(d->N, cd.bn), gy = ceil_div(d->M, cd.bm);
+  p.splits = bs;
+  p.kchunk = bs > 1 ? bkc : d->K;
+  p.remap = (gx * gy >= 16) ? 1 : 0;
+  const dim3 grid(gx, gy, bs > 1 ? bs : nb);
+  hipError_t e;
+  if (cd.bm == 128 && cd.bn == 128) e = launch_lds_tiles<128, 128>(am, bm, grid, s, p);
+  else if (cd.bm == 128) e = launch_lds_tiles<128, 64>(am, bm, grid, s, p);
+  else if (cd.bn == 128) e = launch_lds_tiles<64, 128>(am, bm, grid, s, p);
+  else e = launch_lds_tiles<64, 64>(am, bm, grid, s, p);
+  if (e != hipSuccess) {
+    set_error("sat_gemm: launch failed: %s", hipGetErrorString(e));
+    return SAT_ERR_HIP;
+  }
+  if (bs > 1) {
+    launch_splitk_reduce(d, p, s);
+    SAT_LAUNCH_CHECK("sat_gemm(split-k reduce)");
+  }
+  return SAT_OK;
+}
+
 extern "C" int sat_gemm(const SatGemmDesc* d, void* stream) {
   using namespace sat;
   SAT_CHECK_ARG(d != nullptr, "sat_gemm: null descriptor");
@@ -518,8 +1022,14 @@ extern "C" int sat_gemm(const SatGemmDesc* d, void* stream) {
   p.a_sbatch2 = d->a_sbatch2; p.b_sbatch2 = d->b_sbatch2; p.c_sbatch2 = d->c_sbatch2;
   p.mul_sbatch2 = d->mul_sbatch2;
   p.add = d->add; p.add_sm = d->add_sm; p.add_sbatch = d->add_sbatch;
+  p.probe = t_probe;
   hipStream_t s = as_stream(stream);
   const int nb = d->batch * p.batch2;
+  p.ws = reinterpret_cast<float*>(d->ws);
+  if (gemm_lds_enabled()) {
+    const int r = launch_lds(d, p, nb, s);
+    if (r != 1) return r;   // 1: operand layout not vector-loadable, use the register path
+  }
   // 128x128 tiles when the output is large, and for long-K weight-gradient products whose
   // output is wide enough (split-K then supplies the workgroups; measured per shape with
   // tools/gemm_census.py: 544x1024x16000 354 -> 262 us, 6144x128x6400 191 -> 136 us, while

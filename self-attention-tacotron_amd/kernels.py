@@ -171,6 +171,7 @@ def conv1d(x: torch.Tensor, W: torch.Tensor, bias=None, out=None, act=None, beta
     d.b_mode, d.B, d.b_sk, d.b_sn = 0, _p(W), Cout, 1
     d.C, d.c_sm = _p(out), out.stride(1)
     d.bias, d.act, d.alpha, d.beta = _p(bias), ACT[act], 1.0, beta
+    _with_ws(d, x.device)
     _launch_gemm(d, "sat_gemm(conv1d)")
     return out
 
@@ -188,6 +189,7 @@ def conv1d_dx(dy: torch.Tensor, W: torch.Tensor, out=None, beta=0.0):
     d.b_mode, d.b_taps, d.b_C, d.B = 1, taps, Cout, _p(W)
     d.C, d.c_sm = _p(out), out.stride(1)
     d.alpha, d.beta = 1.0, beta
+    _with_ws(d, dy.device)
     _launch_gemm(d, "sat_gemm(conv1d_dx)")
     return out
 

@@ -78,3 +78,47 @@ def test_rng_fill(cuda):
     assert torch.equal(out, out2)
     kernels.rng_fill(out2, seed, 8, 0.9, 1.0 / 0.9)
     assert not torch.equal(out, out2)
+
+
+# ---- the LDS-DMA kernel (gemm_lds_kernel): every operand mode, ragged tile edges, split-K.
+# Shapes follow the training step's products (SURVEY 8(d) census) at reduced M where possible.
+@pytest.mark.parametrize("M,N,K", [(16000, 256, 256), (300, 1024, 288), (96, 160, 2000),
+                                   (256, 1024, 16000), (544, 1024, 3000), (128, 4, 6400),
+                                   (4, 128, 64), (130, 68, 36)])
+@pytest.mark.parametrize("ta,tb", [(False, False), (True, False), (False, True), (True, True)])
+def test_gemm_lds_modes(cuda, M, N, K, ta, tb):
+    from sat_amd import kernels
+    g = torch.Generator().manual_seed(M + 3 * N + 7 * K)
+    A = torch.randn(K, M, generator=g) if ta else torch.randn(M, K, generator=g)
+    B = torch.randn(N, K, generator=g) if tb else torch.randn(K, N, generator=g)
+    C0 = torch.randn(M, N, generator=g)
+    C = C0.to(cuda)
+    Ad, Bd = A.to(cuda), B.to(cuda)
+    kernels.gemm(Ad.t() if ta else Ad, Bd.t() if tb else Bd, C, alpha=0.75, beta=0.5)
+    Al, Bl = (A.t() if ta else A).double(), (B.t() if tb else B).double()
+    ref = 0.75 * (Al @ Bl) + 0.5 * C0.double()
+    bound = 6e-7 * (Al.abs() @ Bl.abs() + C0.double().abs()) + 1e-7
+    err = (C.double().cpu() - ref).abs()
+    assert bool((err <= bound).all()), float((err / bound).max())
+
+
+@pytest.mark.parametrize("taps,Ci,Co,L", [(1, 128, 128, 100), (3, 128, 128, 77), (8, 128, 128, 200),
+                                          (16, 128, 128, 60), (3, 2048, 128, 50), (3, 128, 64, 33)])
+def test_conv1d_lds_fwd_dx_dw(cuda, taps, Ci, Co, L):
+    from sat_amd import kernels
+    g = torch.Generator().manual_seed(taps * 131 + L)
+    S = 3
+    x = torch.randn(S, L, Ci, generator=g, dtype=torch.float64, requires_grad=True)
+    W = torch.randn(taps, Ci, Co, generator=g, dtype=torch.float64, requires_grad=True)
+    b = torch.randn(Co, generator=g, dtype=torch.float64)
+    y = _conv_ref(x, W, b)
+    dy = torch.randn(S, L, Co, generator=g, dtype=torch.float64)
+    y.backward(dy)
+    xd, Wd = x.detach().float().to(cuda), W.detach().float().to(cuda)
+    yd = kernels.conv1d(xd, Wd, b.float().to(cuda))
+    assert _rel(yd, y.detach()) < 2e-6
+    dxd = kernels.conv1d_dx(dy.float().to(cuda), Wd)
+    assert _rel(dxd, x.grad) < 2e-6
+    dWd = torch.empty_like(Wd)
+    kernels.conv1d_dw(xd, dy.float().to(cuda), dWd)
+    assert _rel(dWd, W.grad) < 2e-6

@@ -25,6 +25,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--top", type=int, default=40)
+    ap.add_argument("--sweep", type=int, default=0,
+                    help="also time every forced LDS-kernel plan on the N costliest shapes")
     a = ap.parse_args()
     hp = hparams.ljspeech_hparams()
     m = engine.Tacotron(hp, "cuda")
@@ -39,11 +41,13 @@ def main():
     log, K.GEMM_LOG = K.GEMM_LOG, None
     lib = _lib.load()
     groups = collections.OrderedDict()
+    descs = {}
     s = torch.cuda.current_stream()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     for tag, d in log:
         key = (tag, d.M, d.N, d.K, d.batch, d.batch2, d.a_mode, d.b_mode, d.a_sk == 1, d.b_sn == 1)
         if key not in groups:
+            descs[key] = d
             for _ in range(2):
                 lib.sat_gemm(ctypes.byref(d), ctypes.c_void_p(s.cuda_stream))
             e0.record()
@@ -66,6 +70,34 @@ def main():
         tag, M, N, Kd, nb, nb2, am, bm, ak, bn = key
         print(f"{tag:22s} {M:6d} {N:6d} {Kd:6d} {nb:4d} {nb2:3d} {am:2d} {bm:2d} {int(ak):2d} {int(bn):2d} "
               f"{cnt:4d} {us:10.1f} {tf:8.1f} {tot_us / 1e3:8.3f}")
+    if a.sweep:
+        sweep(lib, descs, [r[4] for r in rows[:a.sweep]])
+
+
+
+def sweep(lib, descs, keys):
+    """Forced (BM, BN, S) plans of the LDS kernel on the step's own descriptors."""
+    s = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for key in keys:
+        d = descs[key]
+        res = []
+        for bm, bn in ((128, 128), (128, 64), (64, 128), (64, 64)):
+            for sp in (1, 2, 3, 4, 6, 8, 12, 16, 24, 32):
+                if sp > 1 and d.K < 512:
+                    continue
+                lib.sat_gemm_force_plan(bm, bn, sp)
+                for _ in range(2):
+                    lib.sat_gemm(ctypes.byref(d), ctypes.c_void_p(s.cuda_stream))
+                e0.record()
+                for _ in range(10):
+                    lib.sat_gemm(ctypes.byref(d), ctypes.c_void_p(s.cuda_stream))
+                e1.record()
+                torch.cuda.synchronize()
+                res.append((e0.elapsed_time(e1) / 10 * 1e3, bm, bn, sp))
+        lib.sat_gemm_force_plan(0, 0, 0)
+        res.sort()
+        print(key[:6], " ".join(f"{bm}x{bn}/s{sp}:{us:.1f}" for us, bm, bn, sp in res[:5]), flush=True)
 
 
 if __name__ == "__main__":

@@ -28,7 +28,10 @@ def run(M, N, Kd, at=0, conv=0, reps=30):
     import _sat_path
     _sat_path.load()
     import torch
-    from sat_amd import kernels as K
+    from sat_amd import _lib, kernels as K
+    plan = os.environ.get("SAT_GEMM_PLAN")   # "BM,BN,S": force the LDS kernel's plan
+    if plan:
+        _lib.load().sat_gemm_force_plan(*(int(x) for x in plan.split(",")))
     if conv:           # conv-bank-shaped Conv1D: x [32, M/32, N] (*) W [K/N taps, N, 128]
         S = 32
         x = torch.randn(S, M // S, N, device="cuda")
@@ -70,7 +73,7 @@ def summary(base, tag, M, N, Kd, cus=256, xcds=8):
     acc, durs = {}, {}
     for d in sorted(glob.glob(os.path.join(base, f"{tag}_p*"))):
         for kname, cname, v, dur, did in _rows(d):
-            if not re.search(r"gemm_kernel", kname):
+            if not re.search(r"gemm_(lds_)?kernel", kname):
                 continue
             acc.setdefault(cname, []).append(v)
             durs.setdefault(d, {})[did] = dur

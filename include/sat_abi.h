@@ -85,6 +85,38 @@ typedef struct SatGemmDesc {
 } SatGemmDesc;
 
 int sat_gemm(const SatGemmDesc* desc, void* stream);
+/* ---------------------------------------------------------------- CBHG conv bank
+ * The K1..Kmax Conv1D(SAME) bank of ZoneoutCBHG (modules/module.py:77-80 over ext tacotron2
+ * Conv1d, module.py:46-52): max_k convolutions of one input, outputs concatenated on channels.
+ * W holds K1..Kmax back to back, Kk = [k][C][Co] at float offset Co*C*k(k-1)/2 (the parameter
+ * arena order of params.py); bias [max_k*Co] may be NULL.  x rows [S*L][C] (stride x_sm).
+ * fwd: y[:, (k-1)Co : kCo] = x (*) Kk + b_k for every k -- ONE launch over the output column
+ *      blocks (longest reductions dispatched first).
+ * bwd: dX = beta_dx*dX + sum_k conv_dx_k(dY[:, (k-1)Co : kCo]) -- ONE product over all
+ *      (k, tap, channel) reduction indices; dW_k = beta_dw*dW_k + im2col(x)^T dY_k for every k
+ *      -- ONE product over all (k, tap, c) rows.  y is dY here; dx or dW may be NULL.
+ *      ws/ws_bytes: split-K scratch (NULL: no split).  Bias and BatchNorm gradients are column
+ *      sums (sat_colsum / sat_bn_bwd).
+ * Needs C % 64 == 0, Co % 64 == 0, 16-byte aligned rows.  Replaces the 3 x max_k per-conv
+ * launches of the same products (sat_gemm a_mode 1 / 2, b_mode 1). */
+typedef struct SatConvBank {
+  int32_t S, L, C, max_k, Co, pad0;
+  const float* x;
+  int64_t x_sm;
+  const float* W;
+  const float* bias;
+  float* y;
+  int64_t y_sm;
+  float* dx;
+  int64_t dx_sm;
+  float* dW;
+  float beta_dx, beta_dw;
+  void* ws;
+  int64_t ws_bytes;
+} SatConvBank;
+int sat_cbhg_convbank_fwd(const SatConvBank* d, void* stream);
+int sat_cbhg_convbank_bwd(const SatConvBank* d, void* stream);
+
 /* Tuning hook (probes): force the tile (64/128 x 64/128) and split-K factor of the calling
  * thread's subsequent sat_gemm launches on the LDS-staged kernel; bm = 0 restores the planner. */
 int sat_gemm_force_plan(int32_t bm, int32_t bn, int32_t splits);

@@ -66,6 +66,10 @@ SatLstmBwd = _struct("SatLstmBwd", """
     i32:dq_parts i64:dq_pstride i64:dq_bstride ptr:dh_carry ptr:dc_carry ptr:mask_c ptr:mask_h f32:zc f32:zh ptr:lengths
     ptr:dgates ptr:dh_carry_out ptr:dc_carry_out ptr:rec i64:rec_sb""")
 
+SatConvBank = _struct("SatConvBank", """
+    i32:S i32:L i32:C i32:max_k i32:Co i32:pad0 ptr:x i64:x_sm ptr:W ptr:bias ptr:y i64:y_sm
+    ptr:dx i64:dx_sm ptr:dW f32:beta_dx f32:beta_dw ptr:ws i64:ws_bytes""")
+
 SatAdamConfig = _struct("SatAdamConfig", """
     f32:lr0 f32:beta1 f32:beta2 f32:eps f32:clip_norm i32:decay i32:step_factor f32:grad_scale""")
 
@@ -127,6 +131,8 @@ SIGNATURES = {
     "sat_gemm": [ctypes.POINTER(SatGemmDesc), _P],
     "sat_gemm_force_plan": [_I32, _I32, _I32],
     "sat_gemm_probe_mode": [_I32],
+    "sat_cbhg_convbank_fwd": [ctypes.POINTER(SatConvBank), _P],
+    "sat_cbhg_convbank_bwd": [ctypes.POINTER(SatConvBank), _P],
     "sat_rng_fill": [_P, _I64, _P, _U64, _F, _F, _P],
     "sat_counter_add": [_P, _U64, _P],
     "sat_stop_check": [_P, _I64, _I32, _I32, _I32, _P, _P],

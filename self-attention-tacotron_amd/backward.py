@@ -17,7 +17,7 @@ import torch
 
 from . import _lib
 from . import kernels as K
-from .model import _contig_span
+from .model import _contig_span, bank_fused
 from .pipeline import SEQUENTIAL, Pipeline
 
 
@@ -517,10 +517,15 @@ def encoder_bwd(P, G, hp, d, sv, dm1, dm2, lengths, masks, ws):
              _contig_span(G, [f"{n}/bn/gamma" for n in names]),
              _contig_span(G, [f"{n}/bn/beta" for n in names]), ws, training=training)
     K.colsum(dbank_pre.view(-1, KC), _contig_span(G, [f"{n}/bias" for n in names]), ws)
-    for k in range(1, d.max_k + 1):
-        sl = dbank_pre[:, :, (k - 1) * C:k * C]
-        K.conv1d_dw(inp, sl, G[f"{names[k - 1]}/kernel"], beta=1.0)
-        K.conv1d_dx(sl, P[f"{names[k - 1]}/kernel"], out=dinp, beta=1.0)
+    if bank_fused(d, inp):
+        kern = [f"{n}/kernel" for n in names]
+        K.conv_bank_bwd(inp, _contig_span(P, kern), dbank_pre, d.max_k, C, dx=dinp,
+                        dW=_contig_span(G, kern), beta_dx=1.0, beta_dw=1.0)
+    else:
+        for k in range(1, d.max_k + 1):
+            sl = dbank_pre[:, :, (k - 1) * C:k * C]
+            K.conv1d_dw(inp, sl, G[f"{names[k - 1]}/kernel"], beta=1.0)
+            K.conv1d_dx(sl, P[f"{names[k - 1]}/kernel"], out=dinp, beta=1.0)
     # prenets + embedding
     pre = sv["enc_pre"]
     dx = dinp

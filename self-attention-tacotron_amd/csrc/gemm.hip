@@ -48,7 +48,17 @@ struct GemmP {
   float* ws;
   int remap;                   // XCD-aware tile order over the xy plane
   int probe;                   // sat_gemm_probe_mode: 1 skip DMA, 2 skip epilogue (probes only)
+  int grp_co;                  // conv-bank launches: output channels per conv (GRP > 0)
 };
+
+// j -> g with g (g + 1) / 2 <= j < (g + 1) (g + 2) / 2: conv K_{g+1} of the bank owns the
+// (tap, channel-block) pairs j = g (g + 1) / 2 + tap, tap < g + 1 (taps of K1..Kmax in order)
+__device__ __forceinline__ int tri_inv(int j) {
+  int g = (int)((sqrtf(8.f * j + 1.f) - 1.f) * 0.5f);
+  if ((g + 1) * (g + 2) / 2 <= j) ++g;
+  if (g * (g + 1) / 2 > j) --g;
+  return g;
+}
 
 // Operand loader variants, chosen on the host so the main loop carries no mode branches.
 enum AMode { A_K = 0, A_M = 1, A_IM2COL = 2, A_IM2COLT = 3, A_GEN = 4 };
@@ -467,7 +477,11 @@ __device__ __forceinline__ void dma16(const float* src, uint32_t lds_off) {
       : "memory");
 }
 
-template <int BM, int BN, int AM, int BMD>
+// GRP selects the conv-bank launches of sat_cbhg_convbank_fwd/bwd (0 = plain product):
+//   1 forward  : output column block g*Co.. = Conv1D K_{g+1}(x), reduction (g+1)*C per tile;
+//   2 dX       : ONE product over K = sum_g (g+1)*Co, k -> (g, tap, o) of dY's column block g;
+//   3 dW       : ONE product over M = sum_g (g+1)*C, rows (g, tap, ci) read dY's column block g.
+template <int BM, int BN, int AM, int BMD, int GRP = 0>
 __global__ void __launch_bounds__(256) gemm_lds_kernel(GemmP p) {
   constexpr int ST = 3;
   constexpr int WM = BM / 2, WN = BN / 2;             // 2 x 2 waves
@@ -495,11 +509,34 @@ __global__ void __launch_bounds__(256) gemm_lds_kernel(GemmP p) {
   int bz, bz2, split;
   if (p.splits > 1) { bz = 0; bz2 = 0; split = blockIdx.z; }
   else { bz = blockIdx.z / p.batch2; bz2 = blockIdx.z - bz * p.batch2; split = 0; }
+  // conv-bank forward: column blocks have different reductions ((g + 1) * C); the dispatcher
+  // deals workgroup i to XCD i % 8, so rotate the column index by the row index to give every
+  // XCD the same mix of kernel widths, longest first within a row
+  if constexpr (GRP == 1) tx = gridDim.x - 1 - (int)((blockIdx.x + blockIdx.y) % gridDim.x);
   const int m0 = ty * BM, n0 = tx * BN;
   const float* A = p.A + bz * p.a_sbatch + bz2 * p.a_sbatch2;
   const float* B = p.B + bz * p.b_sbatch + bz2 * p.b_sbatch2;
+  int Kt = p.K, shift = p.a_shift, atap = 0, ac0 = 0;
+  if constexpr (GRP == 1) {
+    const int g = n0 / p.grp_co, t = g + 1;
+    Kt = t * p.a_C;
+    shift = (t - 1) / 2;
+    B += (int64_t)p.grp_co * p.a_C * (t * (t - 1) / 2) - (int64_t)g * p.grp_co;
+  }
+  if constexpr (AM == A_IM2COLT) {
+    if constexpr (GRP == 3) {
+      const int j = m0 / p.a_C, g = tri_inv(j);
+      atap = j - g * (g + 1) / 2;
+      ac0 = m0 - j * p.a_C;
+      shift = g / 2;
+      B += (int64_t)g * p.grp_co;
+    } else {
+      atap = m0 / p.a_C;
+      ac0 = m0 - atap * p.a_C;
+    }
+  }
   const int kbeg = split * p.kchunk;
-  const int kend = min(p.K, kbeg + p.kchunk);
+  const int kend = min(Kt, kbeg + p.kchunk);
   const float* zero = g_gemm_zero;
 
   // ---- per-lane loader state, advanced by one K-tile per issue
@@ -530,8 +567,6 @@ __global__ void __launch_bounds__(256) gemm_lds_kernel(GemmP p) {
     }
   }
   const bool amok = AKM ? true : (m0 + amq < p.M);
-  int atap = 0, ac0 = 0;
-  if constexpr (AM == A_IM2COLT) { atap = m0 / p.a_C; ac0 = m0 - atap * p.a_C; }
   const float* bptr[NB];
   int bi[NB];
   const int bnq = BKM ? 0 : 4 * (lane % (BN / 4));
@@ -562,11 +597,20 @@ __global__ void __launch_bounds__(256) gemm_lds_kernel(GemmP p) {
         aptr[i] += BK;
       }
     } else if constexpr (AM == A_IM2COL) {
-      const int tap = k0 / p.a_C, c0 = k0 - tap * p.a_C;
+      int tap, c0, sh = shift;
+      if constexpr (GRP == 2) {   // k -> (conv g, tap, channel) of dY's column block g
+        const int j = k0 / p.grp_co, g = tri_inv(j);
+        tap = j - g * (g + 1) / 2;
+        c0 = k0 - j * p.grp_co + g * p.grp_co;
+        sh = g - g / 2;
+      } else {
+        tap = k0 / p.a_C;
+        c0 = k0 - tap * p.a_C;
+      }
       const bool kok = k0 + kq < kend;
 #pragma unroll
       for (int i = 0; i < NA; ++i) {
-        const int row = ai[i] + tap - p.a_shift;
+        const int row = ai[i] + tap - sh;
         const bool ok = kok && row >= 0 && row < p.a_L;
         dma16(ok ? aptr[i] + (int64_t)row * p.a_sm + c0 + kq : zero, la + (4 * i + w) * 1024);
       }
@@ -582,7 +626,7 @@ __global__ void __launch_bounds__(256) gemm_lds_kernel(GemmP p) {
       for (int i = 0; i < NA; ++i) {
         const int pos = ai[i];
         const int s = pos / p.a_L, n = pos - s * p.a_L;
-        const int row = n + atap - p.a_shift;
+        const int row = n + atap - shift;
         const bool ok = amok && pos < kend && row >= 0 && row < p.a_L;
         dma16(ok ? A + (int64_t)(s * p.a_L + row) * p.a_sm + ac0 + amq : zero,
               la + (4 * i + w) * 1024);
@@ -604,8 +648,15 @@ __global__ void __launch_bounds__(256) gemm_lds_kernel(GemmP p) {
         bptr[i] += BK;
       }
     } else {   // B_FLIP: W[taps-1-tap][n][o], k = tap * C + o (one tap per tile)
-      const int tap = k0 / p.b_C, o0 = k0 - tap * p.b_C;
-      const int64_t off = (int64_t)(p.b_taps - 1 - tap) * p.N * p.b_C + o0;
+      int64_t off;
+      if constexpr (GRP == 2) {   // W_{g+1} of the bank at offset Co * C * g (g + 1) / 2
+        const int j = k0 / p.b_C, g = tri_inv(j), tap = j - g * (g + 1) / 2;
+        off = (int64_t)p.b_C * p.N * (g * (g + 1) / 2) + (int64_t)(g - tap) * p.N * p.b_C +
+              (k0 - j * p.b_C);
+      } else {
+        const int tap = k0 / p.b_C, o0 = k0 - tap * p.b_C;
+        off = (int64_t)(p.b_taps - 1 - tap) * p.N * p.b_C + o0;
+      }
       const bool kok = k0 + kq < kend;
 #pragma unroll
       for (int i = 0; i < NB; ++i)
@@ -885,9 +936,9 @@ static bool gemm_lds_enabled() {
   return on;
 }
 
-static void launch_splitk_reduce(const SatGemmDesc* d, const GemmP& p, hipStream_t s) {
-  const int64_t total = (int64_t)d->M * d->N;
-  const int64_t work = (d->N % 4 == 0) ? total / 4 : total;
+static void launch_splitk_reduce(const GemmP& p, hipStream_t s) {
+  const int64_t total = (int64_t)p.M * p.N;
+  const int64_t work = (p.N % 4 == 0) ? total / 4 : total;
   const int blocks = (int)std::min<int64_t>((work + 255) / 256, 2048);
   hipLaunchKernelGGL(gemm_splitk_reduce, dim3(blocks), dim3(256), 0, s, p);
 }
@@ -910,11 +961,97 @@ static hipError_t launch_lds_tiles(int am, int bm, dim3 grid, hipStream_t s, con
   return hipErrorInvalidValue;
 }
 
+struct LdsPlan { int bm, bn, splits, kchunk; };
+
+// Tile shape and split-K factor minimising a cycle model of the launch: MFMA cycles per CU
+// (tiles spread over 256 CUs, BM*BN*kchunk/128 cycles per tile at an efficiency set by the
+// resident waves x sub-tiles per wave) + an unhidden pipeline fill/drain per residency round
+// (occupancy set by the 3-stage LDS ring) + the split-K reduce (launch + slab traffic).
+// c_div: BM must divide it (im2col-T: one tap per tile); n_div: BN must divide it (conv bank).
+static LdsPlan plan_lds(int M, int N, int K, int nb, bool can_split, int64_t ws_bytes, int c_div,
+                        int n_div) {
+  struct Cand { int bm, bn, occ; };
+  // (ties go to the first: two 128x64 workgroups per CU overlap each other's epilogue)
+  static const Cand cands[4] = {{128, 64, 2}, {64, 128, 2}, {128, 128, 1}, {64, 64, 3}};
+  can_split = can_split && nb == 1 && K >= 512;
+  double best = 1e30;
+  LdsPlan pl{0, 0, 1, K};
+  for (int c = 0; c < 4; ++c) {
+    const Cand& cd = cands[c];
+    if ((c_div && c_div % cd.bm != 0) || (n_div && n_div % cd.bn != 0)) continue;
+    const int gx = ceil_div(N, cd.bn), gy = ceil_div(M, cd.bm);
+    const int64_t base = (int64_t)gx * gy * nb;
+    const int smax = can_split ? std::min(64, std::max(1, K / 256)) : 1;
+    for (int S = 1; S <= smax; S = (S < 4 ? S + 1 : S * 2)) {
+      const int kc = (ceil_div(K, S) + BK - 1) / BK * BK;
+      const int Se = ceil_div(K, kc);
+      if (Se > 1 && (int64_t)Se * M * N * 4 > ws_bytes) break;
+      const int64_t tiles = base * Se;
+      const int64_t per_cu = (tiles + 255) / 256;
+      // MFMA efficiency vs resident waves x 32x32 sub-tiles per wave (probe: gemm_sweep.py)
+      const int conc = (int)std::min<int64_t>(cd.occ, per_cu);
+      const double eta = std::min(0.85, 0.35 + 0.2 * conc * (cd.bm / 64) * (cd.bn / 64));
+      const double mfma = (double)per_cu * cd.bm * cd.bn * std::max(kc, BK) / 128.0 / eta;
+      const double fill = (double)((per_cu + cd.occ - 1) / cd.occ) * 4000.0;
+      // reduce launch: ~5 us measured per launch in the step (rocprof) + its slab traffic
+      const double red = Se > 1 ? 2400.0 * (4.5 + (double)M * N * Se * 4 / 3.0e6) : 0.0;
+      const double cost = mfma + fill + red;
+      if (cost < best * 0.97) { best = cost; pl = {cd.bm, cd.bn, Se, Se > 1 ? kc : K}; }
+    }
+  }
+  if (t_force_bm > 0) {
+    if ((c_div && c_div % t_force_bm != 0) || (n_div && n_div % t_force_bn != 0)) return pl;
+    int bs = can_split ? t_force_s : 1;
+    const int kc = (ceil_div(K, bs) + BK - 1) / BK * BK;
+    bs = ceil_div(K, kc);
+    if (bs > 1 && (int64_t)bs * M * N * 4 > ws_bytes) return LdsPlan{0, 0, 1, K};
+    pl = {t_force_bm, t_force_bn, bs, bs > 1 ? kc : K};
+  }
+  return pl;
+}
+
+template <int BM, int BN, int GRP>
+static hipError_t launch_lds_grp(int am, int bm, dim3 grid, hipStream_t s, const GemmP& p) {
+  if constexpr (GRP == 0) return launch_lds_tiles<BM, BN>(am, bm, grid, s, p);
+  if constexpr (GRP == 1)
+    hipLaunchKernelGGL((gemm_lds_kernel<BM, BN, A_IM2COL, B_N, 1>), grid, dim3(256), 0, s, p);
+  if constexpr (GRP == 2)
+    hipLaunchKernelGGL((gemm_lds_kernel<BM, BN, A_IM2COL, B_FLIP, 2>), grid, dim3(256), 0, s, p);
+  if constexpr (GRP == 3)
+    hipLaunchKernelGGL((gemm_lds_kernel<BM, BN, A_IM2COLT, B_N, 3>), grid, dim3(256), 0, s, p);
+  return hipGetLastError();
+}
+
+template <int GRP>
+static int launch_lds_plan(const LdsPlan& pl, int am, int bm, int nb, GemmP& p, hipStream_t s,
+                           const char* what) {
+  if (pl.bm == 0) {   // only a forced plan (sat_gemm_force_plan) can be infeasible
+    set_error("%s: forced plan does not fit the split-K scratch", what);
+    return SAT_ERR_ARGUMENT;
+  }
+  const int gx = ceil_div(p.N, pl.bn), gy = ceil_div(p.M, pl.bm);
+  p.splits = pl.splits;
+  p.kchunk = pl.kchunk;
+  p.remap = (GRP == 0 && gx * gy >= 16) ? 1 : 0;
+  const dim3 grid(gx, gy, pl.splits > 1 ? pl.splits : nb);
+  hipError_t e;
+  if (pl.bm == 128 && pl.bn == 128) e = launch_lds_grp<128, 128, GRP>(am, bm, grid, s, p);
+  else if (pl.bm == 128) e = launch_lds_grp<128, 64, GRP>(am, bm, grid, s, p);
+  else if (pl.bn == 128) e = launch_lds_grp<64, 128, GRP>(am, bm, grid, s, p);
+  else e = launch_lds_grp<64, 64, GRP>(am, bm, grid, s, p);
+  if (e != hipSuccess) {
+    set_error("%s: launch failed: %s", what, hipGetErrorString(e));
+    return SAT_ERR_HIP;
+  }
+  if (pl.splits > 1) {
+    launch_splitk_reduce(p, s);
+    SAT_LAUNCH_CHECK("split-k reduce");
+  }
+  return SAT_OK;
+}
+
 // Plan + launch on the LDS-DMA kernel.  Returns 1 (nothing launched) when an operand is not
-// vector-loadable.  The tile shape and split-K factor minimise a cycle model of the launch:
-// MFMA cycles per CU (tiles spread over 256 CUs, BM*BN*kchunk/128 cycles per tile) + an
-// unhidden pipeline fill/drain per residency round (occupancy set by the 3-stage LDS ring) +
-// the split-K reduce (launch + slab traffic).
+// vector-loadable.
 static int launch_lds(const SatGemmDesc* d, GemmP& p, int nb, hipStream_t s) {
   const bool astr = (p.a_sbatch % 4 == 0) && (p.a_sbatch2 % 4 == 0) && aligned16(d->A);
   const bool bstr = (p.b_sbatch % 4 == 0) && (p.b_sbatch2 % 4 == 0) && aligned16(d->B);
@@ -937,63 +1074,10 @@ static int launch_lds(const SatGemmDesc* d, GemmP& p, int nb, hipStream_t s) {
   if ((am == A_IM2COL && bm != B_N && bm != B_FLIP) || (am == A_IM2COLT && bm != B_N) ||
       (bm == B_FLIP && am != A_IM2COL))
     return 1;
-  struct Cand { int bm, bn, occ; };
-  // (ties go to the first: two 128x64 workgroups per CU overlap each other's epilogue)
-  static const Cand cands[4] = {{128, 64, 2}, {64, 128, 2}, {128, 128, 1}, {64, 64, 3}};
-  const bool can_split = nb == 1 && d->ws != nullptr && d->K >= 512;
-  double best = 1e30;
-  int bc = 3, bs = 1, bkc = d->K;
-  for (int c = 0; c < 4; ++c) {
-    const Cand& cd = cands[c];
-    if (am == A_IM2COLT && d->a_C % cd.bm != 0) continue;
-    const int gx = ceil_div(d->N, cd.bn), gy = ceil_div(d->M, cd.bm);
-    const int64_t base = (int64_t)gx * gy * nb;
-    const int smax = can_split ? std::min(64, std::max(1, d->K / 256)) : 1;
-    for (int S = 1; S <= smax; S = (S < 4 ? S + 1 : S * 2)) {
-      const int kc = (ceil_div(d->K, S) + BK - 1) / BK * BK;
-      const int Se = ceil_div(d->K, kc);
-      if (Se > 1 && (int64_t)Se * d->M * d->N * 4 > d->ws_bytes) break;
-      const int64_t tiles = base * Se;
-      const int64_t per_cu = (tiles + 255) / 256;
-      // MFMA efficiency vs resident waves x 32x32 sub-tiles per wave (probe: gemm_sweep.py)
-      const int conc = (int)std::min<int64_t>(cd.occ, per_cu);
-      const double eta = std::min(0.85, 0.35 + 0.2 * conc * (cd.bm / 64) * (cd.bn / 64));
-      const double mfma = (double)per_cu * cd.bm * cd.bn * std::max(kc, BK) / 128.0 / eta;
-      const double fill = (double)((per_cu + cd.occ - 1) / cd.occ) * 4000.0;
-      const double red = Se > 1 ? 2400.0 * (2.0 + (double)d->M * d->N * Se * 4 / 3.0e6) : 0.0;
-      const double cost = mfma + fill + red;
-      if (cost < best * 0.97) { best = cost; bc = c; bs = Se; bkc = kc; }
-    }
-  }
-  if (t_force_bm > 0) {
-    for (int c = 0; c < 4; ++c)
-      if (cands[c].bm == t_force_bm && cands[c].bn == t_force_bn) bc = c;
-    if (am == A_IM2COLT && d->a_C % cands[bc].bm != 0) return 1;
-    bs = can_split ? t_force_s : 1;
-    bkc = (ceil_div(d->K, bs) + BK - 1) / BK * BK;
-    bs = ceil_div(d->K, bkc);
-    if (bs > 1 && (int64_t)bs * d->M * d->N * 4 > d->ws_bytes) return 1;
-  }
-  const Cand& cd = cands[bc];
-  const int gx = ceil_div(d->N, cd.bn), gy = ceil_div(d->M, cd.bm);
-  p.splits = bs;
-  p.kchunk = bs > 1 ? bkc : d->K;
-  p.remap = (gx * gy >= 16) ? 1 : 0;
-  const dim3 grid(gx, gy, bs > 1 ? bs : nb);
-  hipError_t e;
-  if (cd.bm == 128 && cd.bn == 128) e = launch_lds_tiles<128, 128>(am, bm, grid, s, p);
-  else if (cd.bm == 128) e = launch_lds_tiles<128, 64>(am, bm, grid, s, p);
-  else if (cd.bn == 128) e = launch_lds_tiles<64, 128>(am, bm, grid, s, p);
-  else e = launch_lds_tiles<64, 64>(am, bm, grid, s, p);
-  if (e != hipSuccess) {
-    set_error("sat_gemm: launch failed: %s", hipGetErrorString(e));
-    return SAT_ERR_HIP;
-  }
-  if (bs > 1) {
-    launch_splitk_reduce(d, p, s);
-    SAT_LAUNCH_CHECK("sat_gemm(split-k reduce)");
-  }
-  return SAT_OK;
+  const LdsPlan pl = plan_lds(d->M, d->N, d->K, nb, nb == 1 && d->ws != nullptr,
+                              d->ws_bytes, am == A_IM2COLT ? d->a_C : 0, 0);
+  if (pl.bm == 0) return 1;
+  return launch_lds_plan<0>(pl, am, bm, nb, p, s, "sat_gemm");
 }
 
 extern "C" int sat_gemm(const SatGemmDesc* d, void* stream) {
@@ -1091,6 +1175,92 @@ extern "C" int sat_gemm(const SatGemmDesc* d, void* stream) {
     const int blocks = (int)std::min<int64_t>((work + 255) / 256, 2048);
     hipLaunchKernelGGL(gemm_splitk_reduce, dim3(blocks), dim3(256), 0, s, p);
     SAT_LAUNCH_CHECK("sat_gemm(split-k reduce)");
+  }
+  return SAT_OK;
+}
+
+// ---------------------------------------------------------------- CBHG conv bank (one launch
+// per direction instead of max_k; see include/sat_abi.h)
+static int convbank_check(const SatConvBank* d) {
+  SAT_CHECK_ARG(d != nullptr, "sat_cbhg_convbank: null descriptor");
+  SAT_CHECK_ARG(d->S > 0 && d->L > 0 && d->max_k >= 1 && d->max_k <= 64,
+                "sat_cbhg_convbank: bad sizes");
+  SAT_CHECK_ARG(d->C > 0 && d->C % 64 == 0 && d->Co > 0 && d->Co % 64 == 0,
+                "sat_cbhg_convbank: C and Co must be multiples of 64");
+  SAT_CHECK_ARG(d->x && d->W && d->y && aligned16(d->x) && aligned16(d->W) && aligned16(d->y) &&
+                    d->x_sm % 4 == 0 && d->y_sm % 4 == 0 && d->x_sm >= d->C &&
+                    d->y_sm >= (int64_t)d->max_k * d->Co,
+                "sat_cbhg_convbank: operands must be 16-byte aligned rows");
+  return SAT_OK;
+}
+
+static GemmP convbank_base(const SatConvBank* d) {
+  GemmP p;
+  std::memset(&p, 0, sizeof(p));
+  p.batch2 = 1;
+  p.alpha = 1.f;
+  p.a_L = d->L;
+  p.grp_co = d->Co;
+  p.ws = reinterpret_cast<float*>(d->ws);
+  p.probe = t_probe;
+  return p;
+}
+
+extern "C" int sat_cbhg_convbank_fwd(const SatConvBank* d, void* stream) {
+  const int r = convbank_check(d);
+  if (r != SAT_OK) return r;
+  GemmP p = convbank_base(d);
+  p.M = d->S * d->L;
+  p.N = d->max_k * d->Co;
+  p.K = d->max_k * d->C;                    // longest reduction (K_max); per tile (k) * C
+  p.a_mode = 1; p.a_C = d->C;
+  p.A = d->x; p.a_sm = d->x_sm; p.a_sk = 1;
+  p.B = d->W; p.b_sk = d->Co; p.b_sn = 1;
+  p.C = d->y; p.c_sm = d->y_sm;
+  p.bias = d->bias;
+  // plan on the mean reduction; no split (3,200 tiles at the C2 shape already fill the chip)
+  LdsPlan pl = plan_lds(p.M, p.N, (d->max_k + 1) * d->C / 2, 1, false, 0, 0, d->Co);
+  // measured at the C2 shape (tools/probes/conv_sol.py): 64x128 352 us, 64x64 384, 128x* 405
+  if (t_force_bm == 0 && d->Co % 128 == 0) pl = {64, 128, 1, p.K};
+  LdsPlan fixed = pl;
+  fixed.splits = 1;
+  fixed.kchunk = p.K;
+  return launch_lds_plan<1>(fixed, A_IM2COL, B_N, 1, p, as_stream(stream),
+                            "sat_cbhg_convbank_fwd");
+}
+
+extern "C" int sat_cbhg_convbank_bwd(const SatConvBank* d, void* stream) {
+  const int r = convbank_check(d);
+  if (r != SAT_OK) return r;
+  hipStream_t s = as_stream(stream);
+  const int pairs = d->max_k * (d->max_k + 1) / 2;     // (k, tap) pairs of the bank
+  if (d->dW) {
+    SAT_CHECK_ARG(aligned16(d->dW), "sat_cbhg_convbank_bwd: dW must be 16-byte aligned");
+    GemmP p = convbank_base(d);
+    p.M = pairs * d->C; p.N = d->Co; p.K = d->S * d->L;
+    p.a_mode = 2; p.a_C = d->C;
+    p.A = d->x; p.a_sm = d->x_sm; p.a_sk = 1;
+    p.B = d->y; p.b_sk = d->y_sm; p.b_sn = 1;
+    p.C = d->dW; p.c_sm = d->Co;
+    p.beta = d->beta_dw;
+    const LdsPlan pl = plan_lds(p.M, p.N, p.K, 1, d->ws != nullptr, d->ws_bytes, d->C, 0);
+    const int e = launch_lds_plan<3>(pl, A_IM2COLT, B_N, 1, p, s, "sat_cbhg_convbank_bwd(dW)");
+    if (e != SAT_OK) return e;
+  }
+  if (d->dx) {
+    SAT_CHECK_ARG(aligned16(d->dx) && d->dx_sm % 4 == 0 && d->dx_sm >= d->C,
+                  "sat_cbhg_convbank_bwd: dx must be 16-byte aligned rows");
+    GemmP p = convbank_base(d);
+    p.M = d->S * d->L; p.N = d->C; p.K = pairs * d->Co;
+    p.a_mode = 1; p.a_C = d->Co;
+    p.A = d->y; p.a_sm = d->y_sm; p.a_sk = 1;
+    p.b_mode = 1; p.b_C = d->Co; p.b_taps = d->max_k;
+    p.B = d->W;
+    p.C = d->dx; p.c_sm = d->dx_sm;
+    p.beta = d->beta_dx;
+    const LdsPlan pl = plan_lds(p.M, p.N, p.K, 1, d->ws != nullptr, d->ws_bytes, 0, 0);
+    const int e = launch_lds_plan<2>(pl, A_IM2COL, B_FLIP, 1, p, s, "sat_cbhg_convbank_bwd(dX)");
+    if (e != SAT_OK) return e;
   }
   return SAT_OK;
 }

@@ -210,6 +210,44 @@ def conv1d_dw(x: torch.Tensor, dy: torch.Tensor, dW: torch.Tensor, beta=0.0):
     return dW
 
 
+
+def _bank_desc(x, W_bank, max_k, Co, y):
+    S, L, C = x.shape
+    assert x.stride(2) == 1 and x.stride(0) == L * x.stride(1)
+    assert y.stride(-1) == 1 and y.stride(0) == L * y.stride(1) and y.shape[-1] == max_k * Co
+    assert W_bank.is_contiguous() and W_bank.numel() == Co * C * max_k * (max_k + 1) // 2
+    d = _lib.SatConvBank()
+    d.S, d.L, d.C, d.max_k, d.Co = S, L, C, max_k, Co
+    d.x, d.x_sm, d.W = _p(x), x.stride(1), _p(W_bank)
+    d.y, d.y_sm = _p(y), y.stride(1)
+    return d
+
+
+def conv_bank(x: torch.Tensor, W_bank: torch.Tensor, bias, y: torch.Tensor, max_k: int, Co: int):
+    """CBHG conv bank (modules/module.py:77-80): y[:, :, (k-1)Co:kCo] = Conv1D_k(x) + b_k for
+    k = 1..max_k in ONE launch.  W_bank = K1..Kmax kernels back to back ([k][C][Co] each)."""
+    d = _bank_desc(x, W_bank, max_k, Co, y)
+    d.bias = _p(bias)
+    _lib.check(_lib.load().sat_cbhg_convbank_fwd(ctypes.byref(d), _stream()),
+               "sat_cbhg_convbank_fwd")
+    return y
+
+
+def conv_bank_bwd(x, W_bank, dy, max_k: int, Co: int, dx=None, dW=None, beta_dx=0.0,
+                  beta_dw=1.0):
+    """Both gradients of conv_bank: dx (= beta_dx dx + sum_k conv_dx_k) and dW (accumulated with
+    beta_dw), each ONE product over the whole bank (split-K scratch from the stream pool)."""
+    d = _bank_desc(x, W_bank, max_k, Co, dy)
+    if dx is not None:
+        assert dx.stride(-1) == 1 and dx.shape == x.shape
+        d.dx, d.dx_sm, d.beta_dx = _p(dx), dx.stride(1), beta_dx
+    if dW is not None:
+        assert dW.is_contiguous() and dW.numel() == W_bank.numel()
+        d.dW, d.beta_dw = _p(dW), beta_dw
+    _with_ws(d, x.device)
+    _lib.check(_lib.load().sat_cbhg_convbank_bwd(ctypes.byref(d), _stream()),
+               "sat_cbhg_convbank_bwd")
+
 def stop_check(stop: torch.Tensor, t: int, min_iters: int, state: torch.Tensor):
     """state[0] := t if (no earlier finish) and t > min_iters and all sigmoid(stop) > 0.5."""
     _lib.call("sat_stop_check", _p(stop), stop.stride(0), stop.shape[0], t, min_iters,

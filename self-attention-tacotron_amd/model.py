@@ -57,6 +57,12 @@ def _contig_span(P: Dict[str, torch.Tensor], names: List[str]) -> torch.Tensor:
     return first.view(-1).as_strided((n,), (1,))
 
 
+def bank_fused(d, inp: torch.Tensor) -> bool:
+    """The conv bank runs as ONE sat_cbhg_convbank launch per direction when its channel counts
+    suit the LDS kernel (the configs' 128/128); otherwise one sat_gemm conv per kernel width."""
+    return d.conv_ch % 64 == 0 and inp.shape[-1] % 64 == 0
+
+
 def mha_fwd(x: torch.Tensor, P, scope: str, heads: int, causal: bool,
             probs_mask: Optional[torch.Tensor], sv: dict, key: str):
     """MultiHeadAttention (modules/self_attention.py:108-128) over x [B, L, W]."""
@@ -119,11 +125,15 @@ def encoder_fwd(P, bn: BNState, hp, d: PR.Dims, ids, lengths, masks, training, w
     C = d.conv_ch
     KC = d.max_k * C
     bank_pre = torch.empty(B, N, KC, device=dev)
-    for k in range(1, d.max_k + 1):                                   # module.py:78
-        sc = f"encoder/cbhg/conv_bank/K{k}"
-        K.conv1d(inp, P[f"{sc}/kernel"], P[f"{sc}/bias"], out=bank_pre[:, :, (k - 1) * C:k * C])
-    bank = torch.empty_like(bank_pre)
     names = [f"encoder/cbhg/conv_bank/K{k}" for k in range(1, d.max_k + 1)]
+    if bank_fused(d, inp):                                            # module.py:78
+        K.conv_bank(inp, _contig_span(P, [f"{n}/kernel" for n in names]),
+                    _contig_span(P, [f"{n}/bias" for n in names]), bank_pre, d.max_k, C)
+    else:
+        for k in range(1, d.max_k + 1):
+            sc = names[k - 1]
+            K.conv1d(inp, P[f"{sc}/kernel"], P[f"{sc}/bias"], out=bank_pre[:, :, (k - 1) * C:k * C])
+    bank = torch.empty_like(bank_pre)
     gam = _contig_span(P, [f"{n}/bn/gamma" for n in names])
     bet = _contig_span(P, [f"{n}/bn/beta" for n in names])
     st_bank = _bn(bank_pre.view(-1, KC), bank.view(-1, KC), gam, bet, bn, f"{names[0]}/bn", KC, True,

@@ -122,3 +122,34 @@ def test_conv1d_lds_fwd_dx_dw(cuda, taps, Ci, Co, L):
     dWd = torch.empty_like(Wd)
     kernels.conv1d_dw(xd, dy.float().to(cuda), dWd)
     assert _rel(dWd, W.grad) < 2e-6
+
+
+@pytest.mark.parametrize("max_k,C,Co,S,L", [(16, 128, 128, 3, 37), (4, 64, 128, 2, 70),
+                                            (5, 128, 64, 4, 9), (16, 128, 128, 32, 200)])
+def test_conv_bank_matches_per_conv_oracle(cuda, max_k, C, Co, S, L):
+    """sat_cbhg_convbank_fwd/bwd (one launch per direction) vs the float64 oracle Conv1D of each
+    kernel width (ext tacotron2 Conv1d, modules/module.py:77-80)."""
+    from sat_amd import kernels
+    g = torch.Generator().manual_seed(max_k * 7 + L)
+    x = torch.randn(S, L, C, generator=g, dtype=torch.float64, requires_grad=True)
+    Ws = [torch.randn(k, C, Co, generator=g, dtype=torch.float64, requires_grad=True) * 0.1
+          for k in range(1, max_k + 1)]
+    Ws = [w.detach().requires_grad_(True) for w in Ws]
+    b = torch.randn(max_k * Co, generator=g, dtype=torch.float64)
+    y = torch.cat([_conv_ref(x, Ws[k], b[k * Co:(k + 1) * Co]) for k in range(max_k)], dim=-1)
+    dy = torch.randn(S, L, max_k * Co, generator=g, dtype=torch.float64)
+    y.backward(dy)
+    Wb = torch.cat([w.detach().reshape(-1) for w in Ws]).float().to(cuda)
+    xd = x.detach().float().to(cuda)
+    yd = torch.empty(S, L, max_k * Co, device=cuda)
+    kernels.conv_bank(xd, Wb, b.float().to(cuda), yd, max_k, Co)
+    assert _rel(yd, y.detach()) < 2e-6
+    dx0 = torch.randn(S, L, C, generator=g)
+    dxd = dx0.to(cuda)
+    dW0 = torch.randn(Wb.numel(), generator=g)
+    dWd = dW0.to(cuda)
+    kernels.conv_bank_bwd(xd, Wb, dy.float().to(cuda), max_k, Co, dx=dxd, dW=dWd,
+                          beta_dx=1.0, beta_dw=1.0)
+    assert _rel(dxd, x.grad + dx0.double()) < 2e-6
+    dW_ref = torch.cat([w.grad.reshape(-1) for w in Ws]) + dW0.double()
+    assert _rel(dWd, dW_ref) < 2e-6

@@ -85,6 +85,56 @@ typedef struct SatGemmDesc {
 } SatGemmDesc;
 
 int sat_gemm(const SatGemmDesc* desc, void* stream);
+/* ---------------------------------------------------------------- multi-head self-attention
+ * MultiHeadAttention.call (modules/self_attention.py:108-128) with the
+ * ScaledDotProductAttentionMechanism (:45-65): Q/K/V = x W + b ([B][L][W] -> [B][L][D]), per
+ * (utterance, head) P = softmax(Q_h K_h^T / sqrt(D/H)) [causal: use_subsequent_mask],
+ * Pd = P * probs_mask (dropout on the probabilities; NULL = none, then Pd may be NULL),
+ * o = concat_h(Pd V_h), y = o Wo + bo ([B][L][out_dim]).  Used by the encoder's
+ * SelfAttentionTransformer (module.py:363-371, 425-438) and the decoder head (:743-765).
+ * fwd writes q, k, v, P, Pd, o (kept for the backward) and y.
+ * bwd reads those plus dy, writes dx and ACCUMULATES dWq..dbo (bias gradients may be NULL).
+ * scratch: sat_mha_scratch_bytes(B, L, D, H, out_dim) bytes of device memory (both
+ * directions); gemm_ws: split-K scratch for the projections' weight gradients (may be NULL). */
+typedef struct SatMha {
+  int32_t B, L, W, D, H, causal;
+  int32_t out_dim, pad0;
+  const float* x;
+  const float* Wq;
+  const float* bq;
+  const float* Wk;
+  const float* bk;
+  const float* Wv;
+  const float* bv;
+  const float* Wo;
+  const float* bo;
+  const float* probs_mask;
+  float* q;
+  float* k;
+  float* v;
+  float* P;
+  float* Pd;
+  float* o;
+  float* y;
+  const float* dy;
+  float* dx;
+  float* dWq;
+  float* dbq;
+  float* dWk;
+  float* dbk;
+  float* dWv;
+  float* dbv;
+  float* dWo;
+  float* dbo;
+  void* scratch;
+  int64_t scratch_bytes;
+  void* gemm_ws;
+  int64_t gemm_ws_bytes;
+} SatMha;
+int64_t sat_mha_scratch_bytes(int32_t B, int32_t L, int32_t D, int32_t H, int32_t out_dim);
+int sat_mha_fwd(const SatMha* d, void* stream);
+int sat_mha_bwd(const SatMha* d, void* stream);
+
 /* ---------------------------------------------------------------- CBHG conv bank
  * The K1..Kmax Conv1D(SAME) bank of ZoneoutCBHG (modules/module.py:77-80 over ext tacotron2
  * Conv1d, module.py:46-52): max_k convolutions of one input, outputs concatenated on channels.

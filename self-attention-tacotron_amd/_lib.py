@@ -70,6 +70,12 @@ SatConvBank = _struct("SatConvBank", """
     i32:S i32:L i32:C i32:max_k i32:Co i32:pad0 ptr:x i64:x_sm ptr:W ptr:bias ptr:y i64:y_sm
     ptr:dx i64:dx_sm ptr:dW f32:beta_dx f32:beta_dw ptr:ws i64:ws_bytes""")
 
+SatMha = _struct("SatMha", """
+    i32:B i32:L i32:W i32:D i32:H i32:causal i32:out_dim i32:pad0 ptr:x ptr:Wq ptr:bq ptr:Wk
+    ptr:bk ptr:Wv ptr:bv ptr:Wo ptr:bo ptr:probs_mask ptr:q ptr:k ptr:v ptr:P ptr:Pd ptr:o ptr:y
+    ptr:dy ptr:dx ptr:dWq ptr:dbq ptr:dWk ptr:dbk ptr:dWv ptr:dbv ptr:dWo ptr:dbo ptr:scratch
+    i64:scratch_bytes ptr:gemm_ws i64:gemm_ws_bytes""")
+
 SatAdamConfig = _struct("SatAdamConfig", """
     f32:lr0 f32:beta1 f32:beta2 f32:eps f32:clip_norm i32:decay i32:step_factor f32:grad_scale""")
 
@@ -132,6 +138,8 @@ SIGNATURES = {
     "sat_gemm_force_plan": [_I32, _I32, _I32],
     "sat_gemm_probe_mode": [_I32],
     "sat_cbhg_convbank_fwd": [ctypes.POINTER(SatConvBank), _P],
+    "sat_mha_fwd": [ctypes.POINTER(SatMha), _P],
+    "sat_mha_bwd": [ctypes.POINTER(SatMha), _P],
     "sat_cbhg_convbank_bwd": [ctypes.POINTER(SatConvBank), _P],
     "sat_rng_fill": [_P, _I64, _P, _U64, _F, _F, _P],
     "sat_counter_add": [_P, _U64, _P],
@@ -183,6 +191,7 @@ SIGNATURES.update({
 RESTYPES = {"sat_workspace_colreduce": (ctypes.c_int64, [_I32, _I32]),
             "sat_workspace_adam": (ctypes.c_int64, []),
             "sat_workspace_loss": (ctypes.c_int64, []),
+            "sat_mha_scratch_bytes": (ctypes.c_int64, [_I32, _I32, _I32, _I32, _I32]),
             "sat_decoder_attention_scratch": (ctypes.c_int64, [_I32, _I32, _P, _P, _P]),
             "sat_decoder_attention_bwd_scratch": (ctypes.c_int64, [_I32, _I32, _P, _P]),
             "sat_decoder_attention_bwd_dq_parts": (ctypes.c_int32, [_I32, _I32]),

@@ -37,32 +37,15 @@ def lin_bwd(x, dy, W, dW, db, ws, dx=None, beta_dx=0.0, need_dx=True):
 
 
 def mha_bwd(P, G, scope, s, dy, ws):
-    """Backward of model.mha_fwd.  Returns dx [B, L, W]."""
-    x, q, k, v, o = s["x"], s["q"], s["k"], s["v"], s["o"]
-    B, L, W = x.shape
-    H, dh = s["heads"], s["dh"]
-    model = q.shape[-1]
-
-    def hv(t):
-        return t.view(B, L, H, dh).permute(0, 2, 1, 3)
-
-    do = lin_bwd(o, dy, P[f"{scope}/output_projection/kernel"],
-                 G[f"{scope}/output_projection/kernel"], G[f"{scope}/output_projection/bias"], ws)
-    dPd = K.gemm(hv(do), hv(v).transpose(-1, -2))                   # [B, H, L, L]
-    dv = torch.empty(B, L, model, device=x.device)
-    K.gemm(s["Pd"].transpose(-1, -2), hv(do), hv(dv))
-    dS = torch.empty_like(dPd)
-    K.softmax_bwd(s["P"], dPd, dS, mask=s["mask"], scale=1.0 / math.sqrt(dh))
-    dq = torch.empty(B, L, model, device=x.device)
-    K.gemm(dS, hv(k), hv(dq))
-    dk = torch.empty(B, L, model, device=x.device)
-    K.gemm(dS.transpose(-1, -2), hv(q), hv(dk))
-    dx = lin_bwd(x, dq, P[f"{scope}/query_projection/kernel"], G[f"{scope}/query_projection/kernel"],
-                 G[f"{scope}/query_projection/bias"], ws)
-    lin_bwd(x, dk, P[f"{scope}/key_projection/kernel"], G[f"{scope}/key_projection/kernel"],
-            G[f"{scope}/key_projection/bias"], ws, dx=dx, beta_dx=1.0)
-    lin_bwd(x, dv, P[f"{scope}/value_projection/kernel"], G[f"{scope}/value_projection/kernel"],
-            G[f"{scope}/value_projection/bias"], ws, dx=dx, beta_dx=1.0)
+    """Backward of model.mha_fwd: ONE sat_mha_bwd call.  Returns dx [B, L, W]."""
+    names = [f"{scope}/{n}_projection/{t}" for n in ("query", "key", "value", "output")
+             for t in ("kernel", "bias")]
+    d, _scratch = K.mha_desc(s["x"], *(P[n] for n in names), s["heads"], s["causal"], s["mask"], s)
+    dx = torch.empty_like(s["x"])
+    dyc = dy.contiguous()
+    d.dy, d.dx = dyc.data_ptr(), dx.data_ptr()
+    d.dWq, d.dbq, d.dWk, d.dbk, d.dWv, d.dbv, d.dWo, d.dbo = (G[n].data_ptr() for n in names)
+    K.mha_bwd(d)
     return dx
 
 

@@ -1,0 +1,186 @@
+// MultiHeadAttention of the self-attention blocks (modules/self_attention.py:108-128, with the
+// ScaledDotProductAttentionMechanism of :45-65) as two C-ABI entries, sat_mha_fwd / sat_mha_bwd.
+//
+// Both are host-side schedules over the library's own kernels -- no new device code: the four
+// projections and the per-(utterance, head) score / context products are sat_gemm launches
+// (fp32 MFMA, heads addressed through the descriptor's two batch strides, so no head
+// split/merge copies), the masked softmax and its gradient are sat_softmax_fwd/bwd, the bias
+// gradients sat_colsum.  Launch-for-launch the same work the Python composition
+// (model.mha_fwd / backward.mha_bwd) issued, reachable from C.
+#include "sat_common.h"
+
+namespace sat {
+namespace {
+
+constexpr int64_t kAlign = 256;
+inline int64_t align_up(int64_t n) { return (n + kAlign - 1) / kAlign * kAlign; }
+
+SatGemmDesc dense_desc() {
+  SatGemmDesc g;
+  std::memset(&g, 0, sizeof(g));
+  g.batch = 1;
+  g.batch2 = 1;
+  g.alpha = 1.f;
+  return g;
+}
+
+// C[R][N] (=| +=) X[R][K] @ W[K][N] + bias    (tf.layers.Dense over the last dim)
+int dense(const float* X, const float* W, const float* bias, float* C, int R, int K, int N,
+          float beta, const SatMha* d, hipStream_t s) {
+  SatGemmDesc g = dense_desc();
+  g.M = R; g.N = N; g.K = K;
+  g.A = X; g.a_sm = K; g.a_sk = 1;
+  g.B = W; g.b_sk = N; g.b_sn = 1;
+  g.C = C; g.c_sm = N;
+  g.bias = bias;
+  g.beta = beta;
+  g.ws = d->gemm_ws; g.ws_bytes = d->gemm_ws_bytes;
+  return sat_gemm(&g, s);
+}
+
+// per (utterance b, head h) product on [B][L][D] activations viewed as [B][H][L][dh]:
+// op(A)[L x K] @ op(B)[K x N]; strides given per operand as (row, col) inside one head block
+struct HeadOp {
+  const float* p;
+  int64_t sr, sc;          // row / column stride inside one (b, h) block
+  int64_t sb, sh;          // batch (utterance) and head strides
+};
+
+int head_gemm(int M, int N, int K, HeadOp a, HeadOp b, float* C, int64_t c_sm, int64_t c_sb,
+              int64_t c_sh, float alpha, const SatMha* d, hipStream_t s) {
+  SatGemmDesc g = dense_desc();
+  g.M = M; g.N = N; g.K = K;
+  g.batch = d->B; g.batch2 = d->H;
+  g.A = a.p; g.a_sm = a.sr; g.a_sk = a.sc; g.a_sbatch = a.sb; g.a_sbatch2 = a.sh;
+  g.B = b.p; g.b_sk = b.sr; g.b_sn = b.sc; g.b_sbatch = b.sb; g.b_sbatch2 = b.sh;
+  g.C = C; g.c_sm = c_sm; g.c_sbatch = c_sb; g.c_sbatch2 = c_sh;
+  g.alpha = alpha;
+  return sat_gemm(&g, s);
+}
+
+int check(const SatMha* d, bool bwd) {
+  SAT_CHECK_ARG(d != nullptr, "sat_mha: null descriptor");
+  SAT_CHECK_ARG(d->B > 0 && d->L > 0 && d->W > 0 && d->D > 0 && d->H > 0 && d->D % d->H == 0 &&
+                    d->out_dim > 0,
+                "sat_mha: bad sizes (D must be a multiple of H)");
+  SAT_CHECK_ARG(d->x && d->Wq && d->Wk && d->Wv && d->Wo && d->q && d->k && d->v && d->P &&
+                    d->o,
+                "sat_mha: null tensor");
+  SAT_CHECK_ARG(!d->probs_mask || d->Pd, "sat_mha: a probability mask needs Pd");
+  if (bwd) {
+    SAT_CHECK_ARG(d->dy && d->dx && d->dWq && d->dWk && d->dWv && d->dWo,
+                  "sat_mha_bwd: null gradient tensor");
+    SAT_CHECK_ARG(d->scratch && d->scratch_bytes >= sat_mha_scratch_bytes(d->B, d->L, d->D, d->H,
+                                                                          d->out_dim),
+                  "sat_mha_bwd: scratch smaller than sat_mha_scratch_bytes()");
+  } else {
+    SAT_CHECK_ARG(d->y && d->scratch &&
+                      d->scratch_bytes >= sat_mha_scratch_bytes(d->B, d->L, d->D, d->H, d->out_dim),
+                  "sat_mha_fwd: needs y and scratch of sat_mha_scratch_bytes()");
+  }
+  return SAT_OK;
+}
+
+#define SAT_TRY(expr)            \
+  do {                           \
+    const int rc_ = (expr);      \
+    if (rc_ != SAT_OK) return rc_; \
+  } while (0)
+
+}  // namespace
+}  // namespace sat
+
+using namespace sat;
+
+extern "C" int64_t sat_mha_scratch_bytes(int32_t B, int32_t L, int32_t D, int32_t H,
+                                         int32_t out_dim) {
+  const int64_t act = (int64_t)B * L * D * 4, score = (int64_t)B * H * L * L * 4;
+  const int64_t cs = sat_workspace_colreduce(B * L, std::max(D, out_dim));
+  // backward: dO, dQ, dK, dV [B L D], dPd, dS [B H L L], column-sum scratch; the forward uses
+  // the first score slab for the raw scores
+  return 4 * align_up(act) + 2 * align_up(score) + align_up(cs);
+}
+
+// y = Wo . concat_h(softmax(Q_h K_h^T / sqrt(dh)) [* mask] V_h) + bo,  Q/K/V = x W + b
+extern "C" int sat_mha_fwd(const SatMha* d, void* stream) {
+  SAT_TRY(check(d, false));
+  hipStream_t s = as_stream(stream);
+  const int B = d->B, L = d->L, D = d->D, H = d->H, dh = D / H, R = B * L;
+  const int64_t LD = (int64_t)L * D, LL = (int64_t)L * L, HLL = H * LL;
+  char* sc = static_cast<char*>(d->scratch) + 4 * align_up((int64_t)B * L * D * 4);
+  float* S = reinterpret_cast<float*>(sc);
+  SAT_TRY(dense(d->x, d->Wq, d->bq, d->q, R, d->W, D, 0.f, d, s));
+  SAT_TRY(dense(d->x, d->Wk, d->bk, d->k, R, d->W, D, 0.f, d, s));
+  SAT_TRY(dense(d->x, d->Wv, d->bv, d->v, R, d->W, D, 0.f, d, s));
+  // S[b,h] = Q_h K_h^T                                               (self_attention.py:55)
+  SAT_TRY(head_gemm(L, L, dh, {d->q, D, 1, LD, dh}, {d->k, 1, D, LD, dh}, S, L, HLL, LL, 1.f, d,
+                    s));
+  float* Pd = d->probs_mask ? d->Pd : d->P;
+  SAT_TRY(sat_softmax_fwd(S, d->P, d->probs_mask ? d->Pd : nullptr, d->probs_mask,
+                          (int64_t)B * H * L, L, L, d->causal, 1.f / std::sqrt((float)dh), s));
+  // O[b, :, h] = Pd[b,h] V_h  (heads written in place of the [B][L][D] concat)
+  SAT_TRY(head_gemm(L, dh, L, {Pd, L, 1, HLL, LL}, {d->v, D, 1, LD, dh}, d->o, D, LD, dh, 1.f, d,
+                    s));
+  SAT_TRY(dense(d->o, d->Wo, d->bo, d->y, R, D, d->out_dim, 0.f, d, s));
+  return SAT_OK;
+}
+
+// Gradients of sat_mha_fwd: parameter gradients ACCUMULATE (+=), dx is written.
+extern "C" int sat_mha_bwd(const SatMha* d, void* stream) {
+  SAT_TRY(check(d, true));
+  hipStream_t s = as_stream(stream);
+  const int B = d->B, L = d->L, D = d->D, H = d->H, dh = D / H, R = B * L, Wi = d->W;
+  const int64_t LD = (int64_t)L * D, LL = (int64_t)L * L, HLL = H * LL;
+  char* p = static_cast<char*>(d->scratch);
+  const int64_t act = align_up((int64_t)B * L * D * 4), score = align_up(HLL * B * 4);
+  float* dO = reinterpret_cast<float*>(p);
+  float* dQ = reinterpret_cast<float*>(p + act);
+  float* dK = reinterpret_cast<float*>(p + 2 * act);
+  float* dV = reinterpret_cast<float*>(p + 3 * act);
+  float* dPd = reinterpret_cast<float*>(p + 4 * act);
+  float* dS = reinterpret_cast<float*>(p + 4 * act + score);
+  void* cs = p + 4 * act + 2 * score;
+  const float* Pd = d->probs_mask ? d->Pd : d->P;
+  auto wgrad = [&](const float* X, int K, const float* dY, int N, float* dW, float* db) -> int {
+    SatGemmDesc g = dense_desc();   // dW += X^T dY
+    g.M = K; g.N = N; g.K = R;
+    g.A = X; g.a_sm = 1; g.a_sk = K;
+    g.B = dY; g.b_sk = N; g.b_sn = 1;
+    g.C = dW; g.c_sm = N; g.beta = 1.f;
+    g.ws = d->gemm_ws; g.ws_bytes = d->gemm_ws_bytes;
+    SAT_TRY(sat_gemm(&g, s));
+    if (db) SAT_TRY(sat_colsum(dY, N, R, N, db, 1.f, cs, s));
+    return SAT_OK;
+  };
+  auto dgrad = [&](const float* dY, int N, const float* W, int K, float* dX, float beta) {
+    SatGemmDesc g = dense_desc();   // dX (=|+=) dY W^T
+    g.M = R; g.N = K; g.K = N;
+    g.A = dY; g.a_sm = N; g.a_sk = 1;
+    g.B = W; g.b_sk = 1; g.b_sn = N;
+    g.C = dX; g.c_sm = K; g.beta = beta;
+    g.ws = d->gemm_ws; g.ws_bytes = d->gemm_ws_bytes;
+    return sat_gemm(&g, s);
+  };
+  // output projection
+  SAT_TRY(wgrad(d->o, D, d->dy, d->out_dim, d->dWo, d->dbo));
+  SAT_TRY(dgrad(d->dy, d->out_dim, d->Wo, D, dO, 0.f));
+  // dPd = dO_h V_h^T ;  dV_h = Pd^T dO_h
+  SAT_TRY(head_gemm(L, L, dh, {dO, D, 1, LD, dh}, {d->v, 1, D, LD, dh}, dPd, L, HLL, LL, 1.f, d,
+                    s));
+  SAT_TRY(head_gemm(L, dh, L, {Pd, 1, L, HLL, LL}, {dO, D, 1, LD, dh}, dV, D, LD, dh, 1.f, d, s));
+  SAT_TRY(sat_softmax_bwd(d->P, dPd, d->probs_mask, dS, (int64_t)B * H * L, L,
+                          1.f / std::sqrt((float)dh), s));
+  // dQ_h = dS K_h ;  dK_h = dS^T Q_h
+  SAT_TRY(head_gemm(L, dh, L, {dS, L, 1, HLL, LL}, {d->k, D, 1, LD, dh}, dQ, D, LD, dh, 1.f, d,
+                    s));
+  SAT_TRY(head_gemm(L, dh, L, {dS, 1, L, HLL, LL}, {d->q, D, 1, LD, dh}, dK, D, LD, dh, 1.f, d,
+                    s));
+  // input projections
+  SAT_TRY(wgrad(d->x, Wi, dQ, D, d->dWq, d->dbq));
+  SAT_TRY(dgrad(dQ, D, d->Wq, Wi, d->dx, 0.f));
+  SAT_TRY(wgrad(d->x, Wi, dK, D, d->dWk, d->dbk));
+  SAT_TRY(dgrad(dK, D, d->Wk, Wi, d->dx, 1.f));
+  SAT_TRY(wgrad(d->x, Wi, dV, D, d->dWv, d->dbv));
+  SAT_TRY(dgrad(dV, D, d->Wv, Wi, d->dx, 1.f));
+  return SAT_OK;
+}

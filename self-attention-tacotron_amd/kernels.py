@@ -607,3 +607,31 @@ def transpose(x: torch.Tensor, out: torch.Tensor = None) -> torch.Tensor:
         out = torch.empty(C, R, device=x.device)
     _lib.call("sat_transpose", _p(x), x.stride(0), _p(out), out.stride(0), R, C, _stream())
     return out
+
+
+def mha_desc(x, Wq, bq, Wk, bk, Wv, bv, Wo, bo, heads: int, causal: bool, probs_mask, saved):
+    """SatMha over x [B, L, W] with the forward's saved tensors (dict of q, k, v, P, Pd, o, y)."""
+    B, L, W = x.shape
+    assert x.is_contiguous()
+    d = _lib.SatMha()
+    d.B, d.L, d.W, d.D, d.H, d.causal = B, L, W, Wq.shape[1], heads, int(causal)
+    d.out_dim = Wo.shape[1]
+    d.x, d.Wq, d.bq, d.Wk, d.bk = _p(x), _p(Wq), _p(bq), _p(Wk), _p(bk)
+    d.Wv, d.bv, d.Wo, d.bo = _p(Wv), _p(bv), _p(Wo), _p(bo)
+    d.probs_mask = _p(probs_mask)
+    for f in ("q", "k", "v", "P", "Pd", "o", "y"):
+        setattr(d, f, _p(saved.get(f)))
+    nbytes = int(_lib.load().sat_mha_scratch_bytes(B, L, d.D, heads, d.out_dim))
+    scratch = torch.empty(nbytes, dtype=torch.uint8, device=x.device)
+    d.scratch, d.scratch_bytes = scratch.data_ptr(), nbytes
+    ws = _gemm_ws(x.device)
+    d.gemm_ws, d.gemm_ws_bytes = ws.data_ptr(), ws.numel()
+    return d, scratch
+
+
+def mha_fwd(d):
+    _lib.check(_lib.load().sat_mha_fwd(ctypes.byref(d), _stream()), "sat_mha_fwd")
+
+
+def mha_bwd(d):
+    _lib.check(_lib.load().sat_mha_bwd(ctypes.byref(d), _stream()), "sat_mha_bwd")

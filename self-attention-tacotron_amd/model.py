@@ -65,28 +65,23 @@ def bank_fused(d, inp: torch.Tensor) -> bool:
 
 def mha_fwd(x: torch.Tensor, P, scope: str, heads: int, causal: bool,
             probs_mask: Optional[torch.Tensor], sv: dict, key: str):
-    """MultiHeadAttention (modules/self_attention.py:108-128) over x [B, L, W]."""
+    """MultiHeadAttention (modules/self_attention.py:108-128) over x [B, L, W]: ONE
+    sat_mha_fwd call (projections, per-head scores, masked softmax, contexts, output)."""
     B, L, W = x.shape
-    q = K.linear(x, P[f"{scope}/query_projection/kernel"], P[f"{scope}/query_projection/bias"])
-    k = K.linear(x, P[f"{scope}/key_projection/kernel"], P[f"{scope}/key_projection/bias"])
-    v = K.linear(x, P[f"{scope}/value_projection/kernel"], P[f"{scope}/value_projection/bias"])
-    model = q.shape[-1]
-    dh = model // heads
-
-    def hv(t):  # [B, L, model] -> [B, H, L, dh] view
-        return t.view(B, L, heads, dh).permute(0, 2, 1, 3)
-
-    S = K.gemm(hv(q), hv(k).transpose(-1, -2))                 # [B, H, L, L]
-    Pm = torch.empty_like(S)
-    Pd = torch.empty_like(S) if probs_mask is not None else Pm
-    K.softmax_fwd(S, Pm, Pd if probs_mask is not None else None, probs_mask, causal=causal,
-                  scale=1.0 / math.sqrt(dh))
-    o = torch.empty(B, L, model, device=x.device)
-    K.gemm(Pd, hv(v), hv(o))                                   # heads written in place
-    y = K.linear(o, P[f"{scope}/output_projection/kernel"], P[f"{scope}/output_projection/bias"])
-    sv[key] = dict(x=x, q=q, k=k, v=v, P=Pm, Pd=Pd, o=o, y=y, mask=probs_mask, heads=heads,
-                   dh=dh)
-    return y
+    model = P[f"{scope}/query_projection/kernel"].shape[1]
+    out = P[f"{scope}/output_projection/kernel"].shape[1]
+    dev = x.device
+    s = dict(x=x, q=torch.empty(B, L, model, device=dev), k=torch.empty(B, L, model, device=dev),
+             v=torch.empty(B, L, model, device=dev), P=torch.empty(B, heads, L, L, device=dev),
+             o=torch.empty(B, L, model, device=dev), y=torch.empty(B, L, out, device=dev),
+             mask=probs_mask, heads=heads, dh=model // heads, causal=causal, scope=scope)
+    s["Pd"] = torch.empty_like(s["P"]) if probs_mask is not None else s["P"]
+    d, _ = K.mha_desc(x, *(P[f"{scope}/{n}_projection/{t}"] for n in ("query", "key", "value",
+                                                                        "output")
+                           for t in ("kernel", "bias")), heads, causal, probs_mask, s)
+    K.mha_fwd(d)
+    sv[key] = s
+    return s["y"]
 
 
 def sa_transformer_fwd(x, P, scope, heads, causal, probs_mask, sv, key):

@@ -85,6 +85,19 @@ typedef struct SatGemmDesc {
 } SatGemmDesc;
 
 int sat_gemm(const SatGemmDesc* desc, void* stream);
+/* ---------------------------------------------------------------- step workspace
+ * Bytes of caller-owned device scratch one teacher-forced training step uses besides the
+ * parameter / gradient arenas and the activations: the sum of every entry's scratch query
+ * (persistent decoder kernels fwd + BPTT, column reductions over the widest bias/BN span,
+ * loss, Adam, both self-attention sites) plus the GEMM split-K budget, each 256-B aligned. */
+typedef struct SatDims {
+  int32_t B, N, Tp;               /* utterances, encoder positions, decoder steps (T / r) */
+  int32_t enc_heads, dec_heads;   /* self-attention heads: encoder, decoder head */
+  int32_t enc_D, dec_D;           /* self-attention model widths */
+  int32_t max_cols;               /* widest column reduction (the 2048-channel conv bank) */
+} SatDims;
+int64_t sat_workspace_size(const SatDims* d);
+
 /* ---------------------------------------------------------------- multi-head self-attention
  * MultiHeadAttention.call (modules/self_attention.py:108-128) with the
  * ScaledDotProductAttentionMechanism (:45-65): Q/K/V = x W + b ([B][L][W] -> [B][L][D]), per

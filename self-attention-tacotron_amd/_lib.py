@@ -76,6 +76,9 @@ SatMha = _struct("SatMha", """
     ptr:dy ptr:dx ptr:dWq ptr:dbq ptr:dWk ptr:dbk ptr:dWv ptr:dbv ptr:dWo ptr:dbo ptr:scratch
     i64:scratch_bytes ptr:gemm_ws i64:gemm_ws_bytes""")
 
+SatDims = _struct("SatDims", """
+    i32:B i32:N i32:Tp i32:enc_heads i32:dec_heads i32:enc_D i32:dec_D i32:max_cols""")
+
 SatAdamConfig = _struct("SatAdamConfig", """
     f32:lr0 f32:beta1 f32:beta2 f32:eps f32:clip_norm i32:decay i32:step_factor f32:grad_scale""")
 
@@ -192,6 +195,7 @@ RESTYPES = {"sat_workspace_colreduce": (ctypes.c_int64, [_I32, _I32]),
             "sat_workspace_adam": (ctypes.c_int64, []),
             "sat_workspace_loss": (ctypes.c_int64, []),
             "sat_mha_scratch_bytes": (ctypes.c_int64, [_I32, _I32, _I32, _I32, _I32]),
+            "sat_workspace_size": (ctypes.c_int64, [ctypes.c_void_p]),
             "sat_decoder_attention_scratch": (ctypes.c_int64, [_I32, _I32, _P, _P, _P]),
             "sat_decoder_attention_bwd_scratch": (ctypes.c_int64, [_I32, _I32, _P, _P]),
             "sat_decoder_attention_bwd_dq_parts": (ctypes.c_int32, [_I32, _I32]),

@@ -53,7 +53,7 @@ def _c_sizeof(struct):
 
 STRUCTS = ["SatGemmDesc", "SatLstmFwd", "SatLstmBwd", "SatAttnStep", "SatAttnStepBwd",
            "SatAttnParamGrad", "SatDecAttnFwd", "SatDecAttnBwd", "SatDecLstmFwd",
-           "SatDecLstmBwd", "SatEncLstmFwd", "SatEncLstmBwd", "SatAdamConfig", "SatConvBank"]
+           "SatDecLstmBwd", "SatEncLstmFwd", "SatEncLstmBwd", "SatAdamConfig", "SatConvBank", "SatMha", "SatDims"]
 
 
 def _c_offsets(struct, fields):
@@ -97,3 +97,26 @@ def test_header_cites_reference_interfaces():
     text = open(os.path.join(ROOT, "include", "sat_abi.h")).read()
     cites = re.findall(r"[\w/]+\.py:\d+", text)
     assert len(cites) >= 10
+
+
+def test_workspace_size_is_the_sum_of_the_entry_queries():
+    """sat_workspace_size = every per-entry scratch query, 256-B aligned, + the
+    32 MB GEMM split-K budget (host-only arithmetic: no GPU needed)."""
+    if not _lib_built():
+        pytest.skip("libsat_hip.so not built")
+    lib = _lib.load()
+    B, N, Tp = 32, 200, 500
+    d = _lib.SatDims(B, N, Tp, 4, 4, 256, 256, 2048)
+    al = lambda n: (n + 255) // 256 * 256   # noqa: E731
+    e, pt, qp, rdp, ya = (ctypes.c_int64() for _ in range(5))
+    ctr = lib.sat_decoder_attention_scratch(B, N, ctypes.byref(e), ctypes.byref(pt), ctypes.byref(qp))
+    bctr = lib.sat_decoder_attention_bwd_scratch(B, N, ctypes.byref(rdp), ctypes.byref(ya))
+    want = sum(al(4 * x) for x in (e.value, pt.value, qp.value, ctr, rdp.value, ya.value, bctr,
+                                   lib.sat_decoder_lstms_scratch(B),
+                                   lib.sat_decoder_lstms_bwd_scratch(B)))
+    want += al(lib.sat_workspace_colreduce(B * Tp, 2048)) + al(lib.sat_workspace_loss()) + \
+        al(lib.sat_workspace_adam())
+    want += al(lib.sat_mha_scratch_bytes(B, N, 256, 4, 256)) + \
+        al(lib.sat_mha_scratch_bytes(B, Tp, 256, 4, 256)) + (32 << 20)
+    assert lib.sat_workspace_size(ctypes.byref(d)) == want
+    assert lib.sat_workspace_size(ctypes.byref(_lib.SatDims())) < 0

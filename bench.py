@@ -110,7 +110,7 @@ def attention_probe(rec, B, N, reps=6):
     traffic, pmc_src = _pmc_traffic()
     return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-            "kernel": "dec_attn_fwd_kernel (sat_decoder_attention_fwd, persistent, T' steps)",
+            "kernel": "dec_attn_fwd8_kernel (sat_decoder_attention_fwd, persistent, T' steps)",
             "bytes_per_launch": int(bytes_launch), "attn_bytes_per_step": int(attn_step),
             "steps_per_launch": T, "avg_launch_us": round(avg_s * 1e6, 1),
             "us_per_step": round(avg_s * 1e6 / T, 3), "launches_timed": reps,

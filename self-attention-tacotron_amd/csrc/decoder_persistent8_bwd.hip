@@ -542,10 +542,15 @@ __global__ void __launch_bounds__(kTh) dec_attn_bwd8_kernel(Bwd8P p) {
         const int r2 = lane & 31, hsel = lane >> 5;
         const float4 wa = *reinterpret_cast<const float4*>(&wc2[r2][16 * wave + 8 * hsel]);
         const float4 wb = *reinterpret_cast<const float4*>(&wc2[r2][16 * wave + 8 * hsel + 4]);
-        f2 a = f2{wa.x, wa.y} * dgp[4 * hsel];
-        a = __builtin_elementwise_fma(f2{wa.z, wa.w}, dgp[4 * hsel + 1], a);
-        a = __builtin_elementwise_fma(f2{wb.x, wb.y}, dgp[4 * hsel + 2], a);
-        a = __builtin_elementwise_fma(f2{wb.z, wb.w}, dgp[4 * hsel + 3], a);
+        // (hsel is per lane: select the 4 gate-gradient pairs explicitly -- indexing the
+        // register array with it compiled to a 16-way v_cmp/v_cndmask chain per operand)
+        const bool hi = hsel != 0;
+        const f2 g0 = hi ? dgp[4] : dgp[0], g1 = hi ? dgp[5] : dgp[1];
+        const f2 g2 = hi ? dgp[6] : dgp[2], g3 = hi ? dgp[7] : dgp[3];
+        f2 a = f2{wa.x, wa.y} * g0;
+        a = __builtin_elementwise_fma(f2{wa.z, wa.w}, g1, a);
+        a = __builtin_elementwise_fma(f2{wb.x, wb.y}, g2, a);
+        a = __builtin_elementwise_fma(f2{wb.z, wb.w}, g3, a);
         const float s = fold32(a.x + a.y);
         if (lane < kM2) wred[wave][kM1 + lane] = s;
       }

@@ -530,13 +530,24 @@ __global__ void __launch_bounds__(kTh) dec_attn_bwd8_kernel(Bwd8P p) {
     // ---- 3. row-dot partial R_t[k] = sum over the own 128 columns of DG0_t[col] W0r[k][col]:
     //         per wave over its 16 columns (lane rows as in the forward), summed over waves
     if (t > 0) {
+      // two rows at a time, each as two 4-deep chains: the compiler otherwise serialises all
+      // 8 rows into one 8-deep dependent pk_fma chain (register pressure at the 256 cap)
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        f2 a = w0[i][0] * dgp[0];
+      for (int i = 0; i < 8; i += 2) {
+        f2 a0 = w0[i][0] * dgp[0], a1 = w0[i][4] * dgp[4];
+        f2 b0 = w0[i + 1][0] * dgp[0], b1 = w0[i + 1][4] * dgp[4];
 #pragma unroll
-        for (int k = 1; k < 8; ++k) a = __builtin_elementwise_fma(w0[i][k], dgp[k], a);
+        for (int k = 1; k < 4; ++k) {
+          a0 = __builtin_elementwise_fma(w0[i][k], dgp[k], a0);
+          a1 = __builtin_elementwise_fma(w0[i][k + 4], dgp[k + 4], a1);
+          b0 = __builtin_elementwise_fma(w0[i + 1][k], dgp[k], b0);
+          b1 = __builtin_elementwise_fma(w0[i + 1][k + 4], dgp[k + 4], b1);
+        }
+        const f2 a = a0 + a1, b2 = b0 + b1;
         const int row = i < 4 ? kC + 64 * i + lane : 64 * (i - 4) + lane;
+        const int row1 = i + 1 < 4 ? kC + 64 * (i + 1) + lane : 64 * (i + 1 - 4) + lane;
         wred[wave][row] = a.x + a.y;
+        wred[wave][row1] = b2.x + b2.y;
       }
       {
         const int r2 = lane & 31, hsel = lane >> 5;

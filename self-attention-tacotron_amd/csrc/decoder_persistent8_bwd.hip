@@ -432,25 +432,32 @@ __global__ void __launch_bounds__(kTh) dec_attn_bwd8_kernel(Bwd8P p) {
     tick(7);
     lds_barrier();
     tick(8);
-    // ---- 5. publish record Q_t (wave 0): dq partial, P1, P2, Y_t(n0), dL/df_t head / tail
+    // ---- 5. publish record Q_t: wave 0 the dq partial; wave 1 the sums word (lane 0) and the
+    //         dL/df_t head / tail words (lanes 1..45), addresses and values chosen branch-free
+    //         (one store per lane; the per-lane-range branches serialised the segment)
     if (wave == 0) {
       const int rq = (((q & 1) * B + b) * kW + j) * kRQ;
       float4 a = qst[0][lane];
 #pragma unroll
       for (int w = 1; w < kW; ++w) a = add4(a, qst[w][lane]);
       stc4x(xl, rRQ, rq / 4 + lane, tagf4(a, bit));
-      if (lane == 0) {
-        float P2 = 0.f;
+    } else if (wave == 1) {
+      const int rq = (((q & 1) * B + b) * kW + j) * kRQ;
+      float P2 = 0.f;
 #pragma unroll
-        for (int w = 0; w < kW; ++w) P2 += pw[w][1];
-        stc4x(xl, rRQ, (rq + kQP) / 4, tagf4(make_float4(pw[0][0], P2, ysh[1 - yb][0], 0.f), bit));
-      } else if (lane >= 1 && lane <= kHR * kF) {           // head: positions n0 .. n0+3
-        const int k = lane - 1;
-        stcx(xl, rRQ, rq + kQDH + k, (k / kF) < nt ? dfh[1 - yb][kHL * kF + k] : tagf(0.f, bit));
-      } else if (lane > kHR * kF && lane <= kHR * kF + kHL * kF) {   // tail: n0+nt-5 .. n0+nt-1
-        const int k = lane - 1 - kHR * kF, i = nt - kHL + k / kF;
-        stcx(xl, rRQ, rq + kQDT + k, i >= 0 ? dfh[1 - yb][(kHL + i) * kF + (k % kF)] : tagf(0.f, bit));
-      }
+      for (int w = 0; w < kW; ++w) P2 += pw[w][1];
+      const float4 pword = tagf4(make_float4(pw[0][0], P2, ysh[1 - yb][0], 0.f), bit);
+      const bool head = lane >= 1 && lane <= kHR * kF;                   // n0 .. n0+3
+      const bool tail = lane > kHR * kF && lane <= kHR * kF + kHL * kF;  // n0+nt-5 .. n0+nt-1
+      const int kh = lane - 1, kt = lane - 1 - kHR * kF;
+      const int it = nt - kHL + kt / kF;
+      const int src = head ? kHL * kF + kh : (kHL + max(it, 0)) * kF + (kt % kF);
+      const float dv = dfh[1 - yb][min(max(src, 0), (kPmax + kHL + kHR) * kF - 1)];
+      const bool valid = head ? (kh / kF) < nt : it >= 0;
+      const float v = valid ? dv : tagf(0.f, bit);
+      const int idx = head ? rq + kQDH + kh : rq + kQDT + kt;
+      if (lane == 0) stc4x(xl, rRQ, (rq + kQP) / 4, pword);
+      else if (head || tail) stcx(xl, rRQ, idx, v);
     }
     tick(9);
 
@@ -506,7 +513,9 @@ __global__ void __launch_bounds__(kTh) dec_attn_bwd8_kernel(Bwd8P p) {
         const float dc_t = dc_c;
         const float gi = z.g4.x, gj = z.g4.y, gf = z.g4.z, go = z.g4.w;
         const float cn = gf * z.cp + gi * gj;
-        const float tc = tanhf(cn);
+        // tanh(c) exactly as the forward formed it (decoder_persistent8.hip: 2 sigm(2c) - 1
+        // with one v_exp and one v_rcp), so the derivative is taken at the forward's value
+        const float tc = fmaf(2.f, __builtin_amdgcn_rcpf(1.f + __expf(-2.f * cn)), -1.f);
         const float dhn = z.dy + v[0] + z.mh * dh_t;
         const float dcn = z.mc * dc_t + dhn * go * (1.f - tc * tc);
         const float d_o = dhn * tc * go * (1.f - go);

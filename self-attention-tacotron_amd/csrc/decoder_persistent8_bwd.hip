@@ -391,9 +391,13 @@ __global__ void __launch_bounds__(kTh) dec_attn_bwd8_kernel(Bwd8P p) {
       const float4 v4 = *reinterpret_cast<const float4*>(&vcat[4 * c]);
       const bool d1 = c < kD1 / 4;
       float4 dqa = make_float4(0.f, 0.f, 0.f, 0.f);
-      float df[32];
+      // dL/df of the wave's 4 positions: taps f < 4 as 16 outputs, tap 4 as 4 (a 32-output
+      // reduction of the 20 values paid 12 exchanges of constant zeros)
+      float dfa[16], dfb[4];
 #pragma unroll
-      for (int k = 0; k < 32; ++k) df[k] = 0.f;
+      for (int k = 0; k < 16; ++k) dfa[k] = 0.f;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) dfb[k] = 0.f;
       float4 lw[kF];
 #pragma unroll
       for (int f = 0; f < kF; ++f) lw[f] = *reinterpret_cast<const float4*>(&locw[f][4 * c]);
@@ -410,20 +414,29 @@ __global__ void __launch_bounds__(kTh) dec_attn_bwd8_kernel(Bwd8P p) {
           for (int f = 0; f < kF; ++f) {        // locw is zero on the D2 chunks
             float a = dp.x * lw[f].x;
             a = fmaf(dp.y, lw[f].y, a); a = fmaf(dp.z, lw[f].z, a); a = fmaf(dp.w, lw[f].w, a);
-            df[i * kF + f] = a;
+            if (f < 4) dfa[4 * i + f] = a; else dfb[i] = a;
           }
         }
       }
       qst[wave][c] = dqa;
-      transpose_reduce32(df, lane);            // lanes 2m, 2m+1: dL/df of (position 4w + m / 5, m % 5)
+      transpose_reduce16(dfa, lane);           // lanes 4m..4m+3: position 4w + m / 4, tap m % 4
+      transpose_reduce4(dfb);                  // lanes 16i..16i+15: position 4w + i, tap 4
       float p2 = 0.f;
-      if ((lane & 1) == 0 && lane < 2 * 4 * kF) {
-        const int m = lane >> 1, i = m / kF, f = m - i * kF, r = 4 * wave + i;
-        if (r < nt) {
-          const float v = tagf(df[0], bit);
-          p.DFH[(((int64_t)t * B + b) * N + n0 + r) * kF + f] = v;
+      {
+        const int r = 4 * wave + (lane >> 4);
+        const int64_t o = (((int64_t)t * B + b) * N + n0 + r) * kF;
+        if ((lane & 3) == 0 && r < nt) {
+          const int f = (lane >> 2) & 3;
+          const float v = tagf(dfa[0], bit);
+          p.DFH[o + f] = v;
           dfh[1 - yb][(kHL + r) * kF + f] = v;
           p2 = v * lfS[r][f];
+        }
+        if ((lane & 15) == 0 && r < nt) {
+          const float v = tagf(dfb[0], bit);
+          p.DFH[o + 4] = v;
+          dfh[1 - yb][(kHL + r) * kF + 4] = v;
+          p2 += v * lfS[r][4];
         }
       }
       p2 = wave_sum_dpp(p2);

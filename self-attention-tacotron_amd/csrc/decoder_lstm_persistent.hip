@@ -206,7 +206,7 @@ __global__ void __launch_bounds__(kThreads) dec_lstm_fwd_kernel(DecLstmFwdP p) {
     const float mc = (masked && on_i) ? mcn : 1.f - p.zc;
     const float mh = (masked && on_i) ? mhn : 1.f - p.zh;
     if (i < T) load_ops(i + 1, xpn, mcn, mhn);
-    __syncthreads();
+    lds_barrier();   // LDS staging only: a __syncthreads would drain the prefetch just issued
     tick(1);
     // ---- dots: v[layer*16 + ub*8 + column]
     float v[32];
@@ -248,12 +248,14 @@ __global__ void __launch_bounds__(kThreads) dec_lstm_fwd_kernel(DecLstmFwdP p) {
     tick(2);
     float hpub = hst;                                   // value published by LSTM2 lanes
     if (cell_step) {
-      const float gi = sigmf(v[0] + xp.x);
-      const float gj = tanhf(gj_ + xp.y);
-      const float gf = sigmf(gf_ + xp.z + 1.0f);   // forget_bias = 1.0
-      const float go = sigmf(go_ + xp.w);
+      // one v_exp + one v_rcp per activation (the libm tanhf / IEEE-division logistic cost
+      // ~5x the instructions on the step's critical path; <= 2 ulp apart)
+      const float gi = sigmoid_fast(v[0] + xp.x);
+      const float gj = tanh_lstm(gj_ + xp.y);
+      const float gf = sigmoid_fast(gf_ + xp.z + 1.0f);   // forget_bias = 1.0
+      const float go = sigmoid_fast(go_ + xp.w);
       const float cn = gf * cst + gi * gj;
-      const float hn = go * tanhf(cn);
+      const float hn = go * tanh_lstm(cn);
       const float c2 = mc * cn + (1.f - mc) * cst;
       const float h2 = mh * hn + (1.f - mh) * hst;
       cst = c2;
@@ -309,7 +311,7 @@ __device__ __forceinline__ float4 lstm_cell_bwd(float4 g4, float cp, float dy, f
                                                 float mc, float mh, float& dhc, float& dcc) {
   const float gi = g4.x, gj = g4.y, gf = g4.z, go = g4.w;
   const float cn = gf * cp + gi * gj;
-  const float tc = tanhf(cn);
+  const float tc = tanh_lstm(cn);   // formed exactly as the forward formed it
   const float dh_t = rec + dhc;
   const float dc_t = dcc;
   const float dhn = dy + mh * dh_t;                 // dL/dh'
@@ -429,7 +431,7 @@ __global__ void __launch_bounds__(kThreads) dec_lstm_bwd_kernel(DecLstmBwdP p) {
       *reinterpret_cast<float4*>(&dg1s[ub][4 * q]) = v1;
     }
     if (jj < T) load_ops(jj + 1, g4n, cpn, dyn, mcn, mhn);   // in flight across the barrier
-    __syncthreads();
+    lds_barrier();   // (a __syncthreads would drain them: its release fence waits on vmcnt)
     tick(1);
     float v[16];
 #pragma unroll

@@ -82,7 +82,7 @@ struct DecAttnP {
 
 typedef float f2 __attribute__((ext_vector_type(2)));
 
-__device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + __expf(-x)); }
+__device__ __forceinline__ float sigm(float x) { return sigmoid_fast(x); }   // as every LSTM kernel
 __device__ __forceinline__ bool any_lane(bool v) { return __builtin_amdgcn_ballot_w64(v) != 0; }
 
 __global__ void __launch_bounds__(256) dec_attn_fwd_kernel(DecAttnP p) {
@@ -369,11 +369,11 @@ __global__ void __launch_bounds__(256) dec_attn_fwd_kernel(DecAttnP p) {
       const unsigned bit = lsb_tag(t);
       if (cell) {
         const float gi = sigm(v[0] + xp.x);
-        const float gj = tanhf(gj_ + xp.y);
+        const float gj = tanh_lstm(gj_ + xp.y);
         const float gf = sigm(gf_ + xp.z + 1.0f);   // forget_bias = 1.0
         const float go = sigm(go_ + xp.w);
         const float cn = gf * c_own + gi * gj;
-        const float hn = go * tanhf(cn);
+        const float hn = go * tanh_lstm(cn);
         const float c2 = mc * cn + (1.f - mc) * c_own;
         const float h2 = tagf(mh * hn + (1.f - mh) * h_own, bit);   // the value every reader sees
         c_own = c2; h_own = h2;

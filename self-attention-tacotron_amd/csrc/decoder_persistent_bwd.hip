@@ -490,7 +490,7 @@ __global__ void __launch_bounds__(kTh) dec_attn_bwd_kernel(DecAttnBwdP p) {
         const float dc_t = dc_c;
         const float gi = z.g4.x, gj = z.g4.y, gf = z.g4.z, go = z.g4.w;
         const float cn = gf * z.cp + gi * gj;
-        const float tc = tanhf(cn);
+        const float tc = tanh_lstm(cn);
         const float dhn = z.dy + qt + z.mh * dh_t;
         const float dcn = z.mc * dc_t + dhn * go * (1.f - tc * tc);
         const float d_o = dhn * tc * go * (1.f - go);

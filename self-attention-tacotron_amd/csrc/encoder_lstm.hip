@@ -110,19 +110,21 @@ __global__ void __launch_bounds__(kTh) enc_lstm_fwd_kernel(EncFwdP p) {
       acc += dpp<0xB1>(acc);                // the pair (lanes t, t ^ 1) of column c
       if (hf == 0) gp[c] = acc + xv;
     }
-    __syncthreads();
+    // LDS-only barriers: a __syncthreads would also drain the prefetch and the history stores
+    lds_barrier();
     // ---- cell
     if (cell) {
       const float4 g = *reinterpret_cast<const float4*>(&gp[4 * u]);
       const int64_t bu = (int64_t)b * kU + u;
       float* Hd = p.H + (int64_t)b * p.h_sb + (int64_t)n * p.h_sn + d * kU + u;
       if (n < len) {
-        const float gi = sigmf(g.x);
-        const float gj = tanhf(g.y);
-        const float gf = sigmf(g.z + 1.0f);   // forget_bias = 1.0
-        const float go = sigmf(g.w);
+        // one v_exp + one v_rcp per activation (decoder_lstm_persistent.hip: same forms)
+        const float gi = sigmoid_fast(g.x);
+        const float gj = tanh_lstm(g.y);
+        const float gf = sigmoid_fast(g.z + 1.0f);   // forget_bias = 1.0
+        const float go = sigmoid_fast(g.w);
         const float cn = gf * cst + gi * gj;
-        const float hn = go * tanhf(cn);
+        const float hn = go * tanh_lstm(cn);
         cst = mc * cn + (1.f - mc) * cst;
         hst = mh * hn + (1.f - mh) * hst;
         *Hd = hn;
@@ -135,7 +137,7 @@ __global__ void __launch_bounds__(kTh) enc_lstm_fwd_kernel(EncFwdP p) {
       p.HS[d][(int64_t)nx * B * kU + bu] = hst;
       hs[u] = hst;
     }
-    __syncthreads();
+    lds_barrier();
   }
 }
 
@@ -213,7 +215,7 @@ __global__ void __launch_bounds__(kTh) enc_lstm_bwd_kernel(EncBwdP p) {
       if (n < len) {
         const float gi = o.g.x, gj = o.g.y, gf = o.g.z, go = o.g.w;
         const float cn = gf * o.cp + gi * gj;
-        const float tc = tanhf(cn);
+        const float tc = tanh_lstm(cn);   // formed exactly as the forward formed it
         const float dhn = o.dy + o.mh * dh_t;               // dL/dh'
         const float dcn = o.mc * dc_t + dhn * go * (1.f - tc * tc);
         dg = make_float4(dcn * gj * gi * (1.f - gi), dcn * gi * (1.f - gj * gj),
@@ -227,7 +229,7 @@ __global__ void __launch_bounds__(kTh) enc_lstm_bwd_kernel(EncBwdP p) {
       reinterpret_cast<float4*>(p.DG[d])[(int64_t)n * B * kU + bu] = dg;
       *reinterpret_cast<float4*>(&dgn[(i + 1) & 1][4 * u]) = dg;
     }
-    __syncthreads();
+    lds_barrier();   // LDS only: a __syncthreads would drain the DG store and the prefetch
   }
 }
 

@@ -106,12 +106,13 @@ __device__ __forceinline__ void lstm_fwd_block(const LstmFwdP& p, int bx, int by
     if (p.gates) reinterpret_cast<float4*>(p.gates)[bu] = make_float4(0.f, 0.f, 0.f, 0.f);
     return;
   }
-  const float gi = sigmf(acc[0] + xp.x);
-  const float gj = tanhf(acc[1] + xp.y);
-  const float gf = sigmf(acc[2] + xp.z + 1.0f);   // forget_bias = 1.0
-  const float go = sigmf(acc[3] + xp.w);
+  // activations formed as in every LSTM kernel (sat_common.h sigmoid_fast / tanh_lstm)
+  const float gi = sigmoid_fast(acc[0] + xp.x);
+  const float gj = tanh_lstm(acc[1] + xp.y);
+  const float gf = sigmoid_fast(acc[2] + xp.z + 1.0f);   // forget_bias = 1.0
+  const float go = sigmoid_fast(acc[3] + xp.w);
   const float cn = gf * cp + gi * gj;
-  const float hn = go * tanhf(cn);
+  const float hn = go * tanh_lstm(cn);
   float c2, h2;
   if (p.mask_c) {
     c2 = mc * cn + (1.f - mc) * cp;
@@ -279,7 +280,7 @@ __device__ __forceinline__ void lstm_bwd_block(const LstmBwdP& p, int bx, int by
   }
   const float gi = g4.x, gj = g4.y, gf = g4.z, go = g4.w;
   const float cn = gf * cp + gi * gj;
-  const float tc = tanhf(cn);
+  const float tc = tanh_lstm(cn);
   if (!p.mask_c) { mc = 1.f - p.zc; mh = 1.f - p.zh; }
   const float dy = dyv + qterm;
   const float dhn = dy + mh * dh_t;                 // dL/dh'

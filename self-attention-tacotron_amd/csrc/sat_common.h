@@ -137,6 +137,15 @@ __device__ __forceinline__ float tanh_fast(float x) {
   const float e = __expf(2.f * x);
   return 1.f - 2.f * __builtin_amdgcn_rcpf(1.f + e);
 }
+// logistic with one v_exp_f32 and one reciprocal (no IEEE division sequence); saturates to 0 / 1
+__device__ __forceinline__ float sigmoid_fast(float x) {
+  return __builtin_amdgcn_rcpf(1.f + __expf(-x));
+}
+// the ZoneoutLSTM cells' tanh, formed as 2 sigmoid(2x) - 1 in EVERY LSTM kernel (persistent and
+// per-step, forward and BPTT), so the training and incremental paths agree on the cell bit for bit
+__device__ __forceinline__ float tanh_lstm(float x) {
+  return fmaf(2.f, sigmoid_fast(2.f * x), -1.f);
+}
 
 // Workgroup barrier for LDS hand-offs only: waits for the wave's own LDS (and scalar) accesses,
 // not for its outstanding global stores.  __syncthreads() also drains vmcnt (its workgroup

@@ -474,7 +474,8 @@ typedef struct SatDecLstmBwd {
   const float* DH2;
   const float* mask1_c; const float* mask1_h; const float* mask2_c; const float* mask2_h;
   float* DG1; float* DG2;
-  uint32_t* ctr;   /* sat_decoder_lstms_bwd_scratch(B) words, zeroed by the call */
+  uint32_t* ctr;   /* sat_decoder_lstms_bwd_scratch(B) words (tagged gate-gradient exchange
+                      slots + placement words), 16-byte aligned, zeroed by the call */
   int32_t* err;
   int64_t* prof;   /* optional [256][4] per-workgroup segment clocks (100 MHz), NULL = off */
 } SatDecLstmBwd;

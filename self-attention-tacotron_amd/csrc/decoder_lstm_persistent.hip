@@ -301,7 +301,8 @@ struct DecLstmBwdP {
   const float* DH2;                                   // [T][B][U]
   const float* m1c; const float* m1h; const float* m2c; const float* m2h;
   float* DG1; float* DG2;                             // [T][B][4U]
-  unsigned* ctr; int* err;
+  unsigned* ctr;   // XG [2 slots][2 streams][B][4U] tagged gate gradients, then XID [256]
+  int* err;
   long long* prof;                                    // [256][4] segment clocks (nullable)
 };
 
@@ -332,9 +333,15 @@ __device__ __forceinline__ float4 lstm_cell_bwd(float4 g4, float cp, float dy, f
 // {r2, y1, r1, pad}) are transpose-reduced across the wave (permlane swaps + DPP), after which
 // lanes 4m..4m+3 hold output m.  Cells: the lane holding r2 runs LSTM2's cell, the lane holding
 // r1 LSTM1's (y1 comes from 4 lanes below by DPP); carries stay in their registers.  Hand-off:
-// the gate-gradient histories themselves (sc1 stores, drained, one group barrier per step, sc1
-// loads; persistent.h).  Cell operands (forward histories, the head's gradient) are prefetched
-// one iteration ahead so their HBM latency hides behind the barrier.
+// data-tagged gate gradients, no barrier (persistent.h lsb_tag rule): each cell writes its
+// tagged dgates to the history (for the weight-gradient GEMMs) and to exchange slot q & 1 of its
+// stream (LSTM2: q = jj, LSTM1: q = jj - 1, so every slot's first occupant is written at q = 0
+// or 1), and the next iteration's staging polls the group's rows of that slot until every word
+// carries bit lsb_tag(q).  A workgroup reaches iteration jj + 2 (overwriting slot q) only after
+// staging every workgroup's iteration jj + 1 rows, which their makers wrote after consuming
+// iteration jj's -- so no slot is overwritten before it is read.  (Replaced a drained store + an
+// agent-scope counter barrier + a reload: 1.06 + 0.99 us of the 3.2 us step.)  Cell operands
+// (forward histories, the head's gradient) are prefetched one iteration ahead.
 __global__ void __launch_bounds__(kThreads) dec_lstm_bwd_kernel(DecLstmBwdP p) {
   __shared__ __attribute__((aligned(16))) float dg2s[kUBmax][4 * kU];
   __shared__ __attribute__((aligned(16))) float dg1s[kUBmax][4 * kU];
@@ -342,7 +349,8 @@ __global__ void __launch_bounds__(kThreads) dec_lstm_bwd_kernel(DecLstmBwdP p) {
   const int g = blockIdx.x % kG, j = blockIdx.x / kG;
   const int u0 = j * kUW;
   const int B = p.B, T = p.T;
-  unsigned* ctr = p.ctr + 64 * g;
+  float* XG = reinterpret_cast<float*>(p.ctr);          // [2][2][B][4U]
+  unsigned* XID = p.ctr + (size_t)16 * B * kU;
 
   float4 wa[2][4], wb[2][4], wc[2][4];
 #pragma unroll
@@ -368,7 +376,7 @@ __global__ void __launch_bounds__(kThreads) dec_lstm_bwd_kernel(DecLstmBwdP p) {
   const int layer = prod == 0 ? 2 : 1;
   float dhc = 0.f, dcc = 0.f;
   const bool masked = p.m1c != nullptr;
-  const auto rDG1 = rsrc(p.DG1), rDG2 = rsrc(p.DG2);
+  const auto rXG = rsrc(XG);
 
   // cell operands of iteration jj (plain loads of read-only inputs).  Branch-free: every lane
   // loads from a clamped in-range address and only cell lanes of live steps use the values, so
@@ -394,7 +402,8 @@ __global__ void __launch_bounds__(kThreads) dec_lstm_bwd_kernel(DecLstmBwdP p) {
 
   // optional segment clocks (thread 0): barrier wait, staging loads, dots, cells + stores
   // hand-off store policy (persistent.h xcd_local_group): plain stores iff the group is on one XCD
-  const bool xl = (p.flags & 1) ? xcd_local_group(p.ctr + kG * 64, g, kG, kGW, p.err) : false;
+  const bool xl = (p.flags & 1) ? xcd_local_group(XID, g, kG, kGW, p.err) : false;
+  bool gave_up = false;
   long long tp[4] = {0, 0, 0, 0};
   long long t0 = wall_clock64();
   auto tick = [&](int seg) {
@@ -414,19 +423,29 @@ __global__ void __launch_bounds__(kThreads) dec_lstm_bwd_kernel(DecLstmBwdP p) {
     const float4 g4 = g4n;
     const float cp = cpn, dyv = dyn;
     const float mc = masked ? mcn : 1.f - p.zc, mh = masked ? mhn : 1.f - p.zh;
-    // stage dgates2_{t2+1} and dgates1_{t1+1} of the group's utterances (sc1 loads): thread =
-    // (utterance slot tid / U, float4 column tid % U); both loads issued before either is used
+    // stage dgates2_{t2+1} (stream 0, q = jj - 1) and dgates1_{t1+1} (stream 1, q = jj - 2) of
+    // the group's utterances from their exchange slots: thread = (utterance slot tid / U, float4
+    // column tid % U); sc1 polls until every word carries the step's tag
     {
       static_assert(kUBmax * kU == kThreads, "staging map");
       const int ub = tid / kU, q = tid - ub * kU, b = g + kG * ub;
       const bool bo = b < B;
       const int bb = bo ? b : 0;
-      const int ta = stage2 ? t2 + 1 : 0, tc = stage1 ? t1 + 1 : 0;
-      float4 v2 = ldc4(rDG2, (((ta * B + bb) * 4 * kU) / 4) + q);
-      float4 v1 = ldc4(rDG1, (((tc * B + bb) * 4 * kU) / 4) + q);
-      const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (!(stage2 && bo)) v2 = z;
-      if (!(stage1 && bo)) v1 = z;
+      const int q2 = jj - 1, q1 = jj - 2;
+      const int i2 = ((((q2 & 1) * 2 + 0) * B + bb) * kU) + q;
+      const int i1 = ((((q1 & 1) * 2 + 1) * B + bb) * kU) + q;
+      const unsigned w2 = lsb_tag(q2), w1 = lsb_tag(q1);
+      float4 v2 = make_float4(0.f, 0.f, 0.f, 0.f), v1 = v2;
+      bool ok2 = !(stage2 && bo), ok1 = !(stage1 && bo);
+      for (unsigned spins = 0;; ++spins) {
+        if (!ok2) v2 = ldc4(rXG, i2);
+        if (!ok1) v1 = ldc4(rXG, i1);
+        ok2 = ok2 || tag_ok4(v2, w2);
+        ok1 = ok1 || tag_ok4(v1, w1);
+        if (__builtin_amdgcn_ballot_w64(!(ok1 && ok2)) == 0 || gave_up) break;
+        if (poll_give_up(spins, p.err)) { gave_up = true; break; }
+        __builtin_amdgcn_s_sleep(1);
+      }
       *reinterpret_cast<float4*>(&dg2s[ub][4 * q]) = v2;
       *reinterpret_cast<float4*>(&dg1s[ub][4 * q]) = v1;
     }
@@ -474,12 +493,13 @@ __global__ void __launch_bounds__(kThreads) dec_lstm_bwd_kernel(DecLstmBwdP p) {
     if (cell_step) {
       const float rec = layer == 2 ? (stage2 ? v[0] : 0.f) : (stage1 ? v[0] : 0.f);
       const float dy = layer == 2 ? dyv : y1v;
-      const float4 dg = lstm_cell_bwd(g4, cp, dy, rec, mc, mh, dhc, dcc);
+      const int qs = layer == 2 ? jj : jj - 1;            // the stream's sequence number
+      const float4 dg = tagf4(lstm_cell_bwd(g4, cp, dy, rec, mc, mh, dhc, dcc), lsb_tag(qs));
       const int64_t bu = ((int64_t)t * B + pb) * kU + pu;
-      stc4x(xl, layer == 2 ? rDG2 : rDG1, (int)bu, dg);
+      reinterpret_cast<float4*>(layer == 2 ? p.DG2 : p.DG1)[bu] = dg;   // history (GEMMs)
+      stc4x(xl, rXG, ((((qs & 1) * 2 + (layer == 2 ? 0 : 1)) * B + pb) * kU) + pu, dg);
     }
     tick(3);
-    if (jj < T) group_barrier(ctr, (unsigned)(jj + 1) * kGW, p.err);
     tick(0);
   }
   if (p.prof && tid == 0)
@@ -509,8 +529,7 @@ extern "C" int64_t sat_decoder_lstms_scratch(int32_t B) {
 }
 
 extern "C" int64_t sat_decoder_lstms_bwd_scratch(int32_t B) {
-  (void)B;
-  return kG * 64 + kG * kGW;         // group counter words + XID
+  return (int64_t)16 * B * kU + kG * kGW;   // XG [2][2][B][4U] tagged gate gradients + XID
 }
 
 extern "C" int sat_decoder_lstms_fwd(const SatDecLstmFwd* a, void* stream) {
@@ -573,7 +592,8 @@ extern "C" int sat_decoder_lstms_bwd(const SatDecLstmBwd* a, void* stream) {
   p.DG1 = a->DG1; p.DG2 = a->DG2; p.ctr = a->ctr; p.err = a->err; p.flags = xcd_local_env();
   p.prof = reinterpret_cast<long long*>(a->prof);
   hipStream_t s = as_stream(stream);
-  if (zero_dwords(a->ctr, (kG * 64 + kG * kGW), s) != hipSuccess ||
+  SAT_CHECK_ARG(aligned16(a->ctr), "%s: 16-byte aligned scratch", nm);
+  if (zero_dwords(a->ctr, sat_decoder_lstms_bwd_scratch(a->B), s) != hipSuccess ||
       zero_words(a->err, 2, s) != hipSuccess) {
     set_error("%s: memset failed", nm);
     return SAT_ERR_HIP;

@@ -50,7 +50,7 @@ class Tacotron:
 
     HEALTH_WORDS = {0: "sat_decoder_attention_fwd hand-off timeout",
                     2: "sat_decoder_lstms_fwd hand-off timeout",
-                    4: "sat_decoder_lstms_bwd group-barrier timeout",
+                    4: "sat_decoder_lstms_bwd hand-off timeout",
                     6: "sat_decoder_attention_bwd group-barrier timeout",
                     8: "embedding id out of range", 9: "speaker id out of range"}
 

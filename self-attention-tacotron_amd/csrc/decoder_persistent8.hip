@@ -313,7 +313,8 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
         }
         if (tid == 0) {
           stat[0] = M1; stat[1] = Z1; stat[2] = A1; stat[3] = M2; stat[4] = Z2;
-          stat[5] = 1.f / Z1; stat[6] = 1.f / A1; stat[7] = 1.f / Z2;
+          stat[5] = __builtin_amdgcn_rcpf(Z1); stat[6] = __builtin_amdgcn_rcpf(A1);
+          stat[7] = __builtin_amdgcn_rcpf(Z2);   // (IEEE divisions sat on the step's critical path)
         }
       }
     }

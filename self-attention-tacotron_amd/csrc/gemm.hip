@@ -481,15 +481,21 @@ __device__ __forceinline__ void dma16(const float* src, uint32_t lds_off) {
 //   1 forward  : output column block g*Co.. = Conv1D K_{g+1}(x), reduction (g+1)*C per tile;
 //   2 dX       : ONE product over K = sum_g (g+1)*Co, k -> (g, tap, o) of dY's column block g;
 //   3 dW       : ONE product over M = sum_g (g+1)*C, rows (g, tap, ci) read dY's column block g.
+// waves per workgroup: 4 (2 x 2) for every tile but 128 x 128, which runs 8 (2 x 4, each wave
+// 64 x 32 as on the 128 x 64 tile) so its one workgroup per CU still has two waves per SIMD
+template <int BM, int BN>
+constexpr int lds_waves() { return (BM == 128 && BN == 128) ? 8 : 4; }
+
 template <int BM, int BN, int AM, int BMD, int GRP = 0>
-__global__ void __launch_bounds__(256) gemm_lds_kernel(GemmP p) {
+__global__ void __launch_bounds__((64 * lds_waves<BM, BN>())) gemm_lds_kernel(GemmP p) {
   constexpr int ST = 3;
-  constexpr int WM = BM / 2, WN = BN / 2;             // 2 x 2 waves
+  constexpr int NWV = lds_waves<BM, BN>(), WGN = NWV / 2;
+  constexpr int WM = BM / 2, WN = BN / WGN;           // 2 x WGN waves
   constexpr int SM = WM / 32, SN = WN / 32;           // 32x32 MFMA sub-tiles per wave
   constexpr bool AKM = (AM == A_K || AM == A_IM2COL); // A image K-major
   constexpr bool BKM = (BMD == B_K || BMD == B_FLIP); // B image K-major
   constexpr int A_SZ = BM * BK, B_SZ = BN * BK, ST_SZ = A_SZ + B_SZ;
-  constexpr int NA = BM / 32, NB = BN / 32;           // 1-KB DMA instructions per wave per tile
+  constexpr int NA = BM / (8 * NWV), NB = BN / (8 * NWV);   // 1-KB DMA instructions per wave per tile
   constexpr int LPT = NA + NB;
   static_assert(LPT <= 24, "vmcnt budget");
   __shared__ __attribute__((aligned(16))) float lds[ST * ST_SZ];
@@ -497,7 +503,7 @@ __global__ void __launch_bounds__(256) gemm_lds_kernel(GemmP p) {
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = (w >> 1) * WM, wn = (w & 1) * WN;
+  const int wm = (w / WGN) * WM, wn = (w % WGN) * WN;
   int tx = blockIdx.x, ty = blockIdx.y;
   if (p.remap) {   // bijective XCD swizzle: consecutive tiles (one A row panel) share an L2
     const int nwg = gridDim.x * gridDim.y, orig = blockIdx.y * gridDim.x + blockIdx.x;
@@ -540,29 +546,29 @@ __global__ void __launch_bounds__(256) gemm_lds_kernel(GemmP p) {
   const float* zero = g_gemm_zero;
 
   // ---- per-lane loader state, advanced by one K-tile per issue
-  // K-major images: instruction i of wave w covers rows (4 i + w) * 8 + (lane >> 3); the lane's
+  // K-major images: instruction i of wave w covers rows (NWV i + w) * 8 + (lane >> 3); the lane's
   // chunk (after the swizzle) is the same for every instruction
   const int kq = 4 * ((lane & 7) ^ ((4 * (w & 1) + (lane >> 4)) & 7));
-  // M/N-major images: instruction i covers k rows (4 i + w) * (256 / rows) + lane / (rows / 4)
+  // M/N-major images: instruction i covers k rows (NWV i + w) * (256 / rows) + lane / (rows / 4)
   const float* aptr[NA];
   int ai[NA];
   const int amq = AKM ? 0 : 4 * (lane % (BM / 4));
 #pragma unroll
   for (int i = 0; i < NA; ++i) {
     if constexpr (AM == A_K) {
-      const int gm = m0 + (4 * i + w) * 8 + (lane >> 3);
+      const int gm = m0 + (NWV * i + w) * 8 + (lane >> 3);
       ai[i] = gm < p.M;
       aptr[i] = A + (int64_t)min(gm, p.M - 1) * p.a_sm + kbeg + kq;
     } else if constexpr (AM == A_IM2COL) {   // (utterance, position) of the output row
-      const int gm = m0 + (4 * i + w) * 8 + (lane >> 3);
+      const int gm = m0 + (NWV * i + w) * 8 + (lane >> 3);
       const int s = gm / p.a_L, n = gm - s * p.a_L;
       aptr[i] = A + (int64_t)s * p.a_L * p.a_sm;
       ai[i] = gm < p.M ? n : -(1 << 28);
     } else if constexpr (AM == A_M) {
-      ai[i] = kbeg + (4 * i + w) * (256 / BM) + lane / (BM / 4);     // k row
+      ai[i] = kbeg + (NWV * i + w) * (256 / BM) + lane / (BM / 4);     // k row
       aptr[i] = A + (int64_t)ai[i] * p.a_sk + m0 + amq;
     } else {
-      ai[i] = kbeg + (4 * i + w) * (256 / BM) + lane / (BM / 4);     // k position
+      ai[i] = kbeg + (NWV * i + w) * (256 / BM) + lane / (BM / 4);     // k position
       aptr[i] = nullptr;
     }
   }
@@ -573,12 +579,12 @@ __global__ void __launch_bounds__(256) gemm_lds_kernel(GemmP p) {
 #pragma unroll
   for (int i = 0; i < NB; ++i) {
     if constexpr (BKM) {
-      const int gn = n0 + (4 * i + w) * 8 + (lane >> 3);
+      const int gn = n0 + (NWV * i + w) * 8 + (lane >> 3);
       bi[i] = gn < p.N;
       const int gc = min(gn, p.N - 1);
       bptr[i] = (BMD == B_K) ? B + (int64_t)gc * p.b_sn + kbeg + kq : B + (int64_t)gc * p.b_C + kq;
     } else {
-      bi[i] = kbeg + (4 * i + w) * (256 / BN) + lane / (BN / 4);
+      bi[i] = kbeg + (NWV * i + w) * (256 / BN) + lane / (BN / 4);
       bptr[i] = B + (int64_t)bi[i] * p.b_sk + n0 + bnq;
     }
   }
@@ -593,7 +599,7 @@ __global__ void __launch_bounds__(256) gemm_lds_kernel(GemmP p) {
       const bool kok = k0 + kq < kend;
 #pragma unroll
       for (int i = 0; i < NA; ++i) {
-        dma16((ai[i] && kok) ? aptr[i] : zero, la + (4 * i + w) * 1024);
+        dma16((ai[i] && kok) ? aptr[i] : zero, la + (NWV * i + w) * 1024);
         aptr[i] += BK;
       }
     } else if constexpr (AM == A_IM2COL) {
@@ -612,12 +618,12 @@ __global__ void __launch_bounds__(256) gemm_lds_kernel(GemmP p) {
       for (int i = 0; i < NA; ++i) {
         const int row = ai[i] + tap - sh;
         const bool ok = kok && row >= 0 && row < p.a_L;
-        dma16(ok ? aptr[i] + (int64_t)row * p.a_sm + c0 + kq : zero, la + (4 * i + w) * 1024);
+        dma16(ok ? aptr[i] + (int64_t)row * p.a_sm + c0 + kq : zero, la + (NWV * i + w) * 1024);
       }
     } else if constexpr (AM == A_M) {
 #pragma unroll
       for (int i = 0; i < NA; ++i) {
-        dma16((amok && ai[i] < kend) ? aptr[i] : zero, la + (4 * i + w) * 1024);
+        dma16((amok && ai[i] < kend) ? aptr[i] : zero, la + (NWV * i + w) * 1024);
         ai[i] += BK;
         aptr[i] += (int64_t)BK * p.a_sk;
       }
@@ -629,14 +635,14 @@ __global__ void __launch_bounds__(256) gemm_lds_kernel(GemmP p) {
         const int row = n + atap - shift;
         const bool ok = amok && pos < kend && row >= 0 && row < p.a_L;
         dma16(ok ? A + (int64_t)(s * p.a_L + row) * p.a_sm + ac0 + amq : zero,
-              la + (4 * i + w) * 1024);
+              la + (NWV * i + w) * 1024);
         ai[i] += BK;
       }
     }
     if constexpr (BMD == B_N) {
 #pragma unroll
       for (int i = 0; i < NB; ++i) {
-        dma16((bnok && bi[i] < kend) ? bptr[i] : zero, lb + (4 * i + w) * 1024);
+        dma16((bnok && bi[i] < kend) ? bptr[i] : zero, lb + (NWV * i + w) * 1024);
         bi[i] += BK;
         bptr[i] += (int64_t)BK * p.b_sk;
       }
@@ -644,7 +650,7 @@ __global__ void __launch_bounds__(256) gemm_lds_kernel(GemmP p) {
       const bool kok = k0 + kq < kend;
 #pragma unroll
       for (int i = 0; i < NB; ++i) {
-        dma16((bi[i] && kok) ? bptr[i] : zero, lb + (4 * i + w) * 1024);
+        dma16((bi[i] && kok) ? bptr[i] : zero, lb + (NWV * i + w) * 1024);
         bptr[i] += BK;
       }
     } else {   // B_FLIP: W[taps-1-tap][n][o], k = tap * C + o (one tap per tile)
@@ -660,7 +666,7 @@ __global__ void __launch_bounds__(256) gemm_lds_kernel(GemmP p) {
       const bool kok = k0 + kq < kend;
 #pragma unroll
       for (int i = 0; i < NB; ++i)
-        dma16((bi[i] && kok) ? bptr[i] + off : zero, lb + (4 * i + w) * 1024);
+        dma16((bi[i] && kok) ? bptr[i] + off : zero, lb + (NWV * i + w) * 1024);
     }
   };
 
@@ -947,7 +953,7 @@ template <int BM, int BN>
 static hipError_t launch_lds_tiles(int am, int bm, dim3 grid, hipStream_t s, const GemmP& p) {
 #define SAT_GEMM_CASE(A_, B_)                                                               \
   if (am == A_ && bm == B_) {                                                               \
-    hipLaunchKernelGGL((gemm_lds_kernel<BM, BN, A_, B_>), grid, dim3(256), 0, s, p);       \
+    hipLaunchKernelGGL((gemm_lds_kernel<BM, BN, A_, B_>), grid, dim3(64 * lds_waves<BM, BN>()), 0, s, p); \
     return hipGetLastError();                                                               \
   }
   SAT_GEMM_CASE(A_K, B_N)
@@ -1014,11 +1020,11 @@ template <int BM, int BN, int GRP>
 static hipError_t launch_lds_grp(int am, int bm, dim3 grid, hipStream_t s, const GemmP& p) {
   if constexpr (GRP == 0) return launch_lds_tiles<BM, BN>(am, bm, grid, s, p);
   if constexpr (GRP == 1)
-    hipLaunchKernelGGL((gemm_lds_kernel<BM, BN, A_IM2COL, B_N, 1>), grid, dim3(256), 0, s, p);
+    hipLaunchKernelGGL((gemm_lds_kernel<BM, BN, A_IM2COL, B_N, 1>), grid, dim3(64 * lds_waves<BM, BN>()), 0, s, p);
   if constexpr (GRP == 2)
-    hipLaunchKernelGGL((gemm_lds_kernel<BM, BN, A_IM2COL, B_FLIP, 2>), grid, dim3(256), 0, s, p);
+    hipLaunchKernelGGL((gemm_lds_kernel<BM, BN, A_IM2COL, B_FLIP, 2>), grid, dim3(64 * lds_waves<BM, BN>()), 0, s, p);
   if constexpr (GRP == 3)
-    hipLaunchKernelGGL((gemm_lds_kernel<BM, BN, A_IM2COLT, B_N, 3>), grid, dim3(256), 0, s, p);
+    hipLaunchKernelGGL((gemm_lds_kernel<BM, BN, A_IM2COLT, B_N, 3>), grid, dim3(64 * lds_waves<BM, BN>()), 0, s, p);
   return hipGetLastError();
 }
 

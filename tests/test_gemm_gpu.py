@@ -153,3 +153,48 @@ def test_conv_bank_matches_per_conv_oracle(cuda, max_k, C, Co, S, L):
     assert _rel(dxd, x.grad + dx0.double()) < 2e-6
     dW_ref = torch.cat([w.grad.reshape(-1) for w in Ws]) + dW0.double()
     assert _rel(dWd, dW_ref) < 2e-6
+
+
+# ---- forced plans: every tile shape incl. the 8-wave 128 x 128 variant, with and without split-K
+@pytest.mark.parametrize("bm,bn,s", [(128, 128, 1), (128, 128, 4), (128, 64, 2), (64, 128, 1),
+                                     (64, 64, 3)])
+@pytest.mark.parametrize("M,N,K", [(1000, 520, 2048), (130, 260, 1024)])
+@pytest.mark.parametrize("ta,tb", [(False, False), (True, False), (False, True), (True, True)])
+def test_gemm_lds_forced_plans(cuda, bm, bn, s, M, N, K, ta, tb):
+    from sat_amd import _lib, kernels
+    g = torch.Generator().manual_seed(M + 5 * N + 11 * K + bm + s)
+    A = torch.randn(K, M, generator=g) if ta else torch.randn(M, K, generator=g)
+    B = torch.randn(N, K, generator=g) if tb else torch.randn(K, N, generator=g)
+    C0 = torch.randn(M, N, generator=g)
+    C = C0.to(cuda)
+    Ad, Bd = A.to(cuda), B.to(cuda)
+    lib = _lib.load()
+    lib.sat_gemm_force_plan(bm, bn, s)
+    try:
+        kernels.gemm(Ad.t() if ta else Ad, Bd.t() if tb else Bd, C, alpha=1.25, beta=0.5)
+        torch.cuda.synchronize()
+    finally:
+        lib.sat_gemm_force_plan(0, 0, 0)
+    Al, Bl = (A.t() if ta else A).double(), (B.t() if tb else B).double()
+    ref = 1.25 * (Al @ Bl) + 0.5 * C0.double()
+    bound = 6e-7 * (Al.abs() @ Bl.abs() + C0.double().abs()) + 1e-7
+    err = (C.double().cpu() - ref).abs()
+    assert bool((err <= bound).all()), float((err / bound).max())
+
+
+@pytest.mark.parametrize("bm,bn", [(128, 128), (64, 64)])
+def test_conv1d_forced_plans(cuda, bm, bn):
+    from sat_amd import _lib, kernels
+    g = torch.Generator().manual_seed(bm + bn)
+    x = torch.randn(6, 50, 128, generator=g)
+    W = torch.randn(5, 128, 256, generator=g)
+    lib = _lib.load()
+    lib.sat_gemm_force_plan(bm, bn, 1)
+    try:
+        y = kernels.conv1d(x.to(cuda), W.to(cuda)).cpu().double()
+        torch.cuda.synchronize()
+    finally:
+        lib.sat_gemm_force_plan(0, 0, 0)
+    xp = torch.nn.functional.pad(x.double().transpose(1, 2), (2, 2))
+    ref = torch.nn.functional.conv1d(xp, W.double().permute(2, 1, 0)).transpose(1, 2)
+    assert float((y - ref).abs().max()) <= 2e-4 * float(ref.abs().max())

@@ -199,6 +199,16 @@ int sat_gemm_rowdot(int32_t M, int32_t N, int32_t K, const float* A, int64_t lda
  * (PreNet, ZoneoutLSTMCell, modules/self_attention.py:60). */
 int sat_rng_fill(float* out, int64_t n, const uint64_t* seed_ptr, uint64_t stream_id,
                  float keep, float on_value, void* stream);
+/* Several masks laid out back to back in one buffer (the training step's mask arena), ONE
+ * launch: segment s covers out[offset, offset + n) and draws exactly what
+ * sat_rng_fill(out + offset, n, seed_ptr, stream_id, keep, on_value) draws.  nseg <= 32. */
+typedef struct SatRngSegment {
+  int64_t offset, n;
+  uint64_t stream_id;
+  float keep, on_value;
+} SatRngSegment;
+int sat_rng_fill_segments(float* out, const SatRngSegment* segs, int32_t nseg,
+                          const uint64_t* seed_ptr, void* stream);
 int sat_counter_add(uint64_t* counter, uint64_t inc, void* stream);
 
 /* Free-running decoding: the termination test of the tacotron2 StopTokenBasedInferenceHelper

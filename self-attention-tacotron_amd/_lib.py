@@ -76,6 +76,11 @@ SatMha = _struct("SatMha", """
     ptr:dy ptr:dx ptr:dWq ptr:dbq ptr:dWk ptr:dbk ptr:dWv ptr:dbv ptr:dWo ptr:dbo ptr:scratch
     i64:scratch_bytes ptr:gemm_ws i64:gemm_ws_bytes""")
 
+class SatRngSegment(ctypes.Structure):      # mirrors include/sat_abi.h
+    _fields_ = [("offset", ctypes.c_int64), ("n", ctypes.c_int64), ("stream_id", ctypes.c_uint64),
+                ("keep", ctypes.c_float), ("on_value", ctypes.c_float)]
+
+
 SatDims = _struct("SatDims", """
     i32:B i32:N i32:Tp i32:enc_heads i32:dec_heads i32:enc_D i32:dec_D i32:max_cols""")
 
@@ -145,6 +150,7 @@ SIGNATURES = {
     "sat_mha_bwd": [ctypes.POINTER(SatMha), _P],
     "sat_cbhg_convbank_bwd": [ctypes.POINTER(SatConvBank), _P],
     "sat_rng_fill": [_P, _I64, _P, _U64, _F, _F, _P],
+    "sat_rng_fill_segments": [_P, ctypes.POINTER(SatRngSegment), _I32, _P, _P],
     "sat_counter_add": [_P, _U64, _P],
     "sat_stop_check": [_P, _I64, _I32, _I32, _I32, _P, _P],
     "sat_lstm_step_fwd": [ctypes.POINTER(SatLstmFwd), _P],

@@ -48,6 +48,38 @@ __global__ void rng_fill_kernel(float* __restrict__ out, int64_t n, const uint64
   }
 }
 
+// sat_rng_fill_segments: the masks of a training step in one launch.  Thread group g of the
+// concatenated group ranges draws exactly what rng_fill_kernel draws for group g - gstart[s] of
+// segment s (same Philox counter and key), so every mask is bit-identical to its own launch.
+constexpr int kMaxRngSeg = 32;
+struct RngSegs {
+  int nseg;
+  int64_t gstart[kMaxRngSeg + 1];
+  SatRngSegment seg[kMaxRngSeg];
+};
+__global__ void rng_fill_segments_kernel(float* __restrict__ out, const uint64_t* seed_ptr,
+                                         RngSegs ss) {
+  const uint64_t seed = seed_ptr[0];
+  const uint2 key = make_uint2((uint32_t)seed, (uint32_t)(seed >> 32));
+  const int64_t total = ss.gstart[ss.nseg];
+  for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < total;
+       g += (int64_t)gridDim.x * blockDim.x) {
+    int s = 0;
+    while (s + 1 < ss.nseg && ss.gstart[s + 1] <= g) ++s;
+    const SatRngSegment sg = ss.seg[s];
+    const int64_t gl = g - ss.gstart[s];
+    const uint4 r = philox(make_uint4((uint32_t)gl, (uint32_t)(gl >> 32), (uint32_t)sg.stream_id,
+                                      (uint32_t)(sg.stream_id >> 32)), key);
+    const uint32_t v[4] = {r.x, r.y, r.z, r.w};
+    const float inv = 2.3283064365386963e-10f;  // 2^-32
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t i = gl * 4 + j;
+      if (i < sg.n) out[sg.offset + i] = ((float)v[j] * inv < sg.keep) ? sg.on_value : 0.f;
+    }
+  }
+}
+
 __global__ void counter_add_kernel(uint64_t* c, uint64_t inc) { c[0] += inc; }
 
 }  // namespace
@@ -83,6 +115,29 @@ extern "C" int sat_rng_fill(float* out, int64_t n, const uint64_t* seed_ptr, uin
   hipLaunchKernelGGL(rng_fill_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), out, n,
                      seed_ptr, stream_id, keep, on_value);
   SAT_LAUNCH_CHECK("sat_rng_fill");
+  return SAT_OK;
+}
+
+extern "C" int sat_rng_fill_segments(float* out, const SatRngSegment* segs, int32_t nseg,
+                                     const uint64_t* seed_ptr, void* stream) {
+  using namespace sat;
+  SAT_CHECK_ARG(nseg >= 0 && nseg <= kMaxRngSeg, "sat_rng_fill_segments: 0 <= nseg <= 32");
+  if (nseg == 0) return SAT_OK;
+  SAT_CHECK_ARG(out && segs && seed_ptr, "sat_rng_fill_segments: null pointer");
+  RngSegs ss;
+  ss.nseg = nseg;
+  ss.gstart[0] = 0;
+  for (int s = 0; s < nseg; ++s) {
+    SAT_CHECK_ARG(segs[s].n >= 0 && segs[s].offset >= 0, "sat_rng_fill_segments: bad segment");
+    ss.seg[s] = segs[s];
+    ss.gstart[s + 1] = ss.gstart[s] + (segs[s].n + 3) / 4;
+  }
+  const int64_t groups = ss.gstart[nseg];
+  if (groups == 0) return SAT_OK;
+  const int blocks = (int)std::min<int64_t>((groups + 255) / 256, 8192);
+  hipLaunchKernelGGL(rng_fill_segments_kernel, dim3(blocks), dim3(256), 0, as_stream(stream),
+                     out, seed_ptr, ss);
+  SAT_LAUNCH_CHECK("sat_rng_fill_segments");
   return SAT_OK;
 }
 

@@ -261,6 +261,22 @@ def rng_fill(out: torch.Tensor, seed_dev: torch.Tensor, stream_id: int, keep: fl
     return out
 
 
+def rng_segments(specs):
+    """ctypes array of SatRngSegment from (offset, n, stream_id, keep, on_value) tuples."""
+    arr = (_lib.SatRngSegment * len(specs))()
+    for i, (off, n, sid, keep, on) in enumerate(specs):
+        arr[i].offset, arr[i].n, arr[i].stream_id = off, n, sid
+        arr[i].keep, arr[i].on_value = keep, on
+    return arr
+
+
+def rng_fill_segments(base: torch.Tensor, segs, seed_dev: torch.Tensor):
+    """Every segment of ``base`` (a flat float32 arena) in ONE launch, each drawing exactly what
+    rng_fill on its own view with the same stream id would draw."""
+    _lib.call("sat_rng_fill_segments", _p(base), segs, len(segs), _p(seed_dev), _stream())
+    return base
+
+
 def seq_mask(x: torch.Tensor, lengths: torch.Tensor, out=None):
     B, N, C = x.shape
     if out is None:

@@ -76,19 +76,22 @@ class Trainer:
             self._mask_arena = torch.empty(need, device=self.m.device)
         self.masks: Dict[str, torch.Tensor] = {}
         off = 0
-        for s in self.specs:
+        segs = []
+        for i, s in enumerate(self.specs):
             n = int(np.prod(s.shape))
             self.masks[s.name] = self._mask_arena[off:off + n].view(s.shape)
+            keep = 1.0 - s.rate
+            on = 1.0 / keep if s.kind == "dropout" else 1.0
+            segs.append((off, n, i + 1, keep, on))
             off += n
+        self._mask_segs = K.rng_segments(segs)
         self.shape = (B, N, Tp)
 
     def draw_masks(self):
-        """One Philox launch per mask tensor; stream ids are fixed per mask, the seed advances
-        on the device every step."""
-        for i, s in enumerate(self.specs):
-            keep = 1.0 - s.rate
-            on = 1.0 / keep if s.kind == "dropout" else 1.0
-            K.rng_fill(self.masks[s.name], self.seed, i + 1, keep, on)
+        """All masks in ONE Philox launch over the mask arena (sat_rng_fill_segments); each
+        mask keeps its fixed stream id, so it is bit-identical to its own sat_rng_fill launch;
+        the seed advances on the device every step."""
+        K.rng_fill_segments(self._mask_arena, self._mask_segs, self.seed)
 
     def forward_backward(self, batch):
         self.draw_masks()

@@ -198,3 +198,25 @@ def test_conv1d_forced_plans(cuda, bm, bn):
     xp = torch.nn.functional.pad(x.double().transpose(1, 2), (2, 2))
     ref = torch.nn.functional.conv1d(xp, W.double().permute(2, 1, 0)).transpose(1, 2)
     assert float((y - ref).abs().max()) <= 2e-4 * float(ref.abs().max())
+
+
+def test_rng_fill_segments_equals_per_mask_fills(cuda):
+    """sat_rng_fill_segments (the step's masks in one launch) draws, per segment, exactly what
+    sat_rng_fill draws on that segment's view with the same stream id."""
+    from sat_amd import kernels
+    sizes = [(5, 0.5, 2.0), (1000, 0.9, 1.0), (4097, 0.1, 10.0), (0, 0.5, 2.0), (64, 0.7, 1.0)]
+    total = sum(n for n, _, _ in sizes) + 7
+    seed = torch.tensor([0x1234_5678_9abc], dtype=torch.int64, device=cuda)
+    base = torch.full((total,), -1.0, device=cuda)
+    segs, off = [], 3
+    for i, (n, keep, on) in enumerate(sizes):
+        segs.append((off, n, 11 + i, keep, on))
+        off += n
+    end = off
+    kernels.rng_fill_segments(base, kernels.rng_segments(segs), seed)
+    for o, n, sid, keep, on in segs:
+        ref = torch.empty(max(n, 1), device=cuda)[:n]
+        if n:
+            kernels.rng_fill(ref, seed, sid, keep, on)
+        assert torch.equal(base[o:o + n], ref)
+    assert float(base[:3].max()) == -1.0 and float(base[end:].max()) == -1.0   # untouched

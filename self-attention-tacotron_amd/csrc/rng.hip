@@ -48,9 +48,9 @@ __global__ void rng_fill_kernel(float* __restrict__ out, int64_t n, const uint64
   }
 }
 
-// sat_rng_fill_segments: the masks of a training step in one launch.  Thread group g of the
-// concatenated group ranges draws exactly what rng_fill_kernel draws for group g - gstart[s] of
-// segment s (same Philox counter and key), so every mask is bit-identical to its own launch.
+// sat_rng_fill_segments: the masks of a training step in one launch.  Group gl of segment s
+// draws exactly what rng_fill_kernel draws for group gl of its own launch (same Philox counter
+// and key), so every mask is bit-identical to its own launch.
 constexpr int kMaxRngSeg = 32;
 struct RngSegs {
   int nseg;
@@ -59,23 +59,28 @@ struct RngSegs {
 };
 __global__ void rng_fill_segments_kernel(float* __restrict__ out, const uint64_t* seed_ptr,
                                          RngSegs ss) {
+  // segment = blockIdx.y (uniform: its fields stay in scalar registers), grid-stride over its
+  // groups along x
   const uint64_t seed = seed_ptr[0];
   const uint2 key = make_uint2((uint32_t)seed, (uint32_t)(seed >> 32));
-  const int64_t total = ss.gstart[ss.nseg];
-  for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < total;
-       g += (int64_t)gridDim.x * blockDim.x) {
-    int s = 0;
-    while (s + 1 < ss.nseg && ss.gstart[s + 1] <= g) ++s;
-    const SatRngSegment sg = ss.seg[s];
-    const int64_t gl = g - ss.gstart[s];
+  const SatRngSegment sg = ss.seg[blockIdx.y];
+  const int64_t groups = (sg.n + 3) / 4;
+  for (int64_t gl = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; gl < groups;
+       gl += (int64_t)gridDim.x * blockDim.x) {
     const uint4 r = philox(make_uint4((uint32_t)gl, (uint32_t)(gl >> 32), (uint32_t)sg.stream_id,
                                       (uint32_t)(sg.stream_id >> 32)), key);
     const uint32_t v[4] = {r.x, r.y, r.z, r.w};
     const float inv = 2.3283064365386963e-10f;  // 2^-32
+    float o[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int64_t i = gl * 4 + j;
-      if (i < sg.n) out[sg.offset + i] = ((float)v[j] * inv < sg.keep) ? sg.on_value : 0.f;
+    for (int j = 0; j < 4; ++j) o[j] = ((float)v[j] * inv < sg.keep) ? sg.on_value : 0.f;
+    const int64_t i0 = sg.offset + gl * 4;
+    if ((reinterpret_cast<uintptr_t>(out + i0) & 15) == 0 && gl * 4 + 3 < sg.n) {   // one 16-B store
+      *reinterpret_cast<float4*>(out + i0) = make_float4(o[0], o[1], o[2], o[3]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (gl * 4 + j < sg.n) out[i0 + j] = o[j];
     }
   }
 }
@@ -132,10 +137,11 @@ extern "C" int sat_rng_fill_segments(float* out, const SatRngSegment* segs, int3
     ss.seg[s] = segs[s];
     ss.gstart[s + 1] = ss.gstart[s] + (segs[s].n + 3) / 4;
   }
-  const int64_t groups = ss.gstart[nseg];
-  if (groups == 0) return SAT_OK;
-  const int blocks = (int)std::min<int64_t>((groups + 255) / 256, 8192);
-  hipLaunchKernelGGL(rng_fill_segments_kernel, dim3(blocks), dim3(256), 0, as_stream(stream),
+  int64_t gmax = 0;
+  for (int s = 0; s < nseg; ++s) gmax = std::max<int64_t>(gmax, (segs[s].n + 3) / 4);
+  if (gmax == 0) return SAT_OK;
+  const int blocks = (int)std::min<int64_t>((gmax + 255) / 256, 1024);
+  hipLaunchKernelGGL(rng_fill_segments_kernel, dim3(blocks, nseg), dim3(256), 0, as_stream(stream),
                      out, seed_ptr, ss);
   SAT_LAUNCH_CHECK("sat_rng_fill_segments");
   return SAT_OK;

@@ -127,7 +127,9 @@ def decoder_bwd(P, G, hp, d, dsv, dH2, masks, ws, attn_tile=32, pipe: Pipeline =
     # [dL/dctx_t | recurrent product of the attention RNN] per step: the per-step row-dot with
     # DG0[t+1] fills both halves at once (the ctx half on top of LSTM1's contribution), so the
     # attention RNN's reverse step only does the query-gradient dot
-    RD = torch.zeros(Tp, B, M1 + M2 + A, **f32)
+    # RD and the per-step path's carries (YA, hc, cc below) zeroed by ONE fill
+    RD, ya0, ya1, hc0, hc1, cc0, cc1 = K.zeros_group(
+        (Tp, B, M1 + M2 + A), (B, N), (B, N), (B, A), (B, A), (B, A), (B, A), device=dev)
     DCTX = RD[:, :, :M1 + M2]
     run2, run1 = _LstmBwd(B, Dd, dev), _LstmBwd(B, Dd, dev)
     m2c, m2h, m1c, m1h = (mk("dec/lstm2/zc"), mk("dec/lstm2/zh"), mk("dec/lstm1/zc"),
@@ -164,7 +166,7 @@ def decoder_bwd(P, G, hp, d, dsv, dH2, masks, ws, attn_tile=32, pipe: Pipeline =
     fwd = d.att1 == "forward"
     ntiles = (N + attn_tile - 1) // attn_tile
     DG0 = torch.empty(Tp, B, 4 * A, **f32)
-    YA = [torch.zeros(B, N, **f32), torch.zeros(B, N, **f32)]   # alignment-recursion grads
+    YA = [ya0, ya1]                                          # alignment-recursion grads
     DFH = torch.empty(Tp, B, N, max(d.loc_f, 1), **f32)     # location-feature gradient history
     DE1 = torch.empty(Tp, B, N, **f32)                      # energy-gradient histories
     DE2 = torch.empty(Tp, B, N, **f32)
@@ -173,8 +175,8 @@ def decoder_bwd(P, G, hp, d, dsv, dH2, masks, ws, attn_tile=32, pipe: Pipeline =
     dq_parts = (int(_lib.load().sat_decoder_attention_bwd_dq_parts(B, N))
                 if S.get("attn_scratch") is not None else ntiles)
     DQP = torch.empty(Tp, B, dq_parts, D1 + D2, **f32)
-    hc = [torch.zeros(B, A, **f32), torch.zeros(B, A, **f32)]
-    cc = [torch.zeros(B, A, **f32), torch.zeros(B, A, **f32)]
+    hc = [hc0, hc1]
+    cc = [cc0, cc1]
     mc0, mh0 = mk("dec/lstm0/zc"), mk("dec/lstm0/zh")
     chain = {"cur": 0}
 

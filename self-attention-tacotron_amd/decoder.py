@@ -126,13 +126,14 @@ def decoder_forward(P: Dict[str, torch.Tensor], hp, d: Dims, m1: torch.Tensor, m
     W0 = P["decoder/attention_lstm/kernel"]          # [p + M1 + M2 + A, 4A] (gate-interleaved)
     X0 = K.linear(pre, W0[:p_w], P["decoder/attention_lstm/bias"])     # [T', B, 4A]
     R0 = M1 + M2 + A                                 # recurrent input [c1 | c2 | h0]
-    REC0 = torch.zeros(Tp + 1, B, R0, **f32)
-    C0 = torch.zeros(Tp + 1, B, A, **f32)
+    # zero-initialised state histories (row 0 = initial state), one fill for all of them and
+    # for the decoder LSTMs' c / h histories below
+    REC0, C0, S1, AL1, c1z, h1z, c2z, h2z = K.zeros_group(
+        (Tp + 1, B, R0), (Tp + 1, B, A), (Tp + 1, B, N), (Tp + 1, B, N),
+        (Tp + 1, B, Dd), (Tp + 1, B, Dd), (Tp + 1, B, Dd), (Tp + 1, B, Dd), device=dev)
     H0RAW = torch.empty(Tp, B, A, **f32)
     G0 = torch.empty(Tp, B, 4 * A, **f32)
     Q = torch.empty(Tp, B, D1 + D2, **f32)
-    S1 = torch.zeros(Tp + 1, B, N, **f32)
-    AL1 = torch.zeros(Tp + 1, B, N, **f32)
     AL1[0, :, 0] = 1.0                               # forward_attention.py:131-133
     S2 = torch.empty(Tp, B, N, **f32)
     ST = torch.empty(Tp, B, 4, **f32)
@@ -182,8 +183,8 @@ def decoder_forward(P: Dict[str, torch.Tensor], hp, d: Dims, m1: torch.Tensor, m
     W2 = P["decoder/lstm2/kernel"]                   # [D + D, 4D]
     X1 = torch.empty(Tp, B, 4 * Dd, **f32)
     X2 = torch.empty(Tp, B, 4 * Dd, **f32)
-    L1 = _lstm_buffers(Tp, B, Dd, f32)
-    L2 = _lstm_buffers(Tp, B, Dd, f32)
+    L1 = _lstm_buffers(Tp, B, Dd, f32, c1z, h1z)
+    L2 = _lstm_buffers(Tp, B, Dd, f32, c2z, h2z)
     m1c, m1h, m2c, m2h = (mk("dec/lstm1/zc"), mk("dec/lstm1/zh"), mk("dec/lstm2/zc"),
                           mk("dec/lstm2/zh"))
 
@@ -272,10 +273,13 @@ def decoder_forward(P: Dict[str, torch.Tensor], hp, d: Dims, m1: torch.Tensor, m
     return H2RAW, DecoderSaved(B, N, Tp, S)
 
 
-def _lstm_buffers(Tp, B, U, f32):
-    """(h_raw [T',B,U], c [T'+1,B,U], h [T'+1,B,U], gates [T',B,4U]) histories."""
-    return (torch.empty(Tp, B, U, **f32), torch.zeros(Tp + 1, B, U, **f32),
-            torch.zeros(Tp + 1, B, U, **f32), torch.empty(Tp, B, 4 * U, **f32))
+def _lstm_buffers(Tp, B, U, f32, c=None, h=None):
+    """(h_raw [T',B,U], c [T'+1,B,U], h [T'+1,B,U], gates [T',B,4U]) histories (c, h zeroed:
+    given from a zeros_group, or allocated here)."""
+    return (torch.empty(Tp, B, U, **f32),
+            c if c is not None else torch.zeros(Tp + 1, B, U, **f32),
+            h if h is not None else torch.zeros(Tp + 1, B, U, **f32),
+            torch.empty(Tp, B, 4 * U, **f32))
 
 
 def _lstm_desc(X, Wr, t, B, U, zc, zh, mc, mh, bufs):

@@ -254,6 +254,20 @@ def stop_check(stop: torch.Tensor, t: int, min_iters: int, state: torch.Tensor):
               _p(state), _stream())
 
 
+def zeros_group(*shapes, device):
+    """Several zero-initialised float32 tensors carved from ONE zeroed buffer (one fill launch
+    instead of one per tensor in the captured step); every piece starts on a 256-byte boundary
+    (the kernels' 16-byte operand alignment)."""
+    sizes = [int(torch.Size(sh).numel()) for sh in shapes]
+    pads = [(n + 63) // 64 * 64 for n in sizes]
+    buf = torch.zeros(sum(pads), device=device, dtype=torch.float32)
+    out, off = [], 0
+    for sh, n, pn in zip(shapes, sizes, pads):
+        out.append(buf[off:off + n].view(sh))
+        off += pn
+    return out
+
+
 def rng_fill(out: torch.Tensor, seed_dev: torch.Tensor, stream_id: int, keep: float,
              on_value: float):
     _lib.call("sat_rng_fill", _p(out), out.numel(), _p(seed_dev), stream_id, keep, on_value,

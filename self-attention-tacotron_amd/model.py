@@ -168,11 +168,12 @@ def encoder_fwd(P, bn: BNState, hp, d: PR.Dims, ids, lengths, masks, training, w
     # the two directions are independent recurrences: step n of the forward cell and step
     # N-1-n of the backward cell run as ONE multi-problem launch (sat_lstm_steps_fwd)
     lstm = {}
-    for dr in ("fw", "bw"):
+    zs = K.zeros_group(*([(N + 1, B, U)] * 4), device=dev)   # c / h histories, one fill
+    for i, dr in enumerate(("fw", "bw")):
         Wk = P[f"encoder/cbhg/lstm_{dr}/kernel"]
         lstm[dr] = dict(
             X=K.linear(hw, Wk[:hw.shape[-1]], P[f"encoder/cbhg/lstm_{dr}/bias"]),  # [B, N, 4U]
-            CS=torch.zeros(N + 1, B, U, device=dev), HS=torch.zeros(N + 1, B, U, device=dev),
+            CS=zs[2 * i], HS=zs[2 * i + 1],
             G=torch.empty(N, B, 4 * U, device=dev))
 
     def enc_step(dr, rev, n):

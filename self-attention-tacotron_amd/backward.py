@@ -82,8 +82,9 @@ class _LstmBwd:
     ping-pong between two buffers)."""
 
     def __init__(self, B, U, dev):
-        self.hc = [torch.zeros(B, U, device=dev), torch.zeros(B, U, device=dev)]
-        self.cc = [torch.zeros(B, U, device=dev), torch.zeros(B, U, device=dev)]
+        h0, h1, c0, c1 = K.zeros_group(*([(B, U)] * 4), device=dev)   # one fill
+        self.hc = [h0, h1]
+        self.cc = [c0, c1]
         self.first = True
         self.cur = 0
 

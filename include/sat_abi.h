@@ -82,6 +82,10 @@ typedef struct SatGemmDesc {
   int64_t add_sm, add_sbatch;
   void* ws;
   int64_t ws_bytes;
+  /* optional: also colsum_out[n] = alpha * sum_k B[k][n] + beta * colsum_out[n] in the same
+   * launch (the bias gradient of a weight-gradient product dW = X^T dY, db = 1^T dY); needs a
+   * batch-1 product without bias / act / mul / add.  NULL = off. */
+  float* colsum_out;
 } SatGemmDesc;
 
 int sat_gemm(const SatGemmDesc* desc, void* stream);

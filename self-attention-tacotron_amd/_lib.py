@@ -41,6 +41,7 @@ class SatGemmDesc(ctypes.Structure):
         ("c_sbatch2", ctypes.c_int64), ("mul_sbatch2", ctypes.c_int64),
         ("add", ctypes.c_void_p), ("add_sm", ctypes.c_int64), ("add_sbatch", ctypes.c_int64),
         ("ws", ctypes.c_void_p), ("ws_bytes", ctypes.c_int64),
+        ("colsum_out", ctypes.c_void_p),
     ]
 
 

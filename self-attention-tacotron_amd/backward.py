@@ -25,9 +25,7 @@ def lin_bwd(x, dy, W, dW, db, ws, dx=None, beta_dx=0.0, need_dx=True):
     """Dense backward: dW += x^T dy, db += colsum(dy), dx (=|+=) dy W^T.  x [.., in], dy [.., out]."""
     x2 = x.reshape(-1, x.shape[-1])
     dy2 = dy.reshape(-1, dy.shape[-1])
-    K.gemm(x2.t(), dy2, dW, beta=1.0)
-    if db is not None:
-        K.colsum(dy2, db, ws, beta=1.0)
+    K.gemm(x2.t(), dy2, dW, beta=1.0, colsum=db)     # db += colsum(dy) in the same launch
     if not need_dx:
         return None
     if dx is None:
@@ -291,10 +289,10 @@ def decoder_bwd(P, G, hp, d, dsv, dH2, masks, ws, attn_tile=32, pipe: Pipeline =
     DG2f = DG2.view(Tp * B, 4 * Dd)
     DG1f = DG1.view(Tp * B, 4 * Dd)
     K.gemm(S["H2S"][:Tp].reshape(Tp * B, Dd).t(), DG2f, dW2[Dd:], beta=1.0)
-    K.gemm(S["H1RAW"].view(Tp * B, Dd).t(), DG2f, dW2[:Dd], beta=1.0)
-    K.colsum(DG2f, G["decoder/lstm2/bias"], ws)
-    K.gemm(S["H1S"][:Tp].reshape(Tp * B, Dd).t(), DG1f, dW1[A + M1 + M2:], beta=1.0)
-    K.colsum(DG1f, G["decoder/lstm1/bias"], ws)
+    K.gemm(S["H1RAW"].view(Tp * B, Dd).t(), DG2f, dW2[:Dd], beta=1.0,
+           colsum=G["decoder/lstm2/bias"])                     # + the bias gradient
+    K.gemm(S["H1S"][:Tp].reshape(Tp * B, Dd).t(), DG1f, dW1[A + M1 + M2:], beta=1.0,
+           colsum=G["decoder/lstm1/bias"])
     ctx_all = S["REC0"][1:].reshape(Tp * B, R0)[:, :M1 + M2]
     K.gemm(S["H0RAW"].view(Tp * B, A).t(), DG1f, dW1[:A], beta=1.0)
     K.gemm(ctx_all.t(), DG1f, dW1[A:A + M1 + M2], beta=1.0)
@@ -445,8 +443,8 @@ def encoder_bwd(P, G, hp, d, sv, dm1, dm2, lengths, masks, ws):
         DGf = DG.view(N * B, 4 * U)
         hprev = st["HS"][1:N + 1] if rev else st["HS"][:N]
         K.gemm(hprev.reshape(N * B, U).t(), DGf, dWk[Win:], beta=1.0)
-        K.gemm(hw_sm.view(N * B, Win).t(), DGf, dWk[:Win], beta=1.0)
-        K.colsum(DGf, G[f"encoder/cbhg/lstm_{dr}/bias"], ws)
+        K.gemm(hw_sm.view(N * B, Win).t(), DGf, dWk[:Win], beta=1.0,
+               colsum=G[f"encoder/cbhg/lstm_{dr}/bias"])      # + the bias gradient
         # dhw[b, n, :] (+)= DG[n, b, :] @ Wx^T  -- batched over n, written transposed
         K.gemm(DG, Wk[:Win].t(), dhw.transpose(0, 1), beta=1.0 if i else 0.0)
     # highway stack

@@ -48,6 +48,10 @@ struct GemmP {
   float* ws;
   int remap;                   // XCD-aware tile order over the xy plane
   int probe;                   // sat_gemm_probe_mode: 1 skip DMA, 2 skip epilogue (probes only)
+  // fused column sums of B (SatGemmDesc.colsum_out): the LDS kernel treats A as having one more
+  // row of ones (index m_real = M - 1), whose output row goes to cs_out instead of C
+  float* cs_out;
+  int m_real;
   int grp_co;                  // conv-bank launches: output channels per conv (GRP > 0)
 };
 
@@ -390,8 +394,11 @@ __global__ void __launch_bounds__(64 * GM * GN) gemm_kernel(GemmP p) {
 // split-K finish: sum S slabs in order, then the same epilogue as gemm_kernel (batch == 1).
 // Four consecutive outputs per thread (16-byte slab loads when N % 4 == 0) and four slab loads
 // in flight per trip: the pass is latency-bound, not bandwidth-bound, at these sizes.
+__device__ __forceinline__ float* out_ptr(const GemmP& p, float* C, int row, int col) {
+  return (p.cs_out && row == p.m_real) ? p.cs_out + col : C + (int64_t)row * p.c_sm + col;
+}
 __device__ __forceinline__ float splitk_epilogue(const GemmP& p, int row, int col, float s) {
-  float* dst = p.C + (int64_t)row * p.c_sm + col;
+  float* dst = out_ptr(p, p.C, row, col);
   float v = p.alpha * s;
   if (p.beta != 0.f) v += p.beta * (*dst);
   v = apply_act(v + (p.bias ? p.bias[col] : 0.f), p.act);
@@ -420,7 +427,7 @@ __global__ void __launch_bounds__(256) gemm_splitk_reduce(GemmP p) {
         a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
       }
       const int row = (int)((4 * i) / p.N), col = (int)(4 * i - (int64_t)row * p.N);
-      float* dst = p.C + (int64_t)row * p.c_sm + col;
+      float* dst = out_ptr(p, p.C, row, col);
       dst[0] = splitk_epilogue(p, row, col, a.x);
       dst[1] = splitk_epilogue(p, row, col + 1, a.y);
       dst[2] = splitk_epilogue(p, row, col + 2, a.z);
@@ -433,7 +440,7 @@ __global__ void __launch_bounds__(256) gemm_splitk_reduce(GemmP p) {
     const int row = (int)(i / p.N), col = (int)(i - (int64_t)row * p.N);
     float s = 0.f;
     for (int k = 0; k < p.splits; ++k) s += p.ws[(int64_t)k * total + i];
-    p.C[(int64_t)row * p.c_sm + col] = splitk_epilogue(p, row, col, s);
+    *out_ptr(p, p.C, row, col) = splitk_epilogue(p, row, col, s);
   }
 }
 
@@ -456,6 +463,11 @@ __global__ void __launch_bounds__(256) gemm_splitk_reduce(GemmP p) {
 // chunk 2 jj + h feeds four consecutive steps.  Out-of-range chunks (tile edges, conv padding)
 // are read from a zero page, so the loads need no branches and no masks.
 __device__ __attribute__((aligned(16))) float g_gemm_zero[64];
+__device__ __attribute__((aligned(16))) float g_gemm_ones[64] = {
+    1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f,
+    1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f,
+    1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f,
+    1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f};
 
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
@@ -544,6 +556,7 @@ __global__ void __launch_bounds__((64 * lds_waves<BM, BN>())) gemm_lds_kernel(Ge
   const int kbeg = split * p.kchunk;
   const int kend = min(Kt, kbeg + p.kchunk);
   const float* zero = g_gemm_zero;
+  const float* ones = g_gemm_ones;
 
   // ---- per-lane loader state, advanced by one K-tile per issue
   // K-major images: instruction i of wave w covers rows (NWV i + w) * 8 + (lane >> 3); the lane's
@@ -553,12 +566,15 @@ __global__ void __launch_bounds__((64 * lds_waves<BM, BN>())) gemm_lds_kernel(Ge
   const float* aptr[NA];
   int ai[NA];
   const int amq = AKM ? 0 : 4 * (lane % (BM / 4));
+  bool aone[NA];                                       // the fused column-sum row of ones
 #pragma unroll
   for (int i = 0; i < NA; ++i) {
+    aone[i] = false;
     if constexpr (AM == A_K) {
       const int gm = m0 + (NWV * i + w) * 8 + (lane >> 3);
-      ai[i] = gm < p.M;
-      aptr[i] = A + (int64_t)min(gm, p.M - 1) * p.a_sm + kbeg + kq;
+      aone[i] = p.cs_out != nullptr && gm == p.m_real;
+      ai[i] = gm < p.M && !aone[i];
+      aptr[i] = A + (int64_t)min(gm, (p.cs_out ? p.m_real : p.M) - 1) * p.a_sm + kbeg + kq;
     } else if constexpr (AM == A_IM2COL) {   // (utterance, position) of the output row
       const int gm = m0 + (NWV * i + w) * 8 + (lane >> 3);
       const int s = gm / p.a_L, n = gm - s * p.a_L;
@@ -572,7 +588,8 @@ __global__ void __launch_bounds__((64 * lds_waves<BM, BN>())) gemm_lds_kernel(Ge
       aptr[i] = nullptr;
     }
   }
-  const bool amok = AKM ? true : (m0 + amq < p.M);
+  const bool aones = !AKM && p.cs_out != nullptr && m0 + amq == p.m_real;   // m_real % 4 == 0
+  const bool amok = AKM ? true : (m0 + amq < p.M && !aones);
   const float* bptr[NB];
   int bi[NB];
   const int bnq = BKM ? 0 : 4 * (lane % (BN / 4));
@@ -599,7 +616,7 @@ __global__ void __launch_bounds__((64 * lds_waves<BM, BN>())) gemm_lds_kernel(Ge
       const bool kok = k0 + kq < kend;
 #pragma unroll
       for (int i = 0; i < NA; ++i) {
-        dma16((ai[i] && kok) ? aptr[i] : zero, la + (NWV * i + w) * 1024);
+        dma16(kok ? (ai[i] ? aptr[i] : (aone[i] ? ones : zero)) : zero, la + (NWV * i + w) * 1024);
         aptr[i] += BK;
       }
     } else if constexpr (AM == A_IM2COL) {
@@ -623,7 +640,8 @@ __global__ void __launch_bounds__((64 * lds_waves<BM, BN>())) gemm_lds_kernel(Ge
     } else if constexpr (AM == A_M) {
 #pragma unroll
       for (int i = 0; i < NA; ++i) {
-        dma16((amok && ai[i] < kend) ? aptr[i] : zero, la + (NWV * i + w) * 1024);
+        dma16(ai[i] < kend ? (amok ? aptr[i] : (aones ? ones : zero)) : zero,
+              la + (NWV * i + w) * 1024);
         ai[i] += BK;
         aptr[i] += (int64_t)BK * p.a_sk;
       }
@@ -814,7 +832,7 @@ __global__ void __launch_bounds__((64 * lds_waves<BM, BN>())) gemm_lds_kernel(Ge
   const float* bias = p.bias ? p.bias + bz * p.bias_sbatch : nullptr;
   const float* mul = p.mul ? p.mul + bz * p.mul_sbatch + bz2 * p.mul_sbatch2 : nullptr;
   const float* add = p.add ? p.add + bz * p.add_sbatch : nullptr;
-  if (full && !mul && !add && p.beta == 0.f && p.act == 0) {
+  if (full && !mul && !add && p.beta == 0.f && p.act == 0 && !p.cs_out) {
     const int64_t cs = p.c_sm;
 #pragma unroll
     for (int i = 0; i < SM; ++i)
@@ -839,7 +857,7 @@ __global__ void __launch_bounds__((64 * lds_waves<BM, BN>())) gemm_lds_kernel(Ge
       for (int r = 0; r < 16; ++r) {
         const int row = m0 + wm + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
         if (row >= p.M) continue;
-        float* dst = C + (int64_t)row * p.c_sm + col;
+        float* dst = out_ptr(p, C, row, col);
         float v = p.alpha * acc[0][i][j][r];
         if (p.beta != 0.f) v += p.beta * (*dst);
         v = apply_act(v + bv, p.act);
@@ -1080,7 +1098,8 @@ static int launch_lds(const SatGemmDesc* d, GemmP& p, int nb, hipStream_t s) {
   if ((am == A_IM2COL && bm != B_N && bm != B_FLIP) || (am == A_IM2COLT && bm != B_N) ||
       (bm == B_FLIP && am != A_IM2COL))
     return 1;
-  const LdsPlan pl = plan_lds(d->M, d->N, d->K, nb, nb == 1 && d->ws != nullptr,
+  if (p.cs_out && am == A_M && p.m_real % 4 != 0) return 1;   // the ones chunk must start at m_real
+  const LdsPlan pl = plan_lds(p.M, d->N, d->K, nb, nb == 1 && d->ws != nullptr,
                               d->ws_bytes, am == A_IM2COLT ? d->a_C : 0, 0);
   if (pl.bm == 0) return 1;
   return launch_lds_plan<0>(pl, am, bm, nb, p, s, "sat_gemm");
@@ -1113,9 +1132,36 @@ extern "C" int sat_gemm(const SatGemmDesc* d, void* stream) {
   p.mul_sbatch2 = d->mul_sbatch2;
   p.add = d->add; p.add_sm = d->add_sm; p.add_sbatch = d->add_sbatch;
   p.probe = t_probe;
+  p.cs_out = nullptr;
+  p.m_real = d->M;
   hipStream_t s = as_stream(stream);
   const int nb = d->batch * p.batch2;
   p.ws = reinterpret_cast<float*>(d->ws);
+  if (d->colsum_out) {
+    // C = alpha A B + beta C and colsum_out = alpha 1^T B + beta colsum_out (the bias gradient of
+    // a weight-gradient product) in ONE launch: A gets a row of ones
+    SAT_CHECK_ARG(nb == 1 && d->a_mode == 0 && d->b_mode == 0 && !d->bias && d->act == 0 &&
+                      !d->mul && !d->add,
+                  "sat_gemm: colsum_out needs a plain batch-1 product (no bias/act/mul/add)");
+    if (gemm_lds_enabled()) {
+      p.cs_out = d->colsum_out;
+      p.M = d->M + 1;
+      const int r = launch_lds(d, p, nb, s);
+      if (r != 1) return r;
+      p.cs_out = nullptr;
+      p.M = d->M;
+    }
+    // operands not vector-loadable: the product, then the column sums as a separate reduction
+    SatGemmDesc d2 = *d;
+    d2.colsum_out = nullptr;
+    const int rc = sat_gemm(&d2, stream);
+    if (rc != SAT_OK) return rc;
+    const int64_t need = sat_workspace_colreduce(d->K, d->N);
+    SAT_CHECK_ARG(d->ws && d->ws_bytes >= need,
+                  "sat_gemm: colsum_out fallback needs ws_bytes >= sat_workspace_colreduce(K, N)");
+    SAT_CHECK_ARG(d->b_sn == 1, "sat_gemm: colsum_out fallback needs B rows contiguous");
+    return sat_colsum(d->B, d->b_sk, d->K, d->N, d->colsum_out, d->beta, d->ws, stream);
+  }
   if (gemm_lds_enabled()) {
     const int r = launch_lds(d, p, nb, s);
     if (r != 1) return r;   // 1: operand layout not vector-loadable, use the register path

@@ -139,7 +139,6 @@ extern "C" int sat_mha_bwd(const SatMha* d, void* stream) {
   float* dV = reinterpret_cast<float*>(p + 3 * act);
   float* dPd = reinterpret_cast<float*>(p + 4 * act);
   float* dS = reinterpret_cast<float*>(p + 4 * act + score);
-  void* cs = p + 4 * act + 2 * score;
   const float* Pd = d->probs_mask ? d->Pd : d->P;
   auto wgrad = [&](const float* X, int K, const float* dY, int N, float* dW, float* db) -> int {
     SatGemmDesc g = dense_desc();   // dW += X^T dY
@@ -148,8 +147,8 @@ extern "C" int sat_mha_bwd(const SatMha* d, void* stream) {
     g.B = dY; g.b_sk = N; g.b_sn = 1;
     g.C = dW; g.c_sm = N; g.beta = 1.f;
     g.ws = d->gemm_ws; g.ws_bytes = d->gemm_ws_bytes;
+    g.colsum_out = db;                // db += colsum(dY) in the same launch
     SAT_TRY(sat_gemm(&g, s));
-    if (db) SAT_TRY(sat_colsum(dY, N, R, N, db, 1.f, cs, s));
     return SAT_OK;
   };
   auto dgrad = [&](const float* dY, int N, const float* W, int K, float* dX, float beta) {

@@ -84,8 +84,11 @@ def _bstrides(t, nd):
 
 
 def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor = None, *, alpha=1.0, beta=0.0,
-         bias=None, act=None, mul=None, add=None) -> torch.Tensor:
+         bias=None, act=None, mul=None, add=None, colsum=None) -> torch.Tensor:
     """C = act(alpha * A @ B + beta * C + bias) * mul + add.
+
+    ``colsum`` [N] (2-D, plain products only): also colsum = alpha * sum over rows of B + beta *
+    colsum in the same launch (a dense layer's bias gradient next to its weight gradient).
 
     A [.., M, K], B [.., K, N] with up to two leading batch dims (any strides: pass ``x.t()`` /
     ``x.transpose(-1, -2)`` views for transposed operands); C gets the broadcast batch shape.
@@ -128,6 +131,11 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor = None, *, alpha=1.0,
         d.add = _p(add)
         d.add_sm = add.stride(-2) if add.dim() >= 2 else 0
         d.add_sbatch = add.stride(0) if add.dim() == 3 else 0
+    if colsum is not None:
+        _f32(colsum, "colsum")
+        if colsum.numel() != N or not colsum.is_contiguous():
+            raise ValueError("gemm: colsum must be a contiguous [N] tensor")
+        d.colsum_out = _p(colsum)
     _with_ws(d, C.device)
     _launch_gemm(d, "sat_gemm")
     return C

@@ -220,3 +220,33 @@ def test_rng_fill_segments_equals_per_mask_fills(cuda):
             kernels.rng_fill(ref, seed, sid, keep, on)
         assert torch.equal(base[o:o + n], ref)
     assert float(base[:3].max()) == -1.0 and float(base[end:].max()) == -1.0   # untouched
+
+
+# ---- fused column sums (SatGemmDesc.colsum_out): dW += X^T dY and db += colsum(dY) in one launch
+@pytest.mark.parametrize("M,N,K", [(256, 1024, 3000), (128, 260, 500), (36, 64, 7000), (6, 40, 50)])
+@pytest.mark.parametrize("ta", [True, False])
+@pytest.mark.parametrize("split", [0, 4])
+def test_gemm_colsum_fused(cuda, M, N, K, ta, split):
+    from sat_amd import _lib, kernels
+    g = torch.Generator().manual_seed(M + 3 * N + K + split)
+    A = torch.randn(K, M, generator=g) if ta else torch.randn(M, K, generator=g)
+    B = torch.randn(K, N, generator=g)
+    C0 = torch.randn(M, N, generator=g)
+    s0 = torch.randn(N, generator=g)
+    C, s = C0.to(cuda), s0.to(cuda)
+    lib = _lib.load()
+    if split:
+        lib.sat_gemm_force_plan(64, 64, split)
+    try:
+        kernels.gemm(A.to(cuda).t() if ta else A.to(cuda), B.to(cuda), C, alpha=1.0, beta=1.0,
+                     colsum=s)
+        torch.cuda.synchronize()
+    finally:
+        lib.sat_gemm_force_plan(0, 0, 0)
+    Al = (A.t() if ta else A).double()
+    ref = Al @ B.double() + C0.double()
+    rs = B.double().sum(0) + s0.double()
+    bound = 6e-7 * (Al.abs() @ B.double().abs() + C0.double().abs()) + 1e-7
+    assert bool(((C.double().cpu() - ref).abs() <= bound).all())
+    bs = 6e-7 * (B.double().abs().sum(0) + s0.double().abs()) + 1e-7
+    assert bool(((s.double().cpu() - rs).abs() <= bs).all()), float(((s.double().cpu() - rs).abs() / bs).max())

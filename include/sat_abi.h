@@ -572,6 +572,16 @@ int sat_bn_bwd(const float* dy, int64_t lddy, const float* x, int64_t ldx, const
 /* out[c] = beta*out[c] + sum_m x[m][c]   (bias gradients) */
 int sat_colsum(const float* x, int64_t ldx, int32_t M, int32_t C, float* out, float beta,
                void* workspace, void* stream);
+/* Column sums of x scattered into separate parameter gradients (the attention parameters'
+ * per-workgroup partial rows, backward.py): for each segment k, columns [col, col+n) go to
+ * dst[0..n): dst[j] = beta*dst[j] + sum_m x[m][col+j].  1 <= nseg <= 8. */
+typedef struct SatColSegment {
+  float* dst;
+  int32_t col, n;
+} SatColSegment;
+int sat_colsum_scatter(const float* x, int64_t ldx, int32_t M, int32_t C,
+                       const SatColSegment* segs, int32_t nseg, float beta, void* workspace,
+                       void* stream);
 
 /* MaxPooling1D(pool 2, stride 1, SAME) over [B][N][C] (modules/module.py:54,80) and its
  * gradient (first index wins ties, as TF MaxPoolGrad). */

@@ -82,6 +82,10 @@ class SatRngSegment(ctypes.Structure):      # mirrors include/sat_abi.h
                 ("keep", ctypes.c_float), ("on_value", ctypes.c_float)]
 
 
+class SatColSegment(ctypes.Structure):      # mirrors include/sat_abi.h
+    _fields_ = [("dst", ctypes.c_void_p), ("col", ctypes.c_int32), ("n", ctypes.c_int32)]
+
+
 SatDims = _struct("SatDims", """
     i32:B i32:N i32:Tp i32:enc_heads i32:dec_heads i32:enc_D i32:dec_D i32:max_cols""")
 
@@ -179,6 +183,8 @@ SIGNATURES = {
     "sat_bn_bwd": [_P, _I64, _P, _I64, _P, _I64, _P, _I64, _I32, _I32, _P, _P, _F, _P, _P, _P,
                    _I32, _F, _P, _P],
     "sat_colsum": [_P, _I64, _I32, _I32, _P, _F, _P, _P],
+    "sat_colsum_scatter": [_P, _I64, _I32, _I32, ctypes.POINTER(SatColSegment), _I32, _F, _P,
+                           _P],
     "sat_maxpool2": [_P, _P, _I32, _I32, _I32, _P],
     "sat_maxpool2_bwd": [_P, _P, _P, _I32, _I32, _I32, _P],
     "sat_highway_fwd": [_P, _P, _P, _P, _I64, _P],

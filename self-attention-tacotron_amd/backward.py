@@ -329,29 +329,19 @@ def decoder_bwd(P, G, hp, d, dsv, dH2, masks, ws, attn_tile=32, pipe: Pipeline =
         locW=P[f"{a1}/location_layer/kernel"] if fwd else None, v2=P[f"{a2}/attention_v"],
         loc=S["LOC"] if fwd else None, s_prev=S["S1"], s_tstride=S["S1"].stride(0),
         de1=DE1, de2=DE2, df=DFH if fwd else None, dK1=dK1, dK2=dK2, pg=PG, pg_stride=pgs)
-    pg_sum = torch.zeros(pgs, **f32)
-    K.colsum(PG, pg_sum, ws, beta=0.0)
-    o = 0
     if fwd:
-        K.axpby(pg_sum[o:o + D1], G[f"{a1}/attention_variable"], 1.0, 1.0); o += D1
-        K.axpby(pg_sum[o:o + F * D1], G[f"{a1}/location_layer/kernel"].view(-1), 1.0, 1.0)
-        o += F * D1
-        K.axpby(pg_sum[o:o + KW * F], G[f"{a1}/location_conv/kernel"].view(-1), 1.0, 1.0)
-        o += KW * F
-        K.axpby(pg_sum[o:o + F], G[f"{a1}/location_conv/bias"], 1.0, 1.0); o += F
+        dsts = [G[f"{a1}/attention_variable"], G[f"{a1}/location_layer/kernel"].view(-1),
+                G[f"{a1}/location_conv/kernel"].view(-1), G[f"{a1}/location_conv/bias"]]
     else:
-        K.axpby(pg_sum[o:o + D1], G[f"{a1}/attention_v"], 1.0, 1.0); o += D1
-    K.axpby(pg_sum[o:o + D2], G[f"{a2}/attention_v"], 1.0, 1.0)
-    # the per-tile partials of every step sum into the query-layer / bias gradients
-    DQf = DQP.view(Tp * B * dq_parts, D1 + D2)
-    if fwd:
-        qsum = torch.zeros(D1 + D2, **f32)
-        K.colsum(DQf, qsum, ws, beta=0.0)
-        K.axpby(qsum[:D1], G[f"{a1}/attention_bias"], 1.0, 1.0)
+        dsts = [G[f"{a1}/attention_v"]]
+    K.colsum_scatter(PG, dsts + [G[f"{a2}/attention_v"]], ws, beta=1.0)
+    # the per-tile partials of every step sum into the query-layer kernels; the attention bias
+    # gradient (the column sum of every tile) rides on each tile's GEMM as its fused colsum row
     H0f = S["H0RAW"].view(Tp * B, A)
     DQt = DQP.view(Tp * B, dq_parts, D1 + D2)
     for tile in range(dq_parts):
-        K.gemm(H0f.t(), DQt[:, tile, :D1], G[f"{a1}/query_layer/kernel"], beta=1.0)
+        K.gemm(H0f.t(), DQt[:, tile, :D1], G[f"{a1}/query_layer/kernel"], beta=1.0,
+               colsum=G[f"{a1}/attention_bias"] if fwd else None)
         K.gemm(H0f.t(), DQt[:, tile, D1:], G[f"{a2}/query_layer/kernel"], beta=1.0)
     # ---- memories: values via the alignment histories, keys via memory_layer
     dV1 = K.gemm(S["AL1"][1:].permute(1, 2, 0), DCTX[:, :, :M1].permute(1, 0, 2))   # [B, N, M1]

@@ -558,8 +558,7 @@ extern "C" int sat_decoder_lstms_fwd(const SatDecLstmFwd* a, void* stream) {
   p.xch = a->xch; p.err = a->err; p.flags = xcd_local_env();
   p.prof = reinterpret_cast<long long*>(a->prof);
   hipStream_t s = as_stream(stream);
-  if (zero_dwords(a->xch, sat_decoder_lstms_scratch(a->B), s) != hipSuccess ||
-      zero_words(a->err, 2, s) != hipSuccess) {
+  if (zero_ranges(s, a->xch, sat_decoder_lstms_scratch(a->B), a->err, 2) != hipSuccess) {
     set_error("%s: memset failed", nm);
     return SAT_ERR_HIP;
   }
@@ -593,8 +592,7 @@ extern "C" int sat_decoder_lstms_bwd(const SatDecLstmBwd* a, void* stream) {
   p.prof = reinterpret_cast<long long*>(a->prof);
   hipStream_t s = as_stream(stream);
   SAT_CHECK_ARG(aligned16(a->ctr), "%s: 16-byte aligned scratch", nm);
-  if (zero_dwords(a->ctr, sat_decoder_lstms_bwd_scratch(a->B), s) != hipSuccess ||
-      zero_words(a->err, 2, s) != hipSuccess) {
+  if (zero_ranges(s, a->ctr, sat_decoder_lstms_bwd_scratch(a->B), a->err, 2) != hipSuccess) {
     set_error("%s: memset failed", nm);
     return SAT_ERR_HIP;
   }

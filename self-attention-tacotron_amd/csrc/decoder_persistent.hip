@@ -754,10 +754,8 @@ extern "C" int sat_decoder_attention_fwd(const SatDecAttnFwd* a, void* stream) {
   // every hand-off slot starts zeroed (tag 0 / LSB 0 never matches steps 0 and 1)
   const int64_t e_total = hx_floats(a->B) + eh_floats(a->B, ntiles) + ah_floats(a->B, ntiles) +
                         kXidWords;
-  if (zero_dwords(a->E, e_total, s) != hipSuccess ||
-      zero_dwords(a->PART, (size_t)2 * a->B * ntiles * kPST, s) != hipSuccess ||
-      zero_dwords(a->QP, (size_t)2 * a->B * kGW * kQ, s) != hipSuccess ||
-      zero_words(a->err, 2, s) != hipSuccess) {
+  if (zero_ranges(s, a->E, e_total, a->PART, (int64_t)2 * a->B * ntiles * kPST, a->QP,
+                  (int64_t)2 * a->B * kGW * kQ, a->err, 2) != hipSuccess) {
     set_error("sat_decoder_attention_fwd: memset failed");
     return SAT_ERR_HIP;
   }

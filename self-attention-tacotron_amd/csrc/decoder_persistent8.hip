@@ -682,8 +682,7 @@ int dec_attn_fwd8_launch(const SatDecAttnFwd* a, hipStream_t s) {
   p.err = a->err;
   p.flags = xcd_local_env();
   p.prof = reinterpret_cast<long long*>(a->prof);
-  if (zero_dwords(a->QP, ra + rb + kGmax * kW, s) != hipSuccess ||
-      zero_words(a->err, 2, s) != hipSuccess) {
+  if (zero_ranges(s, a->QP, ra + rb + kGmax * kW, a->err, 2) != hipSuccess) {
     set_error("sat_decoder_attention_fwd: scratch clear failed");
     return SAT_ERR_HIP;
   }

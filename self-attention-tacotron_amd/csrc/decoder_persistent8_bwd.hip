@@ -643,8 +643,7 @@ int dec_attn_bwd8_launch(const SatDecAttnBwd* a, hipStream_t s) {
   p.err = a->err;
   p.flags = xcd_local_env();
   p.prof = reinterpret_cast<long long*>(a->prof);
-  if (zero_dwords(a->RDP, rq + rr + kGmax * kW, s) != hipSuccess ||
-      zero_words(a->err, 2, s) != hipSuccess) {
+  if (zero_ranges(s, a->RDP, rq + rr + kGmax * kW, a->err, 2) != hipSuccess) {
     set_error("sat_decoder_attention_bwd: scratch clear failed");
     return SAT_ERR_HIP;
   }

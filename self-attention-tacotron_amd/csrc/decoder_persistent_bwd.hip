@@ -586,8 +586,7 @@ extern "C" int sat_decoder_attention_bwd(const SatDecAttnBwd* a, void* stream) {
   p.DFH = a->DFH; p.DQP = a->DQP; p.RDP = a->RDP; p.YA = a->YA; p.ctr = a->ctr; p.err = a->err; p.flags = xcd_local_env();
   p.prof = reinterpret_cast<long long*>(a->prof);
   hipStream_t s = as_stream(stream);
-  if (zero_dwords(a->ctr, (kG * 64 + kG * kGW), s) != hipSuccess ||
-      zero_words(a->err, 2, s) != hipSuccess) {
+  if (zero_ranges(s, a->ctr, (kG * 64 + kG * kGW), a->err, 2) != hipSuccess) {
     set_error("sat_decoder_attention_bwd: memset failed");
     return SAT_ERR_HIP;
   }

@@ -582,6 +582,58 @@ extern "C" int sat_bn_bwd(const float* dy, int64_t lddy, const float* x, int64_t
   return SAT_OK;
 }
 
+// column sums scattered to up to kColSegs destinations: out_k[c - col_k] = beta * out_k[..] + sum
+constexpr int kColSegs = 8;
+struct ColSegs {
+  float* dst[kColSegs];
+  int col[kColSegs];
+  int n[kColSegs];
+  int nseg;
+};
+__global__ void colreduce_scatter_finish_kernel(const double* part1, int RB, int C, ColSegs g,
+                                                float beta) {
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  double s, q;
+  sum_partials(part1, part1, RB, C, c, s, q);
+  if (threadIdx.x < 64 && c < C) {
+    for (int k = 0; k < g.nseg; ++k) {
+      const int j = c - g.col[k];
+      if (j >= 0 && j < g.n[k]) {
+        float* o = g.dst[k] + j;
+        *o = beta != 0.f ? (float)(beta * *o + s) : (float)s;
+      }
+    }
+  }
+}
+
+extern "C" int sat_colsum_scatter(const float* x, int64_t ldx, int32_t M, int32_t C,
+                                  const SatColSegment* segs, int32_t nseg, float beta,
+                                  void* workspace, void* stream) {
+  SAT_CHECK_ARG(x && segs && workspace && M >= 0 && C > 0 && nseg > 0 && nseg <= kColSegs,
+                "sat_colsum_scatter: bad args (nseg 1..%d)", kColSegs);
+  ColSegs g{};
+  g.nseg = nseg;
+  for (int k = 0; k < nseg; ++k) {
+    SAT_CHECK_ARG(segs[k].dst && segs[k].col >= 0 && segs[k].n > 0 && segs[k].col + segs[k].n <= C,
+                  "sat_colsum_scatter: segment %d out of range", k);
+    g.dst[k] = segs[k].dst;
+    g.col[k] = segs[k].col;
+    g.n[k] = segs[k].n;
+  }
+  if (M == 0) return SAT_OK;
+  const int RB = row_blocks(M);
+  double* p1 = reinterpret_cast<double*>(workspace);
+  double* p2 = p1 + (int64_t)RB * C;
+  hipStream_t s = as_stream(stream);
+  hipLaunchKernelGGL(colreduce_kernel, dim3(ceil_div(C, 64), RB), dim3(256), 0, s, x, ldx,
+                     (const float*)nullptr, (int64_t)0, M, C, p1, p2, 2, (const float*)nullptr,
+                     (const float*)nullptr, 0.f, (const float*)nullptr, (int64_t)0);
+  hipLaunchKernelGGL(colreduce_scatter_finish_kernel, dim3(ceil_div(C, 64)), dim3(256), 0, s, p1,
+                     RB, C, g, beta);
+  SAT_LAUNCH_CHECK("sat_colsum_scatter");
+  return SAT_OK;
+}
+
 extern "C" int sat_colsum(const float* x, int64_t ldx, int32_t M, int32_t C, float* out,
                           float beta, void* workspace, void* stream) {
   SAT_CHECK_ARG(x && out && workspace && M >= 0 && C > 0, "sat_colsum: bad args");

@@ -178,4 +178,38 @@ inline hipError_t zero_dwords(void* p, int64_t n, hipStream_t s) {
 }
 inline hipError_t zero_words(int* p, int n, hipStream_t s) { return zero_dwords(p, n, s); }
 
+// Up to four disjoint dword ranges cleared by ONE launch (grid row y = range): a persistent
+// launcher's scratch + error words used to cost two to four ~5 us kernel nodes per call.
+struct ZeroRanges {
+  unsigned* p[4];
+  int64_t n[4];
+};
+__global__ static void zero_ranges_kernel(ZeroRanges r) {
+  unsigned* __restrict__ p = r.p[blockIdx.y];
+  const int64_t n = r.n[blockIdx.y];
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    p[i] = 0u;
+}
+inline hipError_t zero_ranges(hipStream_t s, void* p0, int64_t n0, void* p1, int64_t n1,
+                              void* p2 = nullptr, int64_t n2 = 0, void* p3 = nullptr,
+                              int64_t n3 = 0) {
+  ZeroRanges r{};
+  void* ps[4] = {p0, p1, p2, p3};
+  const int64_t ns[4] = {n0, n1, n2, n3};
+  int k = 0;
+  int64_t nmax = 0;
+  for (int i = 0; i < 4; ++i)
+    if (ps[i] && ns[i] > 0) {
+      r.p[k] = reinterpret_cast<unsigned*>(ps[i]);
+      r.n[k] = ns[i];
+      nmax = std::max(nmax, ns[i]);
+      ++k;
+    }
+  if (k == 0) return hipSuccess;
+  const int blocks = (int)std::min<int64_t>((nmax + 255) / 256, 1024);
+  hipLaunchKernelGGL(zero_ranges_kernel, dim3(blocks, k), dim3(256), 0, s, r);
+  return hipGetLastError();
+}
+
 }  // namespace sat

@@ -584,6 +584,21 @@ def colsum(x2, out, ws, beta=1.0):
     _lib.call("sat_colsum", _p(x2), x2.stride(0), M, C, _p(out), beta, ws.get(M, C), _stream())
 
 
+def colsum_scatter(x2, dsts, ws, beta=1.0):
+    """Column sums of x2 [M, C] split over consecutive destinations (1-D views whose lengths
+    add up to at most C): dst = beta * dst + its columns' sums, ONE reduction for all."""
+    M, C = x2.shape
+    segs = (_lib.SatColSegment * len(dsts))()
+    col = 0
+    for k, d in enumerate(dsts):
+        if not d.is_contiguous():
+            raise ValueError("colsum_scatter: destinations must be contiguous")
+        segs[k].dst, segs[k].col, segs[k].n = _p(d), col, d.numel()
+        col += d.numel()
+    _lib.call("sat_colsum_scatter", _p(x2), x2.stride(0), M, C, segs, len(dsts), beta,
+              ws.get(M, C), _stream())
+
+
 def maxpool2(x, y):
     B, N, C = x.shape
     _lib.call("sat_maxpool2", _p(x), _p(y), B, N, C, _stream())

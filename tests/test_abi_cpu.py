@@ -53,7 +53,7 @@ def _c_sizeof(struct):
 
 STRUCTS = ["SatGemmDesc", "SatLstmFwd", "SatLstmBwd", "SatAttnStep", "SatAttnStepBwd",
            "SatAttnParamGrad", "SatDecAttnFwd", "SatDecAttnBwd", "SatDecLstmFwd",
-           "SatDecLstmBwd", "SatEncLstmFwd", "SatEncLstmBwd", "SatAdamConfig", "SatConvBank", "SatMha", "SatDims", "SatRngSegment"]
+           "SatDecLstmBwd", "SatEncLstmFwd", "SatEncLstmBwd", "SatAdamConfig", "SatConvBank", "SatMha", "SatDims", "SatRngSegment", "SatColSegment"]
 
 
 def _c_offsets(struct, fields):

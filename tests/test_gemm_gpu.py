@@ -250,3 +250,68 @@ def test_gemm_colsum_fused(cuda, M, N, K, ta, split):
     assert bool(((C.double().cpu() - ref).abs() <= bound).all())
     bs = 6e-7 * (B.double().abs().sum(0) + s0.double().abs()) + 1e-7
     assert bool(((s.double().cpu() - rs).abs() <= bs).all()), float(((s.double().cpu() - rs).abs() / bs).max())
+
+
+def test_gemm_colsum_fused_strided_b(cuda):
+    """the attention query-layer shape: B is one tile of a [T'B, tiles, D1+D2] partial arena"""
+    from sat_amd import kernels
+    g = torch.Generator().manual_seed(11)
+    TB, tiles, D1, D2, A = 4000, 3, 128, 64, 128
+    H = torch.randn(TB, A, generator=g)
+    DQ = torch.randn(TB, tiles, D1 + D2, generator=g)
+    W0, b0 = torch.randn(A, D1, generator=g), torch.randn(D1, generator=g)
+    Hd, DQd, W, b = H.to(cuda), DQ.to(cuda), W0.to(cuda), b0.to(cuda)
+    for t in range(tiles):
+        kernels.gemm(Hd.t(), DQd[:, t, :D1], W, beta=1.0, colsum=b)
+    torch.cuda.synchronize()
+    ref = W0.double() + H.double().t() @ DQ[:, :, :D1].double().sum(1)
+    rb = b0.double() + DQ[:, :, :D1].double().sum((0, 1))
+    bound = 1e-6 * (W0.double().abs() + H.double().abs().t() @ DQ[:, :, :D1].double().abs().sum(1)) + 1e-7
+    assert bool(((W.double().cpu() - ref).abs() <= bound).all())
+    bb = 1e-6 * (b0.double().abs() + DQ[:, :, :D1].double().abs().sum((0, 1))) + 1e-7
+    assert bool(((b.double().cpu() - rb).abs() <= bb).all())
+
+
+@pytest.mark.parametrize("M", [1, 700, 25000])
+def test_colsum_scatter(cuda, M):
+    """sat_colsum_scatter == one column sum per destination segment (beta 1 accumulates)"""
+    from sat_amd import kernels
+    from sat_amd.kernels import Workspace
+    g = torch.Generator().manual_seed(M)
+    lens = [128, 32 * 128, 31 * 32, 32, 128]
+    C = sum(lens) + 5                                    # trailing columns feed no segment
+    X = torch.randn(M, C, generator=g)
+    dst0 = [torch.randn(n, generator=g) for n in lens]
+    dst = [d.to(cuda) for d in dst0]
+    kernels.colsum_scatter(X.to(cuda), dst, Workspace(cuda), beta=1.0)
+    torch.cuda.synchronize()
+    cs = X.double().sum(0)
+    o = 0
+    for d0, d in zip(dst0, dst):
+        ref = d0.double() + cs[o:o + d0.numel()]
+        bound = 1e-6 * (d0.double().abs() + X[:, o:o + d0.numel()].double().abs().sum(0)) + 1e-7
+        assert bool(((d.double().cpu() - ref).abs() <= bound).all())
+        o += d0.numel()
+
+
+@pytest.mark.parametrize("M,N,K,bm,bn,split", [(256, 1024, 3000, 64, 64, 8), (100, 36, 5000, 128, 64, 16),
+                                               (130, 257, 4100, 64, 128, 4)])
+def test_gemm_splitk_repeatable(cuda, M, N, K, bm, bn, split):
+    """forced split-K plans: repeated launches on one stream give bit-identical results (the
+    slabs are summed in a fixed order), within the fp32 bound of the float64 product"""
+    from sat_amd import _lib, kernels
+    g = torch.Generator().manual_seed(M * 7 + N + K)
+    A, B = torch.randn(M, K, generator=g), torch.randn(K, N, generator=g)
+    Ad, Bd = A.to(cuda), B.to(cuda)
+    lib = _lib.load()
+    lib.sat_gemm_force_plan(bm, bn, split)
+    try:
+        outs = [kernels.gemm(Ad, Bd) for _ in range(4)]
+        torch.cuda.synchronize()
+    finally:
+        lib.sat_gemm_force_plan(0, 0, 0)
+    for o in outs[1:]:
+        assert torch.equal(o, outs[0])
+    ref = A.double() @ B.double()
+    bound = 6e-7 * (A.double().abs() @ B.double().abs()) + 1e-7
+    assert bool(((outs[0].double().cpu() - ref).abs() <= bound).all())

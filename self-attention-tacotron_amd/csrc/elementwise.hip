@@ -351,6 +351,77 @@ __global__ void softmax_bwd_kernel(const float* __restrict__ P, const float* __r
   }
 }
 
+// Register-resident variants for rows of at most 64*NC columns: each row is read once (every
+// load of the row issued before the first reduction) instead of two / three dependent passes.
+// Same operations in the same per-lane order as the kernels above: bit-identical results.
+template <int NC>
+__global__ void softmax_fwd_reg_kernel(const float* __restrict__ S, float* __restrict__ P,
+                                       float* __restrict__ Pd, const float* __restrict__ mask,
+                                       int64_t R, int L, int Lq, int causal, float scale) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = blockIdx.x * (int64_t)(blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (r >= R) return;
+  const int qi = (int)(r % Lq);
+  const int lim = causal ? min(L, qi + 1) : L;
+  const float* s = S + r * L;
+  float v[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int j = lane + 64 * c;
+    v[c] = j < lim ? s[j] * scale : -INFINITY;
+  }
+  float mx = -INFINITY;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) mx = fmaxf(mx, v[c]);
+  mx = wave_max(mx);
+  float z = 0.f;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    v[c] = lane + 64 * c < lim ? expf(v[c] - mx) : 0.f;
+    z += v[c];
+  }
+  z = wave_sum(z);
+  const float inv = 1.f / z;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int j = lane + 64 * c;
+    if (j >= L) break;
+    const float pv = j < lim ? v[c] * inv : 0.f;
+    P[r * L + j] = pv;
+    if (Pd) Pd[r * L + j] = mask ? pv * mask[r * L + j] : pv;
+  }
+}
+
+template <int NC>
+__global__ void softmax_bwd_reg_kernel(const float* __restrict__ P, const float* __restrict__ dPd,
+                                       const float* __restrict__ mask, float* __restrict__ dS,
+                                       int64_t R, int L, float scale) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = blockIdx.x * (int64_t)(blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (r >= R) return;
+  const float* p = P + r * L;
+  const float* g = dPd + r * L;
+  const float* m = mask ? mask + r * L : nullptr;
+  float pv[NC], dp[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int j = lane + 64 * c;
+    pv[c] = j < L ? p[j] : 0.f;
+    dp[c] = j < L ? (m ? g[j] * m[j] : g[j]) : 0.f;
+  }
+  float acc = 0.f;
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+    if (lane + 64 * c < L) acc += dp[c] * pv[c];
+  acc = wave_sum(acc);
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int j = lane + 64 * c;
+    if (j >= L) break;
+    dS[r * L + j] = scale * pv[c] * (dp[c] - acc);
+  }
+}
+
 // ---------------------------------------------------------------- loss (models/models.py:159-173)
 // pass 1 (one workgroup): sums and non-zero-weight counts
 // Loss pass 1: kLossBlocks workgroups, one wave per target row [M] (float4 when M % 4 == 0),
@@ -708,8 +779,12 @@ extern "C" int sat_axpby(const float* x, float* y, int64_t n, float a, float b, 
 extern "C" int sat_softmax_fwd(const float* S, float* P, float* Pd, const float* mask, int64_t R,
                                int32_t L, int32_t Lq, int32_t causal, float scale, void* stream) {
   SAT_CHECK_ARG(S && P && R >= 0 && L > 0 && Lq > 0, "sat_softmax_fwd: bad args");
-  hipLaunchKernelGGL(softmax_fwd_kernel, dim3(ceil_div(R, 4)), dim3(256), 0, as_stream(stream), S,
-                     P, Pd, mask, R, L, Lq, causal, scale);
+  const dim3 g(ceil_div(R, 4)), b(256);
+  hipStream_t s = as_stream(stream);
+  if (L <= 256) hipLaunchKernelGGL(softmax_fwd_reg_kernel<4>, g, b, 0, s, S, P, Pd, mask, R, L, Lq, causal, scale);
+  else if (L <= 512) hipLaunchKernelGGL(softmax_fwd_reg_kernel<8>, g, b, 0, s, S, P, Pd, mask, R, L, Lq, causal, scale);
+  else if (L <= 1024) hipLaunchKernelGGL(softmax_fwd_reg_kernel<16>, g, b, 0, s, S, P, Pd, mask, R, L, Lq, causal, scale);
+  else hipLaunchKernelGGL(softmax_fwd_kernel, g, b, 0, s, S, P, Pd, mask, R, L, Lq, causal, scale);
   SAT_LAUNCH_CHECK("sat_softmax_fwd");
   return SAT_OK;
 }
@@ -717,8 +792,12 @@ extern "C" int sat_softmax_fwd(const float* S, float* P, float* Pd, const float*
 extern "C" int sat_softmax_bwd(const float* P, const float* dPd, const float* mask, float* dS,
                                int64_t R, int32_t L, float scale, void* stream) {
   SAT_CHECK_ARG(P && dPd && dS && R >= 0 && L > 0, "sat_softmax_bwd: bad args");
-  hipLaunchKernelGGL(softmax_bwd_kernel, dim3(ceil_div(R, 4)), dim3(256), 0, as_stream(stream), P,
-                     dPd, mask, dS, R, L, scale);
+  const dim3 g(ceil_div(R, 4)), b(256);
+  hipStream_t s = as_stream(stream);
+  if (L <= 256) hipLaunchKernelGGL(softmax_bwd_reg_kernel<4>, g, b, 0, s, P, dPd, mask, dS, R, L, scale);
+  else if (L <= 512) hipLaunchKernelGGL(softmax_bwd_reg_kernel<8>, g, b, 0, s, P, dPd, mask, dS, R, L, scale);
+  else if (L <= 1024) hipLaunchKernelGGL(softmax_bwd_reg_kernel<16>, g, b, 0, s, P, dPd, mask, dS, R, L, scale);
+  else hipLaunchKernelGGL(softmax_bwd_kernel, g, b, 0, s, P, dPd, mask, dS, R, L, scale);
   SAT_LAUNCH_CHECK("sat_softmax_bwd");
   return SAT_OK;
 }

@@ -1,0 +1,41 @@
+"""Row softmax of the self-attention layers (sat_softmax_fwd / sat_softmax_bwd): register-resident
+kernels for rows up to 1024 columns, the streaming kernel beyond, against torch fp64 CPU."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("L", [7, 200, 256, 500, 1000, 1500])
+@pytest.mark.parametrize("causal", [False, True])
+@pytest.mark.parametrize("dropout", [False, True])
+def test_softmax_fwd_bwd(cuda, L, causal, dropout):
+    from sat_amd import kernels as K
+    g = torch.Generator().manual_seed(L + 2 * causal + dropout)
+    Bh, Lq = 6, L                        # [B*H, Lq, L] score rows (causal: square)
+    scale = 0.125
+    S = torch.randn(Bh, Lq, L, generator=g) * 4
+    mask = (torch.rand(Bh, Lq, L, generator=g) > 0.1).float() / 0.9 if dropout else None
+    dPd = torch.randn(Bh, Lq, L, generator=g)
+    Sd = S.to(cuda)
+    P = torch.empty_like(Sd)
+    Pd = torch.empty_like(Sd) if dropout else None
+    md = mask.to(cuda) if dropout else None
+    K.softmax_fwd(Sd, P, Pd, mask=md, causal=causal, scale=scale)
+    dS = torch.empty_like(Sd)
+    K.softmax_bwd(P, dPd.to(cuda), dS, mask=md, scale=scale)
+    torch.cuda.synchronize()
+
+    x = S.double() * scale
+    if causal:
+        x = x.masked_fill(torch.ones(Lq, L).triu(1).bool(), float("-inf"))
+    ref = torch.softmax(x, -1)
+    assert float((P.double().cpu() - ref).abs().max()) < 2e-6
+    if dropout:
+        assert float((Pd.double().cpu() - ref * mask.double()).abs().max()) < 2e-5
+    dp = dPd.double() * (mask.double() if dropout else 1.0)
+    dref = scale * ref * (dp - (dp * ref).sum(-1, keepdim=True))
+    assert float((dS.double().cpu() - dref).abs().max()) < 5e-6 * (1 + float(dp.abs().max()))
+    if causal:                          # masked columns are exact zeros
+        up = torch.ones(Lq, L).triu(1).bool().expand(Bh, Lq, L)
+        assert float(P.cpu()[up].abs().max()) == 0.0 if up.any() else True

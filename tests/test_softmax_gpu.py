@@ -1,4 +1,5 @@
-"""Row softmax of the self-attention layers (sat_softmax_fwd / sat_softmax_bwd): register-resident
+"""Row softmax of the self-attention layers (sat_softmax_fwd / sat_softmax_bwd) and the CBHG max
+pooling (sat_maxpool2/_bwd). Softmax: register-resident
 kernels for rows up to 1024 columns, the streaming kernel beyond, against torch fp64 CPU."""
 import pytest
 import torch
@@ -39,3 +40,35 @@ def test_softmax_fwd_bwd(cuda, L, causal, dropout):
     if causal:                          # masked columns are exact zeros
         up = torch.ones(Lq, L).triu(1).bool().expand(Bh, Lq, L)
         assert float(P.cpu()[up].abs().max()) == 0.0 if up.any() else True
+
+
+def _maxpool_ref(x, dy):
+    """MaxPooling1D(2, stride 1, SAME) and its gradient, first index winning ties"""
+    nxt = torch.cat([x[:, 1:], x[:, -1:]], 1)
+    last = torch.zeros_like(x, dtype=torch.bool)
+    last[:, -1] = True
+    y = torch.where(last, x, torch.maximum(x, nxt))
+    own = last | (x >= nxt)
+    dx = torch.where(own, dy, torch.zeros_like(dy))
+    prv = torch.cat([x[:, :1], x[:, :-1]], 1)
+    dprv = torch.cat([torch.zeros_like(dy[:, :1]), dy[:, :-1]], 1)
+    first = torch.zeros_like(x, dtype=torch.bool)
+    first[:, 0] = True
+    dx = dx + torch.where(~first & (prv < x), dprv, torch.zeros_like(dy))
+    return y, dx
+
+
+@pytest.mark.parametrize("B,N,C", [(3, 17, 2048), (2, 1, 128), (4, 9, 7), (32, 200, 128)])
+def test_maxpool2_fwd_bwd(cuda, B, N, C):
+    """float4 path (C % 4 == 0) and scalar path, with ties (quantised inputs)"""
+    from sat_amd import kernels as K
+    g = torch.Generator().manual_seed(B * N + C)
+    x = torch.randint(-3, 4, (B, N, C), generator=g).float()
+    dy = torch.randn(B, N, C, generator=g)
+    xd = x.to(cuda)
+    y = K.maxpool2(xd, torch.empty_like(xd))
+    dx = K.maxpool2_bwd(xd, dy.to(cuda), torch.empty_like(xd))
+    torch.cuda.synchronize()
+    yr, dxr = _maxpool_ref(x, dy)
+    assert torch.equal(y.cpu(), yr)
+    assert torch.equal(dx.cpu(), dxr)

@@ -1,6 +1,7 @@
-"""Row softmax of the self-attention layers (sat_softmax_fwd / sat_softmax_bwd) and the CBHG max
-pooling (sat_maxpool2/_bwd). Softmax: register-resident
-kernels for rows up to 1024 columns, the streaming kernel beyond, against torch fp64 CPU."""
+"""Memory-bound step kernels against CPU references: the self-attention row softmax
+(sat_softmax_fwd/bwd; register-resident rows up to 1024 columns, streaming beyond; torch fp64),
+the CBHG max pooling (sat_maxpool2/_bwd; exact, ties included) and the embedding gradient
+(sat_embedding_bwd; exact row-ordered float32 sums)."""
 import pytest
 import torch
 
@@ -72,3 +73,30 @@ def test_maxpool2_fwd_bwd(cuda, B, N, C):
     yr, dxr = _maxpool_ref(x, dy)
     assert torch.equal(y.cpu(), yr)
     assert torch.equal(dx.cpu(), dxr)
+
+
+@pytest.mark.parametrize("R,D,V,offset", [(6400, 512, 70, 0), (37, 300, 5, 3), (1, 512, 4, 0),
+                                          (1100, 64, 1, 0)])
+def test_embedding_bwd_row_order(cuda, R, D, V, offset):
+    """dtable[v] += sum of the dout rows whose id hits v, added in row order (bit-exact against
+    the same float32 sequence on the CPU); rows never hit stay untouched"""
+    from sat_amd import kernels as K
+    g = torch.Generator().manual_seed(R + D + V)
+    ids = torch.randint(offset, offset + V, (R,), generator=g)
+    if V > 2:
+        ids[ids == offset + 1] = offset     # one table row never hit
+    dout = torch.randn(R, D, generator=g)
+    table0 = torch.randn(V, D, generator=g)
+    dt = table0.to(cuda)
+    K.embedding_bwd(dout.to(cuda), ids.to(cuda), dt, offset=offset)
+    torch.cuda.synchronize()
+    ref = table0.clone()
+    for v in range(V):
+        rows = (ids - offset == v).nonzero().flatten().tolist()
+        if not rows:
+            continue
+        acc = torch.zeros(D)
+        for r in rows:
+            acc = acc + dout[r]
+        ref[v] = ref[v] + acc
+    assert torch.equal(dt.cpu(), ref)

@@ -76,6 +76,57 @@ __global__ void __launch_bounds__(256) embed_bwd_kernel(const float* __restrict_
   if (any && c < D) dtable[(int64_t)v * D + c] += acc;
 }
 
+// Two-phase variant for R <= kEmbRows: (1) the workgroup lists the rows that hit v in
+// ascending order in LDS (every thread's ids loaded up front, then per 256-row chunk a ballot and
+// a popcount prefix place each match); (2) each column thread sums its list entries in list order
+// with kEmbG loads in flight -- the same row-ordered sum as embed_bwd_kernel, without one
+// dependent load latency per hit.
+constexpr int kEmbRows = 8192, kEmbG = 8;
+__global__ void __launch_bounds__(256) embed_bwd_list_kernel(const float* __restrict__ dout,
+                                                             const int64_t* __restrict__ ids,
+                                                             float* __restrict__ dtable, int R,
+                                                             int D, int64_t offset) {
+  __shared__ int list[kEmbRows];
+  __shared__ int wcount[2][4];
+  const int v = blockIdx.x, c = blockIdx.y * 256 + threadIdx.x;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  constexpr int kPer = kEmbRows / 256;
+  bool hit[kPer];
+#pragma unroll
+  for (int i = 0; i < kPer; ++i) {
+    const int r = i * 256 + threadIdx.x;
+    hit[i] = r < R && ids[r] - offset == v;
+  }
+  int n = 0;
+  const unsigned long long below = (1ull << lane) - 1ull;
+#pragma unroll
+  for (int i = 0; i < kPer; ++i) {
+    if (i * 256 >= R) break;
+    const unsigned long long b = __builtin_amdgcn_ballot_w64(hit[i]);
+    if (lane == 0) wcount[i & 1][wave] = __builtin_popcountll(b);
+    __syncthreads();
+    int base = n;
+    for (int w = 0; w < wave; ++w) base += wcount[i & 1][w];
+    if (hit[i]) list[base + __builtin_popcountll(b & below)] = i * 256 + threadIdx.x;
+    n += wcount[i & 1][0] + wcount[i & 1][1] + wcount[i & 1][2] + wcount[i & 1][3];
+  }
+  __syncthreads();
+  if (n == 0 || c >= D) return;
+  float acc = 0.f;
+  for (int j0 = 0; j0 < n; j0 += kEmbG) {
+    float x[kEmbG];
+#pragma unroll
+    for (int k = 0; k < kEmbG; ++k) {
+      const int j = min(j0 + k, n - 1);
+      x[k] = dout[(int64_t)list[j] * D + c];
+    }
+#pragma unroll
+    for (int k = 0; k < kEmbG; ++k)
+      if (j0 + k < n) acc += x[k];
+  }
+  dtable[(int64_t)v * D + c] += acc;
+}
+
 // ---------------------------------------------------------------- column reductions
 // out1[c] = sum_m x[m, c]  (and out2[c] = sum_m x[m,c]*y[m,c] when y != null), fp64 accumulation.
 // Block = 256 threads = 64 columns x 4 row groups; grid = ceil(C/64) x RB row blocks (partials
@@ -625,9 +676,12 @@ extern "C" int sat_embedding_bwd(const float* dout, const int64_t* ids, float* d
                                  int32_t D, int32_t V, int64_t offset, void* stream) {
   SAT_CHECK_ARG(dout && ids && dtable && R >= 0 && D > 0 && V > 0, "sat_embedding_bwd: bad args");
   if (R == 0) return SAT_OK;
-  if (R == 0) return SAT_OK;
-  hipLaunchKernelGGL(embed_bwd_kernel, dim3(V, ceil_div(D, 256)), dim3(256), 0, as_stream(stream),
-                     dout, ids, dtable, R, D, V, offset);
+  if (R <= kEmbRows)
+    hipLaunchKernelGGL(embed_bwd_list_kernel, dim3(V, ceil_div(D, 256)), dim3(256), 0,
+                       as_stream(stream), dout, ids, dtable, (int)R, D, offset);
+  else
+    hipLaunchKernelGGL(embed_bwd_kernel, dim3(V, ceil_div(D, 256)), dim3(256), 0,
+                       as_stream(stream), dout, ids, dtable, R, D, V, offset);
   SAT_LAUNCH_CHECK("sat_embedding_bwd");
   return SAT_OK;
 }

@@ -76,7 +76,7 @@ def test_maxpool2_fwd_bwd(cuda, B, N, C):
 
 
 @pytest.mark.parametrize("R,D,V,offset", [(6400, 512, 70, 0), (37, 300, 5, 3), (1, 512, 4, 0),
-                                          (1100, 64, 1, 0)])
+                                          (1100, 64, 1, 0), (8192, 256, 9, 0), (9000, 64, 3, 0)])
 def test_embedding_bwd_row_order(cuda, R, D, V, offset):
     """dtable[v] += sum of the dout rows whose id hits v, added in row order (bit-exact against
     the same float32 sequence on the CPU); rows never hit stay untouched"""

@@ -515,7 +515,7 @@ __global__ void softmax_bwd_reg_kernel(const float* __restrict__ P, const float*
 
 // ---------------------------------------------------------------- loss (models/models.py:159-173)
 // pass 1 (one workgroup): sums and non-zero-weight counts
-// Loss pass 1: kLossBlocks workgroups, one wave per target row [M] (float4 when M % 4 == 0),
+// Loss pass 1: kLossBlocks workgroups, flat over float4s when M % 4 == 0 (else one wave per row),
 // fp64 partials {sum w|mel-tgt|, #weighted elements, sum w*xent, #weighted stop entries} per
 // workgroup; pass 1b sums them in a fixed order (deterministic) and writes
 // out = {loss, L1, BCE, count1, count2}.
@@ -530,21 +530,30 @@ __global__ void __launch_bounds__(256) loss_partial_kernel(
   double l1 = 0.0, c1 = 0.0, bce = 0.0, c2 = 0.0;
   const int rows = B * T;
   const bool vec = (M & 3) == 0;
-  for (int r = blockIdx.x * 4 + wv; r < rows; r += gridDim.x * 4) {
+  if (vec) {
+    // flat over the float4s of all rows (a wave per row left 44 of 64 lanes idle at M = 80 and
+    // walked 31 dependent row loads per wave); loads are unconditional, the weight selects
+    const int M4 = M >> 2;
+    const int64_t n4 = (int64_t)rows * M4;
+    const float4* m4 = reinterpret_cast<const float4*>(mel);
+    const float4* t4 = reinterpret_cast<const float4*>(tgt);
+#pragma unroll 4
+    for (int64_t e = blockIdx.x * 256 + threadIdx.x; e < n4; e += (int64_t)gridDim.x * 256) {
+      const int64_t r = e / M4;
+      const float w = tmask[r];
+      const float4 x = m4[e], y = t4[e];
+      const float acc = fabsf(x.x - y.x) + fabsf(x.y - y.y) + fabsf(x.z - y.z) + fabsf(x.w - y.w);
+      l1 += w != 0.f ? (double)w * acc : 0.0;
+      c1 += (w != 0.f && e == r * M4) ? (double)M : 0.0;
+    }
+  }
+  for (int r = blockIdx.x * 4 + wv; !vec && r < rows; r += gridDim.x * 4) {
     const float w = tmask[r];
     if (w == 0.f) continue;                       // wave-uniform
     const float* mr = mel + (int64_t)r * M;
     const float* tr = tgt + (int64_t)r * M;
     float acc = 0.f;
-    if (vec) {
-      for (int c = lane; c < (M >> 2); c += 64) {
-        const float4 x = reinterpret_cast<const float4*>(mr)[c];
-        const float4 y = reinterpret_cast<const float4*>(tr)[c];
-        acc += fabsf(x.x - y.x) + fabsf(x.y - y.y) + fabsf(x.z - y.z) + fabsf(x.w - y.w);
-      }
-    } else {
-      for (int c = lane; c < M; c += 64) acc += fabsf(mr[c] - tr[c]);
-    }
+    for (int c = lane; c < M; c += 64) acc += fabsf(mr[c] - tr[c]);
     l1 += (double)w * acc;
     if (lane == 0) c1 += (double)M;
   }

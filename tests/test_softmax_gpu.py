@@ -100,3 +100,33 @@ def test_embedding_bwd_row_order(cuda, R, D, V, offset):
             acc = acc + dout[r]
         ref[v] = ref[v] + acc
     assert torch.equal(dt.cpu(), ref)
+
+
+@pytest.mark.parametrize("B,T,M,Tp", [(32, 1000, 80, 500), (3, 17, 7, 9), (2, 8, 4, 4)])
+def test_loss_partials(cuda, B, T, M, Tp):
+    """sat_loss_fwd_bwd's values against float64 CPU: masked L1 over the mel rows (rows of weight 0
+    skipped even when they hold NaN), masked BCE of the stop logits, their counts"""
+    from sat_amd import kernels as K
+    g = torch.Generator().manual_seed(B * T + M)
+    mel, tgt = torch.randn(B, T, M, generator=g), torch.randn(B, T, M, generator=g)
+    tmask = (torch.rand(B, T, generator=g) > 0.3).float()
+    mel[tmask == 0] = float("nan")
+    stop, done = torch.randn(B, Tp, generator=g), (torch.rand(B, Tp, generator=g) > 0.5).float()
+    dmask = (torch.rand(B, Tp, generator=g) > 0.2).float()
+    out = torch.zeros(8, device=cuda)
+    K.loss_fwd_bwd(mel.to(cuda), tgt.to(cuda), tmask.to(cuda), stop.to(cuda), done.to(cuda),
+                   dmask.to(cuda), out)
+    torch.cuda.synchronize()
+    w = tmask.double()[..., None]
+    d = torch.where(w > 0, (mel.double() - tgt.double()).abs(), torch.zeros(()).double())
+    c1 = max(float(tmask.sum()) * M, 1.0)
+    L1 = float((w * d).sum()) / c1
+    x, z, wd = stop.double(), done.double(), dmask.double()
+    xe = x.clamp(min=0) - x * z + torch.log1p(torch.exp(-x.abs()))
+    cb = max(float((dmask != 0).sum()), 1.0)
+    BCE = float((wd * xe).sum()) / cb
+    o = out.cpu().double()
+    assert abs(float(o[1]) - L1) <= 1e-6 * abs(L1) + 1e-7
+    assert abs(float(o[2]) - BCE) <= 1e-6 * abs(BCE) + 1e-7
+    assert float(o[3]) == c1 and float(o[4]) == cb
+    assert abs(float(o[0]) - (0.1 * L1 + BCE)) <= 1e-6 * (0.1 * L1 + BCE) + 1e-7

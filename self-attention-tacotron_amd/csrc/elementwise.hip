@@ -695,7 +695,8 @@ extern "C" int sat_embedding_bwd(const float* dout, const int64_t* ids, float* d
   return SAT_OK;
 }
 
-static int row_blocks(int M) { return std::max(1, std::min(64, (M + 127) / 128)); }
+// 64 rows per workgroup (one unrolled trip of 16 rows per row group), up to 256 row blocks
+static int row_blocks(int M) { return std::max(1, std::min(256, (M + 63) / 64)); }
 
 extern "C" int64_t sat_workspace_colreduce(int32_t M, int32_t C) {
   // bytes: fp64 partials [2][RB][C] + two fp32 sums [C] used by the column reductions below

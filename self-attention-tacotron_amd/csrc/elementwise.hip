@@ -339,6 +339,69 @@ __global__ void maxpool_fwd4_kernel(const float4* __restrict__ x, float4* __rest
     }
   }
 }
+// chunked variant: a thread owns kMpL consecutive positions of one (utterance, float4 column),
+// loads its x / dy window (positions n0-1 .. n0+kMpL) once, all loads in flight together,
+// instead of every position re-reading both neighbours (≈ 2.5x the bytes through L2)
+constexpr int kMpL = 8;
+__global__ void maxpool_bwd4c_kernel(const float4* __restrict__ x, const float4* __restrict__ dy,
+                                     float4* __restrict__ dx, int N, int C4, int nchunk,
+                                     int total) {
+  const int tid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (tid >= total) return;
+  const int c = tid % C4;
+  const int rest = tid / C4;
+  const int ch = rest % nchunk, b = rest / nchunk;
+  const int n0 = ch * kMpL;
+  const int64_t base = (int64_t)b * N * C4 + c;
+  float4 xv[kMpL + 2], dv[kMpL + 1];
+#pragma unroll
+  for (int k = 0; k < kMpL + 2; ++k) {        // xv[k] = x at position n0 - 1 + k (clamped)
+    const int n = min(max(n0 - 1 + k, 0), N - 1);
+    xv[k] = x[base + (int64_t)n * C4];
+  }
+#pragma unroll
+  for (int k = 0; k < kMpL + 1; ++k) {        // dv[k] = dy at position n0 - 1 + k (clamped)
+    const int n = min(max(n0 - 1 + k, 0), N - 1);
+    dv[k] = dy[base + (int64_t)n * C4];
+  }
+#pragma unroll
+  for (int k = 1; k <= kMpL; ++k) {
+    const int n = n0 - 1 + k;
+    if (n >= N) break;
+    const bool last = n + 1 >= N, first = n == 0;
+    const float4 a = xv[k], nx = xv[k + 1], px = xv[k - 1], d = dv[k], pd = dv[k - 1];
+    dx[base + (int64_t)n * C4] =
+        make_float4(maxpool_grad1(a.x, nx.x, px.x, d.x, pd.x, last, first),
+                    maxpool_grad1(a.y, nx.y, px.y, d.y, pd.y, last, first),
+                    maxpool_grad1(a.z, nx.z, px.z, d.z, pd.z, last, first),
+                    maxpool_grad1(a.w, nx.w, px.w, d.w, pd.w, last, first));
+  }
+}
+__global__ void maxpool_fwd4c_kernel(const float4* __restrict__ x, float4* __restrict__ y, int N,
+                                     int C4, int nchunk, int total) {
+  const int tid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (tid >= total) return;
+  const int c = tid % C4;
+  const int rest = tid / C4;
+  const int ch = rest % nchunk, b = rest / nchunk;
+  const int n0 = ch * kMpL;
+  const int64_t base = (int64_t)b * N * C4 + c;
+  float4 xv[kMpL + 1];
+#pragma unroll
+  for (int k = 0; k < kMpL + 1; ++k) {        // xv[k] = x at position n0 + k (clamped)
+    const int n = min(n0 + k, N - 1);
+    xv[k] = x[base + (int64_t)n * C4];
+  }
+#pragma unroll
+  for (int k = 0; k < kMpL; ++k) {
+    const int n = n0 + k;
+    if (n >= N) break;
+    const float4 a = xv[k], b2 = xv[k + 1];
+    y[base + (int64_t)n * C4] = n + 1 < N ? make_float4(fmaxf(a.x, b2.x), fmaxf(a.y, b2.y),
+                                                        fmaxf(a.z, b2.z), fmaxf(a.w, b2.w))
+                                          : a;
+  }
+}
 __global__ void maxpool_bwd4_kernel(const float4* __restrict__ x, const float4* __restrict__ dy,
                                     float4* __restrict__ dx, unsigned N, unsigned C4,
                                     unsigned total4) {
@@ -830,7 +893,13 @@ extern "C" int sat_maxpool2(const float* x, float* y, int32_t B, int32_t N, int3
                             void* stream) {
   SAT_CHECK_ARG(x && y && B > 0 && N > 0 && C > 0, "sat_maxpool2: bad args");
   const int64_t total = (int64_t)B * N * C;
-  if (C % 4 == 0 && total < (1LL << 31) && aligned16(x) && aligned16(y))
+  const int64_t nthreads = (int64_t)B * ((N + kMpL - 1) / kMpL) * (C / 4);
+  if (C % 4 == 0 && total < (1LL << 31) && aligned16(x) && aligned16(y) && nthreads >= 65536)
+    hipLaunchKernelGGL(maxpool_fwd4c_kernel, dim3(ceil_div(nthreads, 256)), dim3(256), 0,
+                       as_stream(stream), reinterpret_cast<const float4*>(x),
+                       reinterpret_cast<float4*>(y), N, C / 4, (N + kMpL - 1) / kMpL,
+                       (int)nthreads);
+  else if (C % 4 == 0 && total < (1LL << 31) && aligned16(x) && aligned16(y))
     hipLaunchKernelGGL(maxpool_fwd4_kernel, dim3(grid_for(total / 4)), dim3(256), 0,
                        as_stream(stream), reinterpret_cast<const float4*>(x),
                        reinterpret_cast<float4*>(y), (unsigned)N, (unsigned)(C / 4),
@@ -846,7 +915,14 @@ extern "C" int sat_maxpool2_bwd(const float* x, const float* dy, float* dx, int3
                                 int32_t C, void* stream) {
   SAT_CHECK_ARG(x && dy && dx && B > 0 && N > 0 && C > 0, "sat_maxpool2_bwd: bad args");
   const int64_t total = (int64_t)B * N * C;
-  if (C % 4 == 0 && total < (1LL << 31) && aligned16(x) && aligned16(dy) && aligned16(dx))
+  const int64_t nthreads = (int64_t)B * ((N + kMpL - 1) / kMpL) * (C / 4);
+  if (C % 4 == 0 && total < (1LL << 31) && aligned16(x) && aligned16(dy) && aligned16(dx) &&
+      nthreads >= 65536)
+    hipLaunchKernelGGL(maxpool_bwd4c_kernel, dim3(ceil_div(nthreads, 256)), dim3(256), 0,
+                       as_stream(stream), reinterpret_cast<const float4*>(x),
+                       reinterpret_cast<const float4*>(dy), reinterpret_cast<float4*>(dx), N,
+                       C / 4, (N + kMpL - 1) / kMpL, (int)nthreads);
+  else if (C % 4 == 0 && total < (1LL << 31) && aligned16(x) && aligned16(dy) && aligned16(dx))
     hipLaunchKernelGGL(maxpool_bwd4_kernel, dim3(grid_for(total / 4)), dim3(256), 0,
                        as_stream(stream), reinterpret_cast<const float4*>(x),
                        reinterpret_cast<const float4*>(dy), reinterpret_cast<float4*>(dx),

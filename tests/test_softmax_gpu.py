@@ -59,9 +59,11 @@ def _maxpool_ref(x, dy):
     return y, dx
 
 
-@pytest.mark.parametrize("B,N,C", [(3, 17, 2048), (2, 1, 128), (4, 9, 7), (32, 200, 128)])
+@pytest.mark.parametrize("B,N,C", [(3, 17, 2048), (2, 1, 128), (4, 9, 7), (32, 200, 128),
+                                   (32, 200, 2048), (16, 203, 2048), (64, 9, 1024)])
 def test_maxpool2_fwd_bwd(cuda, B, N, C):
-    """float4 path (C % 4 == 0) and scalar path, with ties (quantised inputs)"""
+    """float4 paths (C % 4 == 0; chunked backward at >= 65536 threads, ragged last chunk
+    included) and the scalar path, with ties (quantised inputs)"""
     from sat_amd import kernels as K
     g = torch.Generator().manual_seed(B * N + C)
     x = torch.randint(-3, 4, (B, N, C), generator=g).float()

@@ -264,6 +264,88 @@ __global__ void bn_apply_kernel(const float* __restrict__ x, int64_t ldx, float*
   }
 }
 
+// float4 variants of the two BN element passes (C and every leading dimension % 4 == 0,
+// 16-byte aligned, M*C < 2^31): 32-bit row arithmetic once per four channels and 16-byte
+// accesses; per element the same expressions as the scalar kernels (bit-identical)
+__global__ void bn_apply4_kernel(const float* __restrict__ x, int ldx, float* __restrict__ y,
+                                 int ldy, int M, int C, const float* __restrict__ mean,
+                                 const float* __restrict__ var, float eps,
+                                 const float* __restrict__ gamma, const float* __restrict__ beta,
+                                 int relu, const float* __restrict__ res, int ldr) {
+  const int C4 = C >> 2, n4 = M * C4;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < n4; e += gridDim.x * blockDim.x) {
+    const int m = e / C4, c = 4 * (e - m * C4);
+    const float4 xv = *reinterpret_cast<const float4*>(x + m * ldx + c);
+    const float4 mu = *reinterpret_cast<const float4*>(mean + c);
+    const float4 va = *reinterpret_cast<const float4*>(var + c);
+    const float4 ga = *reinterpret_cast<const float4*>(gamma + c);
+    const float4 be = *reinterpret_cast<const float4*>(beta + c);
+    float4 rv = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (res) rv = *reinterpret_cast<const float4*>(res + m * ldr + c);
+    const float xs[4] = {xv.x, xv.y, xv.z, xv.w}, ms[4] = {mu.x, mu.y, mu.z, mu.w};
+    const float vs[4] = {va.x, va.y, va.z, va.w}, gs[4] = {ga.x, ga.y, ga.z, ga.w};
+    const float bs[4] = {be.x, be.y, be.z, be.w}, rs[4] = {rv.x, rv.y, rv.z, rv.w};
+    float o[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float v = gs[k] * (xs[k] - ms[k]) * rsqrtf(vs[k] + eps) + bs[k];
+      if (relu) v = fmaxf(v, 0.f);
+      if (res) v += rs[k];
+      o[k] = v;
+    }
+    *reinterpret_cast<float4*>(y + m * ldy + c) = make_float4(o[0], o[1], o[2], o[3]);
+  }
+}
+
+__global__ void bn_bwd_apply4_kernel(const float* __restrict__ dy, int lddy,
+                                     const float* __restrict__ x, int ldx,
+                                     const float* __restrict__ gate, int ldg,
+                                     float* __restrict__ dx, int lddx, int M, int C,
+                                     const float* __restrict__ mean, const float* __restrict__ var,
+                                     float eps, const float* __restrict__ gamma,
+                                     const float* __restrict__ sum_dy,
+                                     const float* __restrict__ sum_dyx, int training,
+                                     float beta_out) {
+  const int C4 = C >> 2, n4 = M * C4;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < n4; e += gridDim.x * blockDim.x) {
+    const int m = e / C4, c = 4 * (e - m * C4);
+    const float4 gv = *reinterpret_cast<const float4*>(dy + m * lddy + c);
+    float4 gt = make_float4(1.f, 1.f, 1.f, 1.f), xv = gt, ov = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (gate) gt = *reinterpret_cast<const float4*>(gate + m * ldg + c);
+    if (training) xv = *reinterpret_cast<const float4*>(x + m * ldx + c);
+    if (beta_out != 0.f) ov = *reinterpret_cast<const float4*>(dx + m * lddx + c);
+    const float4 va = *reinterpret_cast<const float4*>(var + c);
+    const float4 ga = *reinterpret_cast<const float4*>(gamma + c);
+    float4 mu = make_float4(0.f, 0.f, 0.f, 0.f), s1 = mu, s2 = mu;
+    if (training) {
+      mu = *reinterpret_cast<const float4*>(mean + c);
+      s1 = *reinterpret_cast<const float4*>(sum_dy + c);
+      s2 = *reinterpret_cast<const float4*>(sum_dyx + c);
+    }
+    const float gs[4] = {gv.x, gv.y, gv.z, gv.w}, ts[4] = {gt.x, gt.y, gt.z, gt.w};
+    const float xs[4] = {xv.x, xv.y, xv.z, xv.w}, os[4] = {ov.x, ov.y, ov.z, ov.w};
+    const float vs[4] = {va.x, va.y, va.z, va.w}, gms[4] = {ga.x, ga.y, ga.z, ga.w};
+    const float ms[4] = {mu.x, mu.y, mu.z, mu.w}, s1s[4] = {s1.x, s1.y, s1.z, s1.w};
+    const float s2s[4] = {s2.x, s2.y, s2.z, s2.w};
+    float o[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float g = gs[k];
+      if (gate && ts[k] <= 0.f) g = 0.f;
+      const float rs = rsqrtf(vs[k] + eps);
+      float v;
+      if (training) {
+        const float xh = (xs[k] - ms[k]) * rs;
+        v = gms[k] * rs * (g - s1s[k] / M - xh * s2s[k] / M);
+      } else {
+        v = gms[k] * rs * g;
+      }
+      o[k] = beta_out != 0.f ? beta_out * os[k] + v : v;
+    }
+    *reinterpret_cast<float4*>(dx + m * lddx + c) = make_float4(o[0], o[1], o[2], o[3]);
+  }
+}
+
 // dx = gamma*rstd*(g - s1/M - xhat*s2/M)   (training) ; gamma*rstd*g (eval), g = gated dy
 __global__ void bn_bwd_apply_kernel(const float* __restrict__ dy, int64_t lddy, const float* __restrict__ x,
                                     int64_t ldx, const float* __restrict__ gate, int64_t ldg,
@@ -788,9 +870,18 @@ extern "C" int sat_bn_apply(const float* x, int64_t ldx, float* y, int64_t ldy, 
                             const float* gamma, const float* beta, int32_t relu, const float* res,
                             int64_t ldr, void* stream) {
   SAT_CHECK_ARG(x && y && mean && var && gamma && beta && M > 0 && C > 0, "sat_bn_apply: bad args");
-  hipLaunchKernelGGL(bn_apply_kernel, dim3(grid_for((int64_t)M * C)), dim3(256), 0,
-                     as_stream(stream), x, ldx, y, ldy, M, C, mean, var, eps, gamma, beta, relu,
-                     res, ldr);
+  const bool v4 = C % 4 == 0 && ldx % 4 == 0 && ldy % 4 == 0 && (!res || ldr % 4 == 0) &&
+                  aligned16(x) && aligned16(y) && (!res || aligned16(res)) && aligned16(mean) &&
+                  aligned16(var) && aligned16(gamma) && aligned16(beta) &&
+                  (int64_t)M * std::max<int64_t>({ldx, ldy, ldr, C}) < (1LL << 31);
+  if (v4)
+    hipLaunchKernelGGL(bn_apply4_kernel, dim3(grid_for((int64_t)M * C / 4)), dim3(256), 0,
+                       as_stream(stream), x, (int)ldx, y, (int)ldy, M, C, mean, var, eps, gamma,
+                       beta, relu, res, (int)ldr);
+  else
+    hipLaunchKernelGGL(bn_apply_kernel, dim3(grid_for((int64_t)M * C)), dim3(256), 0,
+                       as_stream(stream), x, ldx, y, ldy, M, C, mean, var, eps, gamma, beta, relu,
+                       res, ldr);
   SAT_LAUNCH_CHECK("sat_bn_apply");
   return SAT_OK;
 }
@@ -813,9 +904,19 @@ extern "C" int sat_bn_bwd(const float* dy, int64_t lddy, const float* x, int64_t
   // dbeta += sum(g), dgamma += sum(g * xhat)  (gradients accumulate into the grad arena)
   hipLaunchKernelGGL(colreduce_finish_kernel, dim3(ceil_div(C, 64)), dim3(256), 0, s, p1, p2, RB, C,
                      sum1, sum2, 0.f, dbeta, dgamma);
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_for((int64_t)M * C)), dim3(256), 0, s, dy,
-                     lddy, x, ldx, gate, ldg, dx, lddx, M, C, mean, var, eps, gamma, sum1, sum2,
-                     training, beta_out);
+  const bool v4 = C % 4 == 0 && lddy % 4 == 0 && ldx % 4 == 0 && lddx % 4 == 0 &&
+                  (!gate || ldg % 4 == 0) && aligned16(dy) && aligned16(x) && aligned16(dx) &&
+                  (!gate || aligned16(gate)) && aligned16(mean) && aligned16(var) &&
+                  aligned16(gamma) && aligned16(sum1) && aligned16(sum2) &&
+                  (int64_t)M * std::max<int64_t>({lddy, ldx, lddx, ldg, C}) < (1LL << 31);
+  if (v4)
+    hipLaunchKernelGGL(bn_bwd_apply4_kernel, dim3(grid_for((int64_t)M * C / 4)), dim3(256), 0, s,
+                       dy, (int)lddy, x, (int)ldx, gate, (int)ldg, dx, (int)lddx, M, C, mean, var,
+                       eps, gamma, sum1, sum2, training, beta_out);
+  else
+    hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_for((int64_t)M * C)), dim3(256), 0, s, dy,
+                       lddy, x, ldx, gate, ldg, dx, lddx, M, C, mean, var, eps, gamma, sum1, sum2,
+                       training, beta_out);
   SAT_LAUNCH_CHECK("sat_bn_bwd");
   return SAT_OK;
 }

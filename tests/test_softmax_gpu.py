@@ -132,3 +132,47 @@ def test_loss_partials(cuda, B, T, M, Tp):
     assert abs(float(o[2]) - BCE) <= 1e-6 * abs(BCE) + 1e-7
     assert float(o[3]) == c1 and float(o[4]) == cb
     assert abs(float(o[0]) - (0.1 * L1 + BCE)) <= 1e-6 * (0.1 * L1 + BCE) + 1e-7
+
+
+@pytest.mark.parametrize("M,C,strided", [(6400, 128, False), (6400, 2048, False), (37, 6, False),
+                                         (300, 64, True)])
+def test_batchnorm_passes(cuda, M, C, strided):
+    """sat_bn_stats / sat_bn_apply (ReLU, residual) / sat_bn_bwd (ReLU gate, beta_out) against
+    float64 CPU; float4 paths (C % 4 == 0) and scalar path, row-strided views included"""
+    from sat_amd import kernels as K
+    g = torch.Generator().manual_seed(M + C)
+    eps = 1e-3
+    xb = torch.randn(M, 2 * C if strided else C, generator=g) * 2 + 0.5
+    x = xb[:, :C]
+    gamma, beta = torch.rand(C, generator=g) + 0.5, torch.randn(C, generator=g)
+    res, dy = torch.randn(M, C, generator=g), torch.randn(M, C, generator=g)
+    dx0 = torch.randn(M, C, generator=g)
+    ws = K.Workspace(cuda)
+    xd = xb.to(cuda)[:, :C]
+    mean, var = torch.empty(C, device=cuda), torch.empty(C, device=cuda)
+    K.bn_stats(xd, mean, var, ws)
+    y = torch.empty(M, C, device=cuda)
+    gd, bd = gamma.to(cuda), beta.to(cuda)
+    K.bn_apply(xd, y, mean, var, gd, bd, relu=True, res=res.to(cuda), eps=eps)
+    # backward through the ReLU: gate = post-BN ReLU output (before the residual)
+    gate = (y - res.to(cuda))
+    dgam, dbet = torch.zeros(C, device=cuda), torch.zeros(C, device=cuda)
+    dx = dx0.to(cuda)
+    K.bn_bwd(dy.to(cuda), xd, gate, dx, mean, var, gd, dgam, dbet, ws, training=True,
+             beta_out=1.0, eps=eps)
+    torch.cuda.synchronize()
+
+    xx = x.double()
+    mu, vr = xx.mean(0), xx.var(0, unbiased=False)
+    assert float((mean.cpu().double() - mu).abs().max()) < 1e-5
+    assert float((var.cpu().double() - vr).abs().max()) < 1e-5 * float(vr.max())
+    xh = (xx - mu) / torch.sqrt(vr + eps)
+    pre = gamma.double() * xh + beta.double()
+    yr = pre.clamp(min=0) + res.double()
+    assert float((y.cpu().double() - yr).abs().max()) < 2e-5
+    # the gate as the kernel saw it (y - res can round a tiny positive pre-activation to 0)
+    gg = torch.where(gate.cpu() > 0, dy.double(), torch.zeros(()).double())
+    dxr = gamma.double() / torch.sqrt(vr + eps) * (gg - gg.mean(0) - xh * (gg * xh).mean(0))
+    assert float((dx.cpu().double() - (dx0.double() + dxr)).abs().max()) < 5e-5
+    assert float((dbet.cpu().double() - gg.sum(0)).abs().max()) < 1e-3
+    assert float((dgam.cpu().double() - (gg * xh).sum(0)).abs().max()) < 1e-3

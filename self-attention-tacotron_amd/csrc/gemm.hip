@@ -444,7 +444,39 @@ __global__ void __launch_bounds__(256) gemm_splitk_reduce(GemmP p) {
   }
 }
 
+// Degenerate plain products (the stop-token projection, `stop = x w + b` and its input
+// gradient): tiles of 64 columns or 16-deep K slices would be almost all padding there.
+// N == 1 with row-contiguous A: one wave per output row, lanes over K (float4 when aligned).
+__global__ void __launch_bounds__(256) gemm_n1_kernel(GemmP p, int vec) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= p.M) return;
+  const float* a = p.A + (int64_t)row * p.a_sm;
+  float s = 0.f;
+  if (vec) {
+    for (int k = 4 * lane; k < p.K; k += 256) {
+      const float4 av = *reinterpret_cast<const float4*>(a + k);
+      s += av.x * p.B[(int64_t)k * p.b_sk] + av.y * p.B[(int64_t)(k + 1) * p.b_sk] +
+           av.z * p.B[(int64_t)(k + 2) * p.b_sk] + av.w * p.B[(int64_t)(k + 3) * p.b_sk];
+    }
+  } else {
+    for (int k = lane; k < p.K; k += 64) s += a[k] * p.B[(int64_t)k * p.b_sk];
+  }
+  s = wave_sum(s);
+  if (lane == 0) p.C[(int64_t)row * p.c_sm] = splitk_epilogue(p, row, 0, s);
+}
+// K == 1: the outer product C = epilogue(alpha a b^T), one thread per output element
+__global__ void __launch_bounds__(256) gemm_k1_kernel(GemmP p) {
+  const int total = p.M * p.N;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int row = i / p.N, col = i - row * p.N;
+    const float s = p.A[(int64_t)row * p.a_sm] * p.B[(int64_t)col * p.b_sn];
+    p.C[(int64_t)row * p.c_sm + col] = splitk_epilogue(p, row, col, s);
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
+// LDS-DMA pipelined variant// ---------------------------------------------------------------------------------------------
 // LDS-DMA pipelined variant (the default for every vector-loadable operand mode).
 //
 // Operand tiles go global -> LDS with global_load_lds_dwordx4 (no VGPR staging, no ds_write
@@ -1161,6 +1193,19 @@ extern "C" int sat_gemm(const SatGemmDesc* d, void* stream) {
                   "sat_gemm: colsum_out fallback needs ws_bytes >= sat_workspace_colreduce(K, N)");
     SAT_CHECK_ARG(d->b_sn == 1, "sat_gemm: colsum_out fallback needs B rows contiguous");
     return sat_colsum(d->B, d->b_sk, d->K, d->N, d->colsum_out, d->beta, d->ws, stream);
+  }
+  if (nb == 1 && d->a_mode == 0 && d->b_mode == 0 && !t_probe &&
+      ((d->N == 1 && d->a_sk == 1) || (d->K == 1 && (int64_t)d->M * d->N < (1LL << 31)))) {
+    if (d->N == 1) {
+      const int vec = (d->K % 4 == 0 && d->a_sm % 4 == 0 && aligned16(d->A)) ? 1 : 0;
+      hipLaunchKernelGGL(gemm_n1_kernel, dim3(ceil_div(d->M, 4)), dim3(256), 0, s, p, vec);
+    } else {
+      const int64_t total = (int64_t)d->M * d->N;
+      hipLaunchKernelGGL(gemm_k1_kernel, dim3((int)std::min<int64_t>((total + 255) / 256, 4096)),
+                         dim3(256), 0, s, p);
+    }
+    SAT_LAUNCH_CHECK("sat_gemm (degenerate shape)");
+    return SAT_OK;
   }
   if (gemm_lds_enabled()) {
     const int r = launch_lds(d, p, nb, s);

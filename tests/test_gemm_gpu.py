@@ -315,3 +315,26 @@ def test_gemm_splitk_repeatable(cuda, M, N, K, bm, bn, split):
     ref = A.double() @ B.double()
     bound = 6e-7 * (A.double().abs() @ B.double().abs()) + 1e-7
     assert bool(((outs[0].double().cpu() - ref).abs() <= bound).all())
+
+
+@pytest.mark.parametrize("M,N,K,ta", [(16000, 1, 256, False), (37, 1, 5, False), (300, 1, 1024, True),
+                                      (16000, 256, 1, False), (5, 3, 1, False), (1, 1, 1, False)])
+@pytest.mark.parametrize("act", [None, "sigmoid"])
+def test_gemm_degenerate_shapes(cuda, M, N, K, ta, act):
+    """N == 1 (row-contiguous A: one wave per row; transposed A: the tiled path) and K == 1
+    (outer product) with bias, activation and beta, against float64"""
+    from sat_amd import kernels
+    g = torch.Generator().manual_seed(M + 7 * N + 3 * K)
+    A = torch.randn(K, M, generator=g) if ta else torch.randn(M, K, generator=g)
+    B = torch.randn(K, N, generator=g)
+    bias, C0 = torch.randn(N, generator=g), torch.randn(M, N, generator=g)
+    C = C0.to(cuda)
+    Ad = A.to(cuda).t() if ta else A.to(cuda)
+    kernels.gemm(Ad, B.to(cuda), C, alpha=0.5, beta=0.75, bias=bias.to(cuda), act=act)
+    torch.cuda.synchronize()
+    Al = (A.t() if ta else A).double()
+    ref = 0.5 * (Al @ B.double()) + 0.75 * C0.double() + bias.double()
+    if act == "sigmoid":
+        ref = torch.sigmoid(ref)
+    bound = 2e-6 * (0.5 * (Al.abs() @ B.double().abs()) + C0.double().abs() + 1) + 1e-6
+    assert bool(((C.double().cpu() - ref).abs() <= bound).all())

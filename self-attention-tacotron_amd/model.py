@@ -282,7 +282,7 @@ def model_forward(P, bn: BNState, hp, d: PR.Dims, batch: Dict[str, torch.Tensor]
     mel_r, stop = head_fwd(P, hp, d, dout, masks, sv)
     B, Tp, _ = mel_r.shape
     mel = mel_r.view(B, Tp * d.r, d.num_mels)                         # module.py:1561
-    loss = torch.zeros(8, device=m1.device)
+    loss = torch.empty(8, device=m1.device)          # sat_loss_fwd_bwd writes [0:5]; [5:8] unused
     dmel = dstop = None
     if compute_grad_seeds:
         dmel = torch.empty_like(mel)

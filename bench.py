@@ -58,6 +58,8 @@ def parse():
                     help="skip the attention-kernel probe (profiling runs of the step alone)")
     ap.add_argument("--cpu-baseline-batch", type=int, default=2)
     ap.add_argument("--cpu-baseline-steps", type=int, default=4)
+    ap.add_argument("--cpu-baseline-c2-steps", type=int, default=1,
+                    help="steps of the C2-shape (B=32) CPU oracle leg, 0 = skip")
     ap.add_argument("--attn-tile", type=int, default=32)
     ap.add_argument("--pipeline-chunk", type=int, default=40,
                     help="decoder steps per chunk of the multi-stream recurrence pipeline (0 = off)")
@@ -103,7 +105,8 @@ def attention_probe(rec, B, N, reps=6):
     f = 4  # fp32
     # per decoder step 4 (549 B N + 67,191) bytes = K1/V1/K2/V2 + the two
     # alignment states of every utterance + the attention's own weights (query, location, v)
-    attn_step = f * (B * N * (D1 + M1 + D2 + M2 + 5) + (M1 + M2) * (D1 + D2)
+    # (d_q = U = 256 query rows: the query layers are [U, D1] and [U, D2])
+    attn_step = f * (B * N * (D1 + M1 + D2 + M2 + 5) + U * (D1 + D2)
                      + F * (KW + 1) + F * D1 + 2 * D1 + D2)
     bytes_launch = T * attn_step
     achieved = bytes_launch / avg_s / 1e9
@@ -138,13 +141,15 @@ def _pmc_traffic():
         return None, "unreadable PMC summary"
 
 
-def cpu_baseline(hp, args):
+def cpu_baseline(hp, args, B=None, steps=None):
     """The CPU oracle (float32 PyTorch-CPU restatement, test infrastructure) timed on this box's
-    host cores on a bounded sample of the same workload: C1 = LJSpeech B=2 x (200 chars,
-    1000 frames), one full training step (forward + autograd BPTT + Adam)."""
+    host cores on a bounded sample of the same workload: by default C1 = LJSpeech B=2 x
+    (200 chars, 1000 frames) full training steps (forward + autograd BPTT + Adam); with
+    B = 32, one step of the C2 shape itself."""
     from oracle import sat_oracle as O
     from sat_amd import data, params
-    B = args.cpu_baseline_batch
+    B = args.cpu_baseline_batch if B is None else B
+    nsteps = args.cpu_baseline_steps if steps is None else steps
     # the box's OMP_NUM_THREADS share (16 there); the affinity mask can list the whole machine
     torch.set_num_threads(int(os.environ.get("OMP_NUM_THREADS", "0"))
                           or min(16, len(os.sched_getaffinity(0))))
@@ -158,7 +163,7 @@ def cpu_baseline(hp, args):
     m = {k: torch.zeros_like(v) for k, v in p.items()}
     v2 = {k: torch.zeros_like(v) for k, v in p.items()}
     t0 = time.perf_counter()
-    for s in range(args.cpu_baseline_steps):
+    for s in range(nsteps):
         for q in p.values():
             q.grad = None
         out = O.model_forward(p, bufs, hp, batch, masks, training=True)
@@ -169,11 +174,11 @@ def cpu_baseline(hp, args):
             for (k, q), g in zip(p.items(), grads):
                 new, m[k], v2[k] = O.adam_tf(q, g, m[k], v2[k], lr, s + 1)
                 q.copy_(new)
-    dt = (time.perf_counter() - t0) / args.cpu_baseline_steps
+    dt = (time.perf_counter() - t0) / nsteps
     return {"value": round(B * args.frames / dt, 2), "unit": "frames/s",
             "cores": torch.get_num_threads(), "kind": "port",
             "sample": f"CPU oracle (float32 PyTorch-CPU restatement, not TF1.x), LJSpeech B={B} x "
-                      f"{args.chars} chars x {args.frames} frames, {args.cpu_baseline_steps} "
+                      f"{args.chars} chars x {args.frames} frames, {nsteps} "
                       f"full training step(s) (fwd + BPTT + Adam), {dt:.2f} s/step"}
 
 
@@ -299,6 +304,8 @@ def main():
         extra["c5_free_running"] = c5_free_running(args)
     if rank == 0:
         cpu = None if args.no_cpu_baseline else cpu_baseline(hp, args)
+        cpu_c2 = (None if args.no_cpu_baseline or args.cpu_baseline_c2_steps <= 0
+                  else cpu_baseline(hp, args, B=B, steps=args.cpu_baseline_c2_steps))
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "frames/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * dt / args.steps, 3),
@@ -311,7 +318,7 @@ def main():
                        "decoder_steps": T // hp.outputs_per_step, "parallelism": f"dp{world}",
                        "hip_graph": not args.no_graph, "params": model.num_params},
             "median_ms_per_step": round(float(np.median(step_ms)), 3),
-            "roofline": roof, "cpu_baseline": cpu, **extra,
+            "roofline": roof, "cpu_baseline": cpu, "cpu_baseline_c2": cpu_c2, **extra,
             "loss_first_timed": round(loss0, 5), "loss_last": round(loss1, 5),
         }
         print(json.dumps(line), flush=True)

@@ -494,6 +494,45 @@ typedef struct SatDecLstmBwd {
   int64_t* prof;   /* optional [256][4] per-workgroup segment clocks (100 MHz), NULL = off */
 } SatDecLstmBwd;
 
+/* ---------------------------------------------------------------- the whole decoder loop
+ * SURVEY.md 8(b)'s single C entry for the teacher-forced decoder recurrence: DecoderRNNV2
+ * (MultiRNNCell[DualSourceAttentionRNN, ZoneoutLSTM, ZoneoutLSTM], ext tacotron2, built at
+ * modules/module.py:1531-1540) driven by TransformerTrainingHelper (modules/helpers.py:13-58)
+ * over all T' steps, i.e. what decoder.py decoder_forward orchestrates on the persistent path:
+ *   1. sat_decoder_attention_fwd(&attn)   -- attention RNN + query + dual-source attention,
+ *                                            all T' steps, one persistent launch;
+ *   2. X1 = H0RAW W1x[0:U] + b1 + ctx W1x[U:U+M1+M2]  -- LSTM1's input projection for all
+ *      steps as two GEMMs (ctx = REC0 rows 1..T', columns 0..M1+M2; ConcatOutputAndAttention);
+ *   3. sat_decoder_lstms_fwd(&lstm)       -- both ZoneoutLSTM layers, one persistent launch.
+ * lstm.X1 must point at the X1 buffer [T'][B][4U]; attn.H0RAW / attn.REC0 are read as LSTM1's
+ * input.  W1x = LSTM1 kernel input rows [U + M1 + M2][4U] (gate-interleaved), b1 its bias.
+ * ws / ws_bytes: GEMM split-K scratch (as SatGemmDesc.ws).  Every buffer is caller-owned. */
+typedef struct SatDecoderLoopFwd {
+  SatDecAttnFwd attn;
+  SatDecLstmFwd lstm;
+  const float* W1x; const float* b1;
+  void* ws; int64_t ws_bytes;
+} SatDecoderLoopFwd;
+int sat_decoder_loop_fwd(const SatDecoderLoopFwd* args, void* stream);
+
+/* Its BPTT (backward.py decoder_bwd, persistent path): sat_decoder_lstms_bwd(&lstm) -> DH0 =
+ * DG1 W1x[0:U]^T and RD[:, :, 0:M1+M2] = DG1 W1x[U:U+M1+M2]^T (LSTM1's input gradients) ->
+ * sat_decoder_attention_bwd(&attn).  attn.DH0 must point at DH0 [T'][B][U] and attn.RD at RD
+ * [T'][B][M1+M2+U] (zeroed here first); lstm.DG1 is read as LSTM1's gate gradients. */
+typedef struct SatDecoderLoopBwd {
+  SatDecLstmBwd lstm;
+  SatDecAttnBwd attn;
+  const float* W1x;
+  float* DH0;
+  void* ws; int64_t ws_bytes;
+} SatDecoderLoopBwd;
+int sat_decoder_loop_bwd(const SatDecoderLoopBwd* args, void* stream);
+
+/* SURVEY.md 8(b)'s names for one ZoneoutLSTM step (ext tacotron2 ZoneoutLSTMCell around TF
+ * LSTMCell, modules/module.py:1522-1527): the same entries as sat_lstm_step_fwd / _bwd. */
+int sat_zlstm_step_fwd(const SatLstmFwd* args, void* stream);
+int sat_zlstm_step_bwd(const SatLstmBwd* args, void* stream);
+
 /* Persistent encoder BiLSTM: all N steps of both directions of ZoneoutCBHG's bidirectional
  * ZoneoutLSTM (modules/module.py:93-110, TF bidirectional_dynamic_rnn with sequence_length;
  * zoneout LSTM cell of ext tacotron2) in ONE launch each way.  Replaces the per-step

@@ -127,6 +127,16 @@ SatDecLstmBwd = _struct("SatDecLstmBwd", """
     i32:B i32:T i32:U f32:zc f32:zh ptr:W1r ptr:W2 ptr:G1 ptr:C1S ptr:G2 ptr:C2S ptr:DH2
     ptr:mask1_c ptr:mask1_h ptr:mask2_c ptr:mask2_h ptr:DG1 ptr:DG2 ptr:ctr ptr:err ptr:prof""")
 
+class SatDecoderLoopFwd(ctypes.Structure):   # mirrors include/sat_abi.h
+    _fields_ = [("attn", SatDecAttnFwd), ("lstm", SatDecLstmFwd), ("W1x", _P), ("b1", _P),
+                ("ws", _P), ("ws_bytes", _I64)]
+
+
+class SatDecoderLoopBwd(ctypes.Structure):   # mirrors include/sat_abi.h
+    _fields_ = [("lstm", SatDecLstmBwd), ("attn", SatDecAttnBwd), ("W1x", _P), ("DH0", _P),
+                ("ws", _P), ("ws_bytes", _I64)]
+
+
 SatEncLstmFwd = _struct("SatEncLstmFwd", """
     i32:B i32:N i32:U f32:zc f32:zh ptr:X_fw ptr:X_bw i64:x_sb i64:x_sn ptr:W_fw ptr:W_bw
     ptr:mc_fw ptr:mh_fw ptr:mc_bw ptr:mh_bw ptr:lengths ptr:H i64:h_sb i64:h_sn
@@ -173,6 +183,10 @@ SIGNATURES = {
     "sat_encoder_lstm_fwd": [ctypes.POINTER(SatEncLstmFwd), _P],
     "sat_encoder_lstm_bwd": [ctypes.POINTER(SatEncLstmBwd), _P],
     "sat_decoder_lstms_bwd": [ctypes.POINTER(SatDecLstmBwd), _P],
+    "sat_decoder_loop_fwd": [ctypes.POINTER(SatDecoderLoopFwd), _P],
+    "sat_decoder_loop_bwd": [ctypes.POINTER(SatDecoderLoopBwd), _P],
+    "sat_zlstm_step_fwd": [ctypes.POINTER(SatLstmFwd), _P],
+    "sat_zlstm_step_bwd": [ctypes.POINTER(SatLstmBwd), _P],
     "sat_attn_param_grad_rows": [_I32, _I32],
     "sat_attn_param_grads": [ctypes.POINTER(SatAttnParamGrad), _P],
     "sat_seq_mask": [_P, _P, _I32, _I32, _I32, _P, _P],

@@ -973,6 +973,36 @@ extern "C" int sat_colsum_scatter(const float* x, int64_t ldx, int32_t M, int32_
   return SAT_OK;
 }
 
+// out = alpha * colsum(x) + beta * out (the GEMM's colsum_out fallback, sat_gemm: alpha applies
+// to the column sums exactly as the fused LDS path applies it)
+__global__ void colreduce_finish_alpha_kernel(const double* part1, int RB, int C, float* out,
+                                              float alpha, float beta) {
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  double s, q;
+  sum_partials(part1, part1, RB, C, c, s, q);
+  if (threadIdx.x < 64 && c < C)
+    out[c] = beta != 0.f ? (float)(beta * out[c] + (double)alpha * s) : (float)((double)alpha * s);
+}
+
+int sat::colsum_alpha(const float* x, int64_t ldx, int32_t M, int32_t C, float* out, float alpha,
+                 float beta, void* workspace, hipStream_t s) {
+  SAT_CHECK_ARG(x && out && workspace && M >= 0 && C > 0, "sat_gemm colsum_out: bad args");
+  if (M == 0 && beta == 1.f) return SAT_OK;
+  const int RB = row_blocks(std::max(M, 1));
+  double* p1 = reinterpret_cast<double*>(workspace);
+  double* p2 = p1 + (int64_t)RB * C;
+  if (M > 0)
+    hipLaunchKernelGGL(colreduce_kernel, dim3(ceil_div(C, 64), RB), dim3(256), 0, s, x, ldx,
+                       (const float*)nullptr, (int64_t)0, M, C, p1, p2, 2, (const float*)nullptr,
+                       (const float*)nullptr, 0.f, (const float*)nullptr, (int64_t)0);
+  else
+    (void)zero_dwords(p1, 2 * (int64_t)RB * C, s);
+  hipLaunchKernelGGL(colreduce_finish_alpha_kernel, dim3(ceil_div(C, 64)), dim3(256), 0, s, p1,
+                     RB, C, out, alpha, beta);
+  SAT_LAUNCH_CHECK("sat_gemm colsum_out");
+  return SAT_OK;
+}
+
 extern "C" int sat_colsum(const float* x, int64_t ldx, int32_t M, int32_t C, float* out,
                           float beta, void* workspace, void* stream) {
   SAT_CHECK_ARG(x && out && workspace && M >= 0 && C > 0, "sat_colsum: bad args");

@@ -1192,7 +1192,7 @@ extern "C" int sat_gemm(const SatGemmDesc* d, void* stream) {
     SAT_CHECK_ARG(d->ws && d->ws_bytes >= need,
                   "sat_gemm: colsum_out fallback needs ws_bytes >= sat_workspace_colreduce(K, N)");
     SAT_CHECK_ARG(d->b_sn == 1, "sat_gemm: colsum_out fallback needs B rows contiguous");
-    return sat_colsum(d->B, d->b_sk, d->K, d->N, d->colsum_out, d->beta, d->ws, stream);
+    return colsum_alpha(d->B, d->b_sk, d->K, d->N, d->colsum_out, d->alpha, d->beta, d->ws, s);
   }
   if (nb == 1 && d->a_mode == 0 && d->b_mode == 0 && !t_probe &&
       ((d->N == 1 && d->a_sk == 1) || (d->K == 1 && (int64_t)d->M * d->N < (1LL << 31)))) {

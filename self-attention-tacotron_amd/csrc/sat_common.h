@@ -156,6 +156,10 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
+// out = alpha * (column sums of x [M, C]) + beta * out, fp64 partials (elementwise.hip)
+int colsum_alpha(const float* x, int64_t ldx, int32_t M, int32_t C, float* out, float alpha,
+                 float beta, void* workspace, hipStream_t s);
+
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 inline int ceil_div(int64_t a, int64_t b) { return static_cast<int>((a + b - 1) / b); }

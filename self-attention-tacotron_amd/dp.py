@@ -44,6 +44,18 @@ def allreduce_grads(flat: torch.Tensor, group=None) -> None:
         tdist.all_reduce(flat, op=tdist.ReduceOp.SUM, group=group)
 
 
+def combine_health(words: torch.Tensor, group=None) -> None:
+    """MAX over replicas of the step's int32 health words, in place (before the optimiser).
+
+    Each rank's persistent kernels raise their own error words (a hand-off timeout, an id out
+    of range).  The gradient all-reduce has already mixed a bad rank's gradients into every
+    replica, so the guarded Adam step must skip on EVERY rank or on none: with the words
+    combined, all ranks skip together and all raise on their next ``check_health`` (instead of
+    the healthy ranks applying the update and then blocking in the next collective)."""
+    if world_size(group) > 1:
+        tdist.all_reduce(words, op=tdist.ReduceOp.MAX, group=group)
+
+
 def average_buffer(flat: torch.Tensor, group=None) -> None:
     """Mean over replicas in place (BatchNorm moving statistics: the replicas' updates are
     averaged each step so every rank holds the same EVAL / checkpoint state; TF1

@@ -330,9 +330,17 @@ class FreeRunningDecoder:
             return
         g = pl.graphs.get(a)
         if g is None:
-            # capture on a side stream (the current stream's pending work is joined first);
-            # the graph's private pool keeps every per-step temporary alive across replays
-            s = torch.cuda.Stream(device=self.m.device)
+            # capture on the plan's ONE side stream (the current stream's pending work is
+            # joined first); the graph's private pool keeps every per-step temporary alive
+            # across replays.  One stream per plan: the GEMM split-K workspace is keyed by
+            # stream, so a fresh stream per chunk would allocate (and pin) a new workspace
+            # inside every chunk's pool; the plan's stream gets its workspace before the first
+            # capture, outside any pool.
+            s = getattr(pl, "capture_stream", None)
+            if s is None:
+                s = pl.capture_stream = torch.cuda.Stream(device=self.m.device)
+                with torch.cuda.stream(s):
+                    K._gemm_ws(self.m.device)
             s.wait_stream(torch.cuda.current_stream())
             g = torch.cuda.CUDAGraph()
             with torch.cuda.stream(s):
@@ -385,8 +393,10 @@ class FreeRunningDecoder:
                     break
         T_ = steps
         r, M = d.r, d.num_mels
-        mel = pl.MEL[:T_].permute(1, 0, 2).reshape(B, T_ * r, M)
-        stop = pl.STOP[:T_, :, 0].transpose(0, 1).contiguous()
+        # copies, never views of the plan's buffers: the next run() on this shape zeroes and
+        # rewrites them (with B == 1 reshape / contiguous would return views)
+        mel = pl.MEL[:T_].permute(1, 0, 2).reshape(B, T_ * r, M).clone()
+        stop = pl.STOP[:T_, :, 0].transpose(0, 1).clone()
         return {"mel": mel, "stop": stop, "steps": T_,
                 "alignment1": pl.AL1[1:T_ + 1].permute(1, 2, 0).contiguous(),   # [B, N, T']
                 "alignment2": pl.S2[:T_].permute(1, 2, 0).contiguous(),

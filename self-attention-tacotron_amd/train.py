@@ -103,8 +103,10 @@ class Trainer:
 
     def reduce_grads(self):
         """The step's one gradient exchange (SUM; 1/world folded into Adam) plus the mean of
-        the BatchNorm moving statistics (a few KB) so replicas never drift apart."""
+        the BatchNorm moving statistics (a few KB) so replicas never drift apart, and the MAX
+        of the 16 health words so the guarded update is skipped on every rank or on none."""
         dp.allreduce_grads(self.m.grads, self.pg)
+        dp.combine_health(self.m.health, self.pg)
         bn = getattr(self.m, "bn", None)
         if bn is not None and self.world > 1:
             dp.average_buffer(bn.buf, self.pg)

@@ -53,7 +53,8 @@ def _c_sizeof(struct):
 
 STRUCTS = ["SatGemmDesc", "SatLstmFwd", "SatLstmBwd", "SatAttnStep", "SatAttnStepBwd",
            "SatAttnParamGrad", "SatDecAttnFwd", "SatDecAttnBwd", "SatDecLstmFwd",
-           "SatDecLstmBwd", "SatEncLstmFwd", "SatEncLstmBwd", "SatAdamConfig", "SatConvBank", "SatMha", "SatDims", "SatRngSegment", "SatColSegment"]
+           "SatDecLstmBwd", "SatEncLstmFwd", "SatEncLstmBwd", "SatAdamConfig", "SatConvBank", "SatMha", "SatDims", "SatRngSegment", "SatColSegment",
+           "SatDecoderLoopFwd", "SatDecoderLoopBwd"]
 
 
 def _c_offsets(struct, fields):

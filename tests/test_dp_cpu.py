@@ -33,34 +33,57 @@ def _worker(rank, world, port, q):
         p = torch.full((1000,), float(rank + 1))
         dp.broadcast_params(p)
         res["bcast"] = bool(torch.all(p == 1.0))
-        # one SUM all-reduce of the flat gradient arena + 1/world folded into Adam's config
+        # every rank holds DIFFERENT local gradients, BN buffers and health words; the
+        # exchange must leave each rank with the global-batch state
         hp = hparams.ljspeech_hparams()
+        n = 4096
+
+        def local_grad(r):
+            g = torch.Generator().manual_seed(100 + r)
+            return torch.randn(n, generator=g) * (1e-4 * (0.5 + r))   # global norm < clip_norm
+
+        def local_bn(r):
+            return torch.linspace(-1.0, 1.0, 64) * (r + 1) + 0.25 * r
+
         model = types.SimpleNamespace(
-            hp=hp, device=torch.device("cpu"), params=torch.zeros(4096),
-            grads=torch.arange(4096, dtype=torch.float32) * (rank + 1),
+            hp=hp, device=torch.device("cpu"), params=torch.zeros(n),
+            grads=local_grad(rank).clone(),
             health=torch.zeros(16, dtype=torch.int32),
-            bn=types.SimpleNamespace(buf=torch.full((64,), float(rank))))
+            bn=types.SimpleNamespace(buf=local_bn(rank).clone()))
+        if rank == 1:
+            model.health[3] = 1          # a hand-off timeout on rank 1 only
         tr = train.Trainer(model, B=2, N=8, Tp=4)
         tr.reduce_grads()
-        expect = torch.arange(4096, dtype=torch.float32) * sum(r + 1 for r in range(world))
-        res["sum"] = bool(torch.equal(model.grads, expect))
+        gsum = sum(local_grad(r) for r in range(world))
+        res["sum"] = bool(torch.equal(model.grads, gsum))
         res["scale"] = tr.cfg.grad_scale
         res["world"] = tr.world
-        # BatchNorm moving statistics: averaged over the replicas in the same exchange
-        res["bn"] = bool(torch.allclose(model.bn.buf, torch.full((64,), (world - 1) / 2)))
-        # the optimiser applied on every rank to the reduced arena (a host restatement of the
-        # fused clip + Adam step with grad_scale = 1/world) leaves bit-identical replicas
+        # BatchNorm moving statistics: the mean of the replicas' buffers
+        bn_mean = sum(local_bn(r) for r in range(world)) / world
+        res["bn"] = bool(torch.allclose(model.bn.buf, bn_mean, rtol=0, atol=1e-6))
+        # health words combined by MAX: every rank sees rank 1's error, so the guarded update
+        # is skipped everywhere (not applied on rank 0 and skipped on rank 1)
+        res["health"] = model.health.tolist()
+        # the optimiser on the reduced arena (host restatement of the fused clip + Adam step,
+        # gradient scaled by cfg.grad_scale) == ONE process stepping on the global-batch mean
+        # gradient; and the replicas agree
         from oracle import sat_oracle as O
-        p = torch.linspace(-1, 1, 4096, dtype=torch.float64)
-        mo = torch.zeros_like(p)
-        vo = torch.zeros_like(p)
-        for step in range(1, 3):
-            g = model.grads.double() * tr.cfg.grad_scale
-            (g,), _ = O.clip_by_global_norm([g], 1.0)
-            p, mo, vo = O.adam_tf(p, g, mo, vo,
-                                  O.learning_rate(hp.initial_learning_rate, step - 1), step)
-        gathered = [torch.empty_like(p) for _ in range(world)]
-        tdist.all_gather(gathered, p)
+
+        def adam_steps(g_fn):
+            p = torch.linspace(-1, 1, n, dtype=torch.float64)
+            mo = torch.zeros_like(p)
+            vo = torch.zeros_like(p)
+            for step in range(1, 3):
+                (g,), _ = O.clip_by_global_norm([g_fn()], 1.0)
+                p, mo, vo = O.adam_tf(p, g, mo, vo,
+                                      O.learning_rate(hp.initial_learning_rate, step - 1), step)
+            return p
+
+        p_dp = adam_steps(lambda: model.grads.double() * tr.cfg.grad_scale)
+        p_one = adam_steps(lambda: sum(local_grad(r).double() for r in range(world)) / world)
+        res["matches_single"] = bool(torch.allclose(p_dp, p_one, rtol=0, atol=1e-12))
+        gathered = [torch.empty_like(p_dp) for _ in range(world)]
+        tdist.all_gather(gathered, p_dp)
         res["replicas_equal"] = all(torch.equal(gathered[0], x) for x in gathered[1:])
         # masks are drawn per replica: the model_fn seed offset differs by rank
         res["seed_offset"] = 1000003 * dp.rank()
@@ -87,6 +110,8 @@ def test_dp_world2_gloo():
         res = out[r]
         assert isinstance(res, dict), res
         assert res["bcast"] and res["sum"] and res["bn"] and res["replicas_equal"]
+        assert res["matches_single"]
+        assert res["health"][3] == 1 and sum(res["health"]) == 1
         assert res["seed_offset"] == 1000003 * r
         assert res["scale"] == pytest.approx(0.5) and res["world"] == 2
         assert res["max"] == pytest.approx(1.5)

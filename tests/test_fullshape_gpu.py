@@ -12,8 +12,13 @@ show.  Every case runs the persistent kernels that the bench times (any B <= 32 
 * C2 (B=32: 4 utterances per hand-off group) forward in eval mode.
 
 Tolerances (written per assertion): mel mean-L1 <= 1e-4 (north_star); loss within 1e-5
-relative; stop logits mean-abs <= 1e-4; every parameter gradient within 1e-3 of
-max(|g_ref|, 1e-4 max|g|) (fp32 BPTT over 500 steps against float64 autograd).
+relative; stop logits mean-abs <= 1e-4; every parameter gradient within 2e-4 of
+max(|g_ref|, 1e-4 max|g|) (fp32 BPTT over 500 steps against float64 autograd; achieved
+5.5e-5, profiles/r02_parity_fullshape.jsonl).
+
+* C4 (VCTK multi-speaker, B=32, N=200, T=1000: speaker embedding + MultiSpeakerPreNet,
+  modules/multi_speaker_modules.py:11-37, models/models.py:43-46): eval and train with
+  injected masks, same bars.
 Set SAT_PARITY_REPORT=<file> to append the achieved numbers as JSON lines."""
 import json
 import os
@@ -32,11 +37,11 @@ def _report(name, **vals):
             f.write(json.dumps({"case": name, **vals}) + "\n")
 
 
-def _run(cuda, B, N, T, train, shape="max", seed=11, grads=False):
+def _run(cuda, B, N, T, train, shape="max", seed=11, grads=False, preset="ljspeech"):
     from sat_amd import data, engine, hparams, params
     from sat_amd.decoder import persistent_eligible
     from oracle import sat_oracle as O
-    hp = hparams.ljspeech_hparams()
+    hp = getattr(hparams, f"{preset}_hparams")()
     vals = params.init_params(hp, seed=5)
     b = data.synthetic_batch(hp, B, N=N, T=T, shape=shape, seed=seed)
     Np, Tp = b["source"].shape[1], b["mel"].shape[1] // hp.outputs_per_step
@@ -92,6 +97,17 @@ def test_c2_full_shape_forward_matches_oracle(cuda):
     _compare_outputs("c2_eval", out, ref, b)
 
 
+@pytest.mark.parametrize("train", [False, True], ids=["eval", "train_masks"])
+def test_c4_vctk_full_shape_matches_oracle(cuda, train):
+    """C4: VCTK multi-speaker self-attention-tacotron.json at the bench shape (B=32, N=200,
+    T=1000 -> 500 steps): speaker rows through the MultiSpeakerPreNet's softsign epilogue and
+    zero-batch-stride residual, persistent kernels, vs the float64 oracle."""
+    hp, m, out, ref, _, b = _run(cuda, 32, 200, 1000, train, seed=41, preset="vctk")
+    assert hp.use_speaker_embedding and m.d.multi_speaker
+    assert "speaker_id" in b and int(b["speaker_id"].min()) >= 225
+    _compare_outputs(f"c4_{'train' if train else 'eval'}", out, ref, b)
+
+
 def test_gradients_full_length_match_oracle(cuda):
     """BPTT over 500 steps at B=8, N<=200 (ragged; up to 7 tiles with halos), T<=1000, train
     mode with injected masks: loss and every parameter gradient vs float64 autograd."""
@@ -106,7 +122,7 @@ def test_gradients_full_length_match_oracle(cuda):
         scale = max(np.abs(g_ref).max(), 1e-4 * gmax)
         err = float(np.abs(grads[name].astype(np.float64) - g_ref).max() / scale)
         worst = max(worst, err)
-        if not err <= 1e-3:
+        if not err <= 2e-4:
             bad.append((name, err))
     _report("grad_b8", worst_rel_grad_err=worst, steps=int(b["mel"].shape[1] // 2))
     assert not bad, bad

@@ -226,7 +226,10 @@ def test_rng_fill_segments_equals_per_mask_fills(cuda):
 @pytest.mark.parametrize("M,N,K", [(256, 1024, 3000), (128, 260, 500), (36, 64, 7000), (6, 40, 50)])
 @pytest.mark.parametrize("ta", [True, False])
 @pytest.mark.parametrize("split", [0, 4])
-def test_gemm_colsum_fused(cuda, M, N, K, ta, split):
+@pytest.mark.parametrize("alpha", [1.0, -0.75])
+def test_gemm_colsum_fused(cuda, M, N, K, ta, split, alpha):
+    """alpha applies to the product AND the column sums, on the fused LDS path and on the
+    separate-reduction fallback (M % 4 != 0 with a transposed A is not vector-loadable)"""
     from sat_amd import _lib, kernels
     g = torch.Generator().manual_seed(M + 3 * N + K + split)
     A = torch.randn(K, M, generator=g) if ta else torch.randn(M, K, generator=g)
@@ -238,17 +241,17 @@ def test_gemm_colsum_fused(cuda, M, N, K, ta, split):
     if split:
         lib.sat_gemm_force_plan(64, 64, split)
     try:
-        kernels.gemm(A.to(cuda).t() if ta else A.to(cuda), B.to(cuda), C, alpha=1.0, beta=1.0,
+        kernels.gemm(A.to(cuda).t() if ta else A.to(cuda), B.to(cuda), C, alpha=alpha, beta=1.0,
                      colsum=s)
         torch.cuda.synchronize()
     finally:
         lib.sat_gemm_force_plan(0, 0, 0)
     Al = (A.t() if ta else A).double()
-    ref = Al @ B.double() + C0.double()
-    rs = B.double().sum(0) + s0.double()
-    bound = 6e-7 * (Al.abs() @ B.double().abs() + C0.double().abs()) + 1e-7
+    ref = alpha * (Al @ B.double()) + C0.double()
+    rs = alpha * B.double().sum(0) + s0.double()
+    bound = 6e-7 * (abs(alpha) * (Al.abs() @ B.double().abs()) + C0.double().abs()) + 1e-7
     assert bool(((C.double().cpu() - ref).abs() <= bound).all())
-    bs = 6e-7 * (B.double().abs().sum(0) + s0.double().abs()) + 1e-7
+    bs = 6e-7 * (abs(alpha) * B.double().abs().sum(0) + s0.double().abs()) + 1e-7
     assert bool(((s.double().cpu() - rs).abs() <= bs).all()), float(((s.double().cpu() - rs).abs() / bs).max())
 
 

@@ -240,3 +240,81 @@ def test_graph_decode_equals_eager(cuda):
     val_g = FreeRunningDecoder(m, helper="validation", feed="softmax", graphs=True,
                                check_every=5).run(gb)
     assert torch.equal(val_e["mel"], val_g["mel"])
+
+
+# ---- C5 at its configured size (BASELINE configs[4]: LJSpeech, B=8, N=200, 500 free-running
+#      decoder steps feeding back the predicted mel; modules/module.py:766-784,
+#      predict_mel.py:36-75)
+def _c5_batch(cuda, seed=55):
+    return _vbatch(cuda, B=8, N=200, T=1000, seed=seed)
+
+
+def test_c5_first_100_steps_match_oracle(cuda):
+    """The first 100 free-running steps at B=8, N=200 (mel feedback, KV-cached head) vs the
+    oracle's restatement (TransformerWrapper re-running the causal self-attention over the whole
+    history each step).  The decode feeds its own fp32 output back, so the fp32-vs-float64
+    difference compounds through the recurrence: mel within 1e-3 absolute (max) and 2e-5
+    mean-abs over the 100 steps, alignments within 1e-4."""
+    from sat_amd import params
+    from sat_amd.inference import FreeRunningDecoder
+    hp, vals, m, b, gb, O = _c5_batch(cuda)
+    T = 100
+    out = FreeRunningDecoder(m, max_iters=T, min_iters=T, check_every=25, graphs=True).run(gb)
+    ref = O.infer_free_running(O.to_torch(vals), O.to_torch(params.init_bn_buffers(hp)), hp,
+                               O.to_torch(b), max_iters=T, min_iters=T)
+    assert out["steps"] == ref["steps"] == T
+    d = np.abs(out["mel"].double().cpu().numpy() - ref["mel"].numpy())
+    da = np.abs(out["alignment1"].double().cpu().numpy()
+                - ref["alignment1"].permute(0, 2, 1).numpy())
+    path = os.environ.get("SAT_PARITY_REPORT")
+    if path:
+        with open(path, "a") as f:
+            f.write(json.dumps({"case": "c5_first100", "mel_max_abs": float(d.max()),
+                                "mel_mean_abs": float(d.mean()),
+                                "align1_max_abs": float(da.max())}) + "\n")
+    assert float(d.max()) <= 1e-3 and float(d.mean()) <= 2e-5, (float(d.max()), float(d.mean()))
+    assert float(da.max()) <= 1e-4
+    np.testing.assert_allclose(out["stop"].cpu().numpy(), ref["stop"].numpy(), atol=1e-3)
+
+
+def test_c5_full_length_closure(cuda):
+    """All 500 free-running steps at B=8, N=200 closed on themselves: the teacher-forced
+    training branch (persistent kernels, batched causal head) fed the decode's OWN predicted
+    frames as targets reproduces those frames (TransformerTrainingHelper feeds
+    targets[:, t-1, -80:], modules/helpers.py:54-58 -- exactly the frame the stop-token helper
+    fed back).  Same bars as the A17 test: the two paths share no kernel of the loop."""
+    from sat_amd.inference import FreeRunningDecoder
+    hp, vals, m, b, gb, O = _c5_batch(cuda)
+    T = 500
+    fr = FreeRunningDecoder(m, max_iters=T, min_iters=T, check_every=25, graphs=True).run(gb)
+    assert fr["steps"] == T and fr["mel"].shape == gb["mel"].shape
+    tb = dict(gb)
+    tb["mel"] = fr["mel"].contiguous()
+    with torch.no_grad():
+        tr, _ = m.forward(tb, None, training=False, need_grad=False)
+    d_mel = (tr["mel"] - fr["mel"]).abs()
+    d_stop = (tr["stop"].view_as(fr["stop"]) - fr["stop"]).abs()
+    path = os.environ.get("SAT_PARITY_REPORT")
+    if path:
+        with open(path, "a") as f:
+            f.write(json.dumps({"case": "c5_closure_500", "mel_max_abs": float(d_mel.max()),
+                                "mel_mean_abs": float(d_mel.mean()),
+                                "stop_max_abs": float(d_stop.max())}) + "\n")
+    assert float(d_mel.max()) <= 5e-5 and float(d_mel.mean()) <= 2e-6
+    assert float(d_stop.max()) <= 5e-5
+
+
+def test_run_results_survive_the_next_run(cuda):
+    """run() returns copies, never views of the per-shape plan's buffers: with B == 1 (where a
+    reshape / contiguous of the step-major history would be a view), a second run on the same
+    decoder and shape leaves the first result untouched."""
+    from sat_amd.inference import FreeRunningDecoder
+    hp, vals, m, b, gb, O = _vbatch(cuda, B=1, N=11, T=20, seed=12)
+    dec = FreeRunningDecoder(m, max_iters=12, min_iters=12, check_every=4)
+    r1 = dec.run(gb)
+    mel1, stop1 = r1["mel"].clone(), r1["stop"].clone()
+    gb2 = dict(gb)
+    gb2["source"] = torch.flip(gb["source"], [1]).contiguous()   # a different utterance
+    r2 = dec.run(gb2)
+    assert not torch.equal(r2["mel"], mel1)
+    assert torch.equal(r1["mel"], mel1) and torch.equal(r1["stop"], stop1)

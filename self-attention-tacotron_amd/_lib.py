@@ -12,7 +12,8 @@ import os
 from typing import Optional
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG_DIR, "libsat_hip.so")
+# SAT_LIB_OVERRIDE: an instrumented build for the probes under tools/ (never set by the product)
+LIB_PATH = os.environ.get("SAT_LIB_OVERRIDE") or os.path.join(PKG_DIR, "libsat_hip.so")
 
 
 class SatLibraryError(RuntimeError):

@@ -104,7 +104,8 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
   __shared__ __attribute__((aligned(16))) float v2s[kPmax][kM2];
   __shared__ __attribute__((aligned(16))) float wqs[kUW][kQ];
   __shared__ __attribute__((aligned(16))) float wc2[kM2][4 * kUW + 4];   // padded rows (banks)
-  __shared__ __attribute__((aligned(16))) float locw[kF][kQ];        // columns >= D1 zero
+  // the location term folded: l[n] = f[n] W_loc = convb W_loc + sum_k s[n-4+k] (W_conv[k] W_loc)
+  __shared__ __attribute__((aligned(16))) float cwl[kKW][kQ];        // W_conv W_loc, cols >= D1 zero
   __shared__ __attribute__((aligned(16))) float vcat[kQ];            // [v1 | v2]
   __shared__ float cw[kKW * kF + kF];
   // per step
@@ -115,12 +116,10 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
   __shared__ __attribute__((aligned(16))) float hst[kUW];        // own units' h_t (tagged)
   __shared__ __attribute__((aligned(16))) float hraw[kUW];       // own units' raw outputs
   __shared__ float gsum[8][64];             // h part of the gate sums (transpose-reduced)
-  __shared__ float stat[8];                 // combined statistics of step t-1 (+ reciprocals)
   __shared__ float halo[12];                // e_{t-1} left 4 | right 5 ; alpha_{t-2} at n0-2, n0-1
   __shared__ float eown[kPmax], e2own[kPmax];
   __shared__ float alf[2][kPmax + 1];       // alf[t & 1][k] = alpha_{t-1} at n0 - 1 + k
   __shared__ float sp[kPmax + kKW];         // s_{t-1} on n0-4 .. n0+nt+4
-  __shared__ __attribute__((aligned(16))) float fs[kPmax][8];         // location features
   __shared__ __attribute__((aligned(16))) float wsc[8][2][kPmax];     // per-wave alignment weights
   __shared__ long long tp[16];              // optional segment clocks of thread 0
 
@@ -167,8 +166,22 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
   }
   for (int i = tid0; i < kPmax * kQ; i += kTh) {
     const int r = i / kQ, c = i - r * kQ;
-    kc[r][c] = r >= nt ? 0.f : c < kD1 ? p.K1[(bN + n0 + r) * kD1 + c] + p.b1[c]
+    float lb = 0.f;                              // convb W_loc (the location term's constant)
+    if (c < kD1) {
+#pragma unroll
+      for (int f = 0; f < kF; ++f) lb = fmaf(p.convb[f], p.locW[f * kD1 + c], lb);
+    }
+    kc[r][c] = r >= nt ? 0.f : c < kD1 ? p.K1[(bN + n0 + r) * kD1 + c] + p.b1[c] + lb
                                        : p.K2[(bN + n0 + r) * kD2 + (c - kD1)];
+  }
+  for (int i = tid0; i < kKW * kQ; i += kTh) {
+    const int k = i / kQ, c = i - k * kQ;
+    float a = 0.f;
+    if (c < kD1) {
+#pragma unroll
+      for (int f = 0; f < kF; ++f) a = fmaf(p.convW[k * kF + f], p.locW[f * kD1 + c], a);
+    }
+    cwl[k][c] = a;
   }
   for (int i = tid0; i < kPmax * kM1 / 4; i += kTh) {
     const int r = i / (kM1 / 4), c4 = i - r * (kM1 / 4);
@@ -179,11 +192,7 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
     const int r = i / kM2, c = i - r * kM2;
     v2s[r][c] = r < nt ? p.V2[(bN + n0 + r) * kM2 + c] : 0.f;
   }
-  for (int d = tid0; d < kQ; d += kTh) {
-    vcat[d] = d < kD1 ? p.v1[d] : p.v2[d - kD1];
-#pragma unroll
-    for (int f = 0; f < kF; ++f) locw[f][d] = d < kD1 ? p.locW[f * kD1 + d] : 0.f;
-  }
+  for (int d = tid0; d < kQ; d += kTh) vcat[d] = d < kD1 ? p.v1[d] : p.v2[d - kD1];
   if (tid0 < kKW * kF) cw[tid0] = p.convW[tid0];
   if (tid0 < kF) cw[kKW * kF + tid0] = p.convb[tid0];
   if (tid0 < kU) hbuf[tid0] = 0.f;                                  // h_{-1}
@@ -227,6 +236,23 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
     }
   };
   bool gave_up = false;
+  // location features f_t of the own positions from s_{t-1} in sp (the BPTT's LOC history;
+  // the forward itself uses the folded form, section 4)
+  auto store_loc = [&](int tt, int lane_) {
+    if (!p.LOC) return;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int o = lane_ + 64 * h;
+      if (o < nt * kF) {
+        const int i = o / kF, f = o - i * kF;
+        float a = cw[kKW * kF + f];
+#pragma unroll
+        for (int k = 0; k < kKW; ++k) a = fmaf(sp[i + k], cw[k * kF + f], a);
+        p.LOC[(((int64_t)tt * B + b) * N + n0) * kF + o] = a;
+      }
+    }
+  };
+  if ((tid0 >> 6) == 5) store_loc(0, tid0 & 63);   // f_0 from the initial state s_{-1}
 #if SAT_FWD8_TRACE
   // per-wave event clocks of workgroup 0 over steps 100..107: prof[4096 + ...] (build with
   // -DSAT_FWD8_TRACE=1; tools/probes/fwd8_profile.py prints them)
@@ -291,8 +317,12 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
       tick(1);
     ev(2);
       // combine: thread d < 288 one context dim; the record scales from lanes 0..7 of each
-      // wave (DPP, identical arithmetic in every workgroup of the group), broadcast by readlane
-      if (wave < (kC + 63) / 64) {
+      // wave (DPP, identical arithmetic in every workgroup of the group), broadcast by readlane.
+      // Waves 5 and 6 normalise step t-1 on the own positions meanwhile (the statistics
+      // formed the same way): s_{t-1} on the convolution window (the next energies' location
+      // term reads it) and alpha_{t-1} (tagged for record B_t) -- off the step's critical
+      // path, which used to run them after publishing A_t.
+      {
         const int jj = lane & 7;
         const float4 st = recs[jj][0];
         const float z2 = recs[jj][1].x;
@@ -300,21 +330,67 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
         const float sc1 = __expf(st.x - M1), sc2 = __expf(st.w - M2);
         const float Z1 = lanes8_sum(st.y * sc1), A1 = lanes8_sum(st.z * sc1);
         const float Z2 = lanes8_sum(z2 * sc2);
-        if (tid < kC) {
-          const bool first = wave < kM1 / 64;      // wave-uniform: c1 dims (waves 0..3) or c2
-          const float sc = first ? sc1 : sc2;
-          const float* rf = reinterpret_cast<const float*>(&recs[0][2]) + tid;
-          float a = 0.f;
+        if (wave < (kC + 63) / 64) {
+          if (tid < kC) {
+            const bool first = wave < kM1 / 64;    // wave-uniform: c1 dims (waves 0..3) or c2
+            const float sc = first ? sc1 : sc2;
+            const float* rf = reinterpret_cast<const float*>(&recs[0][2]) + tid;
+            float a = 0.f;
 #pragma unroll
-          for (int k = 0; k < kW; ++k) a = fmaf(rf[k * kR4 * 4], rdl(sc, k), a);
-          a *= __builtin_amdgcn_rcpf(first ? A1 : Z2);
-          cbuf[tid] = a;
-          if (j == 0) p.REC0[((int64_t)t * B + b) * kK0 + tid] = a;
-        }
-        if (tid == 0) {
-          stat[0] = M1; stat[1] = Z1; stat[2] = A1; stat[3] = M2; stat[4] = Z2;
-          stat[5] = __builtin_amdgcn_rcpf(Z1); stat[6] = __builtin_amdgcn_rcpf(A1);
-          stat[7] = __builtin_amdgcn_rcpf(Z2);   // (IEEE divisions sat on the step's critical path)
+            for (int k = 0; k < kW; ++k) a = fmaf(rf[k * kR4 * 4], rdl(sc, k), a);
+            a *= __builtin_amdgcn_rcpf(first ? A1 : Z2);
+            cbuf[tid] = a;
+            if (j == 0) p.REC0[((int64_t)t * B + b) * kK0 + tid] = a;
+          }
+        } else if (wave < 7) {
+          const unsigned bit = lsb_tag(t);
+          auto e_at = [&](int n) -> float {       // e_{t-1}(n) on the window, -inf where masked
+            if (n < 0 || n >= len) return -INFINITY;
+            if (n < n0) return halo[n - n0 + kPadL];
+            if (n < n0 + nt) return eown[n - n0];
+            return halo[kPadL + (n - n0 - nt)];
+          };
+          if (wave == 5) {
+            // s_{t-1} = softmax on n0-4 .. n0+nt+4, then (same wave, no barrier) the location
+            // features f_t of the own positions for the LOC history of the BPTT
+            if (lane < nt + kKW - 1) {
+              const float e = e_at(n0 - kPadL + lane);
+              const float sv = e == -INFINITY ? 0.f : __expf(e - M1) * __builtin_amdgcn_rcpf(Z1);
+              sp[lane] = sv;
+              if (lane >= kPadL && lane < nt + kPadL)
+                p.S1[((int64_t)t * B + b) * N + n0 + lane - kPadL] = sv;
+            }
+            if (t < T && 4 * 7 < nt) {         // no idle energy wave (N > 224): here
+              asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+              store_loc(t, lane);
+            }
+          } else {
+            const float* ap = alf[(t - 1) & 1];      // alpha_{t-2} at n0-1+k
+            if (lane <= nt) {
+              const int k = lane, n = n0 - 1 + k;
+              float av = 0.f;
+              if (n >= 0) {
+                // alpha_{t-2} at n and n-1: own from ap, n0-1 / n0-2 from the left halo
+                const float a_n = k >= 1 ? ap[k] : halo[kPadL + kPadR + 1];
+                const float a_m = k >= 2 ? ap[k - 1] : halo[kPadL + kPadR + k];
+                const float e = e_at(n);
+                const float pe = e == -INFINITY ? 0.f : __expf(e - M1);
+                av = ((1.f - u) * a_n + u * a_m + 1e-7f) * pe * __builtin_amdgcn_rcpf(A1);
+              }
+              const float at = tagf(av, bit);
+              alf[t & 1][k] = at;
+              if (k >= 1) p.AL1[((int64_t)t * B + b) * N + n] = at;
+            }
+            if (lane < nt) {
+              const float e2 = e2own[lane];
+              p.S2[((int64_t)s * B + b) * N + n0 + lane] =
+                  e2 == -INFINITY ? 0.f : __expf(e2 - M2) * __builtin_amdgcn_rcpf(Z2);
+            }
+            if (j == 0 && lane == 0) {
+              float* stp = p.ST + ((int64_t)s * B + b) * 4;
+              stp[0] = M1; stp[1] = Z1; stp[2] = A1 / Z1; stp[3] = Z2;
+            }
+          }
         }
       }
     }
@@ -412,80 +488,29 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
     ev(7);
     }
 
-    // ============ 3. normalise step t-1 on the own positions (alpha tagged for record B_t)
-    if (t > 0) {
-      const float M1 = stat[0], M2 = stat[3], rZ1 = stat[5], rA1 = stat[6], rZ2 = stat[7];
-      const unsigned bit = lsb_tag(t);
-      const float* ap = alf[(t - 1) & 1];        // alpha_{t-2} at n0-1+k
-      auto e_at = [&](int n) -> float {         // e_{t-1}(n) on the window, -inf where masked
-        if (n < 0 || n >= len) return -INFINITY;
-        if (n < n0) return halo[n - n0 + kPadL];
-        if (n < n0 + nt) return eown[n - n0];
-        return halo[kPadL + (n - n0 - nt)];
-      };
-      if (tid < nt + kKW - 1) {
-        const float e = e_at(n0 - kPadL + tid);
-        sp[tid] = e == -INFINITY ? 0.f : __expf(e - M1) * rZ1;
-      } else if (tid >= 64 && tid - 64 <= nt) {
-        const int k = tid - 64, n = n0 - 1 + k;
-        float av = 0.f;
-        if (n >= 0) {
-          // alpha_{t-2} at n and n-1: own from ap, n0-1 / n0-2 from the left halo
-          const float a_n = k >= 1 ? ap[k] : halo[kPadL + kPadR + 1];
-          const float a_m = k >= 2 ? ap[k - 1] : halo[kPadL + kPadR + k];
-          const float e = e_at(n);
-          const float pe = e == -INFINITY ? 0.f : __expf(e - M1);
-          av = ((1.f - u) * a_n + u * a_m + 1e-7f) * pe * rA1;
-        }
-        alf[t & 1][k] = tagf(av, bit);
-      }
-      lds_barrier();
-      if (tid < nt) {
-        const int n = n0 + tid;
-        p.S1[((int64_t)t * B + b) * N + n] = sp[tid + kPadL];
-        p.AL1[((int64_t)t * B + b) * N + n] = alf[t & 1][tid + 1];
-        const float e2 = e2own[tid];
-        p.S2[((int64_t)s * B + b) * N + n] = e2 == -INFINITY ? 0.f : __expf(e2 - M2) * rZ2;
-      }
-      if (j == 0 && tid == 0) {
-        float* st = p.ST + ((int64_t)s * B + b) * 4;
-        st[0] = M1; st[1] = stat[1]; st[2] = stat[2] / stat[1]; st[3] = stat[4];
-      }
-    }
     if (t == T) break;
     tick(7);
     ev(8);
 
-    // ============ 4. location features f_t and the query-independent energy part
-    if (tid < nt * kF) {
-      const int i = tid / kF, f = tid - i * kF;
-      float a = cw[kKW * kF + f];
-#pragma unroll
-      for (int k = 0; k < kKW; ++k) a = fmaf(sp[i + k], cw[k * kF + f], a);
-      fs[i][f] = a;
-      if (p.LOC) p.LOC[(((int64_t)t * B + b) * N + n0) * kF + tid] = a;
-    }
-    lds_barrier();
+    // ============ 4. the query-independent energy part of step t (s_{t-1} came from wave 5
+    //                 before the last barrier): a = K + b1 + convb W_loc + sum_k s_{t-1}[n-4+k]
+    //                 (W_conv[k] W_loc) -- the location convolution and layer folded into one
+    //                 10-tap product (modules/forward_attention.py:98-101)
     // energy role: lane = dim chunk c (4 dims of [D1 | D2]), wave = positions 4w .. 4w+3
     float4 Lr[4];
     if (4 * wave < nt) {
       const int c = lane;
-      float4 lw[kF];
 #pragma unroll
-      for (int f = 0; f < kF; ++f) lw[f] = *reinterpret_cast<const float4*>(&locw[f][4 * c]);
+      for (int i = 0; i < 4; ++i) Lr[i] = *reinterpret_cast<const float4*>(&kc[4 * wave + i][4 * c]);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int r = 4 * wave + i;
-        float4 a = *reinterpret_cast<const float4*>(&kc[r][4 * c]);
-        const float4 f03 = *reinterpret_cast<const float4*>(&fs[r][0]);
-        const float f4 = fs[r][4];
-        const float fl[kF] = {f03.x, f03.y, f03.z, f03.w, f4};
+      for (int k = 0; k < kKW; ++k) {
+        const float4 wk = *reinterpret_cast<const float4*>(&cwl[k][4 * c]);
 #pragma unroll
-        for (int f = 0; f < kF; ++f) {
-          a.x = fmaf(fl[f], lw[f].x, a.x); a.y = fmaf(fl[f], lw[f].y, a.y);
-          a.z = fmaf(fl[f], lw[f].z, a.z); a.w = fmaf(fl[f], lw[f].w, a.w);
+        for (int i = 0; i < 4; ++i) {
+          const float sv = sp[4 * wave + i + k];
+          Lr[i].x = fmaf(sv, wk.x, Lr[i].x); Lr[i].y = fmaf(sv, wk.y, Lr[i].y);
+          Lr[i].z = fmaf(sv, wk.z, Lr[i].z); Lr[i].w = fmaf(sv, wk.w, Lr[i].w);
         }
-        Lr[i] = a;
       }
     }
     tick(8);
@@ -547,9 +572,10 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
         const float ev = valid ? tagf(e[0], bit) : -INFINITY;
         if (m < 4) eown[r] = ev; else e2own[r] = ev;
       }
-    } else if (lane < 8) {                     // idle wave: its positions are padding
+    } else {                                   // idle wave: its positions are padding
       const int r = 4 * wave + (lane & 3);
-      if (lane < 4) eown[r] = -INFINITY; else e2own[r] = -INFINITY;
+      if (lane < 4) eown[r] = -INFINITY; else if (lane < 8) e2own[r] = -INFINITY;
+      if (wave == 7) store_loc(t, lane);       // the LOC history, off the critical path
     }
     tick(11);
     ev(12);

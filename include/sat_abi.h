@@ -222,6 +222,17 @@ int sat_counter_add(uint64_t* counter, uint64_t inc, void* stream);
 int sat_stop_check(const float* stop, int64_t stride, int32_t B, int32_t t, int32_t min_iters,
                    int32_t* state, void* stream);
 
+/* One step of the decoder head's causal self-attention against its key/value cache during
+ * free-running decoding (TransformerWrapper, modules/rnn_wrappers.py:87-124, with
+ * ScaledDotProductAttentionMechanism, modules/self_attention.py:45-65; eval: no dropout):
+ * per utterance b and head h, s_j = scale * q_t . k_j (j = 0..t), p = softmax(s),
+ * o = sum_j p_j v_j.  qkv row (b, j) = qkv + b*qkv_sb + j*qkv_st holds [q (D) | k (D) | v (D)]
+ * of step j (the caller's projection writes row t first); P (nullable) receives p at
+ * ((b*H + h)*Tm + t)*Tm + j; O row b (stride o_sb) receives the heads concatenated. */
+int sat_decode_attention_step(const float* qkv, int64_t qkv_sb, int64_t qkv_st, int32_t B,
+                              int32_t H, int32_t D, int32_t t, float scale, float* P, int32_t Tm,
+                              float* O, int64_t o_sb, void* stream);
+
 /* ---------------------------------------------------------------- (Zoneout)LSTM step
  * One time step of TF LSTMCell wrapped in ext tacotron2 ZoneoutLSTMCell,
  * as used by ZoneoutCBHG's BiLSTM (modules/module.py:93-108) and DecoderRNNV2 /
@@ -246,6 +257,14 @@ typedef struct SatLstmFwd {
   float* c_out;
   float* h_out; int64_t h_out_sb;
   float* gates;                           /* [B][U][4] activated gates for the backward */
+  /* optional further input segments (0 = none): the recurrent input row is
+   * [rin (K - K1 - K2) | rin1 (K1) | rin2 (K2)] against W's K rows in that order, so a layer
+   * whose inputs live in separate buffers (e.g. DecoderRNNV2's LSTM1: [h0' | contexts | h1])
+   * runs its whole product -- input projection included, with xproj = NULL and `bias` -- in
+   * one step launch (free-running decode, inference.py). */
+  const float* rin1; int64_t rin1_sb;
+  const float* rin2; int64_t rin2_sb;
+  int32_t K1, K2;
 } SatLstmFwd;
 
 /* Backward of one step (reverse time).  dL/dh_t = dh_carry + dgates_{t+1} . W[hoff+u, :]

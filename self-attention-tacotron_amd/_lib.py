@@ -60,7 +60,8 @@ def _struct(name, spec):
 SatLstmFwd = _struct("SatLstmFwd", """
     i32:B i32:U i32:K i32:t ptr:xproj i64:xproj_sb ptr:bias ptr:rin i64:rin_sb ptr:W
     ptr:c_prev ptr:h_prev i64:h_prev_sb ptr:mask_c ptr:mask_h f32:zc f32:zh ptr:lengths
-    ptr:h_raw i64:h_raw_sb ptr:c_out ptr:h_out i64:h_out_sb ptr:gates""")
+    ptr:h_raw i64:h_raw_sb ptr:c_out ptr:h_out i64:h_out_sb ptr:gates
+    ptr:rin1 i64:rin1_sb ptr:rin2 i64:rin2_sb i32:K1 i32:K2""")
 
 SatLstmBwd = _struct("SatLstmBwd", """
     i32:B i32:U i32:K i32:hoff i32:t ptr:W ptr:dgates_next ptr:gates ptr:c_prev
@@ -186,6 +187,8 @@ SIGNATURES = {
     "sat_decoder_lstms_bwd": [ctypes.POINTER(SatDecLstmBwd), _P],
     "sat_decoder_loop_fwd": [ctypes.POINTER(SatDecoderLoopFwd), _P],
     "sat_decoder_loop_bwd": [ctypes.POINTER(SatDecoderLoopBwd), _P],
+    "sat_decode_attention_step": [_P, _I64, _I64, _I32, _I32, _I32, _I32, _F, _P, _I32, _P,
+                                  _I64, _P],
     "sat_zlstm_step_fwd": [ctypes.POINTER(SatLstmFwd), _P],
     "sat_zlstm_step_bwd": [ctypes.POINTER(SatLstmBwd), _P],
     "sat_attn_param_grad_rows": [_I32, _I32],

@@ -296,6 +296,12 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
       float4 x1 = make_float4(0.f, 0.f, 0.f, 0.f), x2 = x1;
       float hv = 0.f;
       bool ok1 = false, ok2 = !two, ok3 = !hsrc;
+#if SAT_FWD8_TRACE
+      // trace build: drain the wave's own earlier stores first, then time the poll alone
+      const long long tq0 = wall_clock64();
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const long long tq1 = wall_clock64();
+#endif
       for (unsigned spins = 0;; ++spins) {
         if (!ok1) x1 = ldc4(rRB, (rec + kRBctx) / 4 + lane);
         if (!ok2) x2 = ldc4(rRB, i2);
@@ -307,6 +313,15 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
         if (poll_give_up(spins, p.err)) { gave_up = true; break; }
         __builtin_amdgcn_s_sleep(1);
       }
+#if SAT_FWD8_TRACE
+      {
+        const long long tq2 = wall_clock64();
+        if (evt && t >= 100 && t < 108 && lane == 0) {
+          evt[8 * 8 * 16 + ((t - 100) * 8 + wave) * 4 + 0] = tq1 - tq0;
+          evt[8 * 8 * 16 + ((t - 100) * 8 + wave) * 4 + 1] = tq2 - tq1;
+        }
+      }
+#endif
       recs[wave][2 + lane] = x1;
       if (lane < kM2 / 4) recs[wave][2 + kM1 / 4 + lane] = x2;
       else if (two) recs[wave][lane - kM2 / 4] = x2;
@@ -523,6 +538,11 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
       const bool two = lane < kUW / 4;
       float4 x1 = make_float4(0.f, 0.f, 0.f, 0.f), x2 = x1;
       bool ok1 = false, ok2 = !two;
+#if SAT_FWD8_TRACE
+      const long long tq0 = wall_clock64();
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const long long tq1 = wall_clock64();
+#endif
       for (unsigned spins = 0;; ++spins) {
         if (!ok1) x1 = ldc4(rRA, ra / 4 + lane);
         if (!ok2) x2 = ldc4(rRA, (ra + kQ) / 4 + lane);
@@ -532,6 +552,15 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
         if (poll_give_up(spins, p.err)) { gave_up = true; break; }
         __builtin_amdgcn_s_sleep(1);
       }
+#if SAT_FWD8_TRACE
+      {
+        const long long tq2 = wall_clock64();
+        if (evt && t >= 100 && t < 108 && lane == 0) {
+          evt[8 * 8 * 16 + ((t - 100) * 8 + wave) * 4 + 2] = tq1 - tq0;
+          evt[8 * 8 * 16 + ((t - 100) * 8 + wave) * 4 + 3] = tq2 - tq1;
+        }
+      }
+#endif
       qst[wave][lane] = x1;
       if (two) reinterpret_cast<float4*>(hbuf)[(kUW / 4) * wave + lane] = x2;   // units 32 jj + 4 lane
     }

@@ -36,6 +36,9 @@ struct LstmFwdP {
   float* c_out;
   float* h_out; int64_t h_out_sb;
   float* gates;
+  const float* rin1; int64_t rin1_sb;   // optional input segments: row = [rin | rin1 | rin2]
+  const float* rin2; int64_t rin2_sb;
+  int K1, K2;
 };
 
 // Forward step.  Every global load is issued up front: the workgroup's weight slice
@@ -74,11 +77,16 @@ __device__ __forceinline__ void lstm_fwd_block(const LstmFwdP& p, int bx, int by
     const int k = i / UT, j = i - k * UT;
     Ws[i] = j < nu ? W4[(int64_t)k * p.U + u0 + j] : make_float4(0.f, 0.f, 0.f, 0.f);
   }
-  const int kq = K >> 2;
+  const int kq = K >> 2, k0q = (K - p.K1 - p.K2) >> 2, k1q = k0q + (p.K1 >> 2);
   for (int i = tid; i < BT * kq; i += 256) {
     const int r = i / kq, c = i - r * kq;
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (b0 + r < p.B) v = reinterpret_cast<const float4*>(p.rin + (int64_t)(b0 + r) * p.rin_sb)[c];
+    if (b0 + r < p.B) {
+      const int64_t br = b0 + r;
+      v = c < k0q ? reinterpret_cast<const float4*>(p.rin + br * p.rin_sb)[c]
+        : c < k1q ? reinterpret_cast<const float4*>(p.rin1 + br * p.rin1_sb)[c - k0q]
+                  : reinterpret_cast<const float4*>(p.rin2 + br * p.rin2_sb)[c - k1q];
+    }
     *reinterpret_cast<float4*>(xs + r * xld + 4 * c) = v;
   }
   __syncthreads();
@@ -323,6 +331,10 @@ static int check_fwd(const SatLstmFwd* a, LstmFwdP& p, size_t& shm) {
   SAT_CHECK_ARG(a->K % 4 == 0 && a->rin_sb % 4 == 0, "sat_lstm_step_fwd: K and rin stride must be multiples of 4");
   SAT_CHECK_ARG((a->K == 0 || a->rin) && a->W && a->c_out && a->h_out, "sat_lstm_step_fwd: null pointer");
   SAT_CHECK_ARG((a->mask_c == nullptr) == (a->mask_h == nullptr), "sat_lstm_step_fwd: masks come in pairs");
+  SAT_CHECK_ARG(a->K1 >= 0 && a->K2 >= 0 && a->K1 % 4 == 0 && a->K2 % 4 == 0 &&
+                a->K1 + a->K2 <= a->K && (a->K1 == 0 || (a->rin1 && a->rin1_sb % 4 == 0 && aligned16(a->rin1))) &&
+                (a->K2 == 0 || (a->rin2 && a->rin2_sb % 4 == 0 && aligned16(a->rin2))),
+                "sat_lstm_step_fwd: input segments need K1, K2, strides % 4 and 16-byte alignment");
   p.B = a->B; p.U = a->U; p.K = a->K;
   p.xproj = a->xproj; p.xproj_sb = a->xproj_sb; p.bias = a->bias;
   p.rin = a->rin; p.rin_sb = a->rin_sb; p.W = a->W;
@@ -331,6 +343,8 @@ static int check_fwd(const SatLstmFwd* a, LstmFwdP& p, size_t& shm) {
   p.lengths = a->lengths; p.t = a->t;
   p.h_raw = a->h_raw; p.h_raw_sb = a->h_raw_sb;
   p.c_out = a->c_out; p.h_out = a->h_out; p.h_out_sb = a->h_out_sb; p.gates = a->gates;
+  p.rin1 = a->rin1; p.rin1_sb = a->rin1_sb; p.rin2 = a->rin2; p.rin2_sb = a->rin2_sb;
+  p.K1 = a->K1; p.K2 = a->K2;
   shm = ((size_t)a->K * UT * 4 + (size_t)BT * (a->K + 4)) * sizeof(float);
   SAT_CHECK_ARG(shm <= 160 * 1024, "sat_lstm_step_fwd: K too large for the LDS-staged step");
   return SAT_OK;

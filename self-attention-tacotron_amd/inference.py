@@ -144,11 +144,26 @@ class FreeRunningDecoder:
         pl.FA = ((torch.zeros(B, Tm, N, **f32), torch.zeros(B, Tm, N, **f32))
                  if self.forced is not None else None)
         # ---- state (step-major histories)
-        pl.MEL = MEL = torch.zeros(Tm, B, M * r, **f32)
-        pl.STOP = STOP = torch.zeros(Tm, B, 1, **f32)
+        W0 = P["decoder/attention_lstm/kernel"]
+        W1 = P["decoder/lstm1/kernel"]
+        W2 = P["decoder/lstm2/kernel"]
+        p_w = d.dec_prenet[-1]
+        # mel frame and stop logit of a step share one row [mel (M r) | stop | pad] written by ONE
+        # product with the packed [W_mel | w_stop | 0] (rows 16-byte aligned)
+        MSW = (M * r + 1 + 3) // 4 * 4
+        pl.MS = MS = torch.zeros(Tm, B, MSW, **f32)
+        pl.MEL = MEL = MS[..., :M * r]
+        pl.STOP = STOP = MS[..., M * r:M * r + 1]
+        pl.Wms = torch.zeros(d.dsa, MSW, **f32)
+        pl.bms = torch.zeros(MSW, **f32)
         GO = torch.zeros(B, M * nf, **f32)
         SMX = torch.empty(B, M * r, **f32)                 # softmax feedback (feed="softmax")
-        pl.REC0 = REC0 = torch.zeros(Tm + 1, B, R0, **f32)  # [c1 | c2 | h0] per step
+        MELC = torch.empty(B, M * r, **f32)                 # contiguous copy for that feedback
+        # the attention RNN's whole input row per step: [prenet out (p_w) | c1 | c2 | h0], so its
+        # product (input projection included) is ONE step launch against the full kernel W0
+        RX = p_w + R0
+        pl.REC0X = REC0X = torch.zeros(Tm + 1, B, RX, **f32)
+        pl.REC0 = REC0 = REC0X[..., p_w:]                  # [c1 | c2 | h0] per step (view)
         C0 = torch.zeros(2, B, A, **f32)
         H0RAW = torch.empty(B, A, **f32)
         L1 = [torch.zeros(2, B, Dd, **f32), torch.zeros(2, B, Dd, **f32)]   # c, h ping-pong
@@ -157,9 +172,6 @@ class FreeRunningDecoder:
         H2RAW = torch.empty(B, Dd, **f32)
         GA = torch.empty(B, 4 * A, **f32)                  # activated gates (unused here)
         GD = torch.empty(B, 4 * Dd, **f32)
-        X0 = torch.empty(B, 4 * A, **f32)
-        X1 = torch.empty(B, 4 * Dd, **f32)
-        X2 = torch.empty(B, 4 * Dd, **f32)
         Q = torch.empty(B, D1 + D2, **f32)
         pl.S1 = S1 = torch.zeros(Tm + 1, B, N, **f32)
         pl.AL1 = AL1 = torch.zeros(Tm + 1, B, N, **f32)
@@ -170,67 +182,60 @@ class FreeRunningDecoder:
         E2 = torch.empty(B, N, **f32)
         PART = torch.empty(B, ntiles, pst, **f32)
         pl.QT = QT = torch.empty(D1 + D2, A, **f32)
-        W0 = P["decoder/attention_lstm/kernel"]
-        W1 = P["decoder/lstm1/kernel"]
-        W2 = P["decoder/lstm2/kernel"]
-        p_w = d.dec_prenet[-1]
-        # ---- decoder self-attention key/value caches, one per hop
+        # ---- decoder self-attention: per hop one cache of [q | k | v] rows per step (the
+        # q/k/v projections of a step are ONE product with the packed [Wq | Wk | Wv]), the
+        # packed weights refreshed from the parameters at every run
         H, dsa = d.dec_heads, d.dsa
         dh = dsa // H
-        KC = [torch.zeros(B, Tm, dsa, **f32) for _ in range(d.dec_hops)]
-        VC = [torch.zeros(B, Tm, dsa, **f32) for _ in range(d.dec_hops)]
+        pl.QKVC = QKVC = [torch.zeros(B, Tm, 3 * dsa, **f32) for _ in range(d.dec_hops)]
+        pl.Wqkv = [torch.empty(dsa, 3 * dsa, **f32) for _ in range(d.dec_hops)]
+        pl.bqkv = [torch.empty(3 * dsa, **f32) for _ in range(d.dec_hops)]
+        OH = torch.empty(B, dsa, **f32)
         # row t of each hop's causal probabilities (= the final step's full [T', T'] matrix)
         pl.SA_P = SA_P = [torch.zeros(B, H, Tm, Tm, **f32) for _ in range(d.dec_hops)]
         pl.state = state = torch.full((1,), -1, dtype=torch.int32, device=dev)
-        pl.zero_each_run = [REC0, C0, L1[0], L1[1], L2[0], L2[1], S1, AL1, S2, MEL, STOP]
+        pl.zero_each_run = [REC0X, C0, L1[0], L1[1], L2[0], L2[1], S1, AL1, S2, MS]
         pl.graphs = {}
         lengths, V1, V2, K1, K2 = pl.lengths, pl.V1, pl.V2, pl.K1, pl.K2
         sp, XT, FA = pl.sp, pl.XT, pl.FA
         feed, forced_mode, stop_mode = self.feed, FA is not None, self.helper == "stop_token"
         min_iters = self.min_iters
+        Wqkv, bqkv = pl.Wqkv, pl.bqkv
+        Wms, bms = pl.Wms, pl.bms
 
-        def prenets(x):
+        def prenets(x, out):
+            """the decoder prenets on the fed frame; the last layer writes `out`"""
+            L = len(d.dec_prenet)
             if sp is not None:                             # multi_speaker_modules.py:27-32
                 ms = "decoder/prenet0"
                 y = K.gemm(x, P[f"{ms}/dense0/kernel"], bias=P[f"{ms}/dense0/bias"], act="relu",
                            add=sp)
-                y = K.linear(y, P[f"{ms}/dense/kernel"], P[f"{ms}/dense/bias"], act="relu")
+                y = K.linear(y, P[f"{ms}/dense/kernel"], P[f"{ms}/dense/bias"], act="relu",
+                             out=out if L == 1 else None)
                 start = 1
             else:
                 y, start = x, 0
-            for i in range(start, len(d.dec_prenet)):
+            for i in range(start, L):
                 y = K.linear(y, P[f"decoder/prenet{i}/kernel"], P[f"decoder/prenet{i}/bias"],
-                             act="relu")
-            return y
+                             act="relu", out=out if i == L - 1 else None)
 
         def head_step(h, t):
-            """TransformerWrapper row t + OutputAndStopTokenTransparentWrapper projections."""
+            """TransformerWrapper row t + OutputAndStopTokenTransparentWrapper projections:
+            the packed q/k/v product writes cache row t, one fused launch attends over rows
+            0..t (sat_decode_attention_step), then the output projection, the transform, and
+            one product for the mel frame and the stop logit."""
             z = h
             for hop in range(d.dec_hops):
                 sc = f"decoder/self_attention{hop}"
                 mh = f"{sc}/mha"
-                q = K.linear(z, P[f"{mh}/query_projection/kernel"], P[f"{mh}/query_projection/bias"])
-                K.linear(z, P[f"{mh}/key_projection/kernel"], P[f"{mh}/key_projection/bias"],
-                         out=KC[hop][:, t])
-                K.linear(z, P[f"{mh}/value_projection/kernel"],
-                         P[f"{mh}/value_projection/bias"], out=VC[hop][:, t])
-                qh = q.view(B, 1, H, dh).permute(0, 2, 1, 3)              # [B, H, 1, dh]
-                kh = KC[hop][:, :t + 1].view(B, t + 1, H, dh).permute(0, 2, 3, 1)
-                vh = VC[hop][:, :t + 1].view(B, t + 1, H, dh).permute(0, 2, 1, 3)
-                S = K.gemm(qh, kh)                                        # [B, H, 1, t+1]
-                Pc = torch.empty_like(S)
-                K.softmax_fwd(S, Pc, None, None, causal=False, scale=1.0 / math.sqrt(dh))
-                SA_P[hop][:, :, t:t + 1, :t + 1].copy_(Pc)
-                o = torch.empty(B, dsa, **f32)
-                K.gemm(Pc, vh, o.view(B, 1, H, dh).permute(0, 2, 1, 3))
-                y = K.linear(o, P[f"{mh}/output_projection/kernel"],
+                K.linear(z, Wqkv[hop], bqkv[hop], out=QKVC[hop][:, t])
+                K.decode_attention_step(QKVC[hop], t, H, dsa, 1.0 / math.sqrt(dh), SA_P[hop],
+                                        OH)
+                y = K.linear(OH, P[f"{mh}/output_projection/kernel"],
                              P[f"{mh}/output_projection/bias"])
                 z = K.linear(y, P[f"{sc}/transform/kernel"], P[f"{sc}/transform/bias"],
                              act="tanh", add=z)                           # z + tanh(Dense(.))
-            K.linear(z, P["decoder/out_projection/kernel"], P["decoder/out_projection/bias"],
-                     out=MEL[t])
-            K.linear(z, P["decoder/stop_token_projection/kernel"],
-                     P["decoder/stop_token_projection/bias"], out=STOP[t])
+            K.linear(z, Wms, bms, out=MS[t])
 
         def forced_step(t):
             """TeacherForcing*Attention: alignments = A[:, t]; contexts = A[:, t] . values."""
@@ -252,21 +257,22 @@ class FreeRunningDecoder:
                 convb=P[f"{a1}/location_conv/bias"] if att1_fwd else None,
                 locW=P[f"{a1}/location_layer/kernel"] if att1_fwd else None,
                 v2=P[f"{a2}/attention_v"], e1=E1, e2=E2, part=PART, part_stride=pst,
-                s_out=S1[t + 1], a_out=AL1[t + 1], s2_out=S2[t], ctx=REC0[t + 1], ctx_sb=R0,
+                s_out=S1[t + 1], a_out=AL1[t + 1], s2_out=S2[t], ctx=REC0[t + 1], ctx_sb=RX,
                 stats=None, loc_out=None)
 
         def lstm_stack(t, cur, nxt):
-            K.linear(H0RAW, W1[:A], P["decoder/lstm1/bias"], out=X1)
-            K.gemm(REC0[t + 1][:, :M1 + M2], W1[A:A + M1 + M2], X1, beta=1.0)
-            K.lstm_step_fwd(B=B, U=Dd, K=Dd, t=t, xproj=X1, rin=L1[1][cur],
-                            W=W1[A + M1 + M2:], c_prev=L1[0][cur], h_prev=L1[1][cur],
-                            mask_c=None, mask_h=None, zc=zc, zh=zh, h_raw=H1RAW,
-                            c_out=L1[0][nxt], h_out=L1[1][nxt], gates=GD)
-            K.linear(H1RAW, W2[:Dd], P["decoder/lstm2/bias"], out=X2)
-            K.lstm_step_fwd(B=B, U=Dd, K=Dd, t=t, xproj=X2, rin=L2[1][cur], W=W2[Dd:],
-                            c_prev=L2[0][cur], h_prev=L2[1][cur], mask_c=None, mask_h=None,
-                            zc=zc, zh=zh, h_raw=H2RAW, c_out=L2[0][nxt], h_out=L2[1][nxt],
+            # LSTM1 on [h0'_t | c1_t c2_t | h1_{t-1}] and LSTM2 on [h1'_t | h2_{t-1}], each one
+            # step launch with its whole kernel (input projection included) and bias
+            K.lstm_step_fwd(B=B, U=Dd, K=A + M1 + M2 + Dd, t=t, xproj=None,
+                            bias=P["decoder/lstm1/bias"], rin=H0RAW,
+                            rin1=REC0[t + 1][:, :M1 + M2], rin2=L1[1][cur], W=W1,
+                            c_prev=L1[0][cur], h_prev=L1[1][cur], mask_c=None, mask_h=None,
+                            zc=zc, zh=zh, h_raw=H1RAW, c_out=L1[0][nxt], h_out=L1[1][nxt],
                             gates=GD)
+            K.lstm_step_fwd(B=B, U=Dd, K=Dd + Dd, t=t, xproj=None, bias=P["decoder/lstm2/bias"],
+                            rin=H1RAW, rin1=L2[1][cur], W=W2, c_prev=L2[0][cur],
+                            h_prev=L2[1][cur], mask_c=None, mask_h=None, zc=zc, zh=zh,
+                            h_raw=H2RAW, c_out=L2[0][nxt], h_out=L2[1][nxt], gates=GD)
 
         def step(t):
             cur, nxt = t % 2, (t + 1) % 2
@@ -275,13 +281,15 @@ class FreeRunningDecoder:
             elif feed == "target":                         # OneHotValidationHelper :103
                 x = XT[t]
             elif feed == "softmax":                        # OneHotValidationHelper :100-104
-                K.softmax_fwd(MEL[t - 1].view(B * r, M), SMX.view(B * r, M), causal=False)
+                MELC.copy_(MEL[t - 1])
+                K.softmax_fwd(MELC.view(B * r, M), SMX.view(B * r, M), causal=False)
                 x = SMX[:, M * (r - nf):]
             else:
                 x = MEL[t - 1][:, M * (r - nf):]
-            pre = prenets(x)
-            K.linear(pre, W0[:p_w], P["decoder/attention_lstm/bias"], out=X0)
-            K.lstm_step_fwd(B=B, U=A, K=R0, t=t, xproj=X0, rin=REC0[t], W=W0[p_w:],
+            prenets(x, REC0X[t][:, :p_w])
+            # the attention RNN on [prenet | c1 c2 | h0_{t-1}] against its whole kernel
+            K.lstm_step_fwd(B=B, U=A, K=RX, t=t, xproj=None,
+                            bias=P["decoder/attention_lstm/bias"], rin=REC0X[t], W=W0,
                             c_prev=C0[cur], h_prev=REC0[t, :, M1 + M2:], mask_c=None,
                             mask_h=None, zc=zc, zh=zh, h_raw=H0RAW, c_out=C0[nxt],
                             h_out=REC0[t + 1, :, M1 + M2:], gates=GA)
@@ -311,6 +319,17 @@ class FreeRunningDecoder:
         pl.lengths.copy_(batch["source_length"])
         K.transpose(P["decoder/attention1/query_layer/kernel"], pl.QT[:d.d1])
         K.transpose(P["decoder/attention2/query_layer/kernel"], pl.QT[d.d1:])
+        dsa = d.dsa
+        for hop in range(d.dec_hops):
+            mh = f"decoder/self_attention{hop}/mha"
+            for i, nm in enumerate(("query", "key", "value")):
+                pl.Wqkv[hop][:, i * dsa:(i + 1) * dsa].copy_(P[f"{mh}/{nm}_projection/kernel"])
+                pl.bqkv[hop][i * dsa:(i + 1) * dsa].copy_(P[f"{mh}/{nm}_projection/bias"])
+        Mr = d.num_mels * d.r
+        pl.Wms[:, :Mr].copy_(P["decoder/out_projection/kernel"])
+        pl.Wms[:, Mr:Mr + 1].copy_(P["decoder/stop_token_projection/kernel"])
+        pl.bms[:Mr].copy_(P["decoder/out_projection/bias"])
+        pl.bms[Mr:Mr + 1].copy_(P["decoder/stop_token_projection/bias"])
         if pl.sp is not None:
             ms = "decoder/prenet0"
             K.linear(spk_rows, P[f"{ms}/speaker_projection/kernel"],

@@ -256,6 +256,15 @@ def conv_bank_bwd(x, W_bank, dy, max_k: int, Co: int, dx=None, dW=None, beta_dx=
     _lib.check(_lib.load().sat_cbhg_convbank_bwd(ctypes.byref(d), _stream()),
                "sat_cbhg_convbank_bwd")
 
+def decode_attention_step(qkv: torch.Tensor, t: int, H: int, D: int, scale: float,
+                          P: torch.Tensor, O: torch.Tensor):
+    """sat_decode_attention_step: qkv [B, Tm, 3D] cache (row t written), P [B, H, Tm, Tm]
+    probability rows (row t written), O [B, D] the heads' outputs."""
+    B, Tm = qkv.shape[0], qkv.shape[1]
+    _lib.call("sat_decode_attention_step", _p(qkv), qkv.stride(0), qkv.stride(1), B, H, D, t,
+              scale, _p(P), Tm if P is not None else 0, _p(O), O.stride(0), _stream())
+
+
 def stop_check(stop: torch.Tensor, t: int, min_iters: int, state: torch.Tensor):
     """state[0] := t if (no earlier finish) and t > min_iters and all sigmoid(stop) > 0.5."""
     _lib.call("sat_stop_check", _p(stop), stop.stride(0), stop.shape[0], t, min_iters,
@@ -313,9 +322,13 @@ def _rs(t) -> int:
 
 
 def lstm_fwd_desc(*, B, U, K, t, xproj, rin, W, c_prev, h_prev, mask_c, mask_h, zc, zh,
-                  h_raw, c_out, h_out, gates, lengths=None, bias=None, a=None):
-    """Fill a SatLstmFwd (``a``, or a new one) for one recurrent step."""
+                  h_raw, c_out, h_out, gates, lengths=None, bias=None, rin1=None, rin2=None,
+                  a=None):
+    """Fill a SatLstmFwd (``a``, or a new one) for one recurrent step.  ``rin1`` / ``rin2``:
+    further input segments (row = [rin | rin1 | rin2] against W's K rows)."""
     a = _lib.SatLstmFwd() if a is None else a
+    a.rin1, a.rin1_sb, a.K1 = _p(rin1), _rs(rin1), 0 if rin1 is None else rin1.shape[-1]
+    a.rin2, a.rin2_sb, a.K2 = _p(rin2), _rs(rin2), 0 if rin2 is None else rin2.shape[-1]
     a.B, a.U, a.K, a.t = B, U, K, t
     a.xproj, a.xproj_sb = _p(xproj), _rs(xproj)
     a.bias = _p(bias)

@@ -59,11 +59,11 @@ for k in o_new:
     d = (o_new[k] - o_old[k]).abs()
     print(f"  {k:6s} max|new-old| {float(d.max()):.3e}  mean {float(d.mean()):.3e}")
 os.environ["SAT_ATTN_FWD8"] = "1"
-prof = torch.zeros(256 * 16 + 8 * 8 * 16 + 8 * 8 * 2, dtype=torch.int64, device="cuda")
+prof = torch.zeros(256 * 16 + 8 * 8 * 16 + 8 * 8 * 4, dtype=torch.int64, device="cuda")
 orig(**dict(kw, prof=prof))
 torch.cuda.synchronize()
 ev = prof[256 * 16:256 * 16 + 8 * 8 * 16].view(8, 8, 16).cpu().double() / 100.0   # [step][wave][event] us
-sp = prof[256 * 16 + 8 * 8 * 16:].view(8, 8, 2).cpu().double()   # [step][wave][B, A] poll spins
+sp = prof[256 * 16 + 8 * 8 * 16:].view(8, 8, 4).cpu().double() / 100.0  # [step][wave][B drain, B poll, A drain, A poll] us
 # (all zero unless libsat_hip was built with -DSAT_FWD8_TRACE=1)
 ev = ev - ev[:, 0:1, 0:1]                                          # vs wave 0's loop start
 print("per-wave event clocks of workgroup 0 (us after wave 0's step start, mean of steps 100..107)")
@@ -71,9 +71,9 @@ print("  wave " + " ".join(f"{k:6d}" for k in range(16)))
 m = ev.mean(0)
 for w in range(8):
     print(f"  {w:4d} " + " ".join(f"{float(m[w, k]):6.2f}" for k in range(16)))
-print("poll spins per wave (mean of steps 100..107): B " +
-      " ".join(f"{float(sp[:, w, 0].mean()):.1f}" for w in range(8)) + " | A " +
-      " ".join(f"{float(sp[:, w, 1].mean()):.1f}" for w in range(8)))
+for k, nm in enumerate(["B own-store drain", "B poll (after drain)", "A own-store drain",
+                        "A poll (after drain)"]):
+    print(f"  {nm:22s} us per wave: " + " ".join(f"{float(sp[:, w, k].mean()):.2f}" for w in range(8)))
 pr = prof[:256 * 16].view(256, 16).cpu().double() / 100.0
 names = ["wait B records", "sync (staged)", "combine", "sync (c)", "c-dot + cell",
          "sync (cell)", "q partial + publish A", "normalise", "loc + L", "wait A records",

@@ -444,6 +444,89 @@ __global__ void __launch_bounds__(256) gemm_splitk_reduce(GemmP p) {
   }
 }
 
+// Skinny products (M <= 8 rows: the free-running decoder's per-step projections at batch 8,
+// inference.py): the 64-row tile kernels run such a product on N / 64 workgroups that each
+// stream K x 64 weights alone (8.7 us per launch measured).  Here a workgroup owns 16 columns
+// for all M rows, 256 threads = 16 k-slices x 16 columns: each thread accumulates its slice for
+// the M rows (A staged in LDS, W read as 64-byte row segments), then the 16 slices are summed
+// in a fixed order (2 shuffles + an LDS pass over the 4 waves).  Same epilogue as the tiles.
+constexpr int kSkinnyM = 8;
+__global__ void __launch_bounds__(256) gemm_skinny_kernel(GemmP p) {
+  extern __shared__ __attribute__((aligned(16))) float sk_smem[];
+  float* As = sk_smem;                                  // [M][K]
+  float* red = sk_smem + (size_t)p.M * p.K;             // [4 waves][8 rows][16 cols]
+  const int tid = threadIdx.x, nl = tid & 15, ks = tid >> 4;
+  const int n = blockIdx.x * 16 + nl;
+  const int M = p.M, K = p.K;
+  // A -> LDS, 8 loads per thread in flight per batch (a dependent load / store per element
+  // serialises the round trips: 5 us at K = 256)
+  for (int base = 0; base < M * K; base += 8 * 256) {
+    float v[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int i = base + q * 256 + tid;
+      const int m = i / K, k = i - m * K;
+      v[q] = i < M * K ? p.A[(int64_t)m * p.a_sm + (int64_t)k * p.a_sk] : 0.f;
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int i = base + q * 256 + tid;
+      if (i < M * K) As[i] = v[q];
+    }
+  }
+  __syncthreads();
+  float acc[kSkinnyM];
+#pragma unroll
+  for (int m = 0; m < kSkinnyM; ++m) acc[m] = 0.f;
+  if (n < p.N) {
+    // the slice's weights in chunks of 16 loads issued before any use (one round trip per
+    // chunk: the product is latency-bound at these sizes)
+    const float* wc = p.B + (int64_t)n * p.b_sn;
+    for (int k0 = ks; k0 < K; k0 += 256) {
+      float w[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int k = k0 + 16 * q;
+        w[q] = k < K ? wc[(int64_t)k * p.b_sk] : 0.f;
+      }
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int k = k0 + 16 * q;
+        if (k < K) {
+#pragma unroll
+          for (int m = 0; m < kSkinnyM; ++m)
+            if (m < M) acc[m] = fmaf(As[m * K + k], w[q], acc[m]);
+        }
+      }
+    }
+  }
+  // k-slices ks = 4 wave + (lane >> 4): lanes l, l ^ 16, l ^ 32, l ^ 48 share a column
+#pragma unroll
+  for (int m = 0; m < kSkinnyM; ++m) {
+    acc[m] += __shfl_xor(acc[m], 16, 64);
+    acc[m] += __shfl_xor(acc[m], 32, 64);
+  }
+  const int wave = tid >> 6, lane = tid & 63;
+  if (lane < 16) {
+#pragma unroll
+    for (int m = 0; m < kSkinnyM; ++m) red[(wave * kSkinnyM + m) * 16 + lane] = acc[m];
+  }
+  __syncthreads();
+  if (tid < M * 16) {
+    const int m = tid >> 4, c = tid & 15, col = blockIdx.x * 16 + c;
+    if (col < p.N) {
+      const float sum = ((red[(0 * kSkinnyM + m) * 16 + c] + red[(1 * kSkinnyM + m) * 16 + c]) +
+                         red[(2 * kSkinnyM + m) * 16 + c]) + red[(3 * kSkinnyM + m) * 16 + c];
+      float* dst = p.C + (int64_t)m * p.c_sm + col;
+      float v = p.alpha * sum;
+      if (p.beta != 0.f) v += p.beta * (*dst);
+      v = apply_act(v + (p.bias ? p.bias[col] : 0.f), p.act);
+      if (p.add) v += p.add[(int64_t)m * p.add_sm + col];
+      *dst = v;
+    }
+  }
+}
+
 // Degenerate plain products (the stop-token projection, `stop = x w + b` and its input
 // gradient): tiles of 64 columns or 16-deep K slices would be almost all padding there.
 // N == 1 with row-contiguous A: one wave per output row, lanes over K (float4 when aligned).
@@ -992,6 +1075,15 @@ static bool gemm_lds_enabled() {
   return on;
 }
 
+// SAT_GEMM_SKINNY=0 sends M <= 8 products to the tile kernels (A/B switch).
+static bool gemm_skinny_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("SAT_GEMM_SKINNY");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 static void launch_splitk_reduce(const GemmP& p, hipStream_t s) {
   const int64_t total = (int64_t)p.M * p.N;
   const int64_t work = (p.N % 4 == 0) ? total / 4 : total;
@@ -1193,6 +1285,14 @@ extern "C" int sat_gemm(const SatGemmDesc* d, void* stream) {
                   "sat_gemm: colsum_out fallback needs ws_bytes >= sat_workspace_colreduce(K, N)");
     SAT_CHECK_ARG(d->b_sn == 1, "sat_gemm: colsum_out fallback needs B rows contiguous");
     return colsum_alpha(d->B, d->b_sk, d->K, d->N, d->colsum_out, d->alpha, d->beta, d->ws, s);
+  }
+  if (nb == 1 && d->a_mode == 0 && d->b_mode == 0 && !t_probe && d->M <= kSkinnyM && d->N > 1 &&
+      d->K > 1 && !d->mul && (int64_t)d->M * d->K * 4 + 4 * kSkinnyM * 16 * 4 <= 64 * 1024 &&
+      gemm_skinny_enabled()) {
+    const size_t shm = ((size_t)d->M * d->K + 4 * kSkinnyM * 16) * sizeof(float);
+    hipLaunchKernelGGL(gemm_skinny_kernel, dim3(ceil_div(d->N, 16)), dim3(256), shm, s, p);
+    SAT_LAUNCH_CHECK("sat_gemm (skinny)");
+    return SAT_OK;
   }
   if (nb == 1 && d->a_mode == 0 && d->b_mode == 0 && !t_probe &&
       ((d->N == 1 && d->a_sk == 1) || (d->K == 1 && (int64_t)d->M * d->N < (1LL << 31)))) {

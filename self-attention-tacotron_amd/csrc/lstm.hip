@@ -45,16 +45,22 @@ struct LstmFwdP {
 // W[:, u0:u0+4, :] (K x 16 floats) and its 8 input rows go global -> LDS in one burst of
 // 16-byte loads, the pointwise operands (xproj, c, h, masks) are prefetched into registers,
 // then the K-split dot products run out of LDS.
+// UT_ units x BT_ = 256 / KS_ / UT_ batch rows per workgroup, K split over KS_ lanes.  The
+// training fallback uses <4, 8> (U = 256, B = 32: 256 workgroups); the free-running decode at
+// batch <= 8 uses <1, 32>: one unit per workgroup, so U = 256 still gives 256 workgroups and
+// each streams K x 4 weights instead of K x 16 (inference.py's per-step launches).
+template <int UT_, int KS_>
 __device__ __forceinline__ void lstm_fwd_block(const LstmFwdP& p, int bx, int by, float* smem) {
+  constexpr int BT_ = 256 / KS_ / UT_;
   const int K = p.K;
-  float4* Ws = reinterpret_cast<float4*>(smem);          // [K][UT]
-  float* xs = smem + (size_t)K * UT * 4;                  // [BT][K + 4]
+  float4* Ws = reinterpret_cast<float4*>(smem);          // [K][UT_]
+  float* xs = smem + (size_t)K * UT_ * 4;                 // [BT_][K + 4]
   const int xld = K + 4;
   const int tid = threadIdx.x;
-  const int ks = tid & (KS - 1), pair = tid >> 3;
-  const int u0 = bx * UT, b0 = by * BT;
-  const int u = u0 + (pair & (UT - 1));
-  const int bl = pair >> 2;
+  const int ks = tid & (KS_ - 1), pair = tid / KS_;
+  const int u0 = bx * UT_, b0 = by * BT_;
+  const int u = u0 + (pair % UT_);
+  const int bl = pair / UT_;
   const int b = b0 + bl;
   const bool active = (u < p.U) && (b < p.B);
   // prefetch the pointwise operands of this (b, u)
@@ -72,13 +78,13 @@ __device__ __forceinline__ void lstm_fwd_block(const LstmFwdP& p, int bx, int by
   }
   // weights: K rows x UT float4 (rows are UT*16 contiguous bytes at stride U*16)
   const float4* W4 = reinterpret_cast<const float4*>(p.W);
-  const int nu = min(UT, p.U - u0);
-  for (int i = tid; i < K * UT; i += 256) {
-    const int k = i / UT, j = i - k * UT;
+  const int nu = min(UT_, p.U - u0);
+  for (int i = tid; i < K * UT_; i += 256) {
+    const int k = i / UT_, j = i - k * UT_;
     Ws[i] = j < nu ? W4[(int64_t)k * p.U + u0 + j] : make_float4(0.f, 0.f, 0.f, 0.f);
   }
   const int kq = K >> 2, k0q = (K - p.K1 - p.K2) >> 2, k1q = k0q + (p.K1 >> 2);
-  for (int i = tid; i < BT * kq; i += 256) {
+  for (int i = tid; i < BT_ * kq; i += 256) {
     const int r = i / kq, c = i - r * kq;
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
     if (b0 + r < p.B) {
@@ -92,18 +98,18 @@ __device__ __forceinline__ void lstm_fwd_block(const LstmFwdP& p, int bx, int by
   __syncthreads();
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
   const float* xr = xs + bl * xld;
-  const int ul = pair & (UT - 1);
+  const int ul = pair % UT_;
 #pragma unroll 4
-  for (int k = ks; k < K; k += KS) {
+  for (int k = ks; k < K; k += KS_) {
     const float xv = xr[k];
-    const float4 w = Ws[k * UT + ul];
+    const float4 w = Ws[k * UT_ + ul];
     acc[0] = fmaf(xv, w.x, acc[0]);
     acc[1] = fmaf(xv, w.y, acc[1]);
     acc[2] = fmaf(xv, w.z, acc[2]);
     acc[3] = fmaf(xv, w.w, acc[3]);
   }
 #pragma unroll
-  for (int o = 1; o < KS; o <<= 1)
+  for (int o = 1; o < KS_; o <<= 1)
 #pragma unroll
     for (int g = 0; g < 4; ++g) acc[g] += __shfl_xor(acc[g], o, 64);
   if (!active || ks != 0) return;
@@ -154,7 +160,72 @@ __global__ void __launch_bounds__(256) lstm_fwd_kernel(LstmFwdMulti m) {
     if (j < m.n && (int)blockIdx.x >= m.first[j]) i = j;
   const int local = blockIdx.x - m.first[i];
   const int by = local / m.gx[i], bx = local - by * m.gx[i];
-  lstm_fwd_block(m.p[i], bx, by, smem);
+  lstm_fwd_block<UT, KS>(m.p[i], bx, by, smem);
+}
+
+// One step at batch <= 8 (the free-running decoder, inference.py): one unit per workgroup,
+// thread = (batch row b < 8, k-slice ks < 32); every thread loads its k-slice of the input row
+// and the unit's 4 gate weights straight into registers -- all loads in flight at once, no LDS
+// staging, no barrier -- then 5 xor-shuffles sum the slices.  Same cell as lstm_fwd_block.
+__global__ void __launch_bounds__(256) lstm_fwd_small_kernel(LstmFwdP p) {
+  constexpr int KS_ = 32, KMAX = 1024 / KS_;   // K <= 1024
+  const int tid = threadIdx.x, ks = tid & (KS_ - 1), b = tid / KS_;
+  const int u = blockIdx.x, K = p.K;
+  const bool active = b < p.B;
+  const int k0 = K - p.K1 - p.K2, k1 = k0 + p.K1;
+  const int64_t br = active ? b : 0;
+  const float4* W4 = reinterpret_cast<const float4*>(p.W);
+  float xv[KMAX];
+  float4 wv[KMAX];
+#pragma unroll
+  for (int i = 0; i < KMAX; ++i) {
+    const int k = ks + KS_ * i;
+    xv[i] = 0.f;
+    wv[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (k < K) {
+      wv[i] = W4[(int64_t)k * p.U + u];
+      if (active)
+        xv[i] = k < k0 ? p.rin[br * p.rin_sb + k]
+              : k < k1 ? p.rin1[br * p.rin1_sb + (k - k0)] : p.rin2[br * p.rin2_sb + (k - k1)];
+    }
+  }
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < KMAX; ++i) {
+    acc[0] = fmaf(xv[i], wv[i].x, acc[0]);
+    acc[1] = fmaf(xv[i], wv[i].y, acc[1]);
+    acc[2] = fmaf(xv[i], wv[i].z, acc[2]);
+    acc[3] = fmaf(xv[i], wv[i].w, acc[3]);
+  }
+#pragma unroll
+  for (int o = 1; o < KS_; o <<= 1)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) acc[g] += __shfl_xor(acc[g], o, 64);
+  if (!active || ks != 0) return;
+  const int64_t bu = (int64_t)b * p.U + u;
+  const float4 xp = p.xproj ? reinterpret_cast<const float4*>(p.xproj + (int64_t)b * p.xproj_sb)[u]
+                  : p.bias ? reinterpret_cast<const float4*>(p.bias)[u] : make_float4(0.f, 0.f, 0.f, 0.f);
+  const float cp = p.c_prev ? p.c_prev[bu] : 0.f;
+  const float hp = p.h_prev ? p.h_prev[(int64_t)b * p.h_prev_sb + u] : 0.f;
+  const float gi = sigmoid_fast(acc[0] + xp.x);
+  const float gj = tanh_lstm(acc[1] + xp.y);
+  const float gf = sigmoid_fast(acc[2] + xp.z + 1.0f);   // forget_bias = 1.0
+  const float go = sigmoid_fast(acc[3] + xp.w);
+  const float cn = gf * cp + gi * gj;
+  const float hn = go * tanh_lstm(cn);
+  float c2, h2;
+  if (p.mask_c) {
+    const float mc = p.mask_c[bu], mh = p.mask_h[bu];
+    c2 = mc * cn + (1.f - mc) * cp;
+    h2 = mh * hn + (1.f - mh) * hp;
+  } else {
+    c2 = (1.f - p.zc) * cn + p.zc * cp;
+    h2 = (1.f - p.zh) * hn + p.zh * hp;
+  }
+  p.c_out[bu] = c2;
+  p.h_out[(int64_t)b * p.h_out_sb + u] = h2;
+  if (p.h_raw) p.h_raw[(int64_t)b * p.h_raw_sb + u] = hn;
+  if (p.gates) reinterpret_cast<float4*>(p.gates)[bu] = make_float4(gi, gj, gf, go);
 }
 
 struct LstmBwdP {
@@ -371,6 +442,15 @@ extern "C" int sat_lstm_steps_fwd(const SatLstmFwd* steps, int32_t n, void* stre
 }
 
 extern "C" int sat_lstm_step_fwd(const SatLstmFwd* a, void* stream) {
+  if (a && a->B > 0 && a->B <= 8 && a->U >= 64 && a->K <= 1024 && !a->lengths) {
+    LstmFwdP p;
+    size_t shm = 0;
+    const int rc = check_fwd(a, p, shm);
+    if (rc != SAT_OK) return rc;
+    hipLaunchKernelGGL(lstm_fwd_small_kernel, dim3(a->U), dim3(256), 0, as_stream(stream), p);
+    SAT_LAUNCH_CHECK("sat_lstm_step_fwd");
+    return SAT_OK;
+  }
   return sat_lstm_steps_fwd(a, 1, stream);
 }
 

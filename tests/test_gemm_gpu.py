@@ -341,3 +341,25 @@ def test_gemm_degenerate_shapes(cuda, M, N, K, ta, act):
         ref = torch.sigmoid(ref)
     bound = 2e-6 * (0.5 * (Al.abs() @ B.double().abs()) + C0.double().abs() + 1) + 1e-6
     assert bool(((C.double().cpu() - ref).abs() <= bound).all())
+
+
+# ---- skinny products (M <= 8: the free-running decoder's per-step projections at batch 8)
+@pytest.mark.parametrize("M,N,K", [(1, 256, 80), (3, 164, 256), (8, 768, 256), (8, 1024, 800),
+                                   (5, 37, 19)])
+@pytest.mark.parametrize("act", [None, "relu", "tanh"])
+def test_gemm_skinny(cuda, M, N, K, act):
+    from sat_amd import kernels
+    g = torch.Generator().manual_seed(M * 7 + N + K)
+    A = torch.randn(M, K + 3, generator=g)[:, 2:2 + K]          # strided rows (a_sm = K + 3)
+    B = torch.randn(K, N, generator=g)
+    C0 = torch.randn(M, N, generator=g)
+    bias = torch.randn(N, generator=g)
+    add = torch.randn(M, N, generator=g)
+    C = C0.to(cuda)
+    kernels.gemm(A.to(cuda), B.to(cuda), C, alpha=0.5, beta=1.0, bias=bias.to(cuda), act=act,
+                 add=add.to(cuda))
+    torch.cuda.synchronize()
+    pre = 0.5 * (A.double() @ B.double()) + C0.double() + bias.double()
+    ref = {None: pre, "relu": pre.clamp_min(0), "tanh": torch.tanh(pre)}[act] + add.double()
+    bound = 2e-6 * (0.5 * (A.double().abs() @ B.double().abs()) + C0.double().abs() + 1) + 1e-6
+    assert bool(((C.double().cpu() - ref).abs() <= bound).all())

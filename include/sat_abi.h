@@ -233,6 +233,53 @@ int sat_decode_attention_step(const float* qkv, int64_t qkv_sb, int64_t qkv_st, 
                               int32_t H, int32_t D, int32_t t, float scale, float* P, int32_t Tm,
                               float* O, int64_t o_sb, void* stream);
 
+/* Free-running decoding as ONE persistent launch (C5; the PREDICT branch of RNNTransformer,
+ * modules/module.py:766-784, under StopTokenBasedInferenceHelper, analog
+ * modules/helpers.py:111-160): every decoder step -- prenets on the fed frame, attention RNN,
+ * forward + additive attention, the two ZoneoutLSTMs, the KV-cached causal self-attention head,
+ * the mel / stop projections and the stop test -- inside one launch of 256 workgroups (one
+ * utterance per 32 workgroups).  Replaces the per-step launch sequence of
+ * sat_lstm_step_fwd / sat_attn_step_fwd / sat_gemm / sat_decode_attention_step / sat_stop_check.
+ * Shapes: the LJSpeech decoder (prenet 256/128, attention RNN 256, memories 256 + 32, attention
+ * 224 + 32 with 5 x 10 location filters, LSTMs 256, self-attention 256 x 2 heads, 80 mels x r=2,
+ * one fed frame), B <= 8, N <= 256, T <= 512.  Weights are packed by the caller
+ * (inference.py FreeRunningDecoder._pack_persistent):
+ *   Wzp = W_out[:, 80:160] W_p0, bzp = b_out[80:160] W_p0 + b_p0   (the fed frame folded into
+ *         the first prenet layer; bp0 alone feeds step 0's go frame);
+ *   Wqku = [W_q | W_k | W_v,h W_o,h W_t (h = 0, 1)], bqku = [b_q | b_k | 0],
+ *   bz = (b_v W_o + b_o) W_t + b_t   (value, output projection and transform folded into the
+ *         cached rows: z = h2' + tanh(sum_h softmax_h . u_h + bz));
+ *   Wq = [W_q1 | W_q2] (query layers), Wms = [W_out | w_stop | 0] (row stride 164).
+ * Outputs: MS[t][b] = [mel | stop | pad], AL1[t+1][b][n] (alignments), S2[t][b][n] (second
+ * attention), SA_P[b][h][t][j] (nullable, self-alignment rows); state[0] := first finished step
+ * (stop_mode 1: t > min_iters and sigmoid(stop) > 0.5 for every utterance), left at the caller's
+ * -1 otherwise.  scratch: sat_decode_persistent_scratch_bytes(), 16-byte aligned; err: one word,
+ * cleared by the call, non-zero after a hand-off timeout. */
+typedef struct SatDecodePersistent {
+  int32_t B, N, T, min_iters, stop_mode;
+  float zc, zh, u, scale;
+  const int64_t* lengths;                                  /* [B] */
+  const float* K1; const float* V1;                        /* [B][N][224], [B][N][256] */
+  const float* K2; const float* V2;                        /* [B][N][32], [B][N][32] */
+  const float* Wzp; const float* bzp; const float* bp0;    /* [256][256], [256], [256] */
+  const float* Wp1; const float* bp1;                      /* [256][128], [128] */
+  const float* W0; const float* b0;                        /* [672][256][4], [256][4] */
+  const float* Wq;                                         /* [256][256] */
+  const float* b1; const float* v1;                        /* [224] attention bias, v_a */
+  const float* convW; const float* convb; const float* locW;   /* [10][5], [5], [5][224] */
+  const float* v2;                                         /* [32] */
+  const float* W1; const float* bl1;                       /* [800][256][4], [256][4] */
+  const float* W2; const float* bl2;                       /* [512][256][4], [256][4] */
+  const float* Wqku; const float* bqku; const float* bz;   /* [256][1024], [1024], [256] */
+  const float* Wms; const float* bms;                      /* [256][164], [164] */
+  float* MS; float* AL1; float* S2; float* SA_P;
+  int32_t* state;
+  void* scratch; int64_t scratch_bytes;
+  int32_t* err;
+} SatDecodePersistent;
+int64_t sat_decode_persistent_scratch_bytes(void);
+int sat_decode_persistent(const SatDecodePersistent* a, void* stream);
+
 /* ---------------------------------------------------------------- (Zoneout)LSTM step
  * One time step of TF LSTMCell wrapped in ext tacotron2 ZoneoutLSTMCell,
  * as used by ZoneoutCBHG's BiLSTM (modules/module.py:93-108) and DecoderRNNV2 /

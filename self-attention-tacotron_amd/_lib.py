@@ -129,6 +129,14 @@ SatDecLstmBwd = _struct("SatDecLstmBwd", """
     i32:B i32:T i32:U f32:zc f32:zh ptr:W1r ptr:W2 ptr:G1 ptr:C1S ptr:G2 ptr:C2S ptr:DH2
     ptr:mask1_c ptr:mask1_h ptr:mask2_c ptr:mask2_h ptr:DG1 ptr:DG2 ptr:ctr ptr:err ptr:prof""")
 
+SatDecodePersistent = _struct("SatDecodePersistent", """
+    i32:B i32:N i32:T i32:min_iters i32:stop_mode f32:zc f32:zh f32:u f32:scale
+    ptr:lengths ptr:K1 ptr:V1 ptr:K2 ptr:V2 ptr:Wzp ptr:bzp ptr:bp0 ptr:Wp1 ptr:bp1 ptr:W0 ptr:b0
+    ptr:Wq ptr:b1 ptr:v1 ptr:convW ptr:convb ptr:locW ptr:v2 ptr:W1 ptr:bl1 ptr:W2 ptr:bl2
+    ptr:Wqku ptr:bqku ptr:bz ptr:Wms ptr:bms ptr:MS ptr:AL1 ptr:S2 ptr:SA_P ptr:state
+    ptr:scratch i64:scratch_bytes ptr:err""")
+
+
 class SatDecoderLoopFwd(ctypes.Structure):   # mirrors include/sat_abi.h
     _fields_ = [("attn", SatDecAttnFwd), ("lstm", SatDecLstmFwd), ("W1x", _P), ("b1", _P),
                 ("ws", _P), ("ws_bytes", _I64)]
@@ -189,6 +197,7 @@ SIGNATURES = {
     "sat_decoder_loop_bwd": [ctypes.POINTER(SatDecoderLoopBwd), _P],
     "sat_decode_attention_step": [_P, _I64, _I64, _I32, _I32, _I32, _I32, _F, _P, _I32, _P,
                                   _I64, _P],
+    "sat_decode_persistent": [ctypes.POINTER(SatDecodePersistent), _P],
     "sat_zlstm_step_fwd": [ctypes.POINTER(SatLstmFwd), _P],
     "sat_zlstm_step_bwd": [ctypes.POINTER(SatLstmBwd), _P],
     "sat_attn_param_grad_rows": [_I32, _I32],
@@ -231,6 +240,7 @@ RESTYPES = {"sat_workspace_colreduce": (ctypes.c_int64, [_I32, _I32]),
             "sat_decoder_attention_bwd_scratch": (ctypes.c_int64, [_I32, _I32, _P, _P]),
             "sat_decoder_attention_bwd_dq_parts": (ctypes.c_int32, [_I32, _I32]),
             "sat_decoder_lstms_scratch": (ctypes.c_int64, [_I32]),
+            "sat_decode_persistent_scratch_bytes": (ctypes.c_int64, []),
             "sat_decoder_lstms_bwd_scratch": (ctypes.c_int64, [_I32]),
             "sat_crc32c": (ctypes.c_uint32, [_P, _I64, ctypes.c_uint32]),
             "sat_tfrecord_masked_crc": (ctypes.c_uint32, [_P, _I64]),

@@ -51,6 +51,7 @@ from typing import Dict, Optional
 
 import torch
 
+from . import _lib
 from . import kernels as K
 from .model import BNState, encoder_fwd
 from .params import Dims
@@ -72,11 +73,16 @@ class FreeRunningDecoder:
     ``forced_alignments=(A1, A2)`` replays given alignments (TeacherForcing*Attention) and
     implies the validation helper with T' = A1.shape[1].
     ``check_every`` = decoder steps between host reads of the device-side finished flag (and
-    the steps per captured graph when ``graphs=True``)."""
+    the steps per captured graph when ``graphs=True``).
+    ``persistent``: run the whole decode as ONE launch (``sat_decode_persistent``) -- None picks
+    it whenever the shape allows (mel feedback, no forced alignments, single speaker, the
+    LJSpeech decoder dimensions, B <= 8, N <= 256, T' <= 512), True requires it, False keeps the
+    per-step launches."""
 
     def __init__(self, model, max_iters: Optional[int] = None, min_iters: int = 10,
                  check_every: int = 25, forced_alignments=None, feed: str = "mel",
-                 helper: Optional[str] = None, graphs: bool = False):
+                 helper: Optional[str] = None, graphs: bool = False,
+                 persistent: Optional[bool] = None):
         self.m = model
         self.hp = model.hp
         self.d: Dims = model.d
@@ -108,6 +114,8 @@ class FreeRunningDecoder:
         self.helper = helper
         self.feed = feed
         self.graphs = bool(graphs)
+        self.persistent = persistent
+        self.last_path = None
         self._plans: Dict[tuple, _Plan] = {}
 
     # ------------------------------------------------------------------ plan (static buffers)
@@ -116,8 +124,102 @@ class FreeRunningDecoder:
         pl = self._plans.get(key)
         if pl is None:
             pl = self._build(B, N, Tm)
+            use = self._persistent_ok(B, N, Tm)
+            if self.persistent and not use:
+                raise ValueError("persistent=True: this decode is not eligible for "
+                                 "sat_decode_persistent (" + self._why_not(B, N, Tm) + ")")
+            if use and self.persistent is not False:
+                self._build_persistent(pl)
             self._plans[key] = pl
         return pl
+
+    # ------------------------------------------------------------------ one-launch decode
+    def _why_not(self, B: int, N: int, Tm: int) -> str:
+        d, hp = self.d, self.hp
+        dims = dict(dec_prenet=(256, 128), feed=80, att_rnn=256, m1=256, m2=32, d1=224, d2=32,
+                    loc_k=10, loc_f=5, dec=256, dsa=256, dec_heads=2, dec_hops=1, num_mels=80, r=2,
+                    att1="forward", att2="additive", multi_speaker=False)
+        for k, v in dims.items():
+            if getattr(d, k) != v:
+                return f"{k}={getattr(d, k)!r}, needs {v!r}"
+        if hp.n_feed_frame != 1:
+            return "n_feed_frame != 1"
+        if self.forced is not None or self.feed != "mel":
+            return "forced alignments / non-mel feedback"
+        if not (1 <= B <= 8 and 1 <= N <= 256 and 1 <= Tm <= 512):
+            return f"B={B} (<= 8), N={N} (<= 256), T'={Tm} (<= 512)"
+        if self.m.device.type != "cuda":
+            return "not a GPU model"
+        return ""
+
+    def _persistent_ok(self, B: int, N: int, Tm: int) -> bool:
+        return self._why_not(B, N, Tm) == ""
+
+    def _build_persistent(self, pl: _Plan) -> None:
+        """Packed weights of sat_decode_persistent (refilled from the parameters every run) and
+        its scratch; see include/sat_abi.h SatDecodePersistent."""
+        dev = self.m.device
+        f32 = dict(device=dev, dtype=torch.float32)
+        pl.pk = dict(Wzp=torch.empty(256, 256, **f32), bzp=torch.empty(1, 256, **f32),
+                     Wq=torch.empty(256, 256, **f32), Wqku=torch.empty(256, 1024, **f32),
+                     bqku=torch.zeros(1024, **f32), bz=torch.empty(1, 256, **f32),
+                     tmp=torch.empty(2, 128, 256, **f32), y=torch.empty(1, 256, **f32))
+        pl.scratch = torch.empty(K.decode_persistent_scratch_bytes(), dtype=torch.uint8,
+                                 device=dev)
+        pl.err = torch.zeros(1, dtype=torch.int32, device=dev)
+
+    def _pack_persistent(self, pl: _Plan) -> None:
+        """Fold the fed frame into the first prenet layer and the value / output projection /
+        transform products into the cached rows (exact algebra, fp32 products):
+        Wzp = W_out[:, fed] W_p0, bzp = b_out[fed] W_p0 + b_p0;
+        Wqku = [W_q | W_k | W_v,h (W_o,h W_t)], bz = (b_v W_o + b_o) W_t + b_t."""
+        P, d, pk = self.m.P, self.d, pl.pk
+        M, r = d.num_mels, d.r
+        fed = slice(M * (r - self.hp.n_feed_frame), M * r)
+        Wp0 = P["decoder/prenet0/kernel"]
+        K.gemm(pl.Wms[:, fed], Wp0, pk["Wzp"])
+        K.gemm(pl.bms[fed].unsqueeze(0), Wp0, pk["bzp"], bias=P["decoder/prenet0/bias"])
+        pk["Wq"][:, :d.d1].copy_(P["decoder/attention1/query_layer/kernel"])
+        pk["Wq"][:, d.d1:].copy_(P["decoder/attention2/query_layer/kernel"])
+        mh, sc = "decoder/self_attention0/mha", "decoder/self_attention0"
+        dsa, dh = d.dsa, d.dsa // d.dec_heads
+        Wqku = pk["Wqku"]
+        Wqku[:, :dsa].copy_(P[f"{mh}/query_projection/kernel"])
+        Wqku[:, dsa:2 * dsa].copy_(P[f"{mh}/key_projection/kernel"])
+        pk["bqku"][:dsa].copy_(P[f"{mh}/query_projection/bias"])
+        pk["bqku"][dsa:2 * dsa].copy_(P[f"{mh}/key_projection/bias"])
+        Wv, Wo, Wt = (P[f"{mh}/value_projection/kernel"], P[f"{mh}/output_projection/kernel"],
+                      P[f"{sc}/transform/kernel"])
+        for h in range(d.dec_heads):
+            K.gemm(Wo[h * dh:(h + 1) * dh], Wt, pk["tmp"][h])
+            K.gemm(Wv[:, h * dh:(h + 1) * dh], pk["tmp"][h],
+                   Wqku[:, 2 * dsa + h * dsa:3 * dsa + h * dsa])
+        K.gemm(P[f"{mh}/value_projection/bias"].unsqueeze(0), Wo, pk["y"],
+               bias=P[f"{mh}/output_projection/bias"])
+        K.gemm(pk["y"], Wt, pk["bz"], bias=P[f"{sc}/transform/bias"])
+
+    def _run_persistent(self, pl: _Plan, Tm: int) -> None:
+        P, d, hp = self.m.P, self.d, self.hp
+        a1, a2 = "decoder/attention1", "decoder/attention2"
+        self._pack_persistent(pl)
+        pk = pl.pk
+        K.decode_persistent(
+            B=pl.B, N=pl.N, T=Tm, min_iters=self.min_iters,
+            stop_mode=1 if self.helper == "stop_token" else 0,
+            zc=hp.zoneout_factor_cell, zh=hp.zoneout_factor_output, u=0.5,
+            scale=1.0 / math.sqrt(d.dsa // d.dec_heads),
+            lengths=pl.lengths, K1=pl.K1, V1=pl.V1, K2=pl.K2, V2=pl.V2,
+            Wzp=pk["Wzp"], bzp=pk["bzp"], bp0=P["decoder/prenet0/bias"],
+            Wp1=P["decoder/prenet1/kernel"], bp1=P["decoder/prenet1/bias"],
+            W0=P["decoder/attention_lstm/kernel"], b0=P["decoder/attention_lstm/bias"],
+            Wq=pk["Wq"], b1=P[f"{a1}/attention_bias"], v1=P[f"{a1}/attention_variable"],
+            convW=P[f"{a1}/location_conv/kernel"], convb=P[f"{a1}/location_conv/bias"],
+            locW=P[f"{a1}/location_layer/kernel"], v2=P[f"{a2}/attention_v"],
+            W1=P["decoder/lstm1/kernel"], bl1=P["decoder/lstm1/bias"],
+            W2=P["decoder/lstm2/kernel"], bl2=P["decoder/lstm2/bias"],
+            Wqku=pk["Wqku"], bqku=pk["bqku"], bz=pk["bz"], Wms=pl.Wms, bms=pl.bms,
+            MS=pl.MS, AL1=pl.AL1, S2=pl.S2, SA_P=pl.SA_P[0], state=pl.state,
+            scratch=pl.scratch, scratch_bytes=pl.scratch.numel(), err=pl.err)
 
     def _build(self, B: int, N: int, Tm: int) -> _Plan:
         m, hp, d = self.m, self.hp, self.d
@@ -402,7 +504,18 @@ class FreeRunningDecoder:
 
         stop_mode = self.helper == "stop_token"
         steps = Tm
-        for a in range(0, Tm, self.check_every):
+        if getattr(pl, "pk", None) is not None:
+            self.last_path = "persistent"
+            self._run_persistent(pl, Tm)
+            if int(pl.err.item()) != 0:
+                raise _lib.SatLibraryError("sat_decode_persistent: a hand-off timed out (the "
+                                           "grid was not co-resident?)")
+            first = int(pl.state.item()) if stop_mode else -1
+            if first >= 0:
+                steps = first + 1
+        else:
+            self.last_path = "launches"
+        for a in range(0, Tm if self.last_path == "launches" else 0, self.check_every):
             b = min(Tm, a + self.check_every)
             self._steps(pl, a, b)
             if stop_mode:

@@ -265,6 +265,20 @@ def decode_attention_step(qkv: torch.Tensor, t: int, H: int, D: int, scale: floa
               scale, _p(P), Tm if P is not None else 0, _p(O), O.stride(0), _stream())
 
 
+def decode_persistent_scratch_bytes() -> int:
+    return int(_lib.load().sat_decode_persistent_scratch_bytes())
+
+
+def decode_persistent(**kw):
+    """sat_decode_persistent: the whole free-running decode as one launch (tensor arguments by
+    the SatDecodePersistent field names, scalars as ints / floats)."""
+    d = _lib.SatDecodePersistent()
+    for k, v in kw.items():
+        setattr(d, k, _p(v) if isinstance(v, torch.Tensor) or v is None else v)
+    _lib.check(_lib.load().sat_decode_persistent(ctypes.byref(d), _stream()),
+               "sat_decode_persistent")
+
+
 def stop_check(stop: torch.Tensor, t: int, min_iters: int, state: torch.Tensor):
     """state[0] := t if (no earlier finish) and t > min_iters and all sigmoid(stop) > 0.5."""
     _lib.call("sat_stop_check", _p(stop), stop.stride(0), stop.shape[0], t, min_iters,

@@ -54,7 +54,7 @@ def _c_sizeof(struct):
 STRUCTS = ["SatGemmDesc", "SatLstmFwd", "SatLstmBwd", "SatAttnStep", "SatAttnStepBwd",
            "SatAttnParamGrad", "SatDecAttnFwd", "SatDecAttnBwd", "SatDecLstmFwd",
            "SatDecLstmBwd", "SatEncLstmFwd", "SatEncLstmBwd", "SatAdamConfig", "SatConvBank", "SatMha", "SatDims", "SatRngSegment", "SatColSegment",
-           "SatDecoderLoopFwd", "SatDecoderLoopBwd"]
+           "SatDecoderLoopFwd", "SatDecoderLoopBwd", "SatDecodePersistent"]
 
 
 def _c_offsets(struct, fields):

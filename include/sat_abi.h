@@ -276,6 +276,7 @@ typedef struct SatDecodePersistent {
   int32_t* state;
   void* scratch; int64_t scratch_bytes;
   int32_t* err;
+  int64_t* prof;   /* nullable: per-workgroup phase clocks of the -DSAT_DP_TRACE build */
 } SatDecodePersistent;
 int64_t sat_decode_persistent_scratch_bytes(void);
 int sat_decode_persistent(const SatDecodePersistent* a, void* stream);

@@ -134,7 +134,7 @@ SatDecodePersistent = _struct("SatDecodePersistent", """
     ptr:lengths ptr:K1 ptr:V1 ptr:K2 ptr:V2 ptr:Wzp ptr:bzp ptr:bp0 ptr:Wp1 ptr:bp1 ptr:W0 ptr:b0
     ptr:Wq ptr:b1 ptr:v1 ptr:convW ptr:convb ptr:locW ptr:v2 ptr:W1 ptr:bl1 ptr:W2 ptr:bl2
     ptr:Wqku ptr:bqku ptr:bz ptr:Wms ptr:bms ptr:MS ptr:AL1 ptr:S2 ptr:SA_P ptr:state
-    ptr:scratch i64:scratch_bytes ptr:err""")
+    ptr:scratch i64:scratch_bytes ptr:err ptr:prof""")
 
 
 class SatDecoderLoopFwd(ctypes.Structure):   # mirrors include/sat_abi.h

@@ -489,7 +489,9 @@ class FreeRunningDecoder:
                              f"{tuple(self.forced[0].shape)}")
         pl = self._plan(B, N, Tm)
         sv = {}
-        m1, m2 = encoder_fwd(P, m.bn, hp, d, ids, lengths, None, False, m.ws, sv)
+        # the encoder BiLSTM as one launch (encoder_lstm.hip) like the training step's
+        m1, m2 = encoder_fwd(P, m.bn, hp, d, ids, lengths, None, False, m.ws, sv,
+                             persistent=m.persistent_decoder)
         spk = None
         if d.multi_speaker:
             spk = torch.empty(B, d.spk_dim, device=dev)

@@ -53,8 +53,8 @@ namespace {
 constexpr int kG = 8;             // groups = utterances (B <= 8)
 constexpr int kW = 32;            // workgroups per group
 constexpr int kTh = 512;          // threads per workgroup
-constexpr int kAW = 16;           // attention workgroups per group (memory positions split)
-constexpr int kPM = 16;           // memory positions per attention workgroup (N <= 256)
+constexpr int kAW = 32;           // attention workgroups per group (memory positions split)
+constexpr int kPM = 8;            // memory positions per attention workgroup (N <= 256)
 constexpr int kRM = 16;           // cache rows per workgroup (T <= 512)
 constexpr int kNM = kAW * kPM;    // 256
 constexpr int kMR = 160;          // mel values per step (80 x r=2)
@@ -65,7 +65,7 @@ constexpr int kC1 = 256, kCtx = 288;
 constexpr int kD1 = 224, kQ = 256;
 constexpr int kF = 5, kKW = 10, kPad = 4;
 constexpr int kSD = 256, kSDH = 128, kQKU = 1024, kRow = 768;   // cached row = [k | u0 | u1]
-constexpr int kRec = 8 + 2 * kPM + kCtx;                         // 328
+constexpr int kRec = 8 + 2 * kPM + kCtx;                         // 312
 constexpr int kSaRec = 8 + 2 * kSD;                              // 520
 constexpr float kNeg = -3.0e38f;   // finite stand-in for -inf in tagged words
 constexpr float kNegT = -1.0e38f;  // anything below is "no position"
@@ -88,6 +88,20 @@ constexpr int64_t kCacheFloats = (int64_t)kG * kW * kRM * kRow;
 
 __device__ __forceinline__ float4 fma4(float x, float4 w, float4 a) {
   return make_float4(fmaf(x, w.x, a.x), fmaf(x, w.y, a.y), fmaf(x, w.z, a.z), fmaf(x, w.w, a.w));
+}
+// max / sum over each aligned group of 16 or 32 lanes (result in every lane of the group): the
+// step's small reductions (<= 8 positions, <= 16 cache rows, <= 32 tiles / producers) need no
+// full-wave chain with readlanes
+__device__ __forceinline__ float rdl(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+__device__ __forceinline__ float g16max(float v) {
+  v = group8_max(v);
+  return fmaxf(v, dpp<0x140>(v));
+}
+__device__ __forceinline__ float g32max(float v) {
+  v = g16max(v);
+  return fmaxf(v, __shfl_xor(v, 16, 64));
 }
 __device__ __forceinline__ float4 wave_sum4(float4 v) {
   return make_float4(wave_sum_dpp(v.x), wave_sum_dpp(v.y), wave_sum_dpp(v.z), wave_sum_dpp(v.w));
@@ -215,15 +229,18 @@ __global__ void __launch_bounds__(kTh) decode_persistent_kernel(SatDecodePersist
     for (int j = 0; j < 4; ++j) wk[j][i] = p.Wqku[(size_t)k * kQKU + 32 * w + 4 * wave + j];
   }
   // attention: K1 + b1 / K2 slices of this lane's position (32 lanes per position)
-  const int anl = tid >> 5, apart = tid & 31;
+  // (one wave per position, lane = energy dims lane + 64 j)
+  const int anl = tid >> 6, apart = tid & 63;
   const bool apos = attn && anl < nt;
-  float k1b[7], k2r = 0.f;
+  float k1b[4], k2r = 0.f;
   {
     const size_t rowp = (size_t)g * N + n0 + (apos ? anl : 0);
 #pragma unroll
-    for (int j = 0; j < 7; ++j)
-      k1b[j] = apos ? p.K1[rowp * kD1 + apart + 32 * j] + p.b1[apart + 32 * j] : 0.f;
-    if (apos) k2r = p.K2[rowp * 32 + apart];
+    for (int j = 0; j < 4; ++j) {
+      const int d = apart + 64 * j;
+      k1b[j] = (apos && d < kD1) ? p.K1[rowp * kD1 + d] + p.b1[d] : 0.f;
+    }
+    if (apos && apart < 32) k2r = p.K2[rowp * 32 + apart];
   }
   for (int idx = tid; idx < 9 * 8 * 64; idx += kTh) {
     const int i = idx >> 9, wv = (idx >> 6) & 7, ln = idx & 63;
@@ -267,8 +284,8 @@ __global__ void __launch_bounds__(kTh) decode_persistent_kernel(SatDecodePersist
   const float scale = p.scale;
 
 #if SAT_DP_TRACE
-  __shared__ long long tacc[24], tabs[24];   // thread 0's segment clocks (LDS: no registers)
-  if (threadIdx.x < 24) { tacc[threadIdx.x] = 0; tabs[threadIdx.x] = 0; }
+  __shared__ long long tacc[28], tabs[28];   // thread 0's segment clocks (LDS: no registers)
+  if (threadIdx.x < 28) { tacc[threadIdx.x] = 0; tabs[threadIdx.x] = 0; }
   long long tlast = wall_clock64();
 #define TP(k)                                   \
   if (threadIdx.x == 0) {                       \
@@ -287,7 +304,7 @@ __global__ void __launch_bounds__(kTh) decode_persistent_kernel(SatDecodePersist
     const int tid = tid_, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int uu = 8 * w + wave;
-    const int anl = tid >> 5, apart = tid & 31;
+    const int anl = tid >> 6, apart = tid & 63;
     const int cpre = 8 * w + wave, cmel = w + 32 * wave, cp1 = 4 * w + wave, cq = 8 * w + wave;
     const bool has_mel = wave < 6 && cmel <= kMR;
     const int s = t & 1, sp = s ^ 1;
@@ -385,28 +402,31 @@ __global__ void __launch_bounds__(kTh) decode_persistent_kernel(SatDecodePersist
       {
         float acc = 0.f;
 #pragma unroll
-        for (int j = 0; j < 7; ++j) {
-          const int d = apart + 32 * j;
+        for (int j = 0; j < 4; ++j) {
+          const int d = min(apart + 64 * j, kD1 - 1);   // j = 3: lanes >= 32 carry zero weight
           float pre = k1b[j] + xq[d];
 #pragma unroll
           for (int f = 0; f < kF; ++f) pre = fmaf(fs[anl][f], locw[f][d], pre);
-          acc = fmaf(vv[d], tanh_fast(pre), acc);
+          const float vw = (j < 3 || apart < 32) ? vv[d] : 0.f;
+          acc = fmaf(vw, tanh_fast(pre), acc);
         }
-        float acc2 = vv[kD1 + apart] * tanh_fast(k2r + xq[kD1 + apart]);
-        acc = group32_sum(acc);
-        acc2 = group32_sum(acc2);
-        if (apart == 0 && anl < kPM) {
+        const int d2 = kD1 + (apart & 31);
+        const float acc2 = apart < 32 ? vv[d2] * tanh_fast(k2r + xq[d2]) : 0.f;
+        acc = wave_sum_dpp(acc);
+        const float acc2s = wave_sum_dpp(acc2);
+        if (apart == 0) {
           const bool valid = anl < nt && n0 + anl < len;
           e1s[anl] = valid ? acc : -INFINITY;
-          e2s[anl] = valid ? acc2 : -INFINITY;
+          e2s[anl] = valid ? acc2s : -INFINITY;
         }
       }
       lds_barrier();
+      TP(24)
       const int rb = oREC + (s * kAW + w) * kRec;
       if (wave == 0) {
         const float e1v = lane < nt ? e1s[lane] : -INFINITY;
         const float e2v = lane < nt ? e2s[lane] : -INFINITY;
-        const float m1 = wave_max_dpp(e1v), m2 = wave_max_dpp(e2v);
+        const float m1 = group8_max(e1v), m2 = group8_max(e2v);   // lanes 0-7 = positions
         const float pe = (e1v == -INFINITY) ? 0.f : expf(e1v - m1);
         const float pe2 = (e2v == -INFINITY) ? 0.f : expf(e2v - m2);
         float wg = 0.f;
@@ -416,7 +436,7 @@ __global__ void __launch_bounds__(kTh) decode_persistent_kernel(SatDecodePersist
           wg = ((1.f - uf) * ap[n] + uf * (n > 0 ? ap[n - 1] : 0.f) + 1e-7f) * pe;
         }
         if (lane < kPM) { w1s[lane] = wg; w2s[lane] = lane < nt ? pe2 : 0.f; }
-        const float z1 = wave_sum_dpp(pe), a1 = wave_sum_dpp(wg), z2 = wave_sum_dpp(pe2);
+        const float z1 = group8_sum(pe), a1 = group8_sum(wg), z2 = group8_sum(pe2);
         if (lane < 8) {
           float v = 0.f;
           if (lane == 0) v = m1 == -INFINITY ? kNeg : m1;
@@ -432,6 +452,7 @@ __global__ void __launch_bounds__(kTh) decode_persistent_kernel(SatDecodePersist
         }
       }
       lds_barrier();
+      TP(25)
       if (tid < kCtx) {   // unnormalised partial contexts of the tile
         const float* ws = tid < kC1 ? w1s : w2s;
         float c = 0.f;
@@ -441,7 +462,7 @@ __global__ void __launch_bounds__(kTh) decode_persistent_kernel(SatDecodePersist
     }
     TP(11)
     // ================================================= P6: alignment + contexts (every workgroup)
-    gather<3>(R, (oREC + s * kAW * kRec) / 4, ntiles * kRec / 4, reinterpret_cast<float4*>(&REC[0][0]),
+    gather<5>(R, (oREC + s * kAW * kRec) / 4, ntiles * kRec / 4, reinterpret_cast<float4*>(&REC[0][0]),
               bt, p.err);
     lds_barrier();
     TP(12)
@@ -450,15 +471,16 @@ __global__ void __launch_bounds__(kTh) decode_persistent_kernel(SatDecodePersist
       const float m1j = ok ? REC[lane][0] : kNeg, z1j = ok ? REC[lane][1] : 0.f;
       const float a1j = ok ? REC[lane][2] : 0.f, m2j = ok ? REC[lane][3] : kNeg;
       const float z2j = ok ? REC[lane][4] : 0.f;
-      const float M1 = wave_max_dpp(m1j), M2 = wave_max_dpp(m2j);
+      const float M1 = g32max(m1j), M2 = g32max(m2j);   // lanes 0-31 = tiles
       const float s1 = m1j > kNegT ? expf(m1j - M1) : 0.f;
       const float s2 = m2j > kNegT ? expf(m2j - M2) : 0.f;
       if (lane < kAW) { scs1[lane] = s1; scs2[lane] = s2; }
-      const float Z1 = wave_sum_dpp(z1j * s1), A1 = wave_sum_dpp(a1j * s1);
-      const float Z2 = wave_sum_dpp(z2j * s2);
+      const float Z1 = group32_sum(z1j * s1), A1 = group32_sum(a1j * s1);
+      const float Z2 = group32_sum(z2j * s2);
       if (lane == 0) { hdr[0] = M1; hdr[1] = Z1; hdr[2] = A1; hdr[3] = M2; hdr[4] = Z2; }
     }
     lds_barrier();
+    TP(26)
     {
       const float M1 = hdr[0], Z1 = hdr[1], A1 = hdr[2], M2 = hdr[3], Z2 = hdr[4];
       const float inv1 = 1.f / A1, invz1 = 1.f / Z1, invz2 = 1.f / Z2;
@@ -575,19 +597,19 @@ __global__ void __launch_bounds__(kTh) decode_persistent_kernel(SatDecodePersist
         }
       }
       acc = group16_sum(acc);
-      if (ssub == 0 && sr < nr) sa_s[sr * 2 + sh] = acc * scale;
+      if (ssub == 0 && sr < nr) sa_s[sh * kRM + sr] = acc * scale;
     }
     lds_barrier();
     const int sab = oSA + (s * kW + w) * kSaRec;
     if (wave == 0) {
-      const int r = lane >> 1, h = lane & 1;
+      const int r = lane & 15;   // lanes 0-15 head 0, 16-31 head 1 (row r)
       const bool ok = lane < 2 * kRM && r < nr;
       const float sv = ok ? sa_s[lane] : -INFINITY;
-      const float m0 = wave_max_dpp(h == 0 ? sv : -INFINITY);
-      const float m1 = wave_max_dpp(h == 1 ? sv : -INFINITY);
-      const float pe = ok ? __expf(sv - (h ? m1 : m0)) : 0.f;
+      const float mh = g16max(sv);
+      const float pe = ok ? __expf(sv - mh) : 0.f;
       if (lane < 2 * kRM) sa_pe[lane] = pe;
-      const float z0 = wave_sum_dpp(h == 0 ? pe : 0.f), z1 = wave_sum_dpp(h == 1 ? pe : 0.f);
+      const float zg = group16_sum(pe);
+      const float m0 = rdl(mh, 0), m1 = rdl(mh, 16), z0 = rdl(zg, 0), z1 = rdl(zg, 16);
       if (lane < 4) {
         const float v = lane == 0 ? (nr > 0 ? m0 : kNeg) : lane == 1 ? z0
                       : lane == 2 ? (nr > 0 ? m1 : kNeg) : z1;
@@ -602,7 +624,7 @@ __global__ void __launch_bounds__(kTh) decode_persistent_kernel(SatDecodePersist
       for (int r = 0; r < kRM; ++r) {
         if (r < nr) {
           const float uv = r < nrp ? ureg[r] : xqt[kQ + kSD + vh * kSD + vd];
-          o = fmaf(sa_pe[r * 2 + vh], uv, o);
+          o = fmaf(sa_pe[vh * kRM + r], uv, o);
         }
       }
       stcx(xl, R, sab + 8 + vh * kSD + vd, tagf(o, bt));
@@ -628,10 +650,10 @@ __global__ void __launch_bounds__(kTh) decode_persistent_kernel(SatDecodePersist
       const bool ok = lane < kW;
       const float m0j = ok ? SAG[lane][0] : kNeg, z0j = ok ? SAG[lane][1] : 0.f;
       const float m1j = ok ? SAG[lane][2] : kNeg, z1j = ok ? SAG[lane][3] : 0.f;
-      const float M0 = wave_max_dpp(m0j), M1 = wave_max_dpp(m1j);
+      const float M0 = rdl(g32max(m0j), 0), M1 = rdl(g32max(m1j), 0);
       const float sc0 = m0j > kNegT ? __expf(m0j - M0) : 0.f;
       const float sc1 = m1j > kNegT ? __expf(m1j - M1) : 0.f;
-      const float Z0 = wave_sum_dpp(z0j * sc0), Z1 = wave_sum_dpp(z1j * sc1);
+      const float Z0 = rdl(group32_sum(z0j * sc0), 0), Z1 = rdl(group32_sum(z1j * sc1), 0);
       float v[16];
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
@@ -648,7 +670,7 @@ __global__ void __launch_bounds__(kTh) decode_persistent_kernel(SatDecodePersist
       }
       // this step's probability row of the own cache rows (PREDICT's decoder self-alignments)
       if (p.SA_P && lane < 2 * kRM) {
-        const int r = lane >> 1, h = lane & 1;
+        const int r = lane & 15, h = lane >> 4;
         if (r < nr) {
           const float pr = sa_pe[lane] * __expf(mine[2 * h] - (h ? M1 : M0)) / (h ? Z1 : Z0);
           p.SA_P[(((size_t)g * 2 + h) * T + t) * T + w + kW * r] = pr;
@@ -685,9 +707,9 @@ __global__ void __launch_bounds__(kTh) decode_persistent_kernel(SatDecodePersist
   }
 #if SAT_DP_TRACE
   if (threadIdx.x == 0 && p.prof) {
-    for (int k = 0; k < 24; ++k) p.prof[blockIdx.x * 24 + k] = tacc[k];
-    p.prof[256 * 24 + blockIdx.x] = t;
-    for (int k = 0; k < 24; ++k) p.prof[256 * 25 + blockIdx.x * 24 + k] = tabs[k];
+    for (int k = 0; k < 28; ++k) p.prof[blockIdx.x * 28 + k] = tacc[k];
+    p.prof[256 * 28 + blockIdx.x] = t;
+    for (int k = 0; k < 28; ++k) p.prof[256 * 29 + blockIdx.x * 28 + k] = tabs[k];
   }
 #endif
 #undef TP

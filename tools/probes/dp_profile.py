@@ -23,13 +23,14 @@ SEG = ["loop top->z ready (P1 wait)", "mel|stop", "prenet1 (z fold)", "wait y0",
        "wait p", "attention RNN", "wait h0", "query + LSTM1 rec.", "loc + wait q (attn WGs)",
        "energies + records", "wait records", "alignments + contexts", "LSTM1 + attRNN rec.",
        "wait h1", "LSTM2", "wait h2", "q|k|u + LSTM2 rec.", "cache prefetch + wait qku",
-       "scores + partial O", "wait SA records", "z (head output)", "stop test"]
+       "scores + partial O", "wait SA records", "z (head output)", "stop test",
+       "P5 energies (sub)", "P5 stats (sub)", "P6 headers (sub)"]
 B, steps = 8, 500
 hp = hparams.ljspeech_hparams()
 m = engine.Tacotron(hp, "cuda", seed=1234)
 b = data.synthetic_batch(hp, B, N=200, T=1000, shape="max", seed=55)
 batch = {k: torch.tensor(v).cuda() for k, v in b.items()}
-prof = torch.zeros(256 * 49, dtype=torch.int64, device="cuda")
+prof = torch.zeros(256 * 57, dtype=torch.int64, device="cuda")
 orig = K.decode_persistent
 K.decode_persistent = lambda **kw: orig(**dict(kw, prof=prof))
 dec = FreeRunningDecoder(m, max_iters=steps, min_iters=steps, persistent=True)
@@ -40,8 +41,8 @@ t0 = time.perf_counter()
 dec.run(batch)
 torch.cuda.synchronize()
 print(f"C5 one-launch (trace build): {1e3 * (time.perf_counter() - t0):.2f} ms per decode")
-pr = prof[:256 * 24].view(256, 24).cpu().double() / 100.0 / steps   # us per step
-iters = prof[256 * 24:].cpu()
+pr = prof[:256 * 28].view(256, 28).cpu().double() / 100.0 / steps   # us per step
+iters = prof[256 * 28:256 * 29].cpu()
 print(f"iterations: min {int(iters.min())} max {int(iters.max())}")
 mean = pr.mean(0)
 # workgroup (g, w) = blockIdx g + 8 w: w = 0 is an attention workgroup, w = 20 is not
@@ -52,7 +53,7 @@ for k, name in enumerate(SEG):
 print(f"{'total':34s} {mean.sum():7.3f} {pr[wa].sum():7.3f} {pr[wn].sum():7.3f}")
 
 # absolute clocks of every workgroup at step 300: skew of each marker over the group-0 workgroups
-ab = prof[256 * 25:].view(256, 24).cpu().double() / 100.0
+ab = prof[256 * 29:].view(256, 28).cpu().double() / 100.0
 g0 = [8 * w for w in range(32)]
 base = ab[g0, 1].min()
 print("step 300, group 0: marker  min  median  max (us after the earliest marker 1)")

@@ -7,6 +7,7 @@ records it) and never synchronises or allocates outside torch's allocator.
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 
@@ -51,13 +52,22 @@ def _stream_scratch(device, tag: str, nbytes: int) -> int:
     return buf.data_ptr()
 
 
-# Optional launch log for tools/gemm_census.py: list of (tag, SatGemmDesc copy) when not None.
+# Optional launch log for tools/gemm_census.py: list of (tag, SatGemmDesc copy, call site) when
+# not None.
 GEMM_LOG = None
+
+
+def _call_site() -> str:
+    import traceback
+    for fr in reversed(traceback.extract_stack()[:-2]):
+        if not fr.filename.endswith("kernels.py"):
+            return f"{os.path.basename(fr.filename)}:{fr.lineno}:{fr.name}"
+    return "?"
 
 
 def _launch_gemm(d, tag):
     if GEMM_LOG is not None:
-        GEMM_LOG.append((tag, type(d).from_buffer_copy(d)))
+        GEMM_LOG.append((tag, type(d).from_buffer_copy(d), _call_site()))
     _lib.check(_lib.load().sat_gemm(ctypes.byref(d), _stream()), tag)
 
 

@@ -44,8 +44,10 @@ def main():
     descs = {}
     s = torch.cuda.current_stream()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    for tag, d in log:
+    sites = collections.defaultdict(collections.Counter)
+    for tag, d, site in log:
         key = (tag, d.M, d.N, d.K, d.batch, d.batch2, d.a_mode, d.b_mode, d.a_sk == 1, d.b_sn == 1)
+        sites[key][site] += 1
         if key not in groups:
             descs[key] = d
             for _ in range(2):
@@ -69,7 +71,8 @@ def main():
     for tot_us, cnt, us, tf, key in rows[:a.top]:
         tag, M, N, Kd, nb, nb2, am, bm, ak, bn = key
         print(f"{tag:22s} {M:6d} {N:6d} {Kd:6d} {nb:4d} {nb2:3d} {am:2d} {bm:2d} {int(ak):2d} {int(bn):2d} "
-              f"{cnt:4d} {us:10.1f} {tf:8.1f} {tot_us / 1e3:8.3f}")
+              f"{cnt:4d} {us:10.1f} {tf:8.1f} {tot_us / 1e3:8.3f}  "
+              + ", ".join(f"{k}x{v}" for k, v in sites[key].most_common(3)))
     if a.sweep:
         sweep(lib, descs, [r[4] for r in rows[:a.sweep]])
 

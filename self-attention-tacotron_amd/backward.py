@@ -21,11 +21,47 @@ from .model import _contig_span, bank_fused
 from .pipeline import SEQUENTIAL, Pipeline
 
 
-def lin_bwd(x, dy, W, dW, db, ws, dx=None, beta_dx=0.0, need_dx=True):
-    """Dense backward: dW += x^T dy, db += colsum(dy), dx (=|+=) dy W^T.  x [.., in], dy [.., out]."""
+class Aux:
+    """The backward's second stream for weight gradients nothing downstream reads: each branch
+    forks from the main stream at its call (so it sees the main stream's operands), runs on
+    K.aux_stream, and model_backward joins once after the encoder.  The main stream's dX chain
+    is a string of small launches and the encoder BiLSTM BPTT holds 64 CUs, so the branches
+    fill idle CUs.  Every tensor a branch reads is referenced until the join (the allocator
+    must not hand its block to a later main-stream allocation while the branch may run)."""
+
+    def __init__(self, device):
+        self.s = K.aux_stream(device)
+        self.keep = []
+
+    def run(self, fn, *tensors):
+        self.s.wait_stream(torch.cuda.current_stream())
+        self.keep.extend(tensors)
+        with torch.cuda.stream(self.s):
+            fn()
+
+    def join(self):
+        torch.cuda.current_stream().wait_stream(self.s)
+        self.keep.clear()
+
+
+def _wgrad(aux, fn, *tensors):
+    """run a weight-gradient-only product on the aux stream (inline without one)"""
+    if aux is not None:
+        aux.run(fn, *tensors)
+    else:
+        fn()
+
+
+def lin_bwd(x, dy, W, dW, db, ws, dx=None, beta_dx=0.0, need_dx=True, aux=None):
+    """Dense backward: dW += x^T dy, db += colsum(dy), dx (=|+=) dy W^T.  x [.., in], dy [.., out].
+    With ``aux`` the dW product runs on the aux stream."""
     x2 = x.reshape(-1, x.shape[-1])
     dy2 = dy.reshape(-1, dy.shape[-1])
-    K.gemm(x2.t(), dy2, dW, beta=1.0, colsum=db)     # db += colsum(dy) in the same launch
+    wgrad = lambda: K.gemm(x2.t(), dy2, dW, beta=1.0, colsum=db)  # noqa: E731  (+ db, fused)
+    if aux is not None:
+        aux.run(wgrad, x2, dy2)
+    else:
+        wgrad()
     if not need_dx:
         return None
     if dx is None:
@@ -100,7 +136,8 @@ class _LstmBwd:
         K.lstm_step_bwd(**self.desc(**kw))
 
 
-def decoder_bwd(P, G, hp, d, dsv, dH2, masks, ws, attn_tile=32, pipe: Pipeline = SEQUENTIAL):
+def decoder_bwd(P, G, hp, d, dsv, dH2, masks, ws, attn_tile=32, pipe: Pipeline = SEQUENTIAL,
+                aux: "Aux" = None):
     """Backward of decoder.decoder_forward.  Returns (dm1, dm2) batch-major.
 
     The three reverse recurrences (LSTM2 -> LSTM1 -> attention RNN) run as the mirror image of the
@@ -285,33 +322,52 @@ def decoder_bwd(P, G, hp, d, dsv, dH2, masks, ws, attn_tile=32, pipe: Pipeline =
             if j in dh0_at:
                 dh0_chunk(*dh0_at[j])
         assert pending is None
-    # LSTM weight gradients: one GEMM per weight block over all steps
-    DG2f = DG2.view(Tp * B, 4 * Dd)
-    DG1f = DG1.view(Tp * B, 4 * Dd)
-    K.gemm(S["H2S"][:Tp].reshape(Tp * B, Dd).t(), DG2f, dW2[Dd:], beta=1.0)
-    K.gemm(S["H1RAW"].view(Tp * B, Dd).t(), DG2f, dW2[:Dd], beta=1.0,
-           colsum=G["decoder/lstm2/bias"])                     # + the bias gradient
-    K.gemm(S["H1S"][:Tp].reshape(Tp * B, Dd).t(), DG1f, dW1[A + M1 + M2:], beta=1.0,
-           colsum=G["decoder/lstm1/bias"])
-    ctx_all = S["REC0"][1:].reshape(Tp * B, R0)[:, :M1 + M2]
-    K.gemm(S["H0RAW"].view(Tp * B, A).t(), DG1f, dW1[:A], beta=1.0)
-    K.gemm(ctx_all.t(), DG1f, dW1[A:A + M1 + M2], beta=1.0)
+    # ---- weight gradients nothing downstream reads -- the LSTM stack's and the attention RNN's
+    #      dW, the decoder prenets, the query layers -- run on the aux stream, concurrently with
+    #      the attention parameter pass and the encoder backward (which leave CUs idle: the
+    #      encoder BiLSTM BPTT holds 64 of them); model_backward joins the stream.  Everything the
+    #      branch reads stays referenced until the join; it writes only its own gradient rows.
+    aux_s = aux.s if aux is not None else torch.cuda.current_stream()
+    if aux is not None:
+        aux.s.wait_stream(torch.cuda.current_stream())
+        aux.keep.extend([DG0, DG1, DG2, DQP, S])
+    with torch.cuda.stream(aux_s):
+        # LSTM weight gradients: one GEMM per weight block over all steps
+        DG2f = DG2.view(Tp * B, 4 * Dd)
+        DG1f = DG1.view(Tp * B, 4 * Dd)
+        K.gemm(S["H2S"][:Tp].reshape(Tp * B, Dd).t(), DG2f, dW2[Dd:], beta=1.0)
+        K.gemm(S["H1RAW"].view(Tp * B, Dd).t(), DG2f, dW2[:Dd], beta=1.0,
+               colsum=G["decoder/lstm2/bias"])                     # + the bias gradient
+        K.gemm(S["H1S"][:Tp].reshape(Tp * B, Dd).t(), DG1f, dW1[A + M1 + M2:], beta=1.0,
+               colsum=G["decoder/lstm1/bias"])
+        ctx_all = S["REC0"][1:].reshape(Tp * B, R0)[:, :M1 + M2]
+        K.gemm(S["H0RAW"].view(Tp * B, A).t(), DG1f, dW1[:A], beta=1.0)
+        K.gemm(ctx_all.t(), DG1f, dW1[A:A + M1 + M2], beta=1.0)
 
-    DG0f = DG0.view(Tp * B, 4 * A)
-    K.gemm(S["REC0"][:Tp].reshape(Tp * B, R0).t(), DG0f, dW0[p_w:], beta=1.0)
-    dP = lin_bwd(S["prenet"][-1], DG0, W0[:p_w], dW0[:p_w], G["decoder/attention_lstm/bias"], ws)
-    # decoder prenets (inputs are teacher frames: no input gradient needed for the first one)
-    pres = S["prenet"]
-    ms = S.get("ms_prenet")
-    for i in reversed(range(len(d.dec_prenet))):
-        y = pres[i + 1]
-        dpre = torch.empty_like(y)
-        K.act_bwd(dP, y, dpre, "relu", mask=mk(f"dec/prenet{i}"))
-        sc = "decoder/prenet0/dense" if (ms is not None and i == 0) else f"decoder/prenet{i}"
-        dP = lin_bwd(pres[i], dpre, P[f"{sc}/kernel"], G[f"{sc}/kernel"], G[f"{sc}/bias"], ws,
-                     need_dx=i > 0 or ms is not None)
-    if ms is not None:
-        multi_speaker_prenet_bwd(P, G, d, S, ms, dP, ws)
+        DG0f = DG0.view(Tp * B, 4 * A)
+        K.gemm(S["REC0"][:Tp].reshape(Tp * B, R0).t(), DG0f, dW0[p_w:], beta=1.0)
+        dP = lin_bwd(S["prenet"][-1], DG0, W0[:p_w], dW0[:p_w], G["decoder/attention_lstm/bias"], ws)
+        # decoder prenets (inputs are teacher frames: no input gradient needed for the first one)
+        pres = S["prenet"]
+        ms = S.get("ms_prenet")
+        for i in reversed(range(len(d.dec_prenet))):
+            y = pres[i + 1]
+            dpre = torch.empty_like(y)
+            K.act_bwd(dP, y, dpre, "relu", mask=mk(f"dec/prenet{i}"))
+            sc = "decoder/prenet0/dense" if (ms is not None and i == 0) else f"decoder/prenet{i}"
+            dP = lin_bwd(pres[i], dpre, P[f"{sc}/kernel"], G[f"{sc}/kernel"], G[f"{sc}/bias"], ws,
+                         need_dx=i > 0 or ms is not None)
+        if ms is not None:
+            multi_speaker_prenet_bwd(P, G, d, S, ms, dP, ws)
+
+        # the per-tile partials of every step sum into the query-layer kernels; the attention bias
+        # gradient (the column sum of every tile) rides on each tile's GEMM as its fused colsum row
+        H0f = S["H0RAW"].view(Tp * B, A)
+        DQt = DQP.view(Tp * B, dq_parts, D1 + D2)
+        for tile in range(dq_parts):
+            K.gemm(H0f.t(), DQt[:, tile, :D1], G[f"{a1}/query_layer/kernel"], beta=1.0,
+                   colsum=G[f"{a1}/attention_bias"] if fwd else None)
+            K.gemm(H0f.t(), DQt[:, tile, D1:], G[f"{a2}/query_layer/kernel"], beta=1.0)
 
     # ---- attention parameters: one pass over all steps (sat_attn_param_grads), then a column
     #      sum of its per-workgroup partial rows
@@ -335,14 +391,6 @@ def decoder_bwd(P, G, hp, d, dsv, dH2, masks, ws, attn_tile=32, pipe: Pipeline =
     else:
         dsts = [G[f"{a1}/attention_v"]]
     K.colsum_scatter(PG, dsts + [G[f"{a2}/attention_v"]], ws, beta=1.0)
-    # the per-tile partials of every step sum into the query-layer kernels; the attention bias
-    # gradient (the column sum of every tile) rides on each tile's GEMM as its fused colsum row
-    H0f = S["H0RAW"].view(Tp * B, A)
-    DQt = DQP.view(Tp * B, dq_parts, D1 + D2)
-    for tile in range(dq_parts):
-        K.gemm(H0f.t(), DQt[:, tile, :D1], G[f"{a1}/query_layer/kernel"], beta=1.0,
-               colsum=G[f"{a1}/attention_bias"] if fwd else None)
-        K.gemm(H0f.t(), DQt[:, tile, D1:], G[f"{a2}/query_layer/kernel"], beta=1.0)
     # ---- memories: values via the alignment histories, keys via memory_layer
     dV1 = K.gemm(S["AL1"][1:].permute(1, 2, 0), DCTX[:, :, :M1].permute(1, 0, 2))   # [B, N, M1]
     dV2 = K.gemm(S["S2"].permute(1, 2, 0), DCTX[:, :, M1:].permute(1, 0, 2))        # [B, N, M2]
@@ -373,7 +421,7 @@ def multi_speaker_prenet_bwd(P, G, d, S, ms, dd0, ws):
             G[f"{sc}/dense0/bias"], ws, need_dx=False)
 
 
-def encoder_bwd(P, G, hp, d, sv, dm1, dm2, lengths, masks, ws):
+def encoder_bwd(P, G, hp, d, sv, dm1, dm2, lengths, masks, ws, aux: Aux = None):
     dev = dm1.device
     mk = (lambda n: masks[n]) if masks is not None else (lambda n: None)
     B, N, _ = dm1.shape
@@ -384,7 +432,7 @@ def encoder_bwd(P, G, hp, d, sv, dm1, dm2, lengths, masks, ws):
         dz = sa_transformer_bwd(P, G, f"encoder/self_attention{h}", sv[f"enc_sa{h}"], dz, ws)
     lin_bwd(sv["m1"], dz, P["encoder/self_attention_projection/kernel"],
             G["encoder/self_attention_projection/kernel"],
-            G["encoder/self_attention_projection/bias"], ws, dx=dm1, beta_dx=1.0)
+            G["encoder/self_attention_projection/bias"], ws, dx=dm1, beta_dx=1.0, aux=aux)
     # BiLSTM
     U = d.cbhg_half
     hws = sv["hws"]
@@ -432,9 +480,15 @@ def encoder_bwd(P, G, hp, d, sv, dm1, dm2, lengths, masks, ws):
         DG = DGs[dr]
         DGf = DG.view(N * B, 4 * U)
         hprev = st["HS"][1:N + 1] if rev else st["HS"][:N]
-        K.gemm(hprev.reshape(N * B, U).t(), DGf, dWk[Win:], beta=1.0)
-        K.gemm(hw_sm.view(N * B, Win).t(), DGf, dWk[:Win], beta=1.0,
-               colsum=G[f"encoder/cbhg/lstm_{dr}/bias"])      # + the bias gradient
+
+        def wgrad(hprev=hprev, DGf=DGf, dWk=dWk, dr=dr):
+            K.gemm(hprev.reshape(N * B, U).t(), DGf, dWk[Win:], beta=1.0)
+            K.gemm(hw_sm.view(N * B, Win).t(), DGf, dWk[:Win], beta=1.0,
+                   colsum=G[f"encoder/cbhg/lstm_{dr}/bias"])      # + the bias gradient
+        if aux is not None:
+            aux.run(wgrad, hprev, DGf, hw_sm)
+        else:
+            wgrad()
         # dhw[b, n, :] (+)= DG[n, b, :] @ Wx^T  -- batched over n, written transposed
         K.gemm(DG, Wk[:Win].t(), dhw.transpose(0, 1), beta=1.0 if i else 0.0)
     # highway stack
@@ -448,10 +502,10 @@ def encoder_bwd(P, G, hp, d, sv, dm1, dm2, lengths, masks, ws):
         K.highway_bwd(h, t, x, dy, dh_pre, dt_pre, dx)
         lin_bwd(x, dh_pre, P[f"encoder/cbhg/highway{i}/H/kernel"],
                 G[f"encoder/cbhg/highway{i}/H/kernel"], G[f"encoder/cbhg/highway{i}/H/bias"], ws,
-                dx=dx, beta_dx=1.0)
+                dx=dx, beta_dx=1.0, aux=aux)
         lin_bwd(x, dt_pre, P[f"encoder/cbhg/highway{i}/T/kernel"],
                 G[f"encoder/cbhg/highway{i}/T/kernel"], G[f"encoder/cbhg/highway{i}/T/bias"], ws,
-                dx=dx, beta_dx=1.0)
+                dx=dx, beta_dx=1.0, aux=aux)
         dy = dx
     if d.needs_adjust:
         dy = lin_bwd(sv["hw_in_adjust"], dy, P["encoder/cbhg/adjustment/kernel"],
@@ -465,8 +519,9 @@ def encoder_bwd(P, G, hp, d, sv, dm1, dm2, lengths, masks, ws):
     K.bn_bwd(dy.view(-1, C2), sv["p2_pre"].view(-1, C2), None, dp2.view(-1, C2), s2["mean"],
              s2["var"], s2["gamma"], G["encoder/cbhg/proj2/bn/gamma"],
              G["encoder/cbhg/proj2/bn/beta"], ws, training=training)
-    K.conv1d_dw(sv["p1"], dp2, G["encoder/cbhg/proj2/kernel"], beta=1.0)
-    K.colsum(dp2.view(-1, C2), G["encoder/cbhg/proj2/bias"], ws)
+    _wgrad(aux, lambda: (K.conv1d_dw(sv["p1"], dp2, G["encoder/cbhg/proj2/kernel"], beta=1.0),
+                         K.colsum(dp2.view(-1, C2), G["encoder/cbhg/proj2/bias"], ws)),
+           sv["p1"], dp2)
     dp1 = K.conv1d_dx(dp2, P["encoder/cbhg/proj2/kernel"])
     # proj1: p1 = relu(BN(p1_pre))
     C1 = d.proj1
@@ -476,8 +531,9 @@ def encoder_bwd(P, G, hp, d, sv, dm1, dm2, lengths, masks, ws):
              dp1_pre.view(-1, C1), s1["mean"], s1["var"], s1["gamma"],
              G["encoder/cbhg/proj1/bn/gamma"], G["encoder/cbhg/proj1/bn/beta"], ws,
              training=training)
-    K.conv1d_dw(sv["mp"], dp1_pre, G["encoder/cbhg/proj1/kernel"], beta=1.0)
-    K.colsum(dp1_pre.view(-1, C1), G["encoder/cbhg/proj1/bias"], ws)
+    _wgrad(aux, lambda: (K.conv1d_dw(sv["mp"], dp1_pre, G["encoder/cbhg/proj1/kernel"], beta=1.0),
+                         K.colsum(dp1_pre.view(-1, C1), G["encoder/cbhg/proj1/bias"], ws)),
+           sv["mp"], dp1_pre)
     dmp = K.conv1d_dx(dp1_pre, P["encoder/cbhg/proj1/kernel"])
     # max-pool, conv bank BN (one launch over the concatenated channels), conv bank
     dbank = torch.empty_like(dmp)
@@ -494,7 +550,10 @@ def encoder_bwd(P, G, hp, d, sv, dm1, dm2, lengths, masks, ws):
     if bank_fused(d, inp):
         kern = [f"{n}/kernel" for n in names]
         K.conv_bank_bwd(inp, _contig_span(P, kern), dbank_pre, d.max_k, C, dx=dinp,
-                        dW=_contig_span(G, kern), beta_dx=1.0, beta_dw=1.0)
+                        beta_dx=1.0)
+        _wgrad(aux, lambda: K.conv_bank_bwd(inp, _contig_span(P, kern), dbank_pre, d.max_k, C,
+                                            dW=_contig_span(G, kern), beta_dw=1.0),
+               inp, dbank_pre)
     else:
         for k in range(1, d.max_k + 1):
             sl = dbank_pre[:, :, (k - 1) * C:k * C]
@@ -508,7 +567,7 @@ def encoder_bwd(P, G, hp, d, sv, dm1, dm2, lengths, masks, ws):
         dpre = torch.empty_like(y)
         K.act_bwd(dx, y, dpre, "relu", mask=mk(f"enc/prenet{i}"))
         dx = lin_bwd(pre[i], dpre, P[f"encoder/prenet{i}/kernel"], G[f"encoder/prenet{i}/kernel"],
-                     G[f"encoder/prenet{i}/bias"], ws)
+                     G[f"encoder/prenet{i}/bias"], ws, aux=aux)
     K.embedding_bwd(dx, sv["batch"]["source"], G["embedding"])
 
 
@@ -516,9 +575,12 @@ def model_backward(P, G, hp, d, sv, ws, attn_tile=32, pipe: Pipeline = SEQUENTIA
     """Accumulate dL/dparams of model_forward's loss into G (caller zeroes G)."""
     masks = sv["masks"]
     dH2 = head_bwd(P, G, hp, d, sv, ws)
+    aux = Aux(dH2.device) if dH2.is_cuda else None
     dV1, dV2 = decoder_bwd(P, G, hp, d, sv["dec"], dH2, masks, ws, attn_tile=attn_tile,
-                           pipe=pipe)
+                           pipe=pipe, aux=aux)
     lengths = sv["batch"]["source_length"]
     dm1 = K.seq_mask(dV1, lengths)
     dm2 = K.seq_mask(dV2, lengths)
-    encoder_bwd(P, G, hp, d, sv, dm1, dm2, lengths, masks, ws)
+    encoder_bwd(P, G, hp, d, sv, dm1, dm2, lengths, masks, ws, aux=aux)
+    if aux is not None:
+        aux.join()                                    # every weight-gradient branch

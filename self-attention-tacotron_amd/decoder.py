@@ -56,6 +56,33 @@ def teacher_inputs(targets: torch.Tensor, r: int, n_feed: int) -> torch.Tensor:
     return x
 
 
+def decoder_inputs(P: Dict[str, torch.Tensor], hp, d: Dims, targets: torch.Tensor,
+                   masks: Optional[Dict[str, torch.Tensor]], aux) -> Dict[str, object]:
+    """The part of the teacher-forced decoder that reads only the targets (single speaker):
+    teacher frames, the prenets (dropout fused) and the attention RNN's input projection of the
+    prenet part.  Every output is allocated on the CURRENT stream, then the products run on the
+    stream ``aux`` (forked from the current one); the caller joins ``aux`` before
+    decoder_forward(inputs=...) reads them."""
+    r, nf = d.r, hp.n_feed_frame
+    B, T, M = targets.shape
+    Tp = T // r
+    dev = targets.device
+    mk = (lambda name: masks[name]) if masks is not None else (lambda name: None)
+    xin = torch.zeros(Tp, B, M * nf, device=dev, dtype=targets.dtype)
+    pres = [xin] + [torch.empty(Tp, B, w, device=dev) for w in d.dec_prenet]
+    X0 = torch.empty(Tp, B, 4 * d.att_rnn, device=dev)
+    aux.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(aux):
+        g = targets.view(B, Tp, M * r)
+        xin[1:].copy_(g[:, :-1, M * (r - nf):].transpose(0, 1))
+        for i in range(len(d.dec_prenet)):
+            K.linear(pres[i], P[f"decoder/prenet{i}/kernel"], P[f"decoder/prenet{i}/bias"],
+                     act="relu", mul=mk(f"dec/prenet{i}"), out=pres[i + 1])
+        W0 = P["decoder/attention_lstm/kernel"]
+        K.linear(pres[-1], W0[:pres[-1].shape[-1]], P["decoder/attention_lstm/bias"], out=X0)
+    return {"xin": xin, "pres": pres, "X0": X0}
+
+
 def persistent_eligible(d: Dims, B: int, N: int, attn_tile: int = 32) -> bool:
     """Shapes sat_decoder_attention_fwd and sat_decoder_lstms_fwd are compiled for (the
     self-attention-tacotron configs)."""
@@ -69,13 +96,16 @@ def decoder_forward(P: Dict[str, torch.Tensor], hp, d: Dims, m1: torch.Tensor, m
                     lengths: torch.Tensor, targets: torch.Tensor,
                     masks: Optional[Dict[str, torch.Tensor]], attn_tile: int = 32,
                     spk: Optional[torch.Tensor] = None, pipe: Pipeline = SEQUENTIAL,
-                    persistent: bool = False, scratch=None, keep_tanh: bool = True):
+                    persistent: bool = False, scratch=None, keep_tanh: bool = True,
+                    inputs: Optional[Dict[str, object]] = None):
     """Forward of the teacher-forced decoder; returns (D [T', B, dec], DecoderSaved).
 
     ``persistent`` runs the attention chain (attention RNN + query + dual-source attention) for
     all steps as ONE persistent launch (``sat_decoder_attention_fwd``) when the shapes allow,
     then the two decoder LSTMs as a two-problem wavefront; otherwise the per-step launches.
-    ``keep_tanh`` keeps the energies' tanh for the persistent BPTT (off for inference)."""
+    ``keep_tanh`` keeps the energies' tanh for the persistent BPTT (off for inference).
+    ``inputs``: the teacher frames, prenets and attention-RNN input projection already formed
+    by ``decoder_inputs`` (model_forward runs them on a second stream beside the encoder)."""
     dev = m1.device
     B, N, _ = m1.shape
     r, nf = d.r, hp.n_feed_frame
@@ -95,10 +125,12 @@ def decoder_forward(P: Dict[str, torch.Tensor], hp, d: Dims, m1: torch.Tensor, m
     S.update(V1=V1, V2=V2, K1=K1, K2=K2)
 
     # ---- prenets over all frames (teacher forcing), dropout fused as a multiplicative epilogue
-    xin = teacher_inputs(targets, r, nf)
+    xin = teacher_inputs(targets, r, nf) if inputs is None else inputs["xin"]
     pre = xin
-    pres = [xin]
-    if spk is not None:
+    pres = [xin] if inputs is None else inputs["pres"]
+    if inputs is not None:
+        pre = pres[-1]
+    elif spk is not None:
         # MultiSpeakerPreNet (modules/multi_speaker_modules.py:27-32): the speaker term is one
         # [B, p0] row per utterance, broadcast over the T' steps by a zero batch stride of the
         # step-major [T', B, .] GEMM's residual operand
@@ -114,17 +146,19 @@ def decoder_forward(P: Dict[str, torch.Tensor], hp, d: Dims, m1: torch.Tensor, m
         pre = K.linear(d0, P[f"{ms}/dense/kernel"], P[f"{ms}/dense/bias"], act="relu",
                        mul=mk("dec/prenet0"))
         pres.append(pre)
-    for i in range(len(pres) - 1, len(d.dec_prenet)):
-        pre = K.linear(pre, P[f"decoder/prenet{i}/kernel"], P[f"decoder/prenet{i}/bias"],
-                       act="relu", mul=mk(f"dec/prenet{i}"))
-        pres.append(pre)
+    if inputs is None:
+        for i in range(len(pres) - 1, len(d.dec_prenet)):
+            pre = K.linear(pre, P[f"decoder/prenet{i}/kernel"], P[f"decoder/prenet{i}/bias"],
+                           act="relu", mul=mk(f"dec/prenet{i}"))
+            pres.append(pre)
     S["prenet"] = pres
     S["xin"] = xin
     p_w = pre.shape[-1]
 
     # ---- attention RNN (ZoneoutLSTM A) input projection of the prenet part
     W0 = P["decoder/attention_lstm/kernel"]          # [p + M1 + M2 + A, 4A] (gate-interleaved)
-    X0 = K.linear(pre, W0[:p_w], P["decoder/attention_lstm/bias"])     # [T', B, 4A]
+    X0 = (K.linear(pre, W0[:p_w], P["decoder/attention_lstm/bias"]) if inputs is None
+          else inputs["X0"])                         # [T', B, 4A]
     R0 = M1 + M2 + A                                 # recurrent input [c1 | c2 | h0]
     # zero-initialised state histories (row 0 = initial state), one fill for all of them and
     # for the decoder LSTMs' c / h histories below

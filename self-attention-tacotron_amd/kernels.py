@@ -52,6 +52,19 @@ def _stream_scratch(device, tag: str, nbytes: int) -> int:
     return buf.data_ptr()
 
 
+_AUX = {}
+
+
+def aux_stream(device) -> torch.cuda.Stream:
+    """The step's second stream (independent branches beside the encoder, forward and backward),
+    one per device, made on first use -- the eager warm-up before any graph capture; the GEMM
+    split-K and column-reduction scratch are keyed per stream already."""
+    s = _AUX.get(device.index)
+    if s is None:
+        s = _AUX[device.index] = torch.cuda.Stream(device=device)
+    return s
+
+
 # Optional launch log for tools/gemm_census.py: list of (tag, SatGemmDesc copy, call site) when
 # not None.
 GEMM_LOG = None

@@ -19,7 +19,7 @@ import torch
 
 from . import kernels as K
 from . import params as PR
-from .decoder import decoder_forward
+from .decoder import decoder_forward, decoder_inputs
 
 
 class BNState:
@@ -260,8 +260,17 @@ def model_forward(P, bn: BNState, hp, d: PR.Dims, batch: Dict[str, torch.Tensor]
     error arena -- words 8 and 9 take the embedding / speaker-embedding id-range flags."""
     sv = Saved()
     ids, lengths = batch["source"], batch["source_length"]
+    # the decoder's target-only inputs (prenets, the attention RNN's input projection) on a
+    # second stream beside the encoder, whose BiLSTM holds only 64 CUs (persistent path, single
+    # speaker); joined before the decoder reads them
+    dec_in, aux = None, None
+    if persistent and not d.multi_speaker and ids.is_cuda:
+        aux = K.aux_stream(ids.device)
+        dec_in = decoder_inputs(P, hp, d, batch["mel"], masks, aux)
     m1, m2 = encoder_fwd(P, bn, hp, d, ids, lengths, masks, training, ws, sv,
                          persistent=persistent, err=None if health is None else health[8:9])
+    if aux is not None:
+        torch.cuda.current_stream().wait_stream(aux)
     spk = None
     if d.multi_speaker:                                               # models/models.py:43-46,69
         ids_s = batch["speaker_id"]
@@ -274,7 +283,7 @@ def model_forward(P, bn: BNState, hp, d: PR.Dims, batch: Dict[str, torch.Tensor]
         K.embedding_fwd(P["speaker_embedding"], ids_s, spk, d.spk_offset, sv["spk_err"])
     dout, dsv = decoder_forward(P, hp, d, m1, m2, lengths, batch["mel"], masks,
                                 attn_tile=attn_tile, spk=spk, persistent=persistent,
-                                scratch=scratch, keep_tanh=compute_grad_seeds,
+                                scratch=scratch, keep_tanh=compute_grad_seeds, inputs=dec_in,
                                 **({} if pipe is None else {"pipe": pipe}))
     sv["dec"] = dsv
     if spk is not None:

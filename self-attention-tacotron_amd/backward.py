@@ -549,11 +549,13 @@ def encoder_bwd(P, G, hp, d, sv, dm1, dm2, lengths, masks, ws, aux: Aux = None):
     K.colsum(dbank_pre.view(-1, KC), _contig_span(G, [f"{n}/bias" for n in names]), ws)
     if bank_fused(d, inp):
         kern = [f"{n}/kernel" for n in names]
-        K.conv_bank_bwd(inp, _contig_span(P, kern), dbank_pre, d.max_k, C, dx=dinp,
-                        beta_dx=1.0)
+        # the weight-gradient branch forks BEFORE the dX product is issued: a branch waits for
+        # everything the main stream has issued at its fork, so the other order serialises them
         _wgrad(aux, lambda: K.conv_bank_bwd(inp, _contig_span(P, kern), dbank_pre, d.max_k, C,
                                             dW=_contig_span(G, kern), beta_dw=1.0),
                inp, dbank_pre)
+        K.conv_bank_bwd(inp, _contig_span(P, kern), dbank_pre, d.max_k, C, dx=dinp,
+                        beta_dx=1.0)
     else:
         for k in range(1, d.max_k + 1):
             sl = dbank_pre[:, :, (k - 1) * C:k * C]

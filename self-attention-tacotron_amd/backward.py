@@ -83,31 +83,34 @@ def mha_bwd(P, G, scope, s, dy, ws):
     return dx
 
 
-def sa_transformer_bwd(P, G, scope, s, dz, ws):
+def sa_transformer_bwd(P, G, scope, s, dz, ws, aux=None):
     """z = x + tanh(Dense(MHA(x)))  ->  dx."""
     du = torch.empty_like(dz)
     K.act_bwd(dz, s["u"], du, "tanh")
     dy = lin_bwd(s["y"], du, P[f"{scope}/transform/kernel"], G[f"{scope}/transform/kernel"],
-                 G[f"{scope}/transform/bias"], ws)
+                 G[f"{scope}/transform/bias"], ws, aux=aux)
     dx = mha_bwd(P, G, f"{scope}/mha", s, dy, ws)
     K.axpby(dz, dx, 1.0, 1.0)                                        # residual
     return dx
 
 
-def head_bwd(P, G, hp, d, sv, ws):
-    """RNNTransformer head backward -> dL/dD step-major [T', B, dec]."""
+def head_bwd(P, G, hp, d, sv, ws, aux=None):
+    """RNNTransformer head backward -> dL/dD step-major [T', B, dec].  With ``aux`` the dense
+    layers' weight gradients run on the second stream; the caller joins it before the next
+    persistent launch (the LSTM stack's BPTT needs every CU free to become resident)."""
     Z = sv["Z"]
     B, Tp, _ = Z.shape
     dmel_r = sv["dmel"].view(B, Tp, d.num_mels * d.r)
     dstop = sv["dstop"].view(B, Tp, 1)
     dZ = lin_bwd(Z, dmel_r, P["decoder/out_projection/kernel"], G["decoder/out_projection/kernel"],
-                 G["decoder/out_projection/bias"], ws)
+                 G["decoder/out_projection/bias"], ws, aux=aux)
     lin_bwd(Z, dstop, P["decoder/stop_token_projection/kernel"],
             G["decoder/stop_token_projection/kernel"], G["decoder/stop_token_projection/bias"], ws,
-            dx=dZ, beta_dx=1.0)
+            dx=dZ, beta_dx=1.0, aux=aux)
     dz = dZ
     for h in reversed(range(d.dec_hops)):
-        dz = sa_transformer_bwd(P, G, f"decoder/self_attention{h}", sv[f"dec_sa{h}"], dz, ws)
+        dz = sa_transformer_bwd(P, G, f"decoder/self_attention{h}", sv[f"dec_sa{h}"], dz, ws,
+                                aux=aux)
     return dz.transpose(0, 1).contiguous()                           # [T', B, D] (data movement)
 
 
@@ -429,7 +432,8 @@ def encoder_bwd(P, G, hp, d, sv, dm1, dm2, lengths, masks, ws, aux: Aux = None):
     # encoder self-attention hops
     dz = dm2
     for h in reversed(range(d.enc_hops)):
-        dz = sa_transformer_bwd(P, G, f"encoder/self_attention{h}", sv[f"enc_sa{h}"], dz, ws)
+        dz = sa_transformer_bwd(P, G, f"encoder/self_attention{h}", sv[f"enc_sa{h}"], dz, ws,
+                                aux=aux)
     lin_bwd(sv["m1"], dz, P["encoder/self_attention_projection/kernel"],
             G["encoder/self_attention_projection/kernel"],
             G["encoder/self_attention_projection/bias"], ws, dx=dm1, beta_dx=1.0, aux=aux)
@@ -576,8 +580,10 @@ def encoder_bwd(P, G, hp, d, sv, dm1, dm2, lengths, masks, ws, aux: Aux = None):
 def model_backward(P, G, hp, d, sv, ws, attn_tile=32, pipe: Pipeline = SEQUENTIAL):
     """Accumulate dL/dparams of model_forward's loss into G (caller zeroes G)."""
     masks = sv["masks"]
-    dH2 = head_bwd(P, G, hp, d, sv, ws)
-    aux = Aux(dH2.device) if dH2.is_cuda else None
+    aux = Aux(sv["Z"].device) if sv["Z"].is_cuda else None
+    dH2 = head_bwd(P, G, hp, d, sv, ws, aux=aux)
+    if aux is not None:
+        aux.join()        # before the LSTM stack's BPTT (persistent: all 256 workgroups resident)
     dV1, dV2 = decoder_bwd(P, G, hp, d, sv["dec"], dH2, masks, ws, attn_tile=attn_tile,
                            pipe=pipe, aux=aux)
     lengths = sv["batch"]["source_length"]

@@ -96,9 +96,10 @@ def sa_transformer_fwd(x, P, scope, heads, causal, probs_mask, sv, key):
 
 
 def encoder_fwd(P, bn: BNState, hp, d: PR.Dims, ids, lengths, masks, training, ws, sv,
-                persistent: bool = False, err: Optional[torch.Tensor] = None):
+                persistent: bool = False, err: Optional[torch.Tensor] = None, before_lstm=None):
     """SelfAttentionCBHGEncoder.call (modules/module.py:425-438) -> (M1, M2).  ``err``: the
-    int32 word the embedding's id-range check raises (zeroed here; default a fresh one)."""
+    int32 word the embedding's id-range check raises (zeroed here; default a fresh one).
+    ``before_lstm``: called right before the BiLSTM launch (which holds only 2B CUs)."""
     dev = ids.device
     B, N = ids.shape
     mk = (lambda n: masks[n]) if masks is not None else (lambda n: None)
@@ -189,6 +190,8 @@ def encoder_fwd(P, bn: BNState, hp, d: PR.Dims, ids, lengths, masks, training, w
                     gates=st["G"][n], lengths=lengths)
 
     sv["enc_persistent"] = persistent and U == 128
+    if before_lstm is not None:
+        before_lstm()
     if sv["enc_persistent"]:
         # all N steps of both directions in ONE launch (encoder_lstm.hip: one workgroup per
         # (direction, utterance) keeps the recurrent matrix in registers)
@@ -263,12 +266,17 @@ def model_forward(P, bn: BNState, hp, d: PR.Dims, batch: Dict[str, torch.Tensor]
     # the decoder's target-only inputs (prenets, the attention RNN's input projection) on a
     # second stream beside the encoder, whose BiLSTM holds only 64 CUs (persistent path, single
     # speaker); joined before the decoder reads them
-    dec_in, aux = None, None
+    aux, fork = None, None
+    dec_box = [None]
     if persistent and not d.multi_speaker and ids.is_cuda:
         aux = K.aux_stream(ids.device)
-        dec_in = decoder_inputs(P, hp, d, batch["mel"], masks, aux)
+
+        def fork():      # forked at the BiLSTM launch: it fills the CUs the BiLSTM leaves idle
+            dec_box[0] = decoder_inputs(P, hp, d, batch["mel"], masks, aux)
     m1, m2 = encoder_fwd(P, bn, hp, d, ids, lengths, masks, training, ws, sv,
-                         persistent=persistent, err=None if health is None else health[8:9])
+                         persistent=persistent, err=None if health is None else health[8:9],
+                         before_lstm=fork)
+    dec_in = dec_box[0]
     if aux is not None:
         torch.cuda.current_stream().wait_stream(aux)
     spk = None

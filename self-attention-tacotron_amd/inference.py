@@ -532,8 +532,9 @@ class FreeRunningDecoder:
         mel = pl.MEL[:T_].permute(1, 0, 2).reshape(B, T_ * r, M).clone()
         stop = pl.STOP[:T_, :, 0].transpose(0, 1).clone()
         return {"mel": mel, "stop": stop, "steps": T_,
-                "alignment1": pl.AL1[1:T_ + 1].permute(1, 2, 0).contiguous(),   # [B, N, T']
-                "alignment2": pl.S2[:T_].permute(1, 2, 0).contiguous(),
+                "alignment1": pl.AL1[1:T_ + 1].permute(1, 2, 0).clone(   # [B, N, T']
+                    memory_format=torch.contiguous_format),
+                "alignment2": pl.S2[:T_].permute(1, 2, 0).clone(memory_format=torch.contiguous_format),
                 "decoder_self_alignments": [pl.SA_P[h][:, :, :T_, :T_].clone()
                                             for h in range(d.dec_hops)],
                 "encoder_self_alignments": [sv[f"enc_sa{h}"]["P"] for h in range(d.enc_hops)],

@@ -109,9 +109,25 @@ extern "C" int sat_mha_fwd(const SatMha* d, void* stream) {
   const int64_t LD = (int64_t)L * D, LL = (int64_t)L * L, HLL = H * LL;
   char* sc = static_cast<char*>(d->scratch) + 4 * align_up((int64_t)B * L * D * 4);
   float* S = reinterpret_cast<float*>(sc);
-  SAT_TRY(dense(d->x, d->Wq, d->bq, d->q, R, d->W, D, 0.f, d, s));
-  SAT_TRY(dense(d->x, d->Wk, d->bk, d->k, R, d->W, D, 0.f, d, s));
-  SAT_TRY(dense(d->x, d->Wv, d->bv, d->v, R, d->W, D, 0.f, d, s));
+  // Q/K/V: ONE batched product when the three weights, biases and outputs are equally spaced
+  // (the parameter arena stores query / key / value kernel + bias back to back; model.mha_fwd
+  // allocates q, k, v as one [3][B][L][D] buffer) -- three times the tiles in one launch
+  const int64_t sw = d->Wk - d->Wq, sb = d->bk - d->bq, so = d->k - d->q;
+  if (d->bq && sw == d->Wv - d->Wk && sb == d->bv - d->bk && so == d->v - d->k) {
+    SatGemmDesc g = dense_desc();
+    g.M = R; g.N = D; g.K = d->W;
+    g.batch = 3;
+    g.A = d->x; g.a_sm = d->W; g.a_sk = 1; g.a_sbatch = 0;
+    g.B = d->Wq; g.b_sk = D; g.b_sn = 1; g.b_sbatch = sw;
+    g.C = d->q; g.c_sm = D; g.c_sbatch = so;
+    g.bias = d->bq; g.bias_sbatch = sb;
+    g.ws = d->gemm_ws; g.ws_bytes = d->gemm_ws_bytes;
+    SAT_TRY(sat_gemm(&g, s));
+  } else {
+    SAT_TRY(dense(d->x, d->Wq, d->bq, d->q, R, d->W, D, 0.f, d, s));
+    SAT_TRY(dense(d->x, d->Wk, d->bk, d->k, R, d->W, D, 0.f, d, s));
+    SAT_TRY(dense(d->x, d->Wv, d->bv, d->v, R, d->W, D, 0.f, d, s));
+  }
   // S[b,h] = Q_h K_h^T                                               (self_attention.py:55)
   SAT_TRY(head_gemm(L, L, dh, {d->q, D, 1, LD, dh}, {d->k, 1, D, LD, dh}, S, L, HLL, LL, 1.f, d,
                     s));

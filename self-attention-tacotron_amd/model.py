@@ -71,8 +71,8 @@ def mha_fwd(x: torch.Tensor, P, scope: str, heads: int, causal: bool,
     model = P[f"{scope}/query_projection/kernel"].shape[1]
     out = P[f"{scope}/output_projection/kernel"].shape[1]
     dev = x.device
-    s = dict(x=x, q=torch.empty(B, L, model, device=dev), k=torch.empty(B, L, model, device=dev),
-             v=torch.empty(B, L, model, device=dev), P=torch.empty(B, heads, L, L, device=dev),
+    qkv = torch.empty(3, B, L, model, device=dev)     # one buffer: a single batched Q/K/V product
+    s = dict(x=x, q=qkv[0], k=qkv[1], v=qkv[2], P=torch.empty(B, heads, L, L, device=dev),
              o=torch.empty(B, L, model, device=dev), y=torch.empty(B, L, out, device=dev),
              mask=probs_mask, heads=heads, dh=model // heads, causal=causal, scope=scope)
     s["Pd"] = torch.empty_like(s["P"]) if probs_mask is not None else s["P"]

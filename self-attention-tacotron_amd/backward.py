@@ -119,14 +119,16 @@ class _LstmBwd:
     ping-pong between two buffers)."""
 
     def __init__(self, B, U, dev):
-        h0, h1, c0, c1 = K.zeros_group(*([(B, U)] * 4), device=dev)   # one fill
-        self.hc = [h0, h1]
-        self.cc = [c0, c1]
-        self.first = True
+        self.shape, self.dev = (B, U), dev
+        self.hc = self.cc = None                  # allocated at the first step (the persistent
+        self.first = True                         # paths never take one)
         self.cur = 0
 
     def desc(self, **kw):
         """kwargs of the next reverse step (carries filled in); advances the carry state."""
+        if self.hc is None:
+            h0, h1, c0, c1 = K.zeros_group(*([self.shape] * 4), device=self.dev)   # one fill
+            self.hc, self.cc = [h0, h1], [c0, c1]
         c = self.cur
         kw.update(dh_carry=None if self.first else self.hc[c],
                   dc_carry=None if self.first else self.cc[c],
@@ -442,7 +444,14 @@ def encoder_bwd(P, G, hp, d, sv, dm1, dm2, lengths, masks, ws, aux: Aux = None):
     hws = sv["hws"]
     hw = hws[-1][2] if len(hws) > 1 else hws[0]
     Win = hw.shape[-1]
-    hw_sm = hw.transpose(0, 1).contiguous()                          # [N, B, Win] (data movement)
+    hw_box = []
+
+    def hw_sm_of():
+        # [N, B, Win] (data movement) for the input-weight gradients, made on the stream that
+        # runs them (the aux stream when present: off the main stream's chain)
+        if not hw_box:
+            hw_box.append(hw.transpose(0, 1).contiguous())
+        return hw_box[0]
     dhw = torch.empty(B, N, Win, device=dev)
     zc, zh = hp.zoneout_factor_cell, hp.zoneout_factor_output
     # reverse recurrences of both directions, one multi-problem launch per step (the forward
@@ -487,10 +496,13 @@ def encoder_bwd(P, G, hp, d, sv, dm1, dm2, lengths, masks, ws, aux: Aux = None):
 
         def wgrad(hprev=hprev, DGf=DGf, dWk=dWk, dr=dr):
             K.gemm(hprev.reshape(N * B, U).t(), DGf, dWk[Win:], beta=1.0)
-            K.gemm(hw_sm.view(N * B, Win).t(), DGf, dWk[:Win], beta=1.0,
+            hs = hw_sm_of()
+            K.gemm(hs.view(N * B, Win).t(), DGf, dWk[:Win], beta=1.0,
                    colsum=G[f"encoder/cbhg/lstm_{dr}/bias"])      # + the bias gradient
+            if aux is not None:
+                aux.keep.append(hs)
         if aux is not None:
-            aux.run(wgrad, hprev, DGf, hw_sm)
+            aux.run(wgrad, hprev, DGf, hw)
         else:
             wgrad()
         # dhw[b, n, :] (+)= DG[n, b, :] @ Wx^T  -- batched over n, written transposed

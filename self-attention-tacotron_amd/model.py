@@ -88,8 +88,7 @@ def sa_transformer_fwd(x, P, scope, heads, causal, probs_mask, sv, key):
     """SelfAttentionTransformer.call (modules/module.py:363-371): x + tanh(Dense(MHA(x)))."""
     y = mha_fwd(x, P, f"{scope}/mha", heads, causal, probs_mask, sv, key)
     u = K.linear(y, P[f"{scope}/transform/kernel"], P[f"{scope}/transform/bias"], act="tanh")
-    z = x.clone()                                                    # residual (data movement)
-    K.axpby(u, z, 1.0, 1.0)
+    z = torch.add(x, u)                                              # residual (one launch)
     sv[key]["u"] = u
     sv[key]["z"] = z
     return z

@@ -34,6 +34,9 @@
 #ifndef SAT_FWD8_TRACE
 #define SAT_FWD8_TRACE 0
 #endif
+#ifndef SAT_FWD8_NORM3
+#define SAT_FWD8_NORM3 1     // the normalise window's history stores on wave 7 (A/B switch)
+#endif
 
 namespace sat {
 namespace {
@@ -357,7 +360,7 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
             cbuf[tid] = a;
             if (j == 0) p.REC0[((int64_t)t * B + b) * kK0 + tid] = a;
           }
-        } else if (wave < 7) {
+        } else {
           const unsigned bit = lsb_tag(t);
           auto e_at = [&](int n) -> float {       // e_{t-1}(n) on the window, -inf where masked
             if (n < 0 || n >= len) return -INFINITY;
@@ -372,14 +375,14 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
               const float e = e_at(n0 - kPadL + lane);
               const float sv = e == -INFINITY ? 0.f : __expf(e - M1) * __builtin_amdgcn_rcpf(Z1);
               sp[lane] = sv;
-              if (lane >= kPadL && lane < nt + kPadL)
+              if (!SAT_FWD8_NORM3 && lane >= kPadL && lane < nt + kPadL)
                 p.S1[((int64_t)t * B + b) * N + n0 + lane - kPadL] = sv;
             }
             if (t < T && 4 * 7 < nt) {         // no idle energy wave (N > 224): here
               asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
               store_loc(t, lane);
             }
-          } else {
+          } else if (wave == 6) {
             const float* ap = alf[(t - 1) & 1];      // alpha_{t-2} at n0-1+k
             if (lane <= nt) {
               const int k = lane, n = n0 - 1 + k;
@@ -395,6 +398,16 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
               const float at = tagf(av, bit);
               alf[t & 1][k] = at;
               if (k >= 1) p.AL1[((int64_t)t * B + b) * N + n] = at;
+            }
+          }
+          // wave 7 (idle in this window): the S1 / S2 / ST history stores (S1 recomputed with
+          // wave 5's arithmetic: the same bits), off waves 5 and 6 whose LDS results the next
+          // phases wait for
+          if (SAT_FWD8_NORM3 ? wave == 7 : wave == 6) {
+            if (SAT_FWD8_NORM3 && lane >= kPadL && lane < nt + kPadL) {
+              const float e = e_at(n0 - kPadL + lane);
+              p.S1[((int64_t)t * B + b) * N + n0 + lane - kPadL] =
+                  e == -INFINITY ? 0.f : __expf(e - M1) * __builtin_amdgcn_rcpf(Z1);
             }
             if (lane < nt) {
               const float e2 = e2own[lane];

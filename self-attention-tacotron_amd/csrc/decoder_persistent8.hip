@@ -37,6 +37,9 @@
 #ifndef SAT_FWD8_NORM3
 #define SAT_FWD8_NORM3 1     // the normalise window's history stores on wave 7 (A/B switch)
 #endif
+#ifndef SAT_FWD8_HSTORE7
+#define SAT_FWD8_HSTORE7 1   // the cell's C0 / REC0 / H0RAW / G0 stores on wave 7 (A/B switch)
+#endif
 
 namespace sat {
 namespace {
@@ -118,6 +121,8 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
   __shared__ __attribute__((aligned(16))) float4 recs[kW][kR4];  // staged records B_{t-1}
   __shared__ __attribute__((aligned(16))) float hst[kUW];        // own units' h_t (tagged)
   __shared__ __attribute__((aligned(16))) float hraw[kUW];       // own units' raw outputs
+  __shared__ float cown[kUW];                                    // own units' c_t
+  __shared__ __attribute__((aligned(16))) float4 gown[kUW];      // own units' gates (i, j, f, o)
   __shared__ float gsum[8][64];             // h part of the gate sums (transpose-reduced)
   __shared__ float halo[12];                // e_{t-1} left 4 | right 5 ; alpha_{t-2} at n0-2, n0-1
   __shared__ float eown[kPmax], e2own[kPmax];
@@ -133,6 +138,9 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
   const int b = g;
   const int n0 = j * P, nt = max(0, min(P, N - n0));
   const bool has_left = j > 0, has_right = j + 1 < kW && n0 + P < N;
+  // wave 7 holds no energy positions when nt <= 28: it then stores the cell's histories in the
+  // location-term phase (from LDS) instead of the cell lanes of every wave
+  const bool w7_stores = SAT_FWD8_HSTORE7 && 4 * 7 >= nt;
   const int64_t bN = (int64_t)b * N;
   const int len = (int)p.lengths[b];
   const float u = p.u;
@@ -481,11 +489,16 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
         c_own = c2; h_own = h2;
         hst[4 * wave + cq] = h2;
         hraw[4 * wave + cq] = hn;
-        const int64_t tbu = ((int64_t)t * B + b) * kU + cunit;
-        p.C0[((int64_t)(t + 1) * B + b) * kU + cunit] = c2;
-        p.REC0[((int64_t)(t + 1) * B + b) * kK0 + kC + cunit] = h2;
-        p.H0RAW[tbu] = hn;
-        reinterpret_cast<float4*>(p.G0)[tbu] = make_float4(gi, gj, gf, go);
+        if (w7_stores) {
+          cown[4 * wave + cq] = c2;
+          gown[4 * wave + cq] = make_float4(gi, gj, gf, go);
+        } else {
+          const int64_t tbu = ((int64_t)t * B + b) * kU + cunit;
+          p.C0[((int64_t)(t + 1) * B + b) * kU + cunit] = c2;
+          p.REC0[((int64_t)(t + 1) * B + b) * kK0 + kC + cunit] = h2;
+          p.H0RAW[tbu] = hn;
+          reinterpret_cast<float4*>(p.G0)[tbu] = make_float4(gi, gj, gf, go);
+        }
       }
       load_ops(t + 1, lane, wave, xgn, mcn, mhn);
       tick(4);
@@ -617,7 +630,20 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
     } else {                                   // idle wave: its positions are padding
       const int r = 4 * wave + (lane & 3);
       if (lane < 4) eown[r] = -INFINITY; else if (lane < 8) e2own[r] = -INFINITY;
-      if (wave == 7) store_loc(t, lane);       // the LOC history, off the critical path
+      if (wave == 7) {
+        store_loc(t, lane);                    // the LOC history, off the critical path
+        if (w7_stores && lane < kUW) {
+          // the cell's histories of step t for the own 32 units (in LDS since the cell
+          // barrier; rewritten only by step t+1's cell): one coalesced store each instead of
+          // four scattered ones per cell lane of every wave
+          const int cunit = kUW * j + lane;
+          const int64_t tbu = ((int64_t)t * B + b) * kU + cunit;
+          p.C0[((int64_t)(t + 1) * B + b) * kU + cunit] = cown[lane];
+          p.REC0[((int64_t)(t + 1) * B + b) * kK0 + kC + cunit] = hst[lane];
+          p.H0RAW[tbu] = hraw[lane];
+          reinterpret_cast<float4*>(p.G0)[tbu] = gown[lane];
+        }
+      }
     }
     tick(11);
     ev(12);

@@ -433,7 +433,10 @@ int sat_attn_step_bwd(const SatAttnStepBwd* args, void* stream);
  * b*N + n).  Writes dK1 [B][N][D1], dK2 [B][N][D2] (overwritten) and one partial row per
  * workgroup, pg [sat_attn_param_grad_rows(B, N)][pg_stride] =
  * [dv1 D1 | dW_loc F*D1 | dconvW KW*F | dconvb F | dv2 D2] (F = KW = 0 when !att1_forward),
- * to be column-summed. */
+ * to be column-summed.
+ * zh (optional): the forward's energy-tanh history [T][B][N][D1+D2] (SatDecAttnFwd.ZH).  Given,
+ * the pass reads z from it instead of recomputing the energies (as TF's tanh gradient uses the
+ * forward's output); K1, K2, q, b1 and locW are then not read. */
 typedef struct SatAttnParamGrad {
   int32_t T, B, N, D1, D2, F, KW, att1_forward;
   const float* K1; const float* K2;
@@ -445,6 +448,7 @@ typedef struct SatAttnParamGrad {
   const float* df;
   float* dK1; float* dK2;
   float* pg; int64_t pg_stride;
+  const float* zh;
 } SatAttnParamGrad;
 
 int sat_attn_pg_stride(int32_t D1, int32_t D2, int32_t F, int32_t KW);

@@ -435,8 +435,9 @@ int sat_attn_step_bwd(const SatAttnStepBwd* args, void* stream);
  * [dv1 D1 | dW_loc F*D1 | dconvW KW*F | dconvb F | dv2 D2] (F = KW = 0 when !att1_forward),
  * to be column-summed.
  * zh (optional): the forward's energy-tanh history [T][B][N][D1+D2] (SatDecAttnFwd.ZH).  Given,
- * the pass reads z from it instead of recomputing the energies (as TF's tanh gradient uses the
- * forward's output); K1, K2, q, b1 and locW are then not read. */
+ * zh_share of every 8 position workgroups read z from it instead of recomputing the energies
+ * (HBM-bound vs VALU-bound work, co-resident on each CU); zh_share = 8 reads every z (as TF's
+ * tanh gradient uses the forward's output), 0 recomputes every z. */
 typedef struct SatAttnParamGrad {
   int32_t T, B, N, D1, D2, F, KW, att1_forward;
   const float* K1; const float* K2;
@@ -449,6 +450,7 @@ typedef struct SatAttnParamGrad {
   float* dK1; float* dK2;
   float* pg; int64_t pg_stride;
   const float* zh;
+  int32_t zh_share, pad_zh;   /* with zh: workgroups of every 8 that read z (0..8), the rest recompute */
 } SatAttnParamGrad;
 
 int sat_attn_pg_stride(int32_t D1, int32_t D2, int32_t F, int32_t KW);

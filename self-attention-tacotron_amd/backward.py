@@ -390,7 +390,7 @@ def decoder_bwd(P, G, hp, d, dsv, dH2, masks, ws, attn_tile=32, pipe: Pipeline =
         locW=P[f"{a1}/location_layer/kernel"] if fwd else None, v2=P[f"{a2}/attention_v"],
         loc=S["LOC"] if fwd else None, s_prev=S["S1"], s_tstride=S["S1"].stride(0),
         de1=DE1, de2=DE2, df=DFH if fwd else None, dK1=dK1, dK2=dK2, pg=PG, pg_stride=pgs,
-        zh=None)     # recompute the energy tanh: reading ZH (3.3 GB at C2) measured no faster
+        zh=None)     # recompute every z: reading ZH (3.3 GB at C2), all or in part, measured no faster
     if fwd:
         dsts = [G[f"{a1}/attention_variable"], G[f"{a1}/location_layer/kernel"].view(-1),
                 G[f"{a1}/location_conv/kernel"].view(-1), G[f"{a1}/location_conv/bias"]]

@@ -941,7 +941,7 @@ __device__ __forceinline__ void attn_pg_store(const SatAttnParamGrad& p, const f
                                               const float4 (*adw)[F > 0 ? F : 1], float acw);
 
 template <int SLOTS, int F>
-__global__ void __launch_bounds__(256) attn_param_grad_kernel(SatAttnParamGrad p) {
+__device__ __forceinline__ void pg_recompute_body(const SatAttnParamGrad& p) {
   constexpr int FL = F > 0 ? F : 1;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int nq = (p.N + 3) / 4;
@@ -1115,7 +1115,7 @@ typedef float pg2 __attribute__((ext_vector_type(2)));
 typedef float pg4 __attribute__((ext_vector_type(4)));
 
 template <int SLOTS, int F>
-__global__ void __launch_bounds__(256) attn_param_grad_zh_kernel(SatAttnParamGrad p) {
+__device__ __forceinline__ void pg_zh_body(const SatAttnParamGrad& p) {
   constexpr int FL = F > 0 ? F : 1;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int nq = (p.N + 3) / 4;
@@ -1237,6 +1237,15 @@ __global__ void __launch_bounds__(256) attn_param_grad_zh_kernel(SatAttnParamGra
   attn_pg_store<SLOTS, F>(p, adk, adv, adw, acw);
 }
 
+// One launch over the (utterance, 4-position) workgroups: of every 8 consecutive workgroups the
+// first zh_share read z from ZH (HBM-bound), the others recompute it (VALU-bound), so the two
+// kinds share each CU's issue slots and the memory system at once.
+template <int SLOTS, int F>
+__global__ void __launch_bounds__(256) attn_param_grad_kernel(SatAttnParamGrad p) {
+  if (p.zh && (int)(blockIdx.x & 7) < p.zh_share) pg_zh_body<SLOTS, F>(p);
+  else pg_recompute_body<SLOTS, F>(p);
+}
+
 template <int NT, int WAVES>
 void launch_attn_bwd(const AttnBwdP& p, int F, int blocks, hipStream_t s) {
   const dim3 g(blocks), blk(64 * WAVES);
@@ -1288,15 +1297,8 @@ extern "C" int sat_attn_param_grads(const SatAttnParamGrad* a, void* stream) {
   const dim3 grid(sat_attn_param_grad_rows(a->B, a->N));
   const size_t shm = 4 * (size_t)a->pg_stride * sizeof(float);
   hipStream_t s = as_stream(stream);
-  if (a->zh) {
-    SAT_CHECK_ARG(aligned16(a->zh) && (a->D1 + a->D2) % 4 == 0, "sat_attn_param_grads: zh alignment");
-    if (slots == 1 && F == 5) hipLaunchKernelGGL((attn_param_grad_zh_kernel<1, 5>), grid, dim3(256), shm, s, p);
-    else if (slots == 1 && F == 0) hipLaunchKernelGGL((attn_param_grad_zh_kernel<1, 0>), grid, dim3(256), shm, s, p);
-    else if (F == 0) hipLaunchKernelGGL((attn_param_grad_zh_kernel<2, 0>), grid, dim3(256), shm, s, p);
-    else hipLaunchKernelGGL((attn_param_grad_zh_kernel<2, 8>), grid, dim3(256), shm, s, p);
-    SAT_LAUNCH_CHECK("sat_attn_param_grads");
-    return SAT_OK;
-  }
+  SAT_CHECK_ARG(!a->zh || (aligned16(a->zh) && a->zh_share >= 0 && a->zh_share <= 8),
+                "sat_attn_param_grads: zh alignment / zh_share in 0..8");
   if (slots == 1 && F == 5) hipLaunchKernelGGL((attn_param_grad_kernel<1, 5>), grid, dim3(256), shm, s, p);
   else if (slots == 1 && F == 0) hipLaunchKernelGGL((attn_param_grad_kernel<1, 0>), grid, dim3(256), shm, s, p);
   else if (F == 0) hipLaunchKernelGGL((attn_param_grad_kernel<2, 0>), grid, dim3(256), shm, s, p);

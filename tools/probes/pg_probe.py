@@ -25,23 +25,26 @@ def main():
     PG = torch.empty(K.attn_param_grad_rows(B, N), pgs, device=dev)
     dK1, dK2 = torch.empty(B, N, D1, device=dev), torch.empty(B, N, D2, device=dev)
 
-    def run(z):
+    def run(z, share):
         K.attn_param_grads(T=T, B=B, N=N, D1=D1, D2=D2, F=F, KW=KW, att1_forward=1, K1=K1, K2=K2,
                            q=q, q_tstride=q.stride(0), q_bstride=q.stride(1), b1=b1, v1=v1,
                            locW=locW, v2=v2, loc=loc, s_prev=sp, s_tstride=sp.stride(0),
-                           de1=de1, de2=de2, df=df, dK1=dK1, dK2=dK2, pg=PG, pg_stride=pgs, zh=z)
+                           de1=de1, de2=de2, df=df, dK1=dK1, dK2=dK2, pg=PG, pg_stride=pgs, zh=z,
+                           zh_share=share)
 
-    for name, z in (("recompute", None), ("zh", zh)):
+    for share in range(9):
+        z = zh if share else None
+        name = f"zh {share}/8"
         for _ in range(3):
-            run(z)
+            run(z, share)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for _ in range(20):
-            run(z)
+            run(z, share)
         e1.record()
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) * 1e3 / 20
-        zb = T * B * N * (D1 + D2) * 4 if z is not None else 0
+        zb = T * B * N * (D1 + D2) * 4 * share / 8
         print(f"{name:10s} {us:8.1f} us/launch  ZH stream {zb / us / 1e3:7.1f} GB/s", flush=True)
 
 

@@ -705,6 +705,9 @@ int sat_maxpool2_bwd(const float* x, const float* dy, float* dx, int32_t B, int3
  * its backward to the pre-activations (dh_pre, dt_pre) and the carry path dx. */
 int sat_highway_fwd(const float* h, const float* t, const float* x, float* y, int64_t n,
                     void* stream);
+/* The same layer after ONE batched GEMM of both pre-activations (h, t hold h_pre, t_pre):
+ * h = relu(h), t = sigmoid(t) in place, then y = h*t + x*(1-t). */
+int sat_highway_act_fwd(float* h, float* t, const float* x, float* y, int64_t n, void* stream);
 int sat_highway_bwd(const float* h, const float* t, const float* x, const float* dy,
                     float* dh_pre, float* dt_pre, float* dx, int64_t n, void* stream);
 

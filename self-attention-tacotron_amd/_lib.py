@@ -216,6 +216,7 @@ SIGNATURES = {
     "sat_maxpool2": [_P, _P, _I32, _I32, _I32, _P],
     "sat_maxpool2_bwd": [_P, _P, _P, _I32, _I32, _I32, _P],
     "sat_highway_fwd": [_P, _P, _P, _P, _I64, _P],
+    "sat_highway_act_fwd": [_P, _P, _P, _P, _I64, _P],
     "sat_highway_bwd": [_P, _P, _P, _P, _P, _P, _P, _I64, _P],
     "sat_act_bwd": [_P, _P, _P, _P, _I64, _I32, _F, _P],
     "sat_axpby": [_P, _P, _I64, _F, _F, _P],

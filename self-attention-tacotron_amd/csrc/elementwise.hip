@@ -507,6 +507,20 @@ __global__ void highway_fwd_kernel(const float* __restrict__ h, const float* __r
   GRID_STRIDE(i, n) { y[i] = h[i] * t[i] + x[i] * (1.f - t[i]); }
 }
 
+// the highway layer after ONE batched product of its H and T pre-activations (x [W_H | W_T] +
+// [b_H | b_T] as a batch of two): h = relu(h_pre), t = sigmoid(t_pre) written back in place (the
+// backward's operands; the same arithmetic as the GEMM epilogue's activations), y = h t + x (1 - t)
+__global__ void highway_act_fwd_kernel(float* __restrict__ h, float* __restrict__ t,
+                                       const float* __restrict__ x, float* __restrict__ y,
+                                       int64_t n) {
+  GRID_STRIDE(i, n) {
+    const float hv = fmaxf(h[i], 0.f), tv = 1.f / (1.f + expf(-t[i]));
+    h[i] = hv;
+    t[i] = tv;
+    y[i] = hv * tv + x[i] * (1.f - tv);
+  }
+}
+
 __global__ void highway_bwd_kernel(const float* __restrict__ h, const float* __restrict__ t,
                                    const float* __restrict__ x, const float* __restrict__ dy,
                                    float* __restrict__ dh_pre, float* __restrict__ dt_pre,
@@ -1071,6 +1085,15 @@ extern "C" int sat_highway_fwd(const float* h, const float* t, const float* x, f
   hipLaunchKernelGGL(highway_fwd_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), h, t,
                      x, y, n);
   SAT_LAUNCH_CHECK("sat_highway_fwd");
+  return SAT_OK;
+}
+
+extern "C" int sat_highway_act_fwd(float* h, float* t, const float* x, float* y, int64_t n,
+                                   void* stream) {
+  SAT_CHECK_ARG(h && t && x && y && n >= 0, "sat_highway_act_fwd: bad args");
+  hipLaunchKernelGGL(highway_act_fwd_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), h,
+                     t, x, y, n);
+  SAT_LAUNCH_CHECK("sat_highway_act_fwd");
   return SAT_OK;
 }
 

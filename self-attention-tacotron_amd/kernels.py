@@ -144,7 +144,8 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor = None, *, alpha=1.0,
     d.b_sbatch, d.b_sbatch2 = _bstrides(B, nd)
     d.C, d.c_sm = _p(C), C.stride(-2)
     d.c_sbatch, d.c_sbatch2 = _bstrides(C, nd)
-    d.bias, d.bias_sbatch = _p(bias), 0
+    d.bias, d.bias_sbatch = _p(bias), (bias.stride(0) if bias is not None and bias.dim() == 2
+                                       else 0)
     d.act = ACT[act]
     d.alpha, d.beta = alpha, beta
     if mul is not None:
@@ -664,6 +665,28 @@ def maxpool2_bwd(x, dy, dx):
 def highway_fwd(h, t, x, y):
     _lib.call("sat_highway_fwd", _p(h), _p(t), _p(x), _p(y), y.numel(), _stream())
     return y
+
+
+def highway_act_fwd(h, t, x, y):
+    _lib.call("sat_highway_act_fwd", _p(h), _p(t), _p(x), _p(y), y.numel(), _stream())
+    return y
+
+
+def pair_view(a: torch.Tensor, b: torch.Tensor):
+    """Two equally shaped contiguous views of ONE storage as a [2, ...] batch view (batch stride
+    = their element distance), or None when they cannot be (different storage, overlap).
+    Returns (view, swapped): swapped means view[0] is ``b``."""
+    if (a.shape != b.shape or not a.is_contiguous() or not b.is_contiguous() or
+            a.untyped_storage().data_ptr() != b.untyped_storage().data_ptr()):
+        return None
+    oa, ob = a.storage_offset(), b.storage_offset()
+    swapped = ob < oa
+    lo, d = (ob, oa - ob) if swapped else (oa, ob - oa)
+    if d < a.numel():
+        return None
+    base = a if not swapped else b
+    full = torch.empty(0, device=a.device, dtype=a.dtype).set_(base.untyped_storage())
+    return full.as_strided((2, *a.shape), (d, *a.stride()), lo), swapped
 
 
 def highway_bwd(h, t, x, dy, dh_pre, dt_pre, dx):

@@ -152,12 +152,22 @@ def encoder_fwd(P, bn: BNState, hp, d: PR.Dims, ids, lengths, masks, training, w
         hw = K.linear(hw, P["encoder/cbhg/adjustment/kernel"], P["encoder/cbhg/adjustment/bias"])
     hws = [hw]
     for i in range(d.num_highway):                                    # ext HighwayNet
-        h = K.linear(hw, P[f"encoder/cbhg/highway{i}/H/kernel"],
-                     P[f"encoder/cbhg/highway{i}/H/bias"], act="relu")
-        t = K.linear(hw, P[f"encoder/cbhg/highway{i}/T/kernel"],
-                     P[f"encoder/cbhg/highway{i}/T/bias"], act="sigmoid")
+        sc = f"encoder/cbhg/highway{i}"
         y = torch.empty_like(hw)
-        K.highway_fwd(h, t, hw, y)
+        Wp = K.pair_view(P[f"{sc}/H/kernel"], P[f"{sc}/T/kernel"])
+        bp = K.pair_view(P[f"{sc}/H/bias"], P[f"{sc}/T/bias"])
+        if Wp is not None and bp is not None and Wp[1] == bp[1]:
+            # H and T pre-activations as ONE batched product (the two weights / biases are a
+            # constant distance apart in the parameter arena), activations fused into the combine
+            ht = torch.empty(2, *hw.shape, device=dev)
+            K.gemm(hw.reshape(-1, hw.shape[-1]), Wp[0], ht.view(2, -1, hw.shape[-1]),
+                   bias=bp[0].view(2, -1))
+            h, t = (ht[1], ht[0]) if Wp[1] else (ht[0], ht[1])
+            K.highway_act_fwd(h, t, hw, y)
+        else:
+            h = K.linear(hw, P[f"{sc}/H/kernel"], P[f"{sc}/H/bias"], act="relu")
+            t = K.linear(hw, P[f"{sc}/T/kernel"], P[f"{sc}/T/bias"], act="sigmoid")
+            K.highway_fwd(h, t, hw, y)
         hws.append((h, t, y))
         hw = y
     sv["hws"] = hws
@@ -169,11 +179,20 @@ def encoder_fwd(P, bn: BNState, hp, d: PR.Dims, ids, lengths, masks, training, w
     # N-1-n of the backward cell run as ONE multi-problem launch (sat_lstm_steps_fwd)
     lstm = {}
     zs = K.zeros_group(*([(N + 1, B, U)] * 4), device=dev)   # c / h histories, one fill
+    Win = hw.shape[-1]
+    Wp = K.pair_view(P["encoder/cbhg/lstm_fw/kernel"][:Win], P["encoder/cbhg/lstm_bw/kernel"][:Win])
+    bp = K.pair_view(P["encoder/cbhg/lstm_fw/bias"], P["encoder/cbhg/lstm_bw/bias"])
+    X = None
+    if Wp is not None and bp is not None and Wp[1] == bp[1]:
+        # both directions' input projections as ONE batched product
+        Xp = torch.empty(2, B, N, 4 * U, device=dev)
+        K.gemm(hw.reshape(-1, Win), Wp[0], Xp.view(2, B * N, 4 * U), bias=bp[0].view(2, -1))
+        X = (Xp[1], Xp[0]) if Wp[1] else (Xp[0], Xp[1])
     for i, dr in enumerate(("fw", "bw")):
         Wk = P[f"encoder/cbhg/lstm_{dr}/kernel"]
         lstm[dr] = dict(
-            X=K.linear(hw, Wk[:hw.shape[-1]], P[f"encoder/cbhg/lstm_{dr}/bias"]),  # [B, N, 4U]
-            CS=zs[2 * i], HS=zs[2 * i + 1],
+            X=X[i] if X is not None else K.linear(hw, Wk[:Win], P[f"encoder/cbhg/lstm_{dr}/bias"]),
+            CS=zs[2 * i], HS=zs[2 * i + 1],                       # X: [B, N, 4U]
             G=torch.empty(N, B, 4 * U, device=dev))
 
     def enc_step(dr, rev, n):

@@ -86,6 +86,19 @@ typedef struct SatGemmDesc {
    * launch (the bias gradient of a weight-gradient product dW = X^T dY, db = 1^T dY); needs a
    * batch-1 product without bias / act / mul / add.  NULL = off. */
   float* colsum_out;
+  /* optional second A segment: A's columns k >= k1 come from A2 (row stride a2_sm), i.e.
+   * C = A[:, :k1] B[:k1] + A2 B[k1:] as ONE reduction (two inputs of one layer that live in
+   * different buffers); batch-1 dense product with K-contiguous A, k1 % 32 == 0, 16-byte aligned
+   * rows, no colsum_out.  NULL = off. */
+  const float* A2;
+  int64_t a2_sm;
+  int32_t k1, pad1;
+  /* optional second output: columns n >= n1 of the product go to C2[m][n - n1] (row stride
+   * c2_sm), i.e. two outputs of one A over the column blocks of one B (bias, when given, is
+   * indexed by n); batch-1, no colsum_out / mul / add, n1 % 128 == 0.  NULL = off. */
+  float* C2;
+  int64_t c2_sm;
+  int32_t n1, pad2;
 } SatGemmDesc;
 
 int sat_gemm(const SatGemmDesc* desc, void* stream);

@@ -43,6 +43,14 @@ class SatGemmDesc(ctypes.Structure):
         ("add", ctypes.c_void_p), ("add_sm", ctypes.c_int64), ("add_sbatch", ctypes.c_int64),
         ("ws", ctypes.c_void_p), ("ws_bytes", ctypes.c_int64),
         ("colsum_out", ctypes.c_void_p),
+        ("A2", ctypes.c_void_p),
+        ("a2_sm", ctypes.c_int64),
+        ("k1", ctypes.c_int32),
+        ("pad1", ctypes.c_int32),
+        ("C2", ctypes.c_void_p),
+        ("c2_sm", ctypes.c_int64),
+        ("n1", ctypes.c_int32),
+        ("pad2", ctypes.c_int32),
     ]
 
 

@@ -195,8 +195,12 @@ def decoder_bwd(P, G, hp, d, dsv, dH2, masks, ws, attn_tile=32, pipe: Pipeline =
     def dh0_chunk(a, b):
         n = (b - a) * B
         dg = DG1[a:b].view(n, 4 * Dd)
-        K.gemm(dg, W1[:A].t(), dH0[a:b].view(n, A))
-        K.gemm(dg, W1[A:A + M1 + M2].t(), RD[a:b].view(n, R0)[:, :M1 + M2])
+        if A % 128 == 0:     # dL/dh0' and dL/dctx as the two output blocks of ONE product
+            K.gemm(dg, W1[:A + M1 + M2].t(), dH0[a:b].view(n, A),
+                   C2=RD[a:b].view(n, R0)[:, :M1 + M2])
+        else:
+            K.gemm(dg, W1[:A].t(), dH0[a:b].view(n, A))
+            K.gemm(dg, W1[A:A + M1 + M2].t(), RD[a:b].view(n, R0)[:, :M1 + M2])
 
     # ---- attention RNN + dual-source attention recurrence
     W0 = P["decoder/attention_lstm/kernel"]

@@ -5,7 +5,7 @@
 // (ext tacotron2, built at modules/module.py:1531-1540) under TransformerTrainingHelper
 // (modules/helpers.py:13-58).  Teacher forcing makes the dependency one-way: the attention chain
 // never reads the LSTM stack, so the loop is the attention chain's persistent launch, LSTM1's
-// input projection for all steps (two GEMMs), then the LSTM stack's persistent launch -- the
+// input projection for all steps (one two-segment GEMM), then the LSTM stack's persistent launch -- the
 // sequence decoder.py decoder_forward issues, here behind one call so a C caller does not
 // re-implement it.  The backward mirrors backward.py decoder_bwd's persistent path.
 #include "sat_common.h"
@@ -50,13 +50,22 @@ extern "C" int sat_decoder_loop_fwd(const SatDecoderLoopFwd* a, void* stream) {
   if (rc != SAT_OK) return rc;
   const int U = at.U, R0 = at.M1 + at.M2 + at.U, G = 4 * ls.U, MB = at.T * at.B;
   float* X1 = const_cast<float*>(ls.X1);
-  // X1 = h0'_t W1x[0:U] + b1   (the attention RNN's raw output feeds LSTM1)
-  rc = dense(MB, G, U, at.H0RAW, U, 1, a->W1x, G, 1, X1, G, a->b1, 0.f, a->ws, a->ws_bytes, stream);
-  if (rc != SAT_OK) return rc;
-  // X1 += [c1_t | c2_t] W1x[U:U+M1+M2]   (REC0 row t+1 holds step t's contexts)
-  rc = dense(MB, G, at.M1 + at.M2, at.REC0 + (int64_t)at.B * R0, R0, 1, a->W1x + (int64_t)U * G, G,
-             1, X1, G, nullptr, 1.f, a->ws, a->ws_bytes, stream);
-  if (rc != SAT_OK) return rc;
+  // X1 = [h0'_t | c1_t | c2_t] W1x + b1 as ONE reduction: the attention RNN's raw output and the
+  // contexts (REC0 row t+1 holds step t's) are the two A segments (SatGemmDesc.A2)
+  {
+    SatGemmDesc d;
+    std::memset(&d, 0, sizeof(d));
+    d.M = MB; d.N = G; d.K = U + at.M1 + at.M2; d.batch = 1; d.batch2 = 1;
+    d.A = at.H0RAW; d.a_sm = U; d.a_sk = 1;
+    d.A2 = at.REC0 + (int64_t)at.B * R0; d.a2_sm = R0; d.k1 = U;
+    d.B = a->W1x; d.b_sk = G; d.b_sn = 1;
+    d.C = X1; d.c_sm = G;
+    d.bias = a->b1;
+    d.alpha = 1.f; d.beta = 0.f;
+    d.ws = a->ws; d.ws_bytes = a->ws_bytes;
+    rc = sat_gemm(&d, stream);
+    if (rc != SAT_OK) return rc;
+  }
   return sat_decoder_lstms_fwd(&ls, stream);
 }
 
@@ -74,12 +83,27 @@ extern "C" int sat_decoder_loop_bwd(const SatDecoderLoopBwd* a, void* stream) {
   }
   int rc = sat_decoder_lstms_bwd(&ls, stream);
   if (rc != SAT_OK) return rc;
-  // dL/dh0'_t = DG1_t W1x[0:U]^T ;  dL/dctx_t = DG1_t W1x[U:U+M1+M2]^T  (into RD's ctx half)
-  rc = dense(MB, U, G, ls.DG1, G, 1, a->W1x, 1, G, a->DH0, U, nullptr, 0.f, a->ws, a->ws_bytes,
-             stream);
-  if (rc != SAT_OK) return rc;
-  rc = dense(MB, at.M1 + at.M2, G, ls.DG1, G, 1, a->W1x + (int64_t)U * G, 1, G, at.RD, R0, nullptr,
-             0.f, a->ws, a->ws_bytes, stream);
-  if (rc != SAT_OK) return rc;
+  // dL/dh0'_t = DG1_t W1x[0:U]^T ;  dL/dctx_t = DG1_t W1x[U:U+M1+M2]^T  (into RD's ctx half):
+  // the two output blocks of ONE product (SatGemmDesc.C2) when U is a whole number of tiles
+  if (U % 128 == 0) {
+    SatGemmDesc d;
+    std::memset(&d, 0, sizeof(d));
+    d.M = MB; d.N = R0; d.K = G; d.batch = 1; d.batch2 = 1;
+    d.A = ls.DG1; d.a_sm = G; d.a_sk = 1;
+    d.B = a->W1x; d.b_sk = 1; d.b_sn = G;
+    d.C = a->DH0; d.c_sm = U;
+    d.C2 = at.RD; d.c2_sm = R0; d.n1 = U;
+    d.alpha = 1.f; d.beta = 0.f;
+    d.ws = a->ws; d.ws_bytes = a->ws_bytes;
+    rc = sat_gemm(&d, stream);
+    if (rc != SAT_OK) return rc;
+  } else {
+    rc = dense(MB, U, G, ls.DG1, G, 1, a->W1x, 1, G, a->DH0, U, nullptr, 0.f, a->ws, a->ws_bytes,
+               stream);
+    if (rc != SAT_OK) return rc;
+    rc = dense(MB, at.M1 + at.M2, G, ls.DG1, G, 1, a->W1x + (int64_t)U * G, 1, G, at.RD, R0,
+               nullptr, 0.f, a->ws, a->ws_bytes, stream);
+    if (rc != SAT_OK) return rc;
+  }
   return sat_decoder_attention_bwd(&at, stream);
 }

@@ -53,6 +53,16 @@ struct GemmP {
   float* cs_out;
   int m_real;
   int grp_co;                  // conv-bank launches: output channels per conv (GRP > 0)
+  // second A segment (SatGemmDesc.A2, dense K-contiguous A only): columns k >= k1 of A come
+  // from A2 (row stride a2_sm), i.e. C = A[:, :k1] B[:k1] + A2 B[k1:] in one product
+  const float* A2 = nullptr;
+  int64_t a2_sm = 0;
+  int k1 = 0;
+  // second C segment (SatGemmDesc.C2): output columns n >= n1 go to C2 (row stride c2_sm) at
+  // column n - n1 (n1 a multiple of the tile width: the choice is per tile)
+  float* C2 = nullptr;
+  int64_t c2_sm = 0;
+  int n1 = 0;
 };
 
 // j -> g with g (g + 1) / 2 <= j < (g + 1) (g + 2) / 2: conv K_{g+1} of the bank owns the
@@ -680,6 +690,7 @@ __global__ void __launch_bounds__((64 * lds_waves<BM, BN>())) gemm_lds_kernel(Ge
   // M/N-major images: instruction i covers k rows (NWV i + w) * (256 / rows) + lane / (rows / 4)
   const float* aptr[NA];
   int ai[NA];
+  int arow[NA];                                        // A_K: the lane's (clamped) row per DMA
   const int amq = AKM ? 0 : 4 * (lane % (BM / 4));
   bool aone[NA];                                       // the fused column-sum row of ones
 #pragma unroll
@@ -689,7 +700,9 @@ __global__ void __launch_bounds__((64 * lds_waves<BM, BN>())) gemm_lds_kernel(Ge
       const int gm = m0 + (NWV * i + w) * 8 + (lane >> 3);
       aone[i] = p.cs_out != nullptr && gm == p.m_real;
       ai[i] = gm < p.M && !aone[i];
-      aptr[i] = A + (int64_t)min(gm, (p.cs_out ? p.m_real : p.M) - 1) * p.a_sm + kbeg + kq;
+      arow[i] = min(gm, (p.cs_out ? p.m_real : p.M) - 1);
+      aptr[i] = (p.A2 && kbeg >= p.k1) ? p.A2 + (int64_t)arow[i] * p.a2_sm + (kbeg - p.k1) + kq
+                                       : A + (int64_t)arow[i] * p.a_sm + kbeg + kq;
     } else if constexpr (AM == A_IM2COL) {   // (utterance, position) of the output row
       const int gm = m0 + (NWV * i + w) * 8 + (lane >> 3);
       const int s = gm / p.a_L, n = gm - s * p.a_L;
@@ -729,6 +742,10 @@ __global__ void __launch_bounds__((64 * lds_waves<BM, BN>())) gemm_lds_kernel(Ge
     const uint32_t lb = la + A_SZ * 4;
     if constexpr (AM == A_K) {
       const bool kok = k0 + kq < kend;
+      if (p.A2 && k0 == p.k1) {   // the reduction crosses into the second A segment
+#pragma unroll
+        for (int i = 0; i < NA; ++i) aptr[i] = p.A2 + (int64_t)arow[i] * p.a2_sm + kq;
+      }
 #pragma unroll
       for (int i = 0; i < NA; ++i) {
         dma16(kok ? (ai[i] ? aptr[i] : (aone[i] ? ones : zero)) : zero, la + (NWV * i + w) * 1024);
@@ -944,11 +961,15 @@ __global__ void __launch_bounds__((64 * lds_waves<BM, BN>())) gemm_lds_kernel(Ge
     return;
   }
   float* C = p.C + bz * p.c_sbatch + bz2 * p.c_sbatch2;
+  int64_t cs = p.c_sm;
+  if (p.C2 && n0 >= p.n1) {   // this tile's columns live in the second output (batch 1 only)
+    C = p.C2 - p.n1;
+    cs = p.c2_sm;
+  }
   const float* bias = p.bias ? p.bias + bz * p.bias_sbatch : nullptr;
   const float* mul = p.mul ? p.mul + bz * p.mul_sbatch + bz2 * p.mul_sbatch2 : nullptr;
   const float* add = p.add ? p.add + bz * p.add_sbatch : nullptr;
   if (full && !mul && !add && p.beta == 0.f && p.act == 0 && !p.cs_out) {
-    const int64_t cs = p.c_sm;
 #pragma unroll
     for (int i = 0; i < SM; ++i)
 #pragma unroll
@@ -972,7 +993,7 @@ __global__ void __launch_bounds__((64 * lds_waves<BM, BN>())) gemm_lds_kernel(Ge
       for (int r = 0; r < 16; ++r) {
         const int row = m0 + wm + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
         if (row >= p.M) continue;
-        float* dst = out_ptr(p, C, row, col);
+        float* dst = (p.cs_out && row == p.m_real) ? p.cs_out + col : C + (int64_t)row * cs + col;
         float v = p.alpha * acc[0][i][j][r];
         if (p.beta != 0.f) v += p.beta * (*dst);
         v = apply_act(v + bv, p.act);
@@ -1230,7 +1251,7 @@ static int launch_lds(const SatGemmDesc* d, GemmP& p, int nb, hipStream_t s) {
       (bm == B_FLIP && am != A_IM2COL))
     return 1;
   if (p.cs_out && am == A_M && p.m_real % 4 != 0) return 1;   // the ones chunk must start at m_real
-  const LdsPlan pl = plan_lds(p.M, d->N, d->K, nb, nb == 1 && d->ws != nullptr,
+  const LdsPlan pl = plan_lds(p.M, d->N, d->K, nb, nb == 1 && d->ws != nullptr && !p.C2,
                               d->ws_bytes, am == A_IM2COLT ? d->a_C : 0, 0);
   if (pl.bm == 0) return 1;
   return launch_lds_plan<0>(pl, am, bm, nb, p, s, "sat_gemm");
@@ -1268,6 +1289,31 @@ extern "C" int sat_gemm(const SatGemmDesc* d, void* stream) {
   hipStream_t s = as_stream(stream);
   const int nb = d->batch * p.batch2;
   p.ws = reinterpret_cast<float*>(d->ws);
+  if (d->C2) {
+    // two output column blocks: only the LDS kernel's unsplit epilogue takes them
+    SAT_CHECK_ARG(nb == 1 && !d->colsum_out && !d->mul && !d->add && d->n1 > 0 && d->n1 < d->N &&
+                      d->n1 % 128 == 0 && gemm_lds_enabled() && !t_probe,
+                  "sat_gemm: C2 needs a batch-1 product without colsum_out / mul / add and "
+                  "n1 %% 128 == 0");
+    p.C2 = d->C2; p.c2_sm = d->c2_sm; p.n1 = d->n1;
+  }
+  if (d->A2 || d->C2) {
+    if (!d->A2) {
+      const int r = launch_lds(d, p, nb, s);
+      SAT_CHECK_ARG(r != 1, "sat_gemm: C2 operands are not vector-loadable");
+      return r;
+    }
+    // two A segments over one B: only the LDS kernel's dense K-contiguous A loader takes them
+    SAT_CHECK_ARG(nb == 1 && d->a_mode == 0 && d->a_sk == 1 && d->b_mode == 0 && !d->colsum_out &&
+                      d->k1 > 0 && d->k1 < d->K && d->k1 % BK == 0 && aligned16(d->A2) &&
+                      d->a2_sm % 4 == 0 && gemm_lds_enabled() && !t_probe,
+                  "sat_gemm: A2 needs a batch-1 dense product with K-contiguous A, k1 %% 32 == 0, "
+                  "16-byte aligned rows, no colsum_out");
+    p.A2 = d->A2; p.a2_sm = d->a2_sm; p.k1 = d->k1;
+    const int r = launch_lds(d, p, nb, s);
+    SAT_CHECK_ARG(r != 1, "sat_gemm: A2 operands are not vector-loadable");
+    return r;
+  }
   if (d->colsum_out) {
     // C = alpha A B + beta C and colsum_out = alpha 1^T B + beta colsum_out (the bias gradient of
     // a weight-gradient product) in ONE launch: A gets a row of ones

@@ -225,8 +225,10 @@ def decoder_forward(P: Dict[str, torch.Tensor], hp, d: Dims, m1: torch.Tensor, m
     def x1_chunk(a, b):
         n = (b - a) * B
         x1 = X1[a:b].view(n, 4 * Dd)
-        K.linear(H0RAW[a:b].reshape(n, A), W1[:A], P["decoder/lstm1/bias"], out=x1)
-        K.gemm(REC0[a + 1:b + 1].reshape(n, R0)[:, :M1 + M2], W1[A:A + M1 + M2], x1, beta=1.0)
+        # ONE reduction over [h0'_t | c1_t | c2_t]: the raw attention-RNN output and the contexts
+        # (REC0 row t+1) are the two A segments of W1x
+        K.gemm(H0RAW[a:b].reshape(n, A), W1[:A + M1 + M2], x1, bias=P["decoder/lstm1/bias"],
+               A2=REC0[a + 1:b + 1].reshape(n, R0)[:, :M1 + M2])
 
     def x2_chunk(a, b):
         n = (b - a) * B

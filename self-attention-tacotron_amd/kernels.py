@@ -107,8 +107,13 @@ def _bstrides(t, nd):
 
 
 def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor = None, *, alpha=1.0, beta=0.0,
-         bias=None, act=None, mul=None, add=None, colsum=None) -> torch.Tensor:
+         bias=None, act=None, mul=None, add=None, colsum=None, A2=None, C2=None) -> torch.Tensor:
     """C = act(alpha * A @ B + beta * C + bias) * mul + add.
+
+    ``A2`` [M, K2] (2-D, row-contiguous like A): A is the two column blocks [A | A2] of one
+    reduction over B [K1 + K2, N] (SatGemmDesc.A2: two inputs of a layer in different buffers).
+    ``C2`` [M, N - N1] (2-D, unit column stride): the product's columns split between C [M, N1]
+    and C2 (SatGemmDesc.C2: two outputs of one A over the column blocks of one B).
 
     ``colsum`` [N] (2-D, plain products only): also colsum = alpha * sum over rows of B + beta *
     colsum in the same launch (a dense layer's bias gradient next to its weight gradient).
@@ -118,6 +123,12 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor = None, *, alpha=1.0,
     """
     _f32(A, "A"); _f32(B, "B")
     M, K = A.shape[-2], A.shape[-1]
+    k1 = K
+    if A2 is not None:
+        _f32(A2, "A2")
+        if A.dim() != 2 or A2.dim() != 2 or A2.shape[0] != M or A2.stride(1) != 1:
+            raise ValueError("gemm: A2 must be a row-contiguous [M, K2] matrix beside a 2-D A")
+        K = k1 + A2.shape[1]
     K2, N = B.shape[-2], B.shape[-1]
     if K != K2:
         raise ValueError(f"gemm: inner dims differ {tuple(A.shape)} @ {tuple(B.shape)}")
@@ -160,6 +171,14 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor = None, *, alpha=1.0,
         if colsum.numel() != N or not colsum.is_contiguous():
             raise ValueError("gemm: colsum must be a contiguous [N] tensor")
         d.colsum_out = _p(colsum)
+    if A2 is not None:
+        d.A2, d.a2_sm, d.k1 = _p(A2), A2.stride(0), k1
+    if C2 is not None:
+        _f32(C2, "C2")
+        if nd != 0 or C.dim() != 2 or C2.dim() != 2 or C2.stride(1) != 1 or C2.shape[0] != M or \
+                C.shape[1] + C2.shape[1] != N:
+            raise ValueError("gemm: C2 must be [M, N - N1] beside a 2-D C [M, N1]")
+        d.C2, d.c2_sm, d.n1 = _p(C2), C2.stride(0), C.shape[1]
     _with_ws(d, C.device)
     _launch_gemm(d, "sat_gemm")
     return C

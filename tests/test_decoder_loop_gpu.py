@@ -97,7 +97,7 @@ def test_decoder_loop_entries_match_python_orchestration(cuda, B, N, T):
     # ---- backward: fresh gradient outputs, same forward histories and dL/dh2
     fresh_b = {k: torch.full_like(lb[k], float("nan")) for k in ("DG1", "DG2")}
     fresh_c = {k: torch.full_like(ab[k], float("nan")) for k in
-               ("RD", "DG0", "DE1", "DE2", "DFH", "DQP", "DH0")}
+               ("DH0", "RD", "DG0", "DE1", "DE2", "DFH", "DQP")}
     db = _lib.SatDecoderLoopBwd()
     _fill(db.lstm, lb, fresh_b)
     _fill(db.attn, ab, fresh_c)

@@ -363,3 +363,54 @@ def test_gemm_skinny(cuda, M, N, K, act):
     ref = {None: pre, "relu": pre.clamp_min(0), "tanh": torch.tanh(pre)}[act] + add.double()
     bound = 2e-6 * (0.5 * (A.double().abs() @ B.double().abs()) + C0.double().abs() + 1) + 1e-6
     assert bool(((C.double().cpu() - ref).abs() <= bound).all())
+
+
+@pytest.mark.parametrize("M,N,K1,K2", [(16000, 1024, 256, 288), (300, 260, 64, 96),
+                                       (64, 64, 2048, 4096), (96, 160, 32, 2000)])
+@pytest.mark.parametrize("tb", [False, True])
+def test_gemm_two_a_segments(cuda, M, N, K1, K2, tb):
+    """SatGemmDesc.A2: C = [A | A2] B + bias as ONE reduction, A2 a strided column block of a
+    wider buffer (as LSTM1's context input inside REC0); long K exercises split-K chunks that
+    start inside the second segment."""
+    from sat_amd import kernels
+    g = torch.Generator().manual_seed(M + K2)
+    A = torch.randn(M, K1, generator=g)
+    wide = torch.randn(M, K2 + 40, generator=g)           # A2 = wide[:, :K2] (row stride K2+40)
+    B = torch.randn(N, K1 + K2, generator=g) if tb else torch.randn(K1 + K2, N, generator=g)
+    bias = torch.randn(N, generator=g)
+    Bd = B.to(cuda)
+    wd = wide.to(cuda)
+    C = kernels.gemm(A.to(cuda), Bd.t() if tb else Bd, bias=bias.to(cuda), A2=wd[:, :K2])
+    Al = torch.cat([A, wide[:, :K2]], 1).double()
+    Bl = (B.t() if tb else B).double()
+    ref = Al @ Bl + bias.double()
+    bound = 4e-7 * (Al.abs() @ Bl.abs() + bias.double().abs()) + 1e-7
+    assert bool(((C.double().cpu() - ref).abs() <= bound).all())
+
+
+def test_gemm_two_a_segments_rejects_unaligned_split(cuda):
+    from sat_amd import _lib, kernels
+    A = torch.randn(64, 48, device=cuda)                  # k1 = 48 is not a multiple of 32
+    with pytest.raises(_lib.SatLibraryError):
+        kernels.gemm(A, torch.randn(80, 64, device=cuda), A2=torch.randn(64, 32, device=cuda))
+
+
+@pytest.mark.parametrize("M,N1,N2,K", [(16000, 256, 288, 1024), (300, 128, 100, 64), (70, 256, 4, 2000)])
+@pytest.mark.parametrize("tb", [False, True])
+def test_gemm_two_c_segments(cuda, M, N1, N2, K, tb):
+    """SatGemmDesc.C2: the columns of ONE product split between two outputs (as dL/dh0' and the
+    context gradients inside RD); bits equal the two separate products'."""
+    from sat_amd import kernels
+    g = torch.Generator().manual_seed(M + N2)
+    A = torch.randn(M, K, generator=g).to(cuda)
+    B = torch.randn(N1 + N2, K, generator=g).to(cuda) if tb else \
+        torch.randn(K, N1 + N2, generator=g).to(cuda)
+    Bv = B.t() if tb else B
+    C = torch.empty(M, N1, device=cuda)
+    wide = torch.full((M, N2 + 40), 7.0, device=cuda)     # C2 = wide[:, :N2]
+    kernels.gemm(A, Bv, C, C2=wide[:, :N2])
+    ref = A.double().cpu() @ Bv.double().cpu()
+    full = torch.cat([C, wide[:, :N2]], 1).double().cpu()
+    bound = 4e-7 * (A.double().abs().cpu() @ Bv.double().abs().cpu()) + 1e-7
+    assert bool(((full - ref).abs() <= bound).all())
+    assert bool((wide[:, N2:] == 7.0).all())                # nothing written past C2's columns

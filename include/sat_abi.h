@@ -99,6 +99,12 @@ typedef struct SatGemmDesc {
   float* C2;
   int64_t c2_sm;
   int32_t n1, pad2;
+  /* optional second B segment: B's rows k >= k1 come from B2 (B's layout, stride b2_s along its
+   * non-contiguous dimension), i.e. C = A[:, :k1] B + A[:, k1:] B2 -- with A2 set too, A B + A2 B2:
+   * a sum of two products of different operands as ONE reduction.  Same constraints as A2.
+   * NULL = off. */
+  const float* B2;
+  int64_t b2_s;
 } SatGemmDesc;
 
 int sat_gemm(const SatGemmDesc* desc, void* stream);

@@ -51,6 +51,8 @@ class SatGemmDesc(ctypes.Structure):
         ("c2_sm", ctypes.c_int64),
         ("n1", ctypes.c_int32),
         ("pad2", ctypes.c_int32),
+        ("B2", ctypes.c_void_p),
+        ("b2_s", ctypes.c_int64),
     ]
 
 

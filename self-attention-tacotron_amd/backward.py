@@ -521,12 +521,14 @@ def encoder_bwd(P, G, hp, d, sv, dm1, dm2, lengths, masks, ws, aux: Aux = None):
         dt_pre = torch.empty_like(t)
         dx = torch.empty_like(x)
         K.highway_bwd(h, t, x, dy, dh_pre, dt_pre, dx)
-        lin_bwd(x, dh_pre, P[f"encoder/cbhg/highway{i}/H/kernel"],
-                G[f"encoder/cbhg/highway{i}/H/kernel"], G[f"encoder/cbhg/highway{i}/H/bias"], ws,
-                dx=dx, beta_dx=1.0, aux=aux)
-        lin_bwd(x, dt_pre, P[f"encoder/cbhg/highway{i}/T/kernel"],
-                G[f"encoder/cbhg/highway{i}/T/kernel"], G[f"encoder/cbhg/highway{i}/T/bias"], ws,
-                dx=dx, beta_dx=1.0, aux=aux)
+        sc = f"encoder/cbhg/highway{i}"
+        WH, WT = P[f"{sc}/H/kernel"], P[f"{sc}/T/kernel"]
+        lin_bwd(x, dh_pre, WH, G[f"{sc}/H/kernel"], G[f"{sc}/H/bias"], ws, need_dx=False, aux=aux)
+        lin_bwd(x, dt_pre, WT, G[f"{sc}/T/kernel"], G[f"{sc}/T/bias"], ws, need_dx=False, aux=aux)
+        # dx += dh_pre W_H^T + dt_pre W_T^T as ONE reduction (two-segment operands)
+        w_in = x.shape[-1]
+        K.gemm(dh_pre.reshape(-1, WH.shape[1]), WH.t(), dx.reshape(-1, w_in), beta=1.0,
+               A2=dt_pre.reshape(-1, WT.shape[1]), B2=WT.t())
         dy = dx
     if d.needs_adjust:
         dy = lin_bwd(sv["hw_in_adjust"], dy, P["encoder/cbhg/adjustment/kernel"],

@@ -58,6 +58,10 @@ struct GemmP {
   const float* A2 = nullptr;
   int64_t a2_sm = 0;
   int k1 = 0;
+  // second B segment (SatGemmDesc.B2): rows k >= k1 of B come from B2 (B_K: column stride b2_s,
+  // B_N: row stride b2_s), i.e. C = A[:, :k1] B + A[:, k1:] B2 (with A2: A B + A2 B2)
+  const float* B2 = nullptr;
+  int64_t b2_s = 0;
   // second C segment (SatGemmDesc.C2): output columns n >= n1 go to C2 (row stride c2_sm) at
   // column n - n1 (n1 a multiple of the tile width: the choice is per tile)
   float* C2 = nullptr;
@@ -720,6 +724,7 @@ __global__ void __launch_bounds__((64 * lds_waves<BM, BN>())) gemm_lds_kernel(Ge
   const bool amok = AKM ? true : (m0 + amq < p.M && !aones);
   const float* bptr[NB];
   int bi[NB];
+  int bcol[NB];                                        // B_K: the lane's (clamped) column per DMA
   const int bnq = BKM ? 0 : 4 * (lane % (BN / 4));
 #pragma unroll
   for (int i = 0; i < NB; ++i) {
@@ -727,10 +732,15 @@ __global__ void __launch_bounds__((64 * lds_waves<BM, BN>())) gemm_lds_kernel(Ge
       const int gn = n0 + (NWV * i + w) * 8 + (lane >> 3);
       bi[i] = gn < p.N;
       const int gc = min(gn, p.N - 1);
-      bptr[i] = (BMD == B_K) ? B + (int64_t)gc * p.b_sn + kbeg + kq : B + (int64_t)gc * p.b_C + kq;
+      bcol[i] = gc;
+      bptr[i] = (BMD == B_K) ? ((p.B2 && kbeg >= p.k1) ? p.B2 + (int64_t)gc * p.b2_s + (kbeg - p.k1) + kq
+                                                       : B + (int64_t)gc * p.b_sn + kbeg + kq)
+                             : B + (int64_t)gc * p.b_C + kq;
     } else {
+      bcol[i] = 0;
       bi[i] = kbeg + (NWV * i + w) * (256 / BN) + lane / (BN / 4);
-      bptr[i] = B + (int64_t)bi[i] * p.b_sk + n0 + bnq;
+      bptr[i] = (p.B2 && kbeg >= p.k1) ? p.B2 + (int64_t)(bi[i] - p.k1) * p.b2_s + n0 + bnq
+                                       : B + (int64_t)bi[i] * p.b_sk + n0 + bnq;
     }
   }
   const bool bnok = BKM ? true : (n0 + bnq < p.N);
@@ -790,6 +800,10 @@ __global__ void __launch_bounds__((64 * lds_waves<BM, BN>())) gemm_lds_kernel(Ge
       }
     }
     if constexpr (BMD == B_N) {
+      if (p.B2 && k0 == p.k1) {   // the reduction crosses into the second B segment
+#pragma unroll
+        for (int i = 0; i < NB; ++i) bptr[i] = p.B2 + (int64_t)(bi[i] - p.k1) * p.b2_s + n0 + bnq;
+      }
 #pragma unroll
       for (int i = 0; i < NB; ++i) {
         dma16((bnok && bi[i] < kend) ? bptr[i] : zero, lb + (NWV * i + w) * 1024);
@@ -798,6 +812,10 @@ __global__ void __launch_bounds__((64 * lds_waves<BM, BN>())) gemm_lds_kernel(Ge
       }
     } else if constexpr (BMD == B_K) {
       const bool kok = k0 + kq < kend;
+      if (p.B2 && k0 == p.k1) {
+#pragma unroll
+        for (int i = 0; i < NB; ++i) bptr[i] = p.B2 + (int64_t)bcol[i] * p.b2_s + kq;
+      }
 #pragma unroll
       for (int i = 0; i < NB; ++i) {
         dma16((bi[i] && kok) ? bptr[i] : zero, lb + (NWV * i + w) * 1024);
@@ -1297,21 +1315,23 @@ extern "C" int sat_gemm(const SatGemmDesc* d, void* stream) {
                   "n1 %% 128 == 0");
     p.C2 = d->C2; p.c2_sm = d->c2_sm; p.n1 = d->n1;
   }
-  if (d->A2 || d->C2) {
-    if (!d->A2) {
-      const int r = launch_lds(d, p, nb, s);
-      SAT_CHECK_ARG(r != 1, "sat_gemm: C2 operands are not vector-loadable");
-      return r;
+  if (d->A2 || d->B2 || d->C2) {
+    if (d->A2 || d->B2) {
+      // two reduction segments: A2 (dense K-contiguous A) and / or B2 (dense B, B's layout)
+      SAT_CHECK_ARG(nb == 1 && d->a_mode == 0 && d->b_mode == 0 && !d->colsum_out && d->k1 > 0 &&
+                        d->k1 < d->K && d->k1 % BK == 0 && gemm_lds_enabled() && !t_probe,
+                    "sat_gemm: A2 / B2 need a batch-1 dense product, 0 < k1 < K, k1 %% 32 == 0, "
+                    "no colsum_out");
+      SAT_CHECK_ARG(!d->A2 || (d->a_sk == 1 && aligned16(d->A2) && d->a2_sm % 4 == 0),
+                    "sat_gemm: A2 needs K-contiguous A and 16-byte aligned A2 rows");
+      SAT_CHECK_ARG(!d->B2 || (aligned16(d->B2) && d->b2_s % 4 == 0 &&
+                               (d->b_sn == 1 || d->b_sk == 1)),
+                    "sat_gemm: B2 needs 16-byte aligned rows / columns");
+      p.A2 = d->A2; p.a2_sm = d->a2_sm; p.k1 = d->k1;
+      p.B2 = d->B2; p.b2_s = d->b2_s;
     }
-    // two A segments over one B: only the LDS kernel's dense K-contiguous A loader takes them
-    SAT_CHECK_ARG(nb == 1 && d->a_mode == 0 && d->a_sk == 1 && d->b_mode == 0 && !d->colsum_out &&
-                      d->k1 > 0 && d->k1 < d->K && d->k1 % BK == 0 && aligned16(d->A2) &&
-                      d->a2_sm % 4 == 0 && gemm_lds_enabled() && !t_probe,
-                  "sat_gemm: A2 needs a batch-1 dense product with K-contiguous A, k1 %% 32 == 0, "
-                  "16-byte aligned rows, no colsum_out");
-    p.A2 = d->A2; p.a2_sm = d->a2_sm; p.k1 = d->k1;
     const int r = launch_lds(d, p, nb, s);
-    SAT_CHECK_ARG(r != 1, "sat_gemm: A2 operands are not vector-loadable");
+    SAT_CHECK_ARG(r != 1, "sat_gemm: segmented operands are not vector-loadable");
     return r;
   }
   if (d->colsum_out) {

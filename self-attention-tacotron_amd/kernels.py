@@ -107,13 +107,16 @@ def _bstrides(t, nd):
 
 
 def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor = None, *, alpha=1.0, beta=0.0,
-         bias=None, act=None, mul=None, add=None, colsum=None, A2=None, C2=None) -> torch.Tensor:
+         bias=None, act=None, mul=None, add=None, colsum=None, A2=None, C2=None,
+         B2=None) -> torch.Tensor:
     """C = act(alpha * A @ B + beta * C + bias) * mul + add.
 
     ``A2`` [M, K2] (2-D, row-contiguous like A): A is the two column blocks [A | A2] of one
     reduction over B [K1 + K2, N] (SatGemmDesc.A2: two inputs of a layer in different buffers).
     ``C2`` [M, N - N1] (2-D, unit column stride): the product's columns split between C [M, N1]
     and C2 (SatGemmDesc.C2: two outputs of one A over the column blocks of one B).
+    ``B2`` [K2, N] (B's layout): B is the two row blocks [B ; B2] of one reduction; with ``A2``
+    the launch computes A B + A2 B2 (SatGemmDesc.B2).
 
     ``colsum`` [N] (2-D, plain products only): also colsum = alpha * sum over rows of B + beta *
     colsum in the same launch (a dense layer's bias gradient next to its weight gradient).
@@ -130,6 +133,13 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor = None, *, alpha=1.0,
             raise ValueError("gemm: A2 must be a row-contiguous [M, K2] matrix beside a 2-D A")
         K = k1 + A2.shape[1]
     K2, N = B.shape[-2], B.shape[-1]
+    if B2 is not None:
+        _f32(B2, "B2")
+        if (B.dim() != 2 or B2.dim() != 2 or B2.shape[1] != N or
+                (B.stride(1) == 1) != (B2.stride(1) == 1) or (A2 is not None and K2 != k1)):
+            raise ValueError("gemm: B2 must be a [K2, N] matrix in B's layout beside B [k1, N]")
+        k1 = K2
+        K2 += B2.shape[0]
     if K != K2:
         raise ValueError(f"gemm: inner dims differ {tuple(A.shape)} @ {tuple(B.shape)}")
     lead = A.shape[:-2] if A.dim() >= B.dim() else B.shape[:-2]
@@ -173,6 +183,9 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor = None, *, alpha=1.0,
         d.colsum_out = _p(colsum)
     if A2 is not None:
         d.A2, d.a2_sm, d.k1 = _p(A2), A2.stride(0), k1
+    if B2 is not None:
+        d.B2, d.k1 = _p(B2), k1
+        d.b2_s = B2.stride(0) if B2.stride(1) == 1 else B2.stride(1)
     if C2 is not None:
         _f32(C2, "C2")
         if nd != 0 or C.dim() != 2 or C2.dim() != 2 or C2.stride(1) != 1 or C2.shape[0] != M or \

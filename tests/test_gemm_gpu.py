@@ -414,3 +414,29 @@ def test_gemm_two_c_segments(cuda, M, N1, N2, K, tb):
     bound = 4e-7 * (A.double().abs().cpu() @ Bv.double().abs().cpu()) + 1e-7
     assert bool(((full - ref).abs() <= bound).all())
     assert bool((wide[:, N2:] == 7.0).all())                # nothing written past C2's columns
+
+
+@pytest.mark.parametrize("M,N,K1,K2", [(6400, 128, 128, 128), (300, 260, 64, 96), (64, 64, 2048, 4096)])
+@pytest.mark.parametrize("tb", [False, True])
+@pytest.mark.parametrize("with_a2", [False, True])
+def test_gemm_two_b_segments(cuda, M, N, K1, K2, tb, with_a2):
+    """SatGemmDesc.B2 (+ A2): C = beta C + A B + A2 B2 as ONE reduction over two separately
+    stored operand pairs (as the highway layer's dx += dh W_H^T + dt W_T^T)."""
+    from sat_amd import kernels
+    g = torch.Generator().manual_seed(M + K2 + 2 * tb + with_a2)
+    A = torch.randn(M, K1, generator=g)
+    A2 = torch.randn(M, K2, generator=g)
+    Bs = [torch.randn(N, k, generator=g) if tb else torch.randn(k, N, generator=g) for k in (K1, K2)]
+    C0 = torch.randn(M, N, generator=g)
+    Bd = [b.to(cuda) for b in Bs]
+    Bv = [b.t() if tb else b for b in Bd]
+    C = C0.to(cuda)
+    if with_a2:
+        kernels.gemm(A.to(cuda), Bv[0], C, beta=1.0, A2=A2.to(cuda), B2=Bv[1])
+    else:
+        kernels.gemm(torch.cat([A, A2], 1).to(cuda), Bv[0], C, beta=1.0, B2=Bv[1])
+    Bl = [(b.t() if tb else b).double() for b in Bs]
+    ref = C0.double() + A.double() @ Bl[0] + A2.double() @ Bl[1]
+    bound = 4e-7 * (C0.double().abs() + A.double().abs() @ Bl[0].abs() +
+                    A2.double().abs() @ Bl[1].abs()) + 1e-7
+    assert bool(((C.double().cpu() - ref).abs() <= bound).all())

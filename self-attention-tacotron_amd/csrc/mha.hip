@@ -192,10 +192,23 @@ extern "C" int sat_mha_bwd(const SatMha* d, void* stream) {
                     s));
   // input projections
   SAT_TRY(wgrad(d->x, Wi, dQ, D, d->dWq, d->dbq));
-  SAT_TRY(dgrad(dQ, D, d->Wq, Wi, d->dx, 0.f));
   SAT_TRY(wgrad(d->x, Wi, dK, D, d->dWk, d->dbk));
-  SAT_TRY(dgrad(dK, D, d->Wk, Wi, d->dx, 1.f));
   SAT_TRY(wgrad(d->x, Wi, dV, D, d->dWv, d->dbv));
+  if (D % 32 == 0 && aligned16(d->Wq) && aligned16(d->Wk) && aligned16(dQ) && aligned16(dK)) {
+    // dx = dQ Wq^T + dK Wk^T as ONE reduction (two-segment operands), then += dV Wv^T
+    SatGemmDesc g = dense_desc();
+    g.M = R; g.N = Wi; g.K = 2 * D;
+    g.A = dQ; g.a_sm = D; g.a_sk = 1;
+    g.A2 = dK; g.a2_sm = D; g.k1 = D;
+    g.B = d->Wq; g.b_sk = 1; g.b_sn = D;
+    g.B2 = d->Wk; g.b2_s = D;
+    g.C = d->dx; g.c_sm = Wi; g.beta = 0.f;
+    g.ws = d->gemm_ws; g.ws_bytes = d->gemm_ws_bytes;
+    SAT_TRY(sat_gemm(&g, s));
+  } else {
+    SAT_TRY(dgrad(dQ, D, d->Wq, Wi, d->dx, 0.f));
+    SAT_TRY(dgrad(dK, D, d->Wk, Wi, d->dx, 1.f));
+  }
   SAT_TRY(dgrad(dV, D, d->Wv, Wi, d->dx, 1.f));
   return SAT_OK;
 }

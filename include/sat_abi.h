@@ -88,8 +88,8 @@ typedef struct SatGemmDesc {
   float* colsum_out;
   /* optional second A segment: A's columns k >= k1 come from A2 (row stride a2_sm), i.e.
    * C = A[:, :k1] B[:k1] + A2 B[k1:] as ONE reduction (two inputs of one layer that live in
-   * different buffers); batch-1 dense product with K-contiguous A, k1 % 32 == 0, 16-byte aligned
-   * rows, no colsum_out.  NULL = off. */
+   * different buffers); dense product with K-contiguous A, k1 % 32 == 0, 16-byte aligned rows,
+   * no colsum_out; a batched product offsets A2 by A's batch strides.  NULL = off. */
   const float* A2;
   int64_t a2_sm;
   int32_t k1, pad1;
@@ -101,8 +101,8 @@ typedef struct SatGemmDesc {
   int32_t n1, pad2;
   /* optional second B segment: B's rows k >= k1 come from B2 (B's layout, stride b2_s along its
    * non-contiguous dimension), i.e. C = A[:, :k1] B + A[:, k1:] B2 -- with A2 set too, A B + A2 B2:
-   * a sum of two products of different operands as ONE reduction.  Same constraints as A2.
-   * NULL = off. */
+   * a sum of two products of different operands as ONE reduction.  Same constraints as A2 (B2
+   * offset by B's batch strides).  NULL = off. */
   const float* B2;
   int64_t b2_s;
 } SatGemmDesc;

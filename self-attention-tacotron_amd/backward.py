@@ -491,9 +491,8 @@ def encoder_bwd(P, G, hp, d, sv, dm1, dm2, lengths, masks, ws, aux: Aux = None):
     else:
         for i in range(N):
             K.lstm_steps_bwd([enc_bwd_desc("fw", False, N - 1 - i), enc_bwd_desc("bw", True, i)])
-    for i, (dr, rev) in enumerate(dirs):
+    for dr, rev in dirs:
         st = sv["enc_lstm"][dr]
-        Wk = P[f"encoder/cbhg/lstm_{dr}/kernel"]
         dWk = G[f"encoder/cbhg/lstm_{dr}/kernel"]
         DG = DGs[dr]
         DGf = DG.view(N * B, 4 * U)
@@ -510,8 +509,11 @@ def encoder_bwd(P, G, hp, d, sv, dm1, dm2, lengths, masks, ws, aux: Aux = None):
             aux.run(wgrad, hprev, DGf, hw)
         else:
             wgrad()
-        # dhw[b, n, :] (+)= DG[n, b, :] @ Wx^T  -- batched over n, written transposed
-        K.gemm(DG, Wk[:Win].t(), dhw.transpose(0, 1), beta=1.0 if i else 0.0)
+    # dhw[b, n, :] = DG_fw[n, b, :] @ Wx_fw^T + DG_bw[n, b, :] @ Wx_bw^T -- batched over n,
+    # written transposed, both directions as the two segments of ONE reduction
+    (dr0, _), (dr1, _) = dirs
+    K.gemm(DGs[dr0], P[f"encoder/cbhg/lstm_{dr0}/kernel"][:Win].t(), dhw.transpose(0, 1),
+           A2=DGs[dr1], B2=P[f"encoder/cbhg/lstm_{dr1}/kernel"][:Win].t())
     # highway stack
     dy = dhw
     for i in reversed(range(d.num_highway)):

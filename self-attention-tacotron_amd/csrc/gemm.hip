@@ -663,6 +663,9 @@ __global__ void __launch_bounds__((64 * lds_waves<BM, BN>())) gemm_lds_kernel(Ge
   const int m0 = ty * BM, n0 = tx * BN;
   const float* A = p.A + bz * p.a_sbatch + bz2 * p.a_sbatch2;
   const float* B = p.B + bz * p.b_sbatch + bz2 * p.b_sbatch2;
+  // second reduction segments (A2 / B2) share their operand's batch strides
+  const float* A2 = p.A2 ? p.A2 + bz * p.a_sbatch + bz2 * p.a_sbatch2 : nullptr;
+  const float* B2 = p.B2 ? p.B2 + bz * p.b_sbatch + bz2 * p.b_sbatch2 : nullptr;
   int Kt = p.K, shift = p.a_shift, atap = 0, ac0 = 0;
   if constexpr (GRP == 1) {
     const int g = n0 / p.grp_co, t = g + 1;
@@ -705,7 +708,7 @@ __global__ void __launch_bounds__((64 * lds_waves<BM, BN>())) gemm_lds_kernel(Ge
       aone[i] = p.cs_out != nullptr && gm == p.m_real;
       ai[i] = gm < p.M && !aone[i];
       arow[i] = min(gm, (p.cs_out ? p.m_real : p.M) - 1);
-      aptr[i] = (p.A2 && kbeg >= p.k1) ? p.A2 + (int64_t)arow[i] * p.a2_sm + (kbeg - p.k1) + kq
+      aptr[i] = (A2 && kbeg >= p.k1) ? A2 + (int64_t)arow[i] * p.a2_sm + (kbeg - p.k1) + kq
                                        : A + (int64_t)arow[i] * p.a_sm + kbeg + kq;
     } else if constexpr (AM == A_IM2COL) {   // (utterance, position) of the output row
       const int gm = m0 + (NWV * i + w) * 8 + (lane >> 3);
@@ -733,13 +736,13 @@ __global__ void __launch_bounds__((64 * lds_waves<BM, BN>())) gemm_lds_kernel(Ge
       bi[i] = gn < p.N;
       const int gc = min(gn, p.N - 1);
       bcol[i] = gc;
-      bptr[i] = (BMD == B_K) ? ((p.B2 && kbeg >= p.k1) ? p.B2 + (int64_t)gc * p.b2_s + (kbeg - p.k1) + kq
+      bptr[i] = (BMD == B_K) ? ((B2 && kbeg >= p.k1) ? B2 + (int64_t)gc * p.b2_s + (kbeg - p.k1) + kq
                                                        : B + (int64_t)gc * p.b_sn + kbeg + kq)
                              : B + (int64_t)gc * p.b_C + kq;
     } else {
       bcol[i] = 0;
       bi[i] = kbeg + (NWV * i + w) * (256 / BN) + lane / (BN / 4);
-      bptr[i] = (p.B2 && kbeg >= p.k1) ? p.B2 + (int64_t)(bi[i] - p.k1) * p.b2_s + n0 + bnq
+      bptr[i] = (B2 && kbeg >= p.k1) ? B2 + (int64_t)(bi[i] - p.k1) * p.b2_s + n0 + bnq
                                        : B + (int64_t)bi[i] * p.b_sk + n0 + bnq;
     }
   }
@@ -752,9 +755,9 @@ __global__ void __launch_bounds__((64 * lds_waves<BM, BN>())) gemm_lds_kernel(Ge
     const uint32_t lb = la + A_SZ * 4;
     if constexpr (AM == A_K) {
       const bool kok = k0 + kq < kend;
-      if (p.A2 && k0 == p.k1) {   // the reduction crosses into the second A segment
+      if (A2 && k0 == p.k1) {   // the reduction crosses into the second A segment
 #pragma unroll
-        for (int i = 0; i < NA; ++i) aptr[i] = p.A2 + (int64_t)arow[i] * p.a2_sm + kq;
+        for (int i = 0; i < NA; ++i) aptr[i] = A2 + (int64_t)arow[i] * p.a2_sm + kq;
       }
 #pragma unroll
       for (int i = 0; i < NA; ++i) {
@@ -800,9 +803,9 @@ __global__ void __launch_bounds__((64 * lds_waves<BM, BN>())) gemm_lds_kernel(Ge
       }
     }
     if constexpr (BMD == B_N) {
-      if (p.B2 && k0 == p.k1) {   // the reduction crosses into the second B segment
+      if (B2 && k0 == p.k1) {   // the reduction crosses into the second B segment
 #pragma unroll
-        for (int i = 0; i < NB; ++i) bptr[i] = p.B2 + (int64_t)(bi[i] - p.k1) * p.b2_s + n0 + bnq;
+        for (int i = 0; i < NB; ++i) bptr[i] = B2 + (int64_t)(bi[i] - p.k1) * p.b2_s + n0 + bnq;
       }
 #pragma unroll
       for (int i = 0; i < NB; ++i) {
@@ -812,9 +815,9 @@ __global__ void __launch_bounds__((64 * lds_waves<BM, BN>())) gemm_lds_kernel(Ge
       }
     } else if constexpr (BMD == B_K) {
       const bool kok = k0 + kq < kend;
-      if (p.B2 && k0 == p.k1) {
+      if (B2 && k0 == p.k1) {
 #pragma unroll
-        for (int i = 0; i < NB; ++i) bptr[i] = p.B2 + (int64_t)bcol[i] * p.b2_s + kq;
+        for (int i = 0; i < NB; ++i) bptr[i] = B2 + (int64_t)bcol[i] * p.b2_s + kq;
       }
 #pragma unroll
       for (int i = 0; i < NB; ++i) {
@@ -1318,9 +1321,9 @@ extern "C" int sat_gemm(const SatGemmDesc* d, void* stream) {
   if (d->A2 || d->B2 || d->C2) {
     if (d->A2 || d->B2) {
       // two reduction segments: A2 (dense K-contiguous A) and / or B2 (dense B, B's layout)
-      SAT_CHECK_ARG(nb == 1 && d->a_mode == 0 && d->b_mode == 0 && !d->colsum_out && d->k1 > 0 &&
+      SAT_CHECK_ARG(d->a_mode == 0 && d->b_mode == 0 && !d->colsum_out && d->k1 > 0 &&
                         d->k1 < d->K && d->k1 % BK == 0 && gemm_lds_enabled() && !t_probe,
-                    "sat_gemm: A2 / B2 need a batch-1 dense product, 0 < k1 < K, k1 %% 32 == 0, "
+                    "sat_gemm: A2 / B2 need a dense product, 0 < k1 < K, k1 %% 32 == 0, "
                     "no colsum_out");
       SAT_CHECK_ARG(!d->A2 || (d->a_sk == 1 && aligned16(d->A2) && d->a2_sm % 4 == 0),
                     "sat_gemm: A2 needs K-contiguous A and 16-byte aligned A2 rows");

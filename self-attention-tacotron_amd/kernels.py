@@ -129,15 +129,19 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor = None, *, alpha=1.0,
     k1 = K
     if A2 is not None:
         _f32(A2, "A2")
-        if A.dim() != 2 or A2.dim() != 2 or A2.shape[0] != M or A2.stride(1) != 1:
-            raise ValueError("gemm: A2 must be a row-contiguous [M, K2] matrix beside a 2-D A")
-        K = k1 + A2.shape[1]
+        if (A2.shape[:-1] != A.shape[:-1] or A2.stride(-1) != 1 or
+                A2.stride()[:-2] != A.stride()[:-2]):
+            raise ValueError("gemm: A2 must be [.., M, K2] with A's batch shape and strides and "
+                             "unit column stride")
+        K = k1 + A2.shape[-1]
     K2, N = B.shape[-2], B.shape[-1]
     if B2 is not None:
         _f32(B2, "B2")
-        if (B.dim() != 2 or B2.dim() != 2 or B2.shape[1] != N or
-                (B.stride(1) == 1) != (B2.stride(1) == 1) or (A2 is not None and K2 != k1)):
-            raise ValueError("gemm: B2 must be a [K2, N] matrix in B's layout beside B [k1, N]")
+        if (B2.shape[:-2] != B.shape[:-2] or B2.shape[-1] != N or
+                B2.stride()[:-2] != B.stride()[:-2] or
+                (B.stride(-1) == 1) != (B2.stride(-1) == 1) or (A2 is not None and K2 != k1)):
+            raise ValueError("gemm: B2 must be [.., K2, N] in B's layout and batch strides, "
+                             "beside B [.., k1, N]")
         k1 = K2
         K2 += B2.shape[0]
     if K != K2:
@@ -182,10 +186,10 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor = None, *, alpha=1.0,
             raise ValueError("gemm: colsum must be a contiguous [N] tensor")
         d.colsum_out = _p(colsum)
     if A2 is not None:
-        d.A2, d.a2_sm, d.k1 = _p(A2), A2.stride(0), k1
+        d.A2, d.a2_sm, d.k1 = _p(A2), A2.stride(-2), k1
     if B2 is not None:
         d.B2, d.k1 = _p(B2), k1
-        d.b2_s = B2.stride(0) if B2.stride(1) == 1 else B2.stride(1)
+        d.b2_s = B2.stride(-2) if B2.stride(-1) == 1 else B2.stride(-1)
     if C2 is not None:
         _f32(C2, "C2")
         if nd != 0 or C.dim() != 2 or C2.dim() != 2 or C2.stride(1) != 1 or C2.shape[0] != M or \

@@ -440,3 +440,21 @@ def test_gemm_two_b_segments(cuda, M, N, K1, K2, tb, with_a2):
     bound = 4e-7 * (C0.double().abs() + A.double().abs() @ Bl[0].abs() +
                     A2.double().abs() @ Bl[1].abs()) + 1e-7
     assert bool(((C.double().cpu() - ref).abs() <= bound).all())
+
+
+def test_gemm_two_segments_batched(cuda):
+    """A2 / B2 on a batched product (the encoder BiLSTM's input gradient: per position n,
+    dhw[:, n] = DG_fw[n] Wx_fw^T + DG_bw[n] Wx_bw^T, written transposed)."""
+    from sat_amd import kernels
+    g = torch.Generator().manual_seed(11)
+    N, B, G4, Win = 37, 6, 512, 128
+    DG = [torch.randn(N, B, G4, generator=g) for _ in range(2)]
+    W = [torch.randn(Win + 64, G4, generator=g) for _ in range(2)]   # [Win + U, 4U] kernels
+    out = torch.full((B, N, Win), float("nan"), device=cuda)
+    Wd = [w.to(cuda) for w in W]
+    kernels.gemm(DG[0].to(cuda), Wd[0][:Win].t(), out.transpose(0, 1), A2=DG[1].to(cuda),
+                 B2=Wd[1][:Win].t())
+    ref = sum((DG[i].double() @ W[i][:Win].double().t()).transpose(0, 1) for i in range(2))
+    bound = 4e-7 * sum((DG[i].double().abs() @ W[i][:Win].double().abs().t()).transpose(0, 1)
+                       for i in range(2)) + 1e-7
+    assert bool(((out.double().cpu() - ref).abs() <= bound).all())

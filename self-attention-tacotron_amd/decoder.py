@@ -56,31 +56,47 @@ def teacher_inputs(targets: torch.Tensor, r: int, n_feed: int) -> torch.Tensor:
     return x
 
 
+def _state_shapes(d: Dims, Tp: int, B: int, N: int):
+    """zero-initialised state histories (row 0 = initial state) of the attention RNN and the
+    decoder LSTMs: REC0 [c1 | c2 | h0], C0, S1, AL1, c1, h1, c2, h2"""
+    A, Dd = d.att_rnn, d.dec
+    R0 = d.m1 + d.m2 + A
+    return ((Tp + 1, B, R0), (Tp + 1, B, A), (Tp + 1, B, N), (Tp + 1, B, N),
+            (Tp + 1, B, Dd), (Tp + 1, B, Dd), (Tp + 1, B, Dd), (Tp + 1, B, Dd))
+
+
 def decoder_inputs(P: Dict[str, torch.Tensor], hp, d: Dims, targets: torch.Tensor,
-                   masks: Optional[Dict[str, torch.Tensor]], aux) -> Dict[str, object]:
+                   masks: Optional[Dict[str, torch.Tensor]], aux,
+                   N: Optional[int] = None) -> Dict[str, object]:
     """The part of the teacher-forced decoder that reads only the targets (single speaker):
     teacher frames, the prenets (dropout fused) and the attention RNN's input projection of the
     prenet part.  Every output is allocated on the CURRENT stream, then the products run on the
     stream ``aux`` (forked from the current one); the caller joins ``aux`` before
-    decoder_forward(inputs=...) reads them."""
+    decoder_forward(inputs=...) reads them.  With ``N`` (encoder positions) the decoder's zeroed
+    state histories are made on ``aux`` too ("hist"), off the encoder's critical path."""
     r, nf = d.r, hp.n_feed_frame
     B, T, M = targets.shape
     Tp = T // r
     dev = targets.device
     mk = (lambda name: masks[name]) if masks is not None else (lambda name: None)
-    xin = torch.zeros(Tp, B, M * nf, device=dev, dtype=targets.dtype)
+    xin = torch.empty(Tp, B, M * nf, device=dev, dtype=targets.dtype)
     pres = [xin] + [torch.empty(Tp, B, w, device=dev) for w in d.dec_prenet]
     X0 = torch.empty(Tp, B, 4 * d.att_rnn, device=dev)
+    hist = K.empty_group(*_state_shapes(d, Tp, B, N), device=dev) if N is not None else None
     aux.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(aux):
+        if hist is not None:
+            hist[0].zero_()
+            hist[1][3][0, :, 0] = 1.0                    # AL1 row 0 (forward_attention.py:131-133)
         g = targets.view(B, Tp, M * r)
+        xin[0].zero_()                                   # the go frame
         xin[1:].copy_(g[:, :-1, M * (r - nf):].transpose(0, 1))
         for i in range(len(d.dec_prenet)):
             K.linear(pres[i], P[f"decoder/prenet{i}/kernel"], P[f"decoder/prenet{i}/bias"],
                      act="relu", mul=mk(f"dec/prenet{i}"), out=pres[i + 1])
         W0 = P["decoder/attention_lstm/kernel"]
         K.linear(pres[-1], W0[:pres[-1].shape[-1]], P["decoder/attention_lstm/bias"], out=X0)
-    return {"xin": xin, "pres": pres, "X0": X0}
+    return {"xin": xin, "pres": pres, "X0": X0, "hist": None if hist is None else hist[1]}
 
 
 def persistent_eligible(d: Dims, B: int, N: int, attn_tile: int = 32) -> bool:
@@ -162,13 +178,16 @@ def decoder_forward(P: Dict[str, torch.Tensor], hp, d: Dims, m1: torch.Tensor, m
     R0 = M1 + M2 + A                                 # recurrent input [c1 | c2 | h0]
     # zero-initialised state histories (row 0 = initial state), one fill for all of them and
     # for the decoder LSTMs' c / h histories below
-    REC0, C0, S1, AL1, c1z, h1z, c2z, h2z = K.zeros_group(
-        (Tp + 1, B, R0), (Tp + 1, B, A), (Tp + 1, B, N), (Tp + 1, B, N),
-        (Tp + 1, B, Dd), (Tp + 1, B, Dd), (Tp + 1, B, Dd), (Tp + 1, B, Dd), device=dev)
+    hist = inputs.get("hist") if inputs is not None else None
+    if hist is not None and tuple(hist[2].shape) == (Tp + 1, B, N):
+        REC0, C0, S1, AL1, c1z, h1z, c2z, h2z = hist      # zeroed on the inputs' side stream
+    else:
+        REC0, C0, S1, AL1, c1z, h1z, c2z, h2z = K.zeros_group(*_state_shapes(d, Tp, B, N),
+                                                              device=dev)
+        AL1[0, :, 0] = 1.0                           # forward_attention.py:131-133
     H0RAW = torch.empty(Tp, B, A, **f32)
     G0 = torch.empty(Tp, B, 4 * A, **f32)
     Q = torch.empty(Tp, B, D1 + D2, **f32)
-    AL1[0, :, 0] = 1.0                               # forward_attention.py:131-133
     S2 = torch.empty(Tp, B, N, **f32)
     ST = torch.empty(Tp, B, 4, **f32)
     # location features f_t of every step (forward attention): the backward's parameter-gradient
@@ -186,9 +205,16 @@ def decoder_forward(P: Dict[str, torch.Tensor], hp, d: Dims, m1: torch.Tensor, m
     Wr0 = W0[p_w:]
     # query layers of both mechanisms, transposed once per step so the per-decoder-step query
     # product is a skinny row-dot ([B, A] x [D1+D2, A]^T)
-    QT = torch.empty(D1 + D2, A, **f32)
-    K.transpose(P[f"{a1}/query_layer/kernel"], QT[:D1])
-    K.transpose(P["decoder/attention2/query_layer/kernel"], QT[D1:])
+    # (made on first use: the persistent path reads the kernels directly)
+    qt_box = []
+
+    def query_t():
+        if not qt_box:
+            QT = torch.empty(D1 + D2, A, **f32)
+            K.transpose(P[f"{a1}/query_layer/kernel"], QT[:D1])
+            K.transpose(P["decoder/attention2/query_layer/kernel"], QT[D1:])
+            qt_box.append(QT)
+        return qt_box[0]
     zc0, zh0 = mk("dec/lstm0/zc"), mk("dec/lstm0/zh")
 
     def lstm0_desc(t):
@@ -198,7 +224,7 @@ def decoder_forward(P: Dict[str, torch.Tensor], hp, d: Dims, m1: torch.Tensor, m
                     c_out=C0[t + 1], h_out=REC0[t + 1, :, M1 + M2:], gates=G0[t])
 
     def attention_rest(t):
-        K.rowdot(H0RAW[t], QT, Q[t])
+        K.rowdot(H0RAW[t], query_t(), Q[t])
         K.attn_step_fwd(
             B=B, N=N, D1=D1, M1=M1, D2=D2, M2=M2, F=d.loc_f, KW=d.loc_k, NT=attn_tile,
             ntiles=ntiles, att1_forward=att1_fwd, u=0.5, q=Q[t], q_sb=D1 + D2,

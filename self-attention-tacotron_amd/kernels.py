@@ -345,6 +345,19 @@ def stop_check(stop: torch.Tensor, t: int, min_iters: int, state: torch.Tensor):
               _p(state), _stream())
 
 
+def empty_group(*shapes, device):
+    """zeros_group's carving without the fill: (buffer, pieces); the caller zeroes ``buffer``
+    (e.g. on a side stream, off the critical path)."""
+    sizes = [int(torch.Size(sh).numel()) for sh in shapes]
+    pads = [(n + 63) // 64 * 64 for n in sizes]
+    buf = torch.empty(sum(pads), device=device, dtype=torch.float32)
+    out, off = [], 0
+    for sh, n, pn in zip(shapes, sizes, pads):
+        out.append(buf[off:off + n].view(sh))
+        off += pn
+    return buf, out
+
+
 def zeros_group(*shapes, device):
     """Several zero-initialised float32 tensors carved from ONE zeroed buffer (one fill launch
     instead of one per tensor in the captured step); every piece starts on a 256-byte boundary

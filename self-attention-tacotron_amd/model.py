@@ -290,7 +290,8 @@ def model_forward(P, bn: BNState, hp, d: PR.Dims, batch: Dict[str, torch.Tensor]
         aux = K.aux_stream(ids.device)
 
         def fork():      # forked at the BiLSTM launch: it fills the CUs the BiLSTM leaves idle
-            dec_box[0] = decoder_inputs(P, hp, d, batch["mel"], masks, aux)
+            dec_box[0] = decoder_inputs(P, hp, d, batch["mel"], masks, aux,
+                                        N=batch["source"].shape[1])
     m1, m2 = encoder_fwd(P, bn, hp, d, ids, lengths, masks, training, ws, sv,
                          persistent=persistent, err=None if health is None else health[8:9],
                          before_lstm=fork)

@@ -1278,7 +1278,10 @@ extern "C" int sat_attn_param_grads(const SatAttnParamGrad* a, void* stream) {
   SAT_CHECK_ARG(a->D1 % 4 == 0 && a->D2 % 4 == 0 && a->D1 > 0 && a->D2 > 0 &&
                 (a->D1 + a->D2) / 4 <= 128, "sat_attn_param_grads: D1, D2 multiples of 4, D1+D2 <= 512");
   const int F = a->att1_forward ? a->F : 0, KW = a->att1_forward ? a->KW : 0;
-  SAT_CHECK_ARG(F == 0 || F == 5 || (F >= 1 && F <= 8), "sat_attn_param_grads: F <= 8");
+  // compiled variants: F = 0 (any width), F = 5 with D1 + D2 <= 256, F = 8 (the loc history's
+  // row stride is the template's F, so any other F would be read with the wrong stride)
+  SAT_CHECK_ARG(F == 0 || F == 8 || (F == 5 && (a->D1 + a->D2) <= 256),
+                "sat_attn_param_grads: location features F must be 0, 8 or 5 (D1 + D2 <= 256)");
   SAT_CHECK_ARG(KW * F + F <= 64, "sat_attn_param_grads: location conv needs KW*F + F <= 64");
   SAT_CHECK_ARG(a->pg_stride >= sat_attn_pg_stride(a->D1, a->D2, F, KW) && a->pg_stride <= 8192,
                 "sat_attn_param_grads: pg stride");

@@ -121,3 +121,16 @@ def test_workspace_size_is_the_sum_of_the_entry_queries():
         al(lib.sat_mha_scratch_bytes(B, Tp, 256, 4, 256)) + (32 << 20)
     assert lib.sat_workspace_size(ctypes.byref(d)) == want
     assert lib.sat_workspace_size(ctypes.byref(_lib.SatDims())) < 0
+
+
+def test_attn_param_grads_rejects_uncompiled_location_widths():
+    """F outside the compiled variants is refused before any device work (it used to be read
+    with the F = 8 variant's row stride)."""
+    if not _lib_built():
+        pytest.skip("libsat_hip.so not built")
+    lib = _lib.load()
+    d = _lib.SatAttnParamGrad()
+    d.T, d.B, d.N, d.D1, d.D2, d.F, d.KW, d.att1_forward = 4, 2, 9, 224, 32, 3, 10, 1
+    rc = lib.sat_attn_param_grads(ctypes.byref(d), None)
+    assert rc != 0
+    assert b"location features" in lib.sat_last_error_string()

@@ -9,7 +9,7 @@ step   : one full training step -- dropout/zoneout mask draw, forward (encoder, 
          random-init weights of the LJSpeech self-attention-tacotron.json architecture).
 value  : whole-job frames/s = n_gpus * B * T * steps / max-over-ranks wall time (weak scaling).
 
-Run:  python bench.py [--gpus N --steps K --warmup W]
+Run:  python bench.py [--gpus N --steps K --warmup W]   (N > 1: starts N ranks itself)
       torchrun --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
 Extra objects on the JSON line: ``roofline`` (the persistent decoder attention kernel, the
 step's dominant kernel, timed live with HIP events on the stream it runs on), ``cpu_baseline``
@@ -63,7 +63,64 @@ def parse():
     ap.add_argument("--attn-tile", type=int, default=32)
     ap.add_argument("--pipeline-chunk", type=int, default=40,
                     help="decoder steps per chunk of the multi-stream recurrence pipeline (0 = off)")
+    ap.add_argument("--plumbing", action="store_true",
+                    help="CPU-only launcher check (gloo): each rank times the per-step exchange "
+                         "of the real arena size instead of the training step (tests only)")
     return ap.parse_args()
+
+
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n: int) -> int:
+    """``bench.py --gpus N`` run without an outer launcher: start N rank processes through
+    torch.distributed.run (127.0.0.1 rendezvous) as a CHILD process -- this process has not
+    touched the GPU and never execs -- and return its exit code.  Rank 0 prints the one JSON
+    line (max-over-ranks timing); its stdout is this process's stdout."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={n}", "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+           os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "16")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def plumbing(args, world: int, rank: int) -> None:
+    """--plumbing: the launcher / rendezvous / max-over-ranks / JSON-line path on CPU (gloo).
+    Each rank runs the per-step exchange (dp.exchange) over an arena of the LJSpeech model's
+    exchange size; the line is labelled as such and is not a throughput of the training step."""
+    from sat_amd import dp, hparams, params
+    from sat_amd.model import BNState
+    hp = hparams.ljspeech_hparams()
+    n_p, n_bn = params.Layout(params.param_specs(hp)).num_params, BNState.numel(hp)
+    arena = torch.zeros(n_p + n_bn + 16)
+    health = torch.zeros(16, dtype=torch.int32)
+    ex = lambda: dp.exchange(arena, health, arena[n_p:n_p + n_bn], arena[n_p + n_bn:])  # noqa
+    for _ in range(args.warmup):
+        ex()
+    torch.distributed.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        ex()
+    torch.distributed.barrier()
+    dt = dp.max_over_ranks(time.perf_counter() - t0, "cpu")
+    if rank == 0:
+        print(json.dumps({
+            "metric": METRIC, "value": None, "unit": "frames/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * dt / args.steps, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+            "data": "plumbing: CPU gloo exchange of the model's arena only (no training step)",
+            "config": {"workload": "launcher check", "global_batch": args.batch * world,
+                       "per_gpu_batch": args.batch, "parallelism": f"dp{world}",
+                       "exchange_floats": int(arena.numel())}}), flush=True)
 
 
 class _Recorder:
@@ -248,9 +305,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world == 1 and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
     if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run")
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.plumbing:
+        torch.distributed.init_process_group("gloo")
+        plumbing(args, world, rank)
+        torch.distributed.destroy_process_group()
+        return
     torch.cuda.set_device(local)
     dist = world > 1
     if dist:

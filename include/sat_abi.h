@@ -779,6 +779,15 @@ int sat_adam_step(float* params, const float* grads, float* m, float* v, int64_t
                   const SatAdamConfig* cfg, const int32_t* health, int32_t n_health,
                   int32_t* status, void* stream);
 
+/* Data-parallel exchange (train.py:67,73 MirroredStrategy -> ONE SUM all-reduce per step over
+ * [gradients | BN moving statistics | health tail], sat_amd/dp.py).  pack: tail[i] =
+ * |float(health[i])| and bn *= bn_scale (1/world, so the SUM leaves the replicas' mean);
+ * unpack after the collective: health[i] = int(tail[i]) (non-zero iff some rank's word was;
+ * the code is exact when one rank failed). */
+int sat_exchange_pack(const int32_t* health, int32_t n_health, float* bn, int64_t n_bn,
+                      float* tail, float bn_scale, void* stream);
+int sat_exchange_unpack(const float* tail, int32_t n_health, int32_t* health, void* stream);
+
 /* ---------------------------------------------------------------- dataset records (host)
  * TFRecord framing of the dataset path: datasets/ljspeech/dataset.py:96-112 reads
  * tf.data.TFRecordDataset files written by preprocess/ljspeech.py:23-45 (utils/tfrecord.py:46-49).

@@ -241,6 +241,8 @@ SIGNATURES.update({
     "sat_global_norm_sq": [_P, _I64, _P, _P],
     "sat_adam_step": [_P, _P, _P, _P, _I64, _P, _P, _P, ctypes.POINTER(SatAdamConfig), _P, _I32,
                       _P, _P],
+    "sat_exchange_pack": [_P, _I32, _P, _I64, _P, _F, _P],
+    "sat_exchange_unpack": [_P, _I32, _P, _P],
 })
 
 RESTYPES = {"sat_workspace_colreduce": (ctypes.c_int64, [_I32, _I32]),

@@ -104,10 +104,50 @@ __global__ void __launch_bounds__(256) adam_update_kernel(float* __restrict__ p,
   }
 }
 
+// data-parallel exchange tail (dp.py): health words as floats (|code|: a SUM over ranks is
+// non-zero iff some rank's word was, and exact when one rank failed), BN moving statistics
+// pre-scaled by 1/world (the SUM then leaves their mean)
+__global__ void __launch_bounds__(256) exchange_pack_kernel(const int* __restrict__ health,
+                                                            int n_health, float* __restrict__ bn,
+                                                            int64_t n_bn, float* __restrict__ tail,
+                                                            float bn_scale) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i < n_health) tail[i] = fabsf((float)health[i]);
+  for (int64_t k = i; k < n_bn; k += (int64_t)gridDim.x * blockDim.x) bn[k] *= bn_scale;
+}
+
+__global__ void exchange_unpack_kernel(const float* __restrict__ tail, int n_health,
+                                       int* __restrict__ health) {
+  const int i = threadIdx.x;
+  if (i < n_health) health[i] = (int)fminf(tail[i], 2147483520.f);
+}
+
 }  // namespace
 }  // namespace sat
 
 using namespace sat;
+
+extern "C" int sat_exchange_pack(const int32_t* health, int32_t n_health, float* bn, int64_t n_bn,
+                                 float* tail, float bn_scale, void* stream) {
+  SAT_CHECK_ARG(n_health >= 0 && n_health <= 256 && n_bn >= 0 && (n_health == 0 || (health && tail)) &&
+                    (n_bn == 0 || bn),
+                "sat_exchange_pack: health 0..256 words (+ tail), bn >= 0 floats");
+  const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((n_bn + 255) / 256, 64));
+  hipLaunchKernelGGL(exchange_pack_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), health,
+                     n_health, bn, n_bn, tail, bn_scale);
+  SAT_LAUNCH_CHECK("sat_exchange_pack");
+  return SAT_OK;
+}
+
+extern "C" int sat_exchange_unpack(const float* tail, int32_t n_health, int32_t* health,
+                                   void* stream) {
+  SAT_CHECK_ARG(n_health >= 0 && n_health <= 256 && (n_health == 0 || (health && tail)),
+                "sat_exchange_unpack: health 0..256 words");
+  hipLaunchKernelGGL(exchange_unpack_kernel, dim3(1), dim3(256), 0, as_stream(stream), tail,
+                     n_health, health);
+  SAT_LAUNCH_CHECK("sat_exchange_unpack");
+  return SAT_OK;
+}
 
 // workspace: fp64 norm partials, then the skip word of the health guard
 extern "C" int64_t sat_workspace_adam(void) { return (int64_t)kNormBlocks * sizeof(double) + 16; }

@@ -44,26 +44,37 @@ def allreduce_grads(flat: torch.Tensor, group=None) -> None:
         tdist.all_reduce(flat, op=tdist.ReduceOp.SUM, group=group)
 
 
-def combine_health(words: torch.Tensor, group=None) -> None:
-    """MAX over replicas of the step's int32 health words, in place (before the optimiser).
+def exchange(arena: torch.Tensor, health: torch.Tensor, bn: torch.Tensor, tail: torch.Tensor,
+             group=None) -> None:
+    """A replica's whole per-step exchange as ONE SUM all-reduce over the contiguous arena
+    ``[gradients | bn | tail]`` (``bn`` and ``tail`` are views of it):
 
-    Each rank's persistent kernels raise their own error words (a hand-off timeout, an id out
-    of range).  The gradient all-reduce has already mixed a bad rank's gradients into every
-    replica, so the guarded Adam step must skip on EVERY rank or on none: with the words
-    combined, all ranks skip together and all raise on their next ``check_health`` (instead of
-    the healthy ranks applying the update and then blocking in the next collective)."""
-    if world_size(group) > 1:
-        tdist.all_reduce(words, op=tdist.ReduceOp.MAX, group=group)
+    * gradients: summed (the 1/world averaging is folded into Adam's ``grad_scale``);
+    * BatchNorm moving statistics: pre-scaled by 1/world, so the sum is the replicas' mean;
+    * health words: sent as |code| floats in ``tail`` and read back as ints, so a word is
+      non-zero on every rank iff it was on some rank (the guarded Adam step then skips on every
+      rank or on none) and the code is exact when one rank failed.
 
-
-def average_buffer(flat: torch.Tensor, group=None) -> None:
-    """Mean over replicas in place (BatchNorm moving statistics: the replicas' updates are
-    averaged each step so every rank holds the same EVAL / checkpoint state; TF1
-    MirroredStrategy's exact aggregation of BN moving averages is unpinned)."""
+    On device tensors the pack / unpack are the library's ``sat_exchange_pack/unpack``
+    launches; the host arithmetic below is the same restatement for the ``gloo`` CPU tests."""
     w = world_size(group)
-    if w > 1:
-        tdist.all_reduce(flat, op=tdist.ReduceOp.SUM, group=group)
-        flat.mul_(1.0 / w)
+    if w == 1:
+        return
+    if arena.is_cuda:
+        from . import _lib
+        from . import kernels as K
+        lib = _lib.load()
+        _lib.check(lib.sat_exchange_pack(health.data_ptr(), health.numel(), bn.data_ptr(),
+                                         bn.numel(), tail.data_ptr(), 1.0 / w, K._stream()),
+                   "sat_exchange_pack")
+        tdist.all_reduce(arena, op=tdist.ReduceOp.SUM, group=group)
+        _lib.check(lib.sat_exchange_unpack(tail.data_ptr(), health.numel(), health.data_ptr(),
+                                           K._stream()), "sat_exchange_unpack")
+        return
+    tail[:health.numel()].copy_(health.abs().float())
+    bn.mul_(1.0 / w)
+    tdist.all_reduce(arena, op=tdist.ReduceOp.SUM, group=group)
+    health.copy_(tail[:health.numel()].to(torch.int32))
 
 
 def max_over_ranks(value: float, device, group=None) -> float:

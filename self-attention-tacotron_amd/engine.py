@@ -29,10 +29,15 @@ class Tacotron:
         self.layout = PR.Layout(PR.param_specs(hp))
         vals = init_values if init_values is not None else PR.init_params(hp, seed)
         self.params = torch.tensor(self.layout.pack(vals)).to(self.device)
-        self.grads = torch.zeros_like(self.params)
+        # the data-parallel exchange arena: [gradients | BN moving statistics | health tail],
+        # so a replica's whole per-step exchange is ONE SUM all-reduce (dp.exchange)
+        n_p, n_bn = self.params.numel(), BNState.numel(hp)
+        self.exchange = torch.zeros(n_p + n_bn + self.N_HEALTH, device=self.device)
+        self.grads = self.exchange[:n_p]
         self.P = self.layout.views(self.params)
         self.G = self.layout.views(self.grads)
-        self.bn = BNState(hp, self.device)
+        self.bn = BNState(hp, self.device, storage=self.exchange[n_p:n_p + n_bn])
+        self.health_tail = self.exchange[n_p + n_bn:]
         self.ws = K.Workspace(self.device)
         self.attn_tile = attn_tile
         # wavefront schedule of the decoder recurrences (0 = layer by layer)
@@ -46,8 +51,9 @@ class Tacotron:
         # health arena: int32 error words of one step -- [0:2] attention chain fwd, [2:4] / [4:6]
         # decoder LSTM stack fwd / bwd, [6:8] attention chain bwd, [8] embedding id range,
         # [9] speaker-embedding id range; read on the device by the guarded Adam step
-        self.health = torch.zeros(16, dtype=torch.int32, device=self.device)
+        self.health = torch.zeros(self.N_HEALTH, dtype=torch.int32, device=self.device)
 
+    N_HEALTH = 16
     HEALTH_WORDS = {0: "sat_decoder_attention_fwd hand-off timeout",
                     2: "sat_decoder_lstms_fwd hand-off timeout",
                     4: "sat_decoder_lstms_bwd hand-off timeout",

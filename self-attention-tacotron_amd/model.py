@@ -26,7 +26,10 @@ class BNState:
     """Moving statistics of every BatchNormalization, two flat buffers (means, variances) laid
     out in ``params.bn_buffer_names`` order, so the 16 conv-bank BNs are one contiguous span."""
 
-    def __init__(self, hp, device):
+    def __init__(self, hp, device, storage: Optional[torch.Tensor] = None):
+        """``storage``: an optional flat float view of ``numel(hp)`` elements to live in (the
+        engine's data-parallel exchange arena, so the statistics ride in the gradient
+        all-reduce)."""
         self.names = PR.bn_buffer_names(hp)
         self.offsets = {}
         off = 0
@@ -34,10 +37,20 @@ class BNState:
             self.offsets[scope] = (off, ch)
             off += ch
         # one flat buffer [means | variances]: data-parallel replicas average it in ONE
-        # collective (dp.average_buffer)
-        self.buf = torch.cat([torch.zeros(off), torch.ones(off)]).to(device)
+        # collective (dp.exchange)
+        init = torch.cat([torch.zeros(off), torch.ones(off)])
+        if storage is None:
+            self.buf = init.to(device)
+        else:
+            assert storage.numel() == init.numel(), "BN storage size"
+            self.buf = storage
+            self.buf.copy_(init)
         self.mean = self.buf[:off]
         self.var = self.buf[off:]
+
+    @staticmethod
+    def numel(hp) -> int:
+        return 2 * sum(ch for _, ch in PR.bn_buffer_names(hp))
 
     def span(self, first_scope: str, count_ch: int):
         o, _ = self.offsets[first_scope]

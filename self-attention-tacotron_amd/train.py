@@ -102,14 +102,11 @@ class Trainer:
         return out
 
     def reduce_grads(self):
-        """The step's one gradient exchange (SUM; 1/world folded into Adam) plus the mean of
-        the BatchNorm moving statistics (a few KB) so replicas never drift apart, and the MAX
-        of the 16 health words so the guarded update is skipped on every rank or on none."""
-        dp.allreduce_grads(self.m.grads, self.pg)
-        dp.combine_health(self.m.health, self.pg)
-        bn = getattr(self.m, "bn", None)
-        if bn is not None and self.world > 1:
-            dp.average_buffer(bn.buf, self.pg)
+        """The step's ONE collective (dp.exchange): a SUM all-reduce of the engine's exchange
+        arena -- gradients (1/world folded into Adam), the BatchNorm moving statistics
+        (averaged, so replicas never drift apart) and the health words (non-zero everywhere iff
+        on some rank, so the guarded update is skipped on every rank or on none)."""
+        dp.exchange(self.m.exchange, self.m.health, self.m.bn.buf, self.m.health_tail, self.pg)
 
     def apply(self):
         """Guarded clip + Adam: skipped on the device when any health word of the step is set."""

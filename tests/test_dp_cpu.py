@@ -45,15 +45,27 @@ def _worker(rank, world, port, q):
         def local_bn(r):
             return torch.linspace(-1.0, 1.0, 64) * (r + 1) + 0.25 * r
 
+        # the engine's exchange arena layout: [gradients | BN statistics | health tail]
+        arena = torch.cat([local_grad(rank), local_bn(rank), torch.zeros(16)])
         model = types.SimpleNamespace(
-            hp=hp, device=torch.device("cpu"), params=torch.zeros(n),
-            grads=local_grad(rank).clone(),
+            hp=hp, device=torch.device("cpu"), params=torch.zeros(n), exchange=arena,
+            grads=arena[:n], health_tail=arena[n + 64:],
             health=torch.zeros(16, dtype=torch.int32),
-            bn=types.SimpleNamespace(buf=local_bn(rank).clone()))
+            bn=types.SimpleNamespace(buf=arena[n:n + 64]))
         if rank == 1:
-            model.health[3] = 1          # a hand-off timeout on rank 1 only
+            model.health[3] = 7          # a hand-off timeout on rank 1 only
         tr = train.Trainer(model, B=2, N=8, Tp=4)
+        calls = []
+        real = tdist.all_reduce
+
+        def counting(*a, **k):
+            calls.append(a[0].numel())
+            return real(*a, **k)
+
+        tdist.all_reduce = counting
         tr.reduce_grads()
+        tdist.all_reduce = real
+        res["collectives"] = calls
         gsum = sum(local_grad(r) for r in range(world))
         res["sum"] = bool(torch.equal(model.grads, gsum))
         res["scale"] = tr.cfg.grad_scale
@@ -111,7 +123,8 @@ def test_dp_world2_gloo():
         assert isinstance(res, dict), res
         assert res["bcast"] and res["sum"] and res["bn"] and res["replicas_equal"]
         assert res["matches_single"]
-        assert res["health"][3] == 1 and sum(res["health"]) == 1
+        assert res["health"][3] == 7 and sum(res["health"]) == 7
+        assert res["collectives"] == [4096 + 64 + 16]     # ONE collective per step
         assert res["seed_offset"] == 1000003 * r
         assert res["scale"] == pytest.approx(0.5) and res["world"] == 2
         assert res["max"] == pytest.approx(1.5)

@@ -102,7 +102,10 @@ typedef struct SatGemmDesc {
   /* optional second B segment: B's rows k >= k1 come from B2 (B's layout, stride b2_s along its
    * non-contiguous dimension), i.e. C = A[:, :k1] B + A[:, k1:] B2 -- with A2 set too, A B + A2 B2:
    * a sum of two products of different operands as ONE reduction.  Same constraints as A2 (B2
-   * offset by B's batch strides).  NULL = off. */
+   * offset by B's batch strides).  NULL = off.
+   * A2 / B2 outside those constraints (k1 % 32 != 0, SAT_GEMM_LDS=0, operands not vector-
+   * loadable): two accumulating launches instead (C = A[:, :k1] B[:k1] + beta C + bias + add,
+   * then C += the k >= k1 part), which needs a linear epilogue (no act / mul / C2). */
   const float* B2;
   int64_t b2_s;
 } SatGemmDesc;
@@ -452,11 +455,7 @@ int sat_attn_step_bwd(const SatAttnStepBwd* args, void* stream);
  * b*N + n).  Writes dK1 [B][N][D1], dK2 [B][N][D2] (overwritten) and one partial row per
  * workgroup, pg [sat_attn_param_grad_rows(B, N)][pg_stride] =
  * [dv1 D1 | dW_loc F*D1 | dconvW KW*F | dconvb F | dv2 D2] (F = KW = 0 when !att1_forward),
- * to be column-summed.
- * zh (optional): the forward's energy-tanh history [T][B][N][D1+D2] (SatDecAttnFwd.ZH).  Given,
- * zh_share of every 8 position workgroups read z from it instead of recomputing the energies
- * (HBM-bound vs VALU-bound work, co-resident on each CU); zh_share = 8 reads every z (as TF's
- * tanh gradient uses the forward's output), 0 recomputes every z. */
+ * to be column-summed. */
 typedef struct SatAttnParamGrad {
   int32_t T, B, N, D1, D2, F, KW, att1_forward;
   const float* K1; const float* K2;
@@ -468,8 +467,6 @@ typedef struct SatAttnParamGrad {
   const float* df;
   float* dK1; float* dK2;
   float* pg; int64_t pg_stride;
-  const float* zh;
-  int32_t zh_share, pad_zh;   /* with zh: workgroups of every 8 that read z (0..8), the rest recompute */
 } SatAttnParamGrad;
 
 int sat_attn_pg_stride(int32_t D1, int32_t D2, int32_t F, int32_t KW);

@@ -1104,146 +1104,12 @@ __device__ __forceinline__ void attn_pg_store(const SatAttnParamGrad& p, const f
   }
 }
 
-// The same pass reading z from the forward's energy-tanh history ZH [T][B][N][D1+D2] instead of
-// recomputing it (TF's tanh gradient also takes the forward's output): per (t, position) one
-// coalesced 1-KB row of ZH per wave, the step scalars de1 / de2 / f_t[n] wave-uniform, and
-//   dp = (e v) (1 - z^2),  dK += dp,  dv += e z,  dW_loc[f] += f_t[n][f] dp
-// on dimension pairs (packed fp32 FMAs).  No transcendental and no query / key reads: the pass
-// streams ZH once (B N D T' floats) and is HBM-bound instead of VALU-bound.  The per-lane
-// accumulation order over t is the recompute kernel's.
-typedef float pg2 __attribute__((ext_vector_type(2)));
-typedef float pg4 __attribute__((ext_vector_type(4)));
-
-template <int SLOTS, int F>
-__device__ __forceinline__ void pg_zh_body(const SatAttnParamGrad& p) {
-  constexpr int FL = F > 0 ? F : 1;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int nq = (p.N + 3) / 4;
-  const int b = blockIdx.x / nq, n = 4 * (blockIdx.x - b * nq) + wave;
-  const int nn = min(n, p.N - 1);
-  const int Q1 = p.D1 / 4, Q = Q1 + p.D2 / 4;
-  const int padl = (p.KW - 1) / 2;
-  const int64_t bn = (int64_t)b * p.N + nn;
-  const int64_t TBN = (int64_t)p.B * p.N;
-  const int DQ = p.D1 + p.D2;
-
-  pg2 vlo[SLOTS], vhi[SLOTS];
-  pg2 dklo[SLOTS], dkhi[SLOTS], dvlo[SLOTS], dvhi[SLOTS], dwlo[SLOTS][FL], dwhi[SLOTS][FL];
-  bool m1[SLOTS];
-  int cs[SLOTS];
-  const pg2 zero2 = {0.f, 0.f};
-#pragma unroll
-  for (int s = 0; s < SLOTS; ++s) {
-    const int c = lane + 64 * s;
-    m1[s] = c < Q1;
-    cs[s] = min(c, Q - 1);
-    const int c1 = min(c, Q1 - 1), c2 = min(max(c - Q1, 0), p.D2 / 4 - 1);
-    const float4 v = m1[s] ? reinterpret_cast<const float4*>(p.v1)[c1]
-                           : reinterpret_cast<const float4*>(p.v2)[c2];
-    vlo[s] = pg2{v.x, v.y}; vhi[s] = pg2{v.z, v.w};
-    dklo[s] = dkhi[s] = dvlo[s] = dvhi[s] = zero2;
-#pragma unroll
-    for (int f = 0; f < FL; ++f) dwlo[s][f] = dwhi[s][f] = zero2;
-  }
-  const int nconv = F > 0 ? p.KW * F : 0;
-  const int cj = F > 0 ? lane / FL : 0, cf = F > 0 ? lane - cj * FL : 0;
-  float acw = 0.f;
-  const pg4* zrow = reinterpret_cast<const pg4*>(p.zh + bn * DQ);
-  const int64_t zstep = TBN * DQ / 4;                  // float4s per step
-  constexpr int kS = 4;                                // steps per block (loads one block ahead)
-  constexpr int kG = 64;                               // steps per group of lane-parallel scalars
-  // block loader: z rows and the location-conv operands of steps tb0 .. tb0 + kS - 1
-  auto load = [&](int tb0, pg4 (&zz)[kS][SLOTS], float (&sv)[kS], float (&dv)[kS]) {
-#pragma unroll
-    for (int u = 0; u < kS; ++u) {
-      const int t = min(tb0 + u, p.T - 1);
-      const bool on = tb0 + u < p.T;
-      const int64_t tb = (int64_t)t * TBN + bn;
-#pragma unroll
-      for (int s = 0; s < SLOTS; ++s) zz[u][s] = __builtin_nontemporal_load(zrow + t * zstep + cs[s]);
-      sv[u] = 0.f; dv[u] = 0.f;
-      if (F > 0 && on && lane < nconv + F) {
-        if (lane < nconv) {
-          const int m = nn + cj - padl;
-          sv[u] = (m >= 0 && m < p.N) ? p.s_prev[(int64_t)t * p.s_tstride + (int64_t)b * p.N + m] : 0.f;
-          dv[u] = p.df[tb * F + cf];
-        } else {
-          sv[u] = 1.f;
-          dv[u] = p.df[tb * F + (lane - nconv)];
-        }
-      }
-    }
-  };
-  for (int t0 = 0; t0 < p.T; t0 += kG) {
-    // the wave-uniform step scalars of steps t0 .. t0 + 63, one step per lane (a step past T
-    // contributes exactly zero), broadcast with v_readlane in the block loop
-    const bool onl = t0 + lane < p.T;
-    const int64_t tbl = (int64_t)min(t0 + lane, p.T - 1) * TBN + bn;
-    const float E1 = onl ? p.de1[tbl] : 0.f, E2 = onl ? p.de2[tbl] : 0.f;
-    float FLv[FL];
-#pragma unroll
-    for (int f = 0; f < FL; ++f) FLv[f] = (F > 0 && onl) ? p.loc[tbl * F + f] : 0.f;
-    pg4 zc[kS][SLOTS], zn[kS][SLOTS];
-    float svc[kS], dfc[kS], svn[kS], dfn[kS];
-    load(t0, zc, svc, dfc);
-#pragma unroll
-    for (int k = 0; k < kG / kS; ++k) {
-      if (t0 + kS * k >= p.T) break;                   // wave-uniform
-      if (k + 1 < kG / kS) load(t0 + kS * (k + 1), zn, svn, dfn);
-#pragma unroll
-      for (int u = 0; u < kS; ++u) {
-        const int ls = kS * k + u;
-        const float e1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(E1), ls));
-        const float e2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(E2), ls));
-        acw = fmaf(svc[u], dfc[u], acw);
-#pragma unroll
-        for (int s = 0; s < SLOTS; ++s) {
-          const float e = m1[s] ? e1 : e2;
-          const pg2 ee = {e, e};
-          const pg2 zlo = {zc[u][s].x, zc[u][s].y}, zhi = {zc[u][s].z, zc[u][s].w};
-          const pg2 one2 = {1.f, 1.f};
-          // dp = e v (1 - z^2), as the recompute kernel forms it
-          const pg2 plo = (ee * vlo[s]) * __builtin_elementwise_fma(-zlo, zlo, one2);
-          const pg2 phi = (ee * vhi[s]) * __builtin_elementwise_fma(-zhi, zhi, one2);
-          dklo[s] += plo; dkhi[s] += phi;
-          dvlo[s] = __builtin_elementwise_fma(ee, zlo, dvlo[s]);
-          dvhi[s] = __builtin_elementwise_fma(ee, zhi, dvhi[s]);
-#pragma unroll
-          for (int f = 0; f < F; ++f) {
-            const float fv = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(FLv[f]), ls));
-            const pg2 ff = {fv, fv};
-            dwlo[s][f] = __builtin_elementwise_fma(ff, plo, dwlo[s][f]);
-            dwhi[s][f] = __builtin_elementwise_fma(ff, phi, dwhi[s][f]);
-          }
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < kS; ++u) {
-        svc[u] = svn[u]; dfc[u] = dfn[u];
-#pragma unroll
-        for (int s = 0; s < SLOTS; ++s) zc[u][s] = zn[u][s];
-      }
-    }
-  }
-  float4 adk[SLOTS], adv[SLOTS], adw[SLOTS][FL];
-#pragma unroll
-  for (int s = 0; s < SLOTS; ++s) {
-    adk[s] = make_float4(dklo[s].x, dklo[s].y, dkhi[s].x, dkhi[s].y);
-    adv[s] = make_float4(dvlo[s].x, dvlo[s].y, dvhi[s].x, dvhi[s].y);
-#pragma unroll
-    for (int f = 0; f < FL; ++f)
-      adw[s][f] = make_float4(dwlo[s][f].x, dwlo[s][f].y, dwhi[s][f].x, dwhi[s][f].y);
-  }
-  attn_pg_store<SLOTS, F>(p, adk, adv, adw, acw);
-}
-
-// One launch over the (utterance, 4-position) workgroups: of every 8 consecutive workgroups the
-// first zh_share read z from ZH (HBM-bound), the others recompute it (VALU-bound), so the two
-// kinds share each CU's issue slots and the memory system at once.
+// One launch over the (utterance, 4-position) workgroups.  (Round 3 also built a variant that
+// streamed z from the forward's ZH history instead of recomputing it, alone and mixed per
+// workgroup: no step gain at the same occupancy; removed.)
 template <int SLOTS, int F>
 __global__ void __launch_bounds__(256) attn_param_grad_kernel(SatAttnParamGrad p) {
-  if (p.zh && (int)(blockIdx.x & 7) < p.zh_share) pg_zh_body<SLOTS, F>(p);
-  else pg_recompute_body<SLOTS, F>(p);
+  pg_recompute_body<SLOTS, F>(p);
 }
 
 template <int NT, int WAVES>
@@ -1300,8 +1166,6 @@ extern "C" int sat_attn_param_grads(const SatAttnParamGrad* a, void* stream) {
   const dim3 grid(sat_attn_param_grad_rows(a->B, a->N));
   const size_t shm = 4 * (size_t)a->pg_stride * sizeof(float);
   hipStream_t s = as_stream(stream);
-  SAT_CHECK_ARG(!a->zh || (aligned16(a->zh) && a->zh_share >= 0 && a->zh_share <= 8),
-                "sat_attn_param_grads: zh alignment / zh_share in 0..8");
   if (slots == 1 && F == 5) hipLaunchKernelGGL((attn_param_grad_kernel<1, 5>), grid, dim3(256), shm, s, p);
   else if (slots == 1 && F == 0) hipLaunchKernelGGL((attn_param_grad_kernel<1, 0>), grid, dim3(256), shm, s, p);
   else if (F == 0) hipLaunchKernelGGL((attn_param_grad_kernel<2, 0>), grid, dim3(256), shm, s, p);

@@ -1160,13 +1160,6 @@ struct LdsPlan { int bm, bn, splits, kchunk; };
 // c_div: BM must divide it (im2col-T: one tap per tile); n_div: BN must divide it (conv bank).
 static LdsPlan plan_lds(int M, int N, int K, int nb, bool can_split, int64_t ws_bytes, int c_div,
                         int n_div) {
-  // measured override: LSTM1's context product (B T' x 4U x (M1 + M2) = 16000 x 1024 x 288 at
-  // the bench shape) runs ALONE on the step's critical path between the two persistent
-  // forward launches (profiles/r03_step_timeline.txt); the sweep times 64x64 at 122 us against
-  // the model's 128x64 at 152 us (profiles/r03_gemm_census_sweep.txt).  Same K order: same bits.
-  if (t_force_bm == 0 && c_div == 0 && n_div == 0 && nb == 1 && K == 288 && N == 1024 &&
-      M >= 8192)
-    return LdsPlan{64, 64, 1, K};
   struct Cand { int bm, bn, occ; };
   // (ties go to the first: two 128x64 workgroups per CU overlap each other's epilogue)
   static const Cand cands[4] = {{128, 64, 2}, {64, 128, 2}, {128, 128, 1}, {64, 64, 3}};
@@ -1278,6 +1271,47 @@ static int launch_lds(const SatGemmDesc* d, GemmP& p, int nb, hipStream_t s) {
   return launch_lds_plan<0>(pl, am, bm, nb, p, s, "sat_gemm");
 }
 
+// Can the two reduction segments (A2 / B2) run as ONE LDS-kernel reduction?  Otherwise
+// sat_gemm splits the descriptor into two accumulating launches (gemm_split_segments).
+static bool segments_fused_ok(const SatGemmDesc* d) {
+  return d->a_mode == 0 && d->b_mode == 0 && !d->colsum_out && d->k1 > 0 && d->k1 < d->K &&
+         d->k1 % BK == 0 && gemm_lds_enabled() && !t_probe &&
+         (!d->A2 || (d->a_sk == 1 && aligned16(d->A2) && d->a2_sm % 4 == 0)) &&
+         (!d->B2 || (aligned16(d->B2) && d->b2_s % 4 == 0 && (d->b_sn == 1 || d->b_sk == 1)));
+}
+
+extern "C" int sat_gemm(const SatGemmDesc* d, void* stream);
+
+// A segmented product the fused path cannot take (k1 not a multiple of the K-tile, the LDS
+// kernel switched off by SAT_GEMM_LDS=0, operands not vector-loadable): C = [A | A2] [B ; B2]
+// as  C = alpha A[:, :k1] B[:k1] + beta C + bias + add,  then  C += alpha A[:, k1:] B[k1:]
+// (the epilogue must be linear: no activation / mul, no C2 / colsum_out).  Same result up to
+// the summation order of the two partial products.
+static int gemm_split_segments(const SatGemmDesc* d, void* stream) {
+  SAT_CHECK_ARG(d->a_mode == 0 && d->b_mode == 0 && d->k1 > 0 && d->k1 < d->K && !d->C2 &&
+                    !d->colsum_out && d->act == 0 && !d->mul,
+                "sat_gemm: segmented operands outside the fused path need a dense product "
+                "with 0 < k1 < K and a linear epilogue (no act / mul / C2 / colsum_out)");
+  SatGemmDesc d1 = *d;
+  d1.A2 = nullptr; d1.B2 = nullptr; d1.k1 = 0;
+  d1.K = d->k1;
+  int rc = sat_gemm(&d1, stream);
+  if (rc != SAT_OK) return rc;
+  SatGemmDesc d2 = *d;
+  d2.A2 = nullptr; d2.B2 = nullptr; d2.k1 = 0;
+  d2.K = d->K - d->k1;
+  if (d->A2) { d2.A = d->A2; d2.a_sm = d->a2_sm; d2.a_sk = 1; }
+  else d2.A = d->A + (int64_t)d->k1 * d->a_sk;
+  if (d->B2) {
+    d2.B = d->B2;
+    if (d->b_sn == 1) { d2.b_sk = d->b2_s; d2.b_sn = 1; } else { d2.b_sk = 1; d2.b_sn = d->b2_s; }
+  } else {
+    d2.B = d->B + (int64_t)d->k1 * d->b_sk;
+  }
+  d2.beta = 1.f; d2.bias = nullptr; d2.bias_sbatch = 0; d2.add = nullptr;
+  return sat_gemm(&d2, stream);
+}
+
 extern "C" int sat_gemm(const SatGemmDesc* d, void* stream) {
   using namespace sat;
   SAT_CHECK_ARG(d != nullptr, "sat_gemm: null descriptor");
@@ -1318,6 +1352,7 @@ extern "C" int sat_gemm(const SatGemmDesc* d, void* stream) {
                   "n1 %% 128 == 0");
     p.C2 = d->C2; p.c2_sm = d->c2_sm; p.n1 = d->n1;
   }
+  if ((d->A2 || d->B2) && !segments_fused_ok(d)) return gemm_split_segments(d, stream);
   if (d->A2 || d->B2 || d->C2) {
     if (d->A2 || d->B2) {
       // two reduction segments: A2 (dense K-contiguous A) and / or B2 (dense B, B's layout)
@@ -1334,6 +1369,7 @@ extern "C" int sat_gemm(const SatGemmDesc* d, void* stream) {
       p.B2 = d->B2; p.b2_s = d->b2_s;
     }
     const int r = launch_lds(d, p, nb, s);
+    if (r == 1 && (d->A2 || d->B2) && !d->C2) return gemm_split_segments(d, stream);
     SAT_CHECK_ARG(r != 1, "sat_gemm: segmented operands are not vector-loadable");
     return r;
   }

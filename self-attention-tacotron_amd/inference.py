@@ -221,6 +221,18 @@ class FreeRunningDecoder:
             MS=pl.MS, AL1=pl.AL1, S2=pl.S2, SA_P=pl.SA_P[0], state=pl.state,
             scratch=pl.scratch, scratch_bytes=pl.scratch.numel(), err=pl.err)
 
+    def _try_persistent(self, pl: _Plan, Tm: int) -> Optional[str]:
+        """Run the one-launch decode; None when it ran to the end, else why it did not (the
+        library refused the launch, e.g. SAT_ERR_UNSUPPORTED on a device with fewer than 256
+        co-resident workgroups, or a hand-off timed out and raised the error word)."""
+        try:
+            self._run_persistent(pl, Tm)
+        except _lib.SatLibraryError as e:
+            return str(e)
+        if int(pl.err.item()) != 0:
+            return "a hand-off timed out (the grid was not co-resident?)"
+        return None
+
     def _build(self, B: int, N: int, Tm: int) -> _Plan:
         m, hp, d = self.m, self.hp, self.d
         P, dev = m.P, m.device
@@ -497,26 +509,35 @@ class FreeRunningDecoder:
             spk = torch.empty(B, d.spk_dim, device=dev)
             err = torch.zeros(1, dtype=torch.int32, device=dev)
             K.embedding_fwd(P["speaker_embedding"], batch["speaker_id"], spk, d.spk_offset, err)
-        # ---- memories (TF _prepare_memory + memory_layer) into the plan's buffers
-        self._prepare(pl, batch, spk)
-        K.seq_mask(m1, pl.lengths, out=pl.V1)
-        K.seq_mask(m2, pl.lengths, out=pl.V2)
-        K.linear(pl.V1, P["decoder/attention1/memory_layer/kernel"], out=pl.K1)
-        K.linear(pl.V2, P["decoder/attention2/memory_layer/kernel"], out=pl.K2)
+        def prepare():
+            # ---- memories (TF _prepare_memory + memory_layer) into the plan's buffers
+            self._prepare(pl, batch, spk)
+            K.seq_mask(m1, pl.lengths, out=pl.V1)
+            K.seq_mask(m2, pl.lengths, out=pl.V2)
+            K.linear(pl.V1, P["decoder/attention1/memory_layer/kernel"], out=pl.K1)
+            K.linear(pl.V2, P["decoder/attention2/memory_layer/kernel"], out=pl.K2)
 
+        prepare()
         stop_mode = self.helper == "stop_token"
         steps = Tm
+        self.last_path = "launches"
         if getattr(pl, "pk", None) is not None:
-            self.last_path = "persistent"
-            self._run_persistent(pl, Tm)
-            if int(pl.err.item()) != 0:
-                raise _lib.SatLibraryError("sat_decode_persistent: a hand-off timed out (the "
-                                           "grid was not co-resident?)")
-            first = int(pl.state.item()) if stop_mode else -1
-            if first >= 0:
-                steps = first + 1
-        else:
-            self.last_path = "launches"
+            why = self._try_persistent(pl, Tm)
+            if why is None:
+                self.last_path = "persistent"
+                first = int(pl.state.item()) if stop_mode else -1
+                if first >= 0:
+                    steps = first + 1
+            elif self.persistent:
+                raise _lib.SatLibraryError("sat_decode_persistent: " + why)
+            else:
+                # persistent=None: the one-launch decode is not runnable here (too few
+                # co-resident workgroups on this device, or a hand-off timed out because
+                # another stream held CUs) -- this plan decodes with the per-step launches
+                # from now on, starting again from clean buffers
+                pl.pk = None
+                pl.err.zero_()
+                prepare()
         for a in range(0, Tm if self.last_path == "launches" else 0, self.check_every):
             b = min(Tm, a + self.check_every)
             self._steps(pl, a, b)

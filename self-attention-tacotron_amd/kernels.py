@@ -143,7 +143,7 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor = None, *, alpha=1.0,
             raise ValueError("gemm: B2 must be [.., K2, N] in B's layout and batch strides, "
                              "beside B [.., k1, N]")
         k1 = K2
-        K2 += B2.shape[0]
+        K2 += B2.shape[-2]
     if K != K2:
         raise ValueError(f"gemm: inner dims differ {tuple(A.shape)} @ {tuple(B.shape)}")
     lead = A.shape[:-2] if A.dim() >= B.dim() else B.shape[:-2]

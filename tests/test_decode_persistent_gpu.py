@@ -90,3 +90,37 @@ def test_one_launch_rerun_is_deterministic(cuda):
     a = dec.run(gb)
     c = dec.run(gb)
     assert torch.equal(a["mel"], c["mel"]) and torch.equal(a["alignment1"], c["alignment1"])
+
+
+def test_default_falls_back_when_one_launch_refused(cuda, monkeypatch):
+    """persistent=None: when the library refuses the one-launch decode at run time (e.g.
+    SAT_ERR_UNSUPPORTED on a device with too few co-resident workgroups) or a hand-off times out,
+    the run continues on the per-step launches from clean buffers and gives the launch path's
+    result; persistent=True raises instead."""
+    from sat_amd import _lib
+    from sat_amd import kernels as K
+    from sat_amd.inference import FreeRunningDecoder
+    hp, vals, m, b, gb = _setup(cuda, 3, 15)
+    T = 20
+    ref = FreeRunningDecoder(m, persistent=False, max_iters=T, min_iters=T).run(gb)
+    real = K.decode_persistent
+
+    def refused(**kw):
+        raise _lib.SatLibraryError("sat_decode_persistent: fewer than 256 co-resident workgroups")
+
+    def timed_out(**kw):
+        real(**kw)
+        kw["err"].fill_(1)
+
+    for fake in (refused, timed_out):
+        monkeypatch.setattr(K, "decode_persistent", fake)
+        dec = FreeRunningDecoder(m, max_iters=T, min_iters=T)
+        out = dec.run(gb)
+        assert dec.last_path == "launches"
+        assert out["steps"] == ref["steps"] == T
+        assert torch.equal(out["mel"], ref["mel"])
+        assert torch.equal(out["alignment1"], ref["alignment1"])
+        out2 = dec.run(gb)                  # the plan stays on the launch path
+        assert dec.last_path == "launches" and torch.equal(out2["mel"], ref["mel"])
+        with pytest.raises(_lib.SatLibraryError):
+            FreeRunningDecoder(m, persistent=True, max_iters=T, min_iters=T).run(gb)

@@ -9,7 +9,8 @@ show.  Every case runs the persistent kernels that the bench times (any B <= 32 
   teacher-forced ``loss_with_teacher`` computation, models/models.py:208-231) and train mode
   with injected dropout / zoneout masks;
 * gradients at B=8, N=200 (7 attention tiles and their halos), T=1000, ragged lengths;
-* C2 (B=32: 4 utterances per hand-off group) forward in eval mode.
+* C2 (B=32, every persistent grid on all 256 CUs) forward in eval mode, and train mode with
+  masks including every parameter gradient -- the configuration bench.py times.
 
 Tolerances (written per assertion): mel mean-L1 <= 1e-4 (north_star); loss within 1e-5
 relative; stop logits mean-abs <= 1e-4; every parameter gradient within 2e-4 of
@@ -108,12 +109,7 @@ def test_c4_vctk_full_shape_matches_oracle(cuda, train):
     _compare_outputs(f"c4_{'train' if train else 'eval'}", out, ref, b)
 
 
-def test_gradients_full_length_match_oracle(cuda):
-    """BPTT over 500 steps at B=8, N<=200 (ragged; up to 7 tiles with halos), T<=1000, train
-    mode with injected masks: loss and every parameter gradient vs float64 autograd."""
-    hp, m, out, ref, p64, b = _run(cuda, 8, 200, 1000, True, shape="ljs", seed=31, grads=True)
-    assert b["source"].shape[1] > 160 and b["mel"].shape[1] >= 800   # long, ragged batch
-    _compare_outputs("grad_b8_outputs", out, ref, b)
+def _compare_grads(name, m, p64, b):
     grads = m.grads_dict()
     gmax = max(float(p.grad.abs().max()) for p in p64.values())
     worst, bad = 0.0, []
@@ -124,5 +120,24 @@ def test_gradients_full_length_match_oracle(cuda):
         worst = max(worst, err)
         if not err <= 2e-4:
             bad.append((name, err))
-    _report("grad_b8", worst_rel_grad_err=worst, steps=int(b["mel"].shape[1] // 2))
+    _report(name, worst_rel_grad_err=worst, steps=int(b["mel"].shape[1] // 2))
     assert not bad, bad
+
+
+def test_gradients_full_length_match_oracle(cuda):
+    """BPTT over 500 steps at B=8, N<=200 (ragged; up to 7 tiles with halos), T<=1000, train
+    mode with injected masks: loss and every parameter gradient vs float64 autograd."""
+    hp, m, out, ref, p64, b = _run(cuda, 8, 200, 1000, True, shape="ljs", seed=31, grads=True)
+    assert b["source"].shape[1] > 160 and b["mel"].shape[1] >= 800   # long, ragged batch
+    _compare_outputs("grad_b8_outputs", out, ref, b)
+    _compare_grads("grad_b8", m, p64, b)
+
+
+def test_c2_train_gradients_match_oracle(cuda):
+    """The benched configuration itself: C2 (B=32, N=200, T=1000 -> 500 steps, every persistent
+    grid on all 256 CUs, 32 hand-off groups over the 8 XCDs), train mode with injected dropout /
+    zoneout masks: mel, stop and loss vs the float64 oracle, then every parameter gradient of
+    the BPTT vs float64 autograd (models/models.py:159-189)."""
+    hp, m, out, ref, p64, b = _run(cuda, 32, 200, 1000, True, seed=51, grads=True)
+    _compare_outputs("c2_train_outputs", out, ref, b)
+    _compare_grads("c2_train_grad", m, p64, b)

@@ -345,7 +345,7 @@ def test_gemm_degenerate_shapes(cuda, M, N, K, ta, act):
 
 # ---- skinny products (M <= 8: the free-running decoder's per-step projections at batch 8)
 @pytest.mark.parametrize("M,N,K", [(1, 256, 80), (3, 164, 256), (8, 768, 256), (8, 1024, 800),
-                                   (5, 37, 19)])
+                                   (5, 37, 19), (2, 50, 300), (7, 130, 33)])
 @pytest.mark.parametrize("act", [None, "relu", "tanh"])
 def test_gemm_skinny(cuda, M, N, K, act):
     from sat_amd import kernels
@@ -388,11 +388,30 @@ def test_gemm_two_a_segments(cuda, M, N, K1, K2, tb):
     assert bool(((C.double().cpu() - ref).abs() <= bound).all())
 
 
-def test_gemm_two_a_segments_rejects_unaligned_split(cuda):
+@pytest.mark.parametrize("with_b2", [False, True])
+def test_gemm_segments_outside_fused_path_split(cuda, with_b2):
+    """Segments the fused LDS reduction cannot take (k1 = 48 is not a multiple of the 32-wide
+    K-tile) run as two accumulating launches with the bias / add / beta epilogue applied once;
+    a non-linear epilogue there is refused."""
     from sat_amd import _lib, kernels
-    A = torch.randn(64, 48, device=cuda)                  # k1 = 48 is not a multiple of 32
+    g = torch.Generator().manual_seed(48)
+    A, A2 = torch.randn(64, 48, generator=g), torch.randn(64, 36, generator=g)
+    B = torch.randn(48 + (0 if with_b2 else 36), 80, generator=g)
+    B2 = torch.randn(36, 80, generator=g)
+    C0, bias, add = torch.randn(64, 80, generator=g), torch.randn(80, generator=g), \
+        torch.randn(64, 80, generator=g)
+    C = C0.to(cuda)
+    kernels.gemm(A.to(cuda), B.to(cuda), C, alpha=0.5, beta=-1.0, bias=bias.to(cuda),
+                 add=add.to(cuda), A2=A2.to(cuda), B2=B2.to(cuda) if with_b2 else None)
+    Bf = torch.cat([B, B2]) if with_b2 else B
+    ref = 0.5 * (torch.cat([A, A2], 1).double() @ Bf.double()) - C0.double() + bias.double() + \
+        add.double()
+    bound = 4e-7 * (torch.cat([A, A2], 1).double().abs() @ Bf.double().abs() + C0.double().abs() +
+                    add.double().abs() + 1)
+    assert bool(((C.double().cpu() - ref).abs() <= bound).all())
     with pytest.raises(_lib.SatLibraryError):
-        kernels.gemm(A, torch.randn(80, 64, device=cuda), A2=torch.randn(64, 32, device=cuda))
+        kernels.gemm(A.to(cuda), B.to(cuda), act="relu", A2=A2.to(cuda),
+                     B2=B2.to(cuda) if with_b2 else None)
 
 
 @pytest.mark.parametrize("M,N1,N2,K", [(16000, 256, 288, 1024), (300, 128, 100, 64), (70, 256, 4, 2000)])
@@ -458,3 +477,17 @@ def test_gemm_two_segments_batched(cuda):
     bound = 4e-7 * sum((DG[i].double().abs() @ W[i][:Win].double().abs().t()).transpose(0, 1)
                        for i in range(2)) + 1e-7
     assert bool(((out.double().cpu() - ref).abs() <= bound).all())
+
+
+def test_gemm_batched_b2(cuda):
+    """A batched B2 ([batch, K2, N]): the inner dimension is B2's second-to-last (not its batch
+    count); C[i] = A[i][:, :k1] B[i] + A[i][:, k1:] B2[i]."""
+    from sat_amd import kernels
+    g = torch.Generator().manual_seed(12)
+    nb, M, N, K1, K2 = 3, 70, 96, 64, 32
+    A = torch.randn(nb, M, K1 + K2, generator=g)
+    B, B2 = torch.randn(nb, K1, N, generator=g), torch.randn(nb, K2, N, generator=g)
+    C = kernels.gemm(A.to(cuda), B.to(cuda), B2=B2.to(cuda))
+    ref = A.double() @ torch.cat([B, B2], 1).double()
+    bound = 4e-7 * (A.double().abs() @ torch.cat([B, B2], 1).double().abs()) + 1e-7
+    assert bool(((C.double().cpu() - ref).abs() <= bound).all())

@@ -100,3 +100,28 @@ def test_synthetic_batch_contract(shape):
         assert np.all(b["mel_mask"][i, :tl] == 1) and np.all(b["mel_mask"][i, tl:] == 0)
     if shape == "max":
         assert np.all(b["source_length"] == N) and np.all(b["target_length"] == T)
+
+
+def test_free_running_try_persistent_reports_why():
+    """FreeRunningDecoder._try_persistent (the default decode's eligibility at run time): a
+    library refusal or a raised error word is reported, so run() can fall back to the per-step
+    launches (inference.py)."""
+    import torch
+    from sat_amd import _lib
+    from sat_amd.inference import FreeRunningDecoder
+
+    class Plan:
+        def __init__(self):
+            self.err = torch.zeros(1, dtype=torch.int32)
+
+    dec = FreeRunningDecoder.__new__(FreeRunningDecoder)
+
+    def refused(pl, Tm):
+        raise _lib.SatLibraryError("sat_decode_persistent: SAT_ERR_UNSUPPORTED")
+
+    dec._run_persistent = refused
+    assert "UNSUPPORTED" in dec._try_persistent(Plan(), 5)
+    dec._run_persistent = lambda pl, Tm: pl.err.fill_(1)
+    assert "timed out" in dec._try_persistent(Plan(), 5)
+    dec._run_persistent = lambda pl, Tm: None
+    assert dec._try_persistent(Plan(), 5) is None

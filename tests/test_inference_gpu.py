@@ -257,17 +257,17 @@ def _c5_batch(cuda, seed=55):
     return hp, vals, m, b, gb, O
 
 
-def test_c5_first_100_steps_match_oracle(cuda):
-    """The first 100 free-running steps at B=8, N=200 (mel feedback, KV-cached head) vs the
+def test_c5_first_250_steps_match_oracle(cuda):
+    """The first 250 free-running steps at B=8, N=200 (mel feedback, KV-cached head) vs the
     oracle's restatement (TransformerWrapper re-running the causal self-attention over the whole
     history each step).  The decode feeds its own fp32 output back, so the fp32-vs-float64
     difference could compound through the recurrence: mel within 1e-5 absolute (max) and 1e-6
-    mean-abs over the 100 steps, alignments and stop logits within 1e-5 (achieved: 2.5e-7 /
+    mean-abs over the 250 steps, alignments and stop logits within 1e-5 (achieved: 2.5e-7 /
     4.0e-8 / 1.1e-7, profiles/r03_parity_fullsize.jsonl)."""
     from sat_amd import params
     from sat_amd.inference import FreeRunningDecoder
     hp, vals, m, b, gb, O = _c5_batch(cuda)
-    T = 100
+    T = 250
     out = FreeRunningDecoder(m, max_iters=T, min_iters=T, check_every=25, graphs=True).run(gb)
     ref = O.infer_free_running(O.to_torch(vals), O.to_torch(params.init_bn_buffers(hp)), hp,
                                O.to_torch(b), max_iters=T, min_iters=T)
@@ -278,7 +278,7 @@ def test_c5_first_100_steps_match_oracle(cuda):
     path = os.environ.get("SAT_PARITY_REPORT")
     if path:
         with open(path, "a") as f:
-            f.write(json.dumps({"case": "c5_first100", "mel_max_abs": float(d.max()),
+            f.write(json.dumps({"case": "c5_first250", "mel_max_abs": float(d.max()),
                                 "mel_mean_abs": float(d.mean()),
                                 "align1_max_abs": float(da.max())}) + "\n")
     assert float(d.max()) <= 1e-5 and float(d.mean()) <= 1e-6, (float(d.max()), float(d.mean()))

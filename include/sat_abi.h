@@ -735,6 +735,15 @@ int sat_transpose(const float* in, int64_t ldi, float* out, int64_t ldo, int32_t
                   void* stream);
 /* y = a*x + b*y */
 int sat_axpby(const float* x, float* y, int64_t n, float a, float b, void* stream);
+/* z = x + y (n % 4 == 0, 16-byte aligned): a residual sum whose addend is kept for the backward */
+int sat_add(const float* x, const float* y, float* z, int64_t n, void* stream);
+/* p[i] = bits for n 4-byte words (zero-initialised step buffers and error words inside the
+ * captured training step, in place of a framework fill). */
+int sat_fill32(void* p, int64_t n, uint32_t bits, void* stream);
+/* dst[i*d0 + j*d1 + k] = src[i*s0 + j*s1 + k] for i < n0, j < n1, k < n2 (unit innermost
+ * strides): a transposed view made contiguous, or a strided slice copied into a step buffer. */
+int sat_copy3d(const float* src, int64_t s0, int64_t s1, float* dst, int64_t d0, int64_t d1,
+               int32_t n0, int32_t n1, int32_t n2, void* stream);
 
 /* ScaledDotProductAttentionMechanism softmax (modules/self_attention.py:45-65):
  * P = softmax(scale*S) per row of length L, causal (use_subsequent_mask) masks col > row%Lq,

@@ -229,6 +229,9 @@ SIGNATURES = {
     "sat_highway_bwd": [_P, _P, _P, _P, _P, _P, _P, _I64, _P],
     "sat_act_bwd": [_P, _P, _P, _P, _I64, _I32, _F, _P],
     "sat_axpby": [_P, _P, _I64, _F, _F, _P],
+    "sat_fill32": [_P, _I64, ctypes.c_uint32, _P],
+    "sat_add": [_P, _P, _P, _I64, _P],
+    "sat_copy3d": [_P, _I64, _I64, _P, _I64, _I64, _I32, _I32, _I32, _P],
     "sat_softmax_fwd": [_P, _P, _P, _P, _I64, _I32, _I32, _I32, _F, _P],
     "sat_softmax_bwd": [_P, _P, _P, _P, _I64, _I32, _F, _P],
     "sat_loss_fwd_bwd": [_P, _P, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _F, _P, _P, _P, _P, _P],

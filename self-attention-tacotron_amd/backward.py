@@ -11,6 +11,7 @@ recurrence (dW = sum_t x_t^T dgates_t).
 from __future__ import annotations
 
 import math
+import os
 from typing import Dict
 
 import torch
@@ -76,7 +77,7 @@ def mha_bwd(P, G, scope, s, dy, ws):
              for t in ("kernel", "bias")]
     d, _scratch = K.mha_desc(s["x"], *(P[n] for n in names), s["heads"], s["causal"], s["mask"], s)
     dx = torch.empty_like(s["x"])
-    dyc = dy.contiguous()
+    dyc = K.contiguous(dy)
     d.dy, d.dx = dyc.data_ptr(), dx.data_ptr()
     d.dWq, d.dbq, d.dWk, d.dbk, d.dWv, d.dbv, d.dWo, d.dbo = (G[n].data_ptr() for n in names)
     K.mha_bwd(d)
@@ -111,7 +112,7 @@ def head_bwd(P, G, hp, d, sv, ws, aux=None):
     for h in reversed(range(d.dec_hops)):
         dz = sa_transformer_bwd(P, G, f"decoder/self_attention{h}", sv[f"dec_sa{h}"], dz, ws,
                                 aux=aux)
-    return dz.transpose(0, 1).contiguous()                           # [T', B, D] (data movement)
+    return K.contiguous(dz.transpose(0, 1))                          # [T', B, D] (data movement)
 
 
 class _LstmBwd:
@@ -337,10 +338,18 @@ def decoder_bwd(P, G, hp, d, dsv, dH2, masks, ws, attn_tile=32, pipe: Pipeline =
     #      encoder BiLSTM BPTT holds 64 of them); model_backward joins the stream.  Everything the
     #      branch reads stays referenced until the join; it writes only its own gradient rows.
     aux_s = aux.s if aux is not None else torch.cuda.current_stream()
-    if aux is not None:
-        aux.s.wait_stream(torch.cuda.current_stream())
-        aux.keep.extend([DG0, DG1, DG2, DQP, S])
-    with torch.cuda.stream(aux_s):
+    # SAT_DEC_WGRAD_FORK=pg: fork the branch after the attention parameter pass is issued (the
+    # branch then waits for it), so the pass does not share the chip with these products (A/B)
+    late = os.environ.get("SAT_DEC_WGRAD_FORK", "bptt") == "pg"
+
+    def fork_wgrad():
+        if aux is not None:
+            aux.s.wait_stream(torch.cuda.current_stream())
+            aux.keep.extend([DG0, DG1, DG2, DQP, S])
+        with torch.cuda.stream(aux_s):
+            dec_wgrad()
+
+    def dec_wgrad():
         # LSTM weight gradients: one GEMM per weight block over all steps
         DG2f = DG2.view(Tp * B, 4 * Dd)
         DG1f = DG1.view(Tp * B, 4 * Dd)
@@ -378,6 +387,8 @@ def decoder_bwd(P, G, hp, d, dsv, dH2, masks, ws, attn_tile=32, pipe: Pipeline =
                    colsum=G[f"{a1}/attention_bias"] if fwd else None)
             K.gemm(H0f.t(), DQt[:, tile, D1:], G[f"{a2}/query_layer/kernel"], beta=1.0)
 
+    if not late:
+        fork_wgrad()
     # ---- attention parameters: one pass over all steps (sat_attn_param_grads), then a column
     #      sum of its per-workgroup partial rows
     F, KW = (d.loc_f, d.loc_k) if fwd else (0, 0)
@@ -393,8 +404,9 @@ def decoder_bwd(P, G, hp, d, dsv, dH2, masks, ws, attn_tile=32, pipe: Pipeline =
         v1=P[f"{a1}/attention_variable"] if fwd else P[f"{a1}/attention_v"],
         locW=P[f"{a1}/location_layer/kernel"] if fwd else None, v2=P[f"{a2}/attention_v"],
         loc=S["LOC"] if fwd else None, s_prev=S["S1"], s_tstride=S["S1"].stride(0),
-        de1=DE1, de2=DE2, df=DFH if fwd else None, dK1=dK1, dK2=dK2, pg=PG, pg_stride=pgs,
-        zh=None)     # recompute every z: reading ZH (3.3 GB at C2), all or in part, measured no faster
+        de1=DE1, de2=DE2, df=DFH if fwd else None, dK1=dK1, dK2=dK2, pg=PG, pg_stride=pgs)
+    if late:
+        fork_wgrad()
     if fwd:
         dsts = [G[f"{a1}/attention_variable"], G[f"{a1}/location_layer/kernel"].view(-1),
                 G[f"{a1}/location_conv/kernel"].view(-1), G[f"{a1}/location_conv/bias"]]
@@ -455,7 +467,7 @@ def encoder_bwd(P, G, hp, d, sv, dm1, dm2, lengths, masks, ws, aux: Aux = None):
         # [N, B, Win] (data movement) for the input-weight gradients, made on the stream that
         # runs them (the aux stream when present: off the main stream's chain)
         if not hw_box:
-            hw_box.append(hw.transpose(0, 1).contiguous())
+            hw_box.append(K.contiguous(hw.transpose(0, 1)))
         return hw_box[0]
     dhw = torch.empty(B, N, Win, device=dev)
     zc, zh = hp.zoneout_factor_cell, hp.zoneout_factor_output
@@ -538,7 +550,7 @@ def encoder_bwd(P, G, hp, d, sv, dm1, dm2, lengths, masks, ws, aux: Aux = None):
     # proj2: hw0 = BN(p2_pre) + inp
     inp = sv["enc_pre"][-1]
     C2 = d.proj2
-    dinp = dy.clone()                                                # residual branch
+    dinp = K.copy3d_(torch.empty_like(dy), dy)                       # residual branch
     dp2 = torch.empty_like(sv["p2_pre"])
     s2 = sv["st_p2"]
     K.bn_bwd(dy.view(-1, C2), sv["p2_pre"].view(-1, C2), None, dp2.view(-1, C2), s2["mean"],

@@ -556,6 +556,15 @@ __global__ void axpby_kernel(const float* __restrict__ x, float* __restrict__ y,
   GRID_STRIDE(i, n) { y[i] = a * x[i] + (b != 0.f ? b * y[i] : 0.f); }
 }
 
+// z = x + y on float4 (the self-attention transformer's residual, modules/module.py:363-371)
+__global__ void add3_kernel(const float4* __restrict__ x, const float4* __restrict__ y,
+                            float4* __restrict__ z, int64_t n4) {
+  GRID_STRIDE(i, n4) {
+    const float4 a = x[i], b = y[i];
+    z[i] = make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+  }
+}
+
 // ---------------------------------------------------------------- row softmax (self-attention)
 // P = softmax(scale * S) over the last dim, optional causal mask (col > row-in-sequence -> -inf),
 // Pd = P * mask (dropout on probabilities).  One wave per row.
@@ -805,6 +814,44 @@ __global__ void transpose_kernel(const float* __restrict__ in, int64_t ldi, floa
   }
 }
 
+// dword fill of a buffer (zero-initialised step buffers, error words): dwordx4 stores where the
+// pointer allows, the head / tail one dword at a time
+__global__ void fill32_kernel(unsigned* __restrict__ p, int64_t n, unsigned bits) {
+  const int64_t head = std::min<int64_t>(n, (int64_t)((16 - (reinterpret_cast<uintptr_t>(p) & 15)) & 15) / 4);
+  const int64_t n4 = (n - head) / 4;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint4* q = reinterpret_cast<uint4*>(p + head);
+  const uint4 v = make_uint4(bits, bits, bits, bits);
+  for (int64_t i = i0; i < n4; i += stride) q[i] = v;
+  if (i0 < head) p[i0] = bits;
+  const int64_t t0 = head + 4 * n4;
+  if (i0 < n - t0) p[t0 + i0] = bits;
+}
+
+// dst[i][j][k] = src[i][j][k] over an [n0][n1][n2] box, both with unit innermost stride and any
+// outer strides (a transpose(0, 1) made contiguous, a strided slice copied into a step buffer):
+// one thread per float4 of a row when every row start is 16-byte aligned, else per float
+template <bool V4>
+__global__ void copy3d_kernel(const float* __restrict__ src, int64_t s0, int64_t s1,
+                              float* __restrict__ dst, int64_t d0, int64_t d1, int n0, int n1,
+                              int n2) {
+  const int w = V4 ? n2 / 4 : n2;
+  const int64_t total = (int64_t)n0 * n1 * w;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int k = (int)(e % w);
+    const int64_t r = e / w;
+    const int j = (int)(r % n1), i = (int)(r / n1);
+    if (V4) {
+      *reinterpret_cast<float4*>(dst + i * d0 + j * d1 + 4 * k) =
+          *reinterpret_cast<const float4*>(src + i * s0 + j * s1 + 4 * k);
+    } else {
+      dst[i * d0 + j * d1 + k] = src[i * s0 + j * s1 + k];
+    }
+  }
+}
+
 }  // namespace
 }  // namespace sat
 
@@ -817,6 +864,36 @@ extern "C" int sat_transpose(const float* in, int64_t ldi, float* out, int64_t l
   hipLaunchKernelGGL(transpose_kernel, dim3(ceil_div(C, 32), ceil_div(R, 32)), dim3(256), 0,
                      as_stream(stream), in, ldi, out, ldo, R, C);
   SAT_LAUNCH_CHECK("sat_transpose");
+  return SAT_OK;
+}
+
+extern "C" int sat_fill32(void* p, int64_t n, uint32_t bits, void* stream) {
+  SAT_CHECK_ARG(n >= 0 && (p || n == 0) && (reinterpret_cast<uintptr_t>(p) & 3) == 0,
+                "sat_fill32: bad args (4-byte aligned pointer, n >= 0)");
+  if (n == 0) return SAT_OK;
+  const int64_t blocks = std::min<int64_t>(std::max<int64_t>((n / 4 + 255) / 256, 1), 4096);
+  hipLaunchKernelGGL(fill32_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream),
+                     static_cast<unsigned*>(p), n, bits);
+  SAT_LAUNCH_CHECK("sat_fill32");
+  return SAT_OK;
+}
+
+extern "C" int sat_copy3d(const float* src, int64_t s0, int64_t s1, float* dst, int64_t d0,
+                          int64_t d1, int32_t n0, int32_t n1, int32_t n2, void* stream) {
+  SAT_CHECK_ARG(src && dst && n0 >= 0 && n1 >= 0 && n2 >= 0, "sat_copy3d: bad args");
+  const int64_t total = (int64_t)n0 * n1 * n2;
+  if (total == 0) return SAT_OK;
+  const bool v4 = n2 % 4 == 0 && s0 % 4 == 0 && s1 % 4 == 0 && d0 % 4 == 0 && d1 % 4 == 0 &&
+                  aligned16(src) && aligned16(dst);
+  const int64_t items = v4 ? total / 4 : total;
+  const int64_t blocks = std::min<int64_t>((items + 255) / 256, 8192);
+  if (v4)
+    hipLaunchKernelGGL(copy3d_kernel<true>, dim3((unsigned)blocks), dim3(256), 0,
+                       as_stream(stream), src, s0, s1, dst, d0, d1, n0, n1, n2);
+  else
+    hipLaunchKernelGGL(copy3d_kernel<false>, dim3((unsigned)blocks), dim3(256), 0,
+                       as_stream(stream), src, s0, s1, dst, d0, d1, n0, n1, n2);
+  SAT_LAUNCH_CHECK("sat_copy3d");
   return SAT_OK;
 }
 
@@ -1121,6 +1198,17 @@ extern "C" int sat_axpby(const float* x, float* y, int64_t n, float a, float b, 
   hipLaunchKernelGGL(axpby_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), x, y, n, a,
                      b);
   SAT_LAUNCH_CHECK("sat_axpby");
+  return SAT_OK;
+}
+
+extern "C" int sat_add(const float* x, const float* y, float* z, int64_t n, void* stream) {
+  SAT_CHECK_ARG(x && y && z && n >= 0 && n % 4 == 0 && aligned16(x) && aligned16(y) &&
+                    aligned16(z), "sat_add: 16-byte aligned operands, n % 4 == 0");
+  if (n == 0) return SAT_OK;
+  hipLaunchKernelGGL(add3_kernel, dim3(grid_for(n / 4)), dim3(256), 0, as_stream(stream),
+                     reinterpret_cast<const float4*>(x), reinterpret_cast<const float4*>(y),
+                     reinterpret_cast<float4*>(z), n / 4);
+  SAT_LAUNCH_CHECK("sat_add");
   return SAT_OK;
 }
 

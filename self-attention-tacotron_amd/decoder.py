@@ -50,9 +50,10 @@ def teacher_inputs(targets: torch.Tensor, r: int, n_feed: int) -> torch.Tensor:
     pure data movement."""
     B, T, M = targets.shape
     Tp = T // r
-    x = torch.zeros(Tp, B, M * n_feed, device=targets.device, dtype=targets.dtype)
+    x = torch.empty(Tp, B, M * n_feed, device=targets.device, dtype=targets.dtype)
     g = targets.view(B, Tp, M * r)
-    x[1:].copy_(g[:, :-1, M * (r - n_feed):].transpose(0, 1))
+    K.fill_(x[0])
+    K.copy3d_(x[1:], g[:, :-1, M * (r - n_feed):].transpose(0, 1))
     return x
 
 
@@ -86,11 +87,12 @@ def decoder_inputs(P: Dict[str, torch.Tensor], hp, d: Dims, targets: torch.Tenso
     aux.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(aux):
         if hist is not None:
-            hist[0].zero_()
-            hist[1][3][0, :, 0] = 1.0                    # AL1 row 0 (forward_attention.py:131-133)
+            K.fill_(hist[0])
+            K.copy3d_(hist[1][3][0, :, 0:1], K.ones(B, 1, device=dev))   # AL1 row 0
+            #                                                  (forward_attention.py:131-133)
         g = targets.view(B, Tp, M * r)
-        xin[0].zero_()                                   # the go frame
-        xin[1:].copy_(g[:, :-1, M * (r - nf):].transpose(0, 1))
+        K.fill_(xin[0])                                  # the go frame
+        K.copy3d_(xin[1:], g[:, :-1, M * (r - nf):].transpose(0, 1))
         for i in range(len(d.dec_prenet)):
             K.linear(pres[i], P[f"decoder/prenet{i}/kernel"], P[f"decoder/prenet{i}/bias"],
                      act="relu", mul=mk(f"dec/prenet{i}"), out=pres[i + 1])
@@ -339,8 +341,8 @@ def _lstm_buffers(Tp, B, U, f32, c=None, h=None):
     """(h_raw [T',B,U], c [T'+1,B,U], h [T'+1,B,U], gates [T',B,4U]) histories (c, h zeroed:
     given from a zeros_group, or allocated here)."""
     return (torch.empty(Tp, B, U, **f32),
-            c if c is not None else torch.zeros(Tp + 1, B, U, **f32),
-            h if h is not None else torch.zeros(Tp + 1, B, U, **f32),
+            c if c is not None else K.zeros(Tp + 1, B, U, device=f32["device"]),
+            h if h is not None else K.zeros(Tp + 1, B, U, device=f32["device"]),
             torch.empty(Tp, B, 4 * U, **f32))
 
 

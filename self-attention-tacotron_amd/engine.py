@@ -88,7 +88,7 @@ class Tacotron:
 
     def backward(self, saved, zero: bool = True):
         if zero:
-            self.grads.zero_()
+            K.fill_(self.grads)
         model_backward(self.P, self.G, self.hp, self.d, saved, self.ws, attn_tile=self.attn_tile,
                        pipe=self.pipe)
 

@@ -358,13 +358,78 @@ def empty_group(*shapes, device):
     return buf, out
 
 
+def fill_(t: torch.Tensor, value: float = 0.0) -> torch.Tensor:
+    """t[...] = value (float32 or int32 device tensor, contiguous) with sat_fill32 -- the
+    captured step's zero-initialised buffers and error words without a framework fill."""
+    if not t.is_contiguous() or t.element_size() != 4 or not t.is_cuda:
+        raise ValueError("fill_: contiguous 4-byte device tensor expected")
+    if t.dtype == torch.float32:
+        bits = ctypes.c_uint32.from_buffer(ctypes.c_float(value)).value
+    elif t.dtype == torch.int32:
+        bits = int(value) & 0xFFFFFFFF
+    else:
+        raise ValueError(f"fill_: unsupported dtype {t.dtype}")
+    _lib.call("sat_fill32", _p(t), t.numel(), bits, _stream())
+    return t
+
+
+def zeros(*shape, device, dtype=torch.float32) -> torch.Tensor:
+    """torch.zeros without the framework fill kernel (sat_fill32)."""
+    return fill_(torch.empty(*shape, device=device, dtype=dtype))
+
+
+def copy3d_(dst: torch.Tensor, src: torch.Tensor) -> torch.Tensor:
+    """dst[...] = src[...] for same-shape tensors of up to 3 dims with unit innermost strides
+    (a transposed view made contiguous, a strided slice into a step buffer) -- sat_copy3d."""
+    if dst.shape != src.shape or dst.dim() > 3 or dst.dtype != torch.float32 or \
+            src.dtype != torch.float32:
+        raise ValueError("copy3d_: same-shape float32 tensors of <= 3 dims expected")
+    shp = [1] * (3 - dst.dim()) + list(dst.shape)
+    ss = [0] * (3 - src.dim()) + list(src.stride())
+    ds = [0] * (3 - dst.dim()) + list(dst.stride())
+    if shp[2] > 1 and (ss[2] != 1 or ds[2] != 1):
+        raise ValueError("copy3d_: unit innermost strides expected")
+    _lib.call("sat_copy3d", _p(src), ss[0], ss[1], _p(dst), ds[0], ds[1], shp[0], shp[1], shp[2],
+              _stream())
+    return dst
+
+
+def add(x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+    """x + y (same-shape contiguous float32) as one sat_add launch."""
+    if x.shape != y.shape or not (x.is_contiguous() and y.is_contiguous()):
+        raise ValueError("add: same-shape contiguous tensors expected")
+    z = torch.empty_like(x)
+    _lib.call("sat_add", _p(x), _p(y), _p(z), x.numel(), _stream())
+    return z
+
+
+_ONES = {}
+
+
+def ones(*shape, device) -> torch.Tensor:
+    """A cached read-only float32 tensor of ones (made once per device, before any capture)."""
+    n = int(torch.Size(shape).numel())
+    dev = torch.device(device)
+    buf = _ONES.get(dev)
+    if buf is None or buf.numel() < n:
+        buf = _ONES[dev] = torch.ones(max(n, 4096), device=dev)
+    return buf[:n].view(*shape)
+
+
+def contiguous(x: torch.Tensor) -> torch.Tensor:
+    """x made contiguous with sat_copy3d (x itself when it already is)."""
+    if x.is_contiguous():
+        return x
+    return copy3d_(torch.empty(x.shape, device=x.device, dtype=x.dtype), x)
+
+
 def zeros_group(*shapes, device):
     """Several zero-initialised float32 tensors carved from ONE zeroed buffer (one fill launch
     instead of one per tensor in the captured step); every piece starts on a 256-byte boundary
     (the kernels' 16-byte operand alignment)."""
     sizes = [int(torch.Size(sh).numel()) for sh in shapes]
     pads = [(n + 63) // 64 * 64 for n in sizes]
-    buf = torch.zeros(sum(pads), device=device, dtype=torch.float32)
+    buf = zeros(sum(pads), device=device)
     out, off = [], 0
     for sh, n, pn in zip(shapes, sizes, pads):
         out.append(buf[off:off + n].view(sh))

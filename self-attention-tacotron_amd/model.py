@@ -101,7 +101,7 @@ def sa_transformer_fwd(x, P, scope, heads, causal, probs_mask, sv, key):
     """SelfAttentionTransformer.call (modules/module.py:363-371): x + tanh(Dense(MHA(x)))."""
     y = mha_fwd(x, P, f"{scope}/mha", heads, causal, probs_mask, sv, key)
     u = K.linear(y, P[f"{scope}/transform/kernel"], P[f"{scope}/transform/bias"], act="tanh")
-    z = torch.add(x, u)                                              # residual (one launch)
+    z = K.add(x, u)                                                  # residual (one launch)
     sv[key]["u"] = u
     sv[key]["z"] = z
     return z
@@ -117,9 +117,9 @@ def encoder_fwd(P, bn: BNState, hp, d: PR.Dims, ids, lengths, masks, training, w
     mk = (lambda n: masks[n]) if masks is not None else (lambda n: None)
     emb = torch.empty(B, N, d.embed, device=dev)
     if err is None:
-        err = torch.zeros(1, dtype=torch.int32, device=dev)
+        err = K.zeros(1, dtype=torch.int32, device=dev)
     else:
-        err.zero_()
+        K.fill_(err)
     K.embedding_fwd(P["embedding"], ids, emb, 0, err)
     sv["emb_err"] = err
     x = emb
@@ -269,7 +269,7 @@ def head_fwd(P, hp, d: PR.Dims, dout_sm: torch.Tensor, masks, sv):
     """RNNTransformer training-branch tail (modules/module.py:754-764)."""
     Tp, B, Dd = dout_sm.shape
     mk = (lambda n: masks[n]) if masks is not None else (lambda n: None)
-    D = dout_sm.transpose(0, 1).contiguous()                          # [B, T', D] (data movement)
+    D = K.contiguous(dout_sm.transpose(0, 1))                         # [B, T', D] (data movement)
     z = D
     for h in range(d.dec_hops):
         z = sa_transformer_fwd(z, P, f"decoder/self_attention{h}", d.dec_heads, True,
@@ -316,10 +316,9 @@ def model_forward(P, bn: BNState, hp, d: PR.Dims, batch: Dict[str, torch.Tensor]
         ids_s = batch["speaker_id"]
         spk = torch.empty(ids_s.shape[0], d.spk_dim, device=m1.device)
         if health is None:
-            sv["spk_err"] = torch.zeros(1, dtype=torch.int32, device=m1.device)
+            sv["spk_err"] = K.zeros(1, dtype=torch.int32, device=m1.device)
         else:
-            sv["spk_err"] = health[9:10]
-            sv["spk_err"].zero_()
+            sv["spk_err"] = K.fill_(health[9:10])
         K.embedding_fwd(P["speaker_embedding"], ids_s, spk, d.spk_offset, sv["spk_err"])
     dout, dsv = decoder_forward(P, hp, d, m1, m2, lengths, batch["mel"], masks,
                                 attn_tile=attn_tile, spk=spk, persistent=persistent,

@@ -59,11 +59,12 @@ for k in o_new:
     d = (o_new[k] - o_old[k]).abs()
     print(f"  {k:6s} max|new-old| {float(d.max()):.3e}  mean {float(d.mean()):.3e}")
 os.environ["SAT_ATTN_FWD8"] = "1"
-prof = torch.zeros(256 * 16 + 8 * 8 * 16 + 8 * 8 * 4, dtype=torch.int64, device="cuda")
+prof = torch.zeros(256 * 16 + 8 * 8 * 16 + 8 * 8 * 4 + 8 * 8 * 4 + 64, dtype=torch.int64,
+                   device="cuda")
 orig(**dict(kw, prof=prof))
 torch.cuda.synchronize()
 ev = prof[256 * 16:256 * 16 + 8 * 8 * 16].view(8, 8, 16).cpu().double() / 100.0   # [step][wave][event] us
-sp = prof[256 * 16 + 8 * 8 * 16:].view(8, 8, 4).cpu().double() / 100.0  # [step][wave][B drain, B poll, A drain, A poll] us
+sp = prof[256 * 16 + 8 * 8 * 16:256 * 16 + 8 * 8 * 20].view(8, 8, 4).cpu().double() / 100.0  # [step][wave][B drain, B poll, A drain, A poll] us
 # (all zero unless libsat_hip was built with -DSAT_FWD8_TRACE=1)
 ev = ev - ev[:, 0:1, 0:1]                                          # vs wave 0's loop start
 print("per-wave event clocks of workgroup 0 (us after wave 0's step start, mean of steps 100..107)")
@@ -83,3 +84,12 @@ for i, n in enumerate(names[:15]):
     col = pr[rows, i]
     print(f"  {n:24s} {float(col.mean()) / Tp:6.3f} us/step (max {float(col.max()) / Tp:6.3f})")
 print(f"  total {float(pr[rows].sum(1).mean()) / Tp:.3f} us/step")
+gv = prof[256 * 16 + 8 * 8 * 20:256 * 16 + 8 * 8 * 24].view(8, 8, 4).cpu().double()   # [step][j][ev]
+if float(gv.abs().sum()) > 0:
+    print("group 0 hand-off skew (trace build; us, relative to the earliest A publish of the step)")
+    base = gv[:, :, 0].min(1, keepdim=True).values
+    rel = (gv - base[:, :, None]) / 100.0
+    m = rel[:7].mean(0)      # step 107's B staging lies past the recorded window
+    for j in range(8):
+        print(f"  wg {j}: A published {float(m[j, 0]):5.2f}  A staged {float(m[j, 1]):5.2f}  "
+              f"B published {float(m[j, 2]):5.2f}  B staged {float(m[j, 3]):5.2f}")

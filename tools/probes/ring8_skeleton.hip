@@ -15,9 +15,12 @@ __device__ __forceinline__ float spin(float x, int n) {
 
 // pre: 0 = poll after the shadow compute; 1 = first poll load issued before the shadow (checked
 // after it); 2 = issued halfway through the shadow
+// nbar: further LDS-synchronised phases per hand-off (each: one LDS write, barrier, dependent
+// LDS read of another wave's word) -- the empty-phase floor of the real kernel's schedule
 __global__ void __launch_bounds__(512) ring8_kernel(float* RA, float* RB, int T, int crit,
-                                                    int shadow, int xl_on, int pre, int* err,
-                                                    long long* clk) {
+                                                    int shadow, int xl_on, int pre, int nbar,
+                                                    int* err, long long* clk) {
+  __shared__ float ph_w[8][64];
   __shared__ float4 st[8][64];
   const int g = blockIdx.x % 32, j = blockIdx.x / 32;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -62,6 +65,11 @@ __global__ void __launch_bounds__(512) ring8_kernel(float* RA, float* RB, int T,
       st[wave][lane] = x;
       lds_barrier();
       acc += st[(wave + 1) & 7][lane].x * 1e-6f;
+      for (int k = 0; k < nbar; ++k) {
+        ph_w[wave][lane] = acc;
+        lds_barrier();
+        acc += ph_w[(wave + 1 + k) & 7][lane ^ 1] * 1e-6f;
+      }
       const long long tr = wall_clock64();
       // event record of block 0, wave 0, steps 100..163: {poll start, poll done, after barrier,
       // spins} relative to the step's publish
@@ -77,8 +85,8 @@ __global__ void __launch_bounds__(512) ring8_kernel(float* RA, float* RB, int T,
 }
 
 extern "C" int ring8(float* RA, float* RB, int T, int crit, int shadow, int xl, int pre,
-                     int* err, long long* clk, void* stream) {
+                     int nbar, int* err, long long* clk, void* stream) {
   hipLaunchKernelGGL(ring8_kernel, dim3(256), dim3(512), 0, static_cast<hipStream_t>(stream), RA,
-                     RB, T, crit, shadow, xl, pre, err, clk);
+                     RB, T, crit, shadow, xl, pre, nbar, err, clk);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -8,15 +8,15 @@ import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 so = os.path.join(HERE, "ring8_skeleton.so")
-if True:
+if not os.path.exists(so) or os.path.getmtime(so) < os.path.getmtime(os.path.join(HERE, "ring8_skeleton.hip")):
     subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "--offload-arch=gfx950", "-shared", "-fPIC",
                     "-I" + os.path.join(HERE, "../../include"),
                     os.path.join(HERE, "ring8_skeleton.hip"), "-o", so], check=True)
 lib = ctypes.CDLL(so)
 dev = torch.device("cuda")
 T = 500
-for xl, pre in [(1, 0), (1, 2)]:
-    for crit, shadow in [(0, 0), (0, 25), (0, 50), (0, 100)]:
+for xl, pre, nbar in [(1, 0, 0), (0, 0, 0), (1, 0, 3), (1, 0, 4), (1, 0, 8)]:
+    for crit, shadow in [(0, 0), (0, 50), (25, 0)]:
         RA = torch.zeros(2 * 32 * 8 * 64 * 4, device=dev)
         RB = torch.zeros_like(RA)
         err = torch.zeros(2, dtype=torch.int32, device=dev)
@@ -26,7 +26,7 @@ for xl, pre in [(1, 0), (1, 2)]:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             lib.ring8(ctypes.c_void_p(RA.data_ptr()), ctypes.c_void_p(RB.data_ptr()), T, crit, shadow,
-                      xl, pre, ctypes.c_void_p(err.data_ptr()), ctypes.c_void_p(clk.data_ptr()),
+                      xl, pre, nbar, ctypes.c_void_p(err.data_ptr()), ctypes.c_void_p(clk.data_ptr()),
                       ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
             e1.record()
             torch.cuda.synchronize()
@@ -36,5 +36,5 @@ for xl, pre in [(1, 0), (1, 2)]:
         evs = " ".join(f"ph{ph}: poll@{float(ev[:, ph, 0].mean()) * 10:5.0f}ns done@{float(ev[:, ph, 1].mean()) * 10:5.0f} "
                        f"bar@{float(ev[:, ph, 2].mean()) * 10:5.0f} spins {float(ev[:, ph, 3].mean()):4.1f}"
                        for ph in range(2))
-        print(f"xl={xl} pre={pre} crit={crit:4d} shadow={shadow:4d} FMAs/phase: {us / T:6.3f} us/step "
+        print(f"xl={xl} pre={pre} bars/handoff={1 + nbar} crit={crit:4d} shadow={shadow:4d} FMAs/phase: {us / T:6.3f} us/step "
               f"(in-kernel {inner / T:6.3f}), err {int(err[0])} | {evs}", flush=True)

@@ -990,10 +990,10 @@ int dec_attn_fwd8_launch(const SatDecAttnFwd* a, hipStream_t s) {
     set_error("sat_decoder_attention_fwd: scratch clear failed");
     return SAT_ERR_HIP;
   }
-  // RED needs wave 7 free of energy positions (ceil(N / 8) <= 28); SAT_FWD8_RED=0 forces the
-  // two-barrier staging (A/B switch)
+  // RED needs wave 7 free of energy positions (ceil(N / 8) <= 28); SAT_FWD8_RED=1 selects it
+  // (A/B switch; the two-barrier staging stays the default until measured on hardware)
   const char* red_env = getenv("SAT_FWD8_RED");
-  const bool red = p.P <= 28 && !(red_env && red_env[0] == '0');
+  const bool red = p.P <= 28 && (red_env && red_env[0] == '1');
   if (red) hipLaunchKernelGGL(dec_attn_fwd8_kernel<true>, dim3(kGmax * kW), dim3(kTh), 0, s, p);
   else hipLaunchKernelGGL(dec_attn_fwd8_kernel<false>, dim3(kGmax * kW), dim3(kTh), 0, s, p);
   SAT_LAUNCH_CHECK("sat_decoder_attention_fwd");

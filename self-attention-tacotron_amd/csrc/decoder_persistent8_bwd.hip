@@ -683,9 +683,9 @@ int dec_attn_bwd8_launch(const SatDecAttnBwd* a, hipStream_t s) {
     set_error("sat_decoder_attention_bwd: scratch clear failed");
     return SAT_ERR_HIP;
   }
-  // SAT_BWD8_RED=0: the two-barrier Q staging (A/B switch)
+  // SAT_BWD8_RED=1: the Q records reduced at staging (A/B switch; off by default until measured)
   const char* red_env = getenv("SAT_BWD8_RED");
-  if (!(red_env && red_env[0] == '0'))
+  if (red_env && red_env[0] == '1')
     hipLaunchKernelGGL(dec_attn_bwd8_kernel<true>, dim3(kGmax * kW), dim3(kTh), 0, s, p);
   else
     hipLaunchKernelGGL(dec_attn_bwd8_kernel<false>, dim3(kGmax * kW), dim3(kTh), 0, s, p);

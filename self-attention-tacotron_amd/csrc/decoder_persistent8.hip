@@ -30,7 +30,6 @@
 // up and the grid drains.
 #include "sat_common.h"
 #include "persistent.h"
-#include <cstdlib>
 
 #ifndef SAT_FWD8_TRACE
 #define SAT_FWD8_TRACE 0
@@ -104,30 +103,6 @@ __device__ __forceinline__ float4 quad_gather(float x) {
   return make_float4(x, dpp_mov<0x101>(x), dpp_mov<0x102>(x), dpp_mov<0x103>(x));
 }
 
-// sum / max over lane bits 3..5 (the 8 lanes l & 7 + 8k, one per producer record): row_ror:8,
-// then the 16- and 32-lane swaps; every step adds commuted pairs, so all 8 lanes of a group end
-// with identical bits, and every group (and every wave, every workgroup) forms the same tree
-__device__ __forceinline__ float stride8_sum(float v) {
-  v += dpp_mov<0x128>(v);
-  auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  v = __uint_as_float(r[0]) + __uint_as_float(r[1]);
-  r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
-}
-__device__ __forceinline__ float stride8_max(float v) {
-  v = fmaxf(v, dpp_mov<0x128>(v));
-  auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  v = fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
-  r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
-}
-
-// RED = reduce-at-staging schedule (N <= 224, i.e. wave 7 holds no energy positions): each
-// wave polls ONE slice of all 8 producers' records (lane = producer l >> 3, chunk l & 7) and
-// sums them in registers (stride8_sum), so a hand-off costs one barrier instead of two (stage,
-// then combine / q sum); the normalise of step t-1 moves into A_t's shadow (each energy wave
-// forms its own s_{t-1} window; wave 7 the alignment alpha_{t-1} and the histories).
-template <bool RED>
 __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
   // resident operands
   __shared__ __attribute__((aligned(16))) float kc[kPmax][kQ];       // [K1 + b1 | K2] rows
@@ -143,7 +118,6 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
   __shared__ __attribute__((aligned(16))) float hbuf[kU];        // h_t states (next LSTM input)
   __shared__ __attribute__((aligned(16))) float cbuf[kC];        // c_{t-1}
   __shared__ __attribute__((aligned(16))) float4 qst[kW][64];    // staged query partials
-  __shared__ __attribute__((aligned(16))) float4 qsum4[kQ / 4];  // RED: q_t (summed at staging)
   __shared__ __attribute__((aligned(16))) float4 recs[kW][kR4];  // staged records B_{t-1}
   __shared__ __attribute__((aligned(16))) float hst[kUW];        // own units' h_t (tagged)
   __shared__ __attribute__((aligned(16))) float hraw[kUW];       // own units' raw outputs
@@ -322,80 +296,6 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
 #endif
     };
     ev(0);
-    // statistics of step t-1 (RED: formed by every wave at the B staging, used again in the
-    // normalise of A_t's shadow)
-    float nM1 = 0.f, nZ1 = 1.f, nA1 = 1.f, nM2 = 0.f, nZ2 = 1.f;
-    if constexpr (RED) {
-      // ============ 1'. records B_{t-1}, reduced while staged: lane l = (producer jj = l >> 3,
-      //                  slot qq = l & 7): the c1 chunk 8 wave + qq, the statistics, lanes qq == 0
-      //                  the c2 chunk `wave`; wave 0 lanes 16..26 the halo words
-      if (t > 0) {
-        const int rb0 = ((s & 1) * B + b) * kW;
-        const unsigned want = lsb_tag(s);
-        const int jj = lane >> 3, qq = lane & 7;
-        const int rec4 = (rb0 + jj) * (kRB / 4);
-        const int i1 = rec4 + kRBctx / 4 + 8 * wave + qq;
-        const int i4 = rec4 + (kRBctx + kM1) / 4 + wave;
-        const bool has4 = qq == 0;
-        const int hq = lane - 16;
-        const bool hl = wave == 0 && hq >= 0 && hq < 11;
-        const bool hleft = hq < kPadL || hq >= kPadL + kPadR;
-        const bool hsrc = hl && (hleft ? has_left : has_right);
-        const int hw = (rb0 + (hleft ? j - 1 : j + 1)) * kRB +
-                       (hq < kPadL ? kRBet + hq : hq < kPadL + kPadR ? kRBeh + hq - kPadL
-                                                                     : kRBal + hq - kPadL - kPadR);
-        float4 x1 = make_float4(0.f, 0.f, 0.f, 0.f), x2 = x1, x3 = x1, x4 = x1;
-        float hv = 0.f;
-        bool ok1 = false, ok2 = false, ok3 = false, ok4 = !has4, ok5 = !hsrc;
-        for (unsigned spins = 0;; ++spins) {
-          if (!ok1) x1 = ldc4(rRB, i1);
-          if (!ok2) x2 = ldc4(rRB, rec4);
-          if (!ok3) x3 = ldc4(rRB, rec4 + 1);
-          if (!ok4) x4 = ldc4(rRB, i4);
-          if (!ok5) hv = ldc(rRB, hsrc ? hw : 0);
-          ok1 = tag_ok4(x1, want);
-          ok2 = ok2 || tag_ok4(x2, want);
-          ok3 = ok3 || tag_ok4(x3, want);
-          ok4 = ok4 || tag_ok4(x4, want);
-          ok5 = ok5 || tag_ok(hv, want);
-          if (!any_lane(!(ok1 && ok2 && ok3 && ok4 && ok5)) || gave_up) break;
-          if (poll_give_up(spins, p.err)) { gave_up = true; break; }
-          __builtin_amdgcn_s_sleep(1);
-        }
-        // record scales (identical bits in every lane, wave and workgroup of the group)
-        nM1 = stride8_max(x2.x);
-        nM2 = stride8_max(x2.w);
-        const float sc1 = __expf(x2.x - nM1), sc2 = __expf(x2.w - nM2);
-        nZ1 = stride8_sum(x2.y * sc1);
-        nA1 = stride8_sum(x2.z * sc1);
-        nZ2 = stride8_sum(x3.x * sc2);
-        const float r1 = __builtin_amdgcn_rcpf(nA1), r2 = __builtin_amdgcn_rcpf(nZ2);
-        const float4 c1 = make_float4(stride8_sum(x1.x * sc1) * r1, stride8_sum(x1.y * sc1) * r1,
-                                      stride8_sum(x1.z * sc1) * r1, stride8_sum(x1.w * sc1) * r1);
-        const float4 c2 = make_float4(stride8_sum(x4.x * sc2) * r2, stride8_sum(x4.y * sc2) * r2,
-                                      stride8_sum(x4.z * sc2) * r2, stride8_sum(x4.w * sc2) * r2);
-        float4* cb4 = reinterpret_cast<float4*>(cbuf);
-        float4* rec0 = reinterpret_cast<float4*>(p.REC0 + ((int64_t)t * B + b) * kK0);
-        if (lane < 8) {
-          cb4[8 * wave + lane] = c1;
-          if (j == 0) rec0[8 * wave + lane] = c1;
-        }
-        if (lane == 0) {
-          cb4[kM1 / 4 + wave] = c2;
-          if (j == 0) rec0[kM1 / 4 + wave] = c2;
-        }
-        if (hl) halo[hq] = hv;
-      }
-      tick(0);
-      ev(1);
-      tick(1);
-      ev(2);
-      tick(2);
-      ev(3);
-      lds_barrier();
-      tick(3);
-      ev(4);
-    } else {
     // ============ 1. records B_{t-1}: wave jj stages record jj (wave 0 lanes 16..26 the halos)
     if (t > 0) {
       const int rb0 = ((s & 1) * B + b) * kW;
@@ -544,7 +444,6 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
     lds_barrier();
     tick(3);
     ev(4);
-    }   // !RED
 
     // ============ 2. LSTM step t: c part of the dot, gates (one activation per lane), cell;
     //                 publish record A_t
@@ -649,77 +548,7 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
     //                 10-tap product (modules/forward_attention.py:98-101)
     // energy role: lane = dim chunk c (4 dims of [D1 | D2]), wave = positions 4w .. 4w+3
     float4 Lr[4];
-    if constexpr (RED) {
-      // e_{t-1}(n) on the window, -inf where masked (eown / halo written before the last barriers)
-      auto e_at = [&](int n) -> float {
-        if (n < 0 || n >= len) return -INFINITY;
-        if (n < n0) return halo[n - n0 + kPadL];
-        if (n < n0 + nt) return eown[n - n0];
-        return halo[kPadL + (n - n0 - nt)];
-      };
-      if (4 * wave < nt) {
-        // this wave's s_{t-1} window n0 + 4 wave - 4 .. + 12 (lane < 13), the same arithmetic
-        // as wave 7's S1 history; step 0 reads the initial state the prologue put in sp
-        float sv = 0.f;
-        if (lane < 4 + kKW - 1) {
-          if (t == 0) {
-            sv = 4 * wave + lane < nt + kKW - 1 ? sp[4 * wave + lane] : 0.f;
-          } else {
-            const float e = e_at(n0 - kPadL + 4 * wave + lane);
-            sv = e == -INFINITY ? 0.f : __expf(e - nM1) * __builtin_amdgcn_rcpf(nZ1);
-          }
-        }
-        const int c = lane;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) Lr[i] = *reinterpret_cast<const float4*>(&kc[4 * wave + i][4 * c]);
-#pragma unroll
-        for (int k = 0; k < kKW; ++k) {
-          const float4 wk = *reinterpret_cast<const float4*>(&cwl[k][4 * c]);
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const float sk = rdl(sv, i + k);
-            Lr[i].x = fmaf(sk, wk.x, Lr[i].x); Lr[i].y = fmaf(sk, wk.y, Lr[i].y);
-            Lr[i].z = fmaf(sk, wk.z, Lr[i].z); Lr[i].w = fmaf(sk, wk.w, Lr[i].w);
-          }
-        }
-      } else if (wave == 7 && t > 0) {
-        // normalise step t-1 on the own positions: s_{t-1} on the window (sp, for the LOC
-        // history) and the S1 row, alpha_{t-1} (tagged: it travels in record B_t's halo), the
-        // S2 / ST rows
-        const unsigned bit = lsb_tag(t);
-        if (lane < nt + kKW - 1) {
-          const float e = e_at(n0 - kPadL + lane);
-          const float sv = e == -INFINITY ? 0.f : __expf(e - nM1) * __builtin_amdgcn_rcpf(nZ1);
-          sp[lane] = sv;
-          if (lane >= kPadL && lane < nt + kPadL)
-            p.S1[((int64_t)t * B + b) * N + n0 + lane - kPadL] = sv;
-        }
-        const float* ap = alf[(t - 1) & 1];      // alpha_{t-2} at n0-1+k
-        if (lane <= nt) {
-          const int k = lane, n = n0 - 1 + k;
-          float av = 0.f;
-          if (n >= 0) {
-            const float a_n = k >= 1 ? ap[k] : halo[kPadL + kPadR + 1];
-            const float a_m = k >= 2 ? ap[k - 1] : halo[kPadL + kPadR + k];
-            const float e = e_at(n);
-            const float pe = e == -INFINITY ? 0.f : __expf(e - nM1);
-            av = ((1.f - u) * a_n + u * a_m + 1e-7f) * pe * __builtin_amdgcn_rcpf(nA1);
-          }
-          const float at = tagf(av, bit);
-          alf[t & 1][k] = at;
-          if (k >= 1) p.AL1[((int64_t)t * B + b) * N + n] = at;
-        }
-        if (lane < nt) {
-          const float e2 = e2own[lane];
-          p.S2[((int64_t)s * B + b) * N + n0 + lane] =
-              e2 == -INFINITY ? 0.f : __expf(e2 - nM2) * __builtin_amdgcn_rcpf(nZ2);
-        }
-        if (j == 0 && lane == 0) {
-          float* stp = p.ST + ((int64_t)s * B + b) * 4;
-          stp[0] = nM1; stp[1] = nZ1; stp[2] = nA1 / nZ1; stp[3] = nZ2;
-        }
-      }
-    } else if (4 * wave < nt) {
+    if (4 * wave < nt) {
       const int c = lane;
 #pragma unroll
       for (int i = 0; i < 4; ++i) Lr[i] = *reinterpret_cast<const float4*>(&kc[4 * wave + i][4 * c]);
@@ -737,32 +566,8 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
     tick(8);
     ev(9);
 
-    // ============ 5. records A_t
-    if constexpr (RED) {
-      // lane l = (producer jj = l >> 3, query chunk 8 wave + (l & 7)), summed over the producers
-      // in registers; lanes < 8 also stage producer `wave`'s h_t words
-      const unsigned want = lsb_tag(t);
-      const int ra0 = ((t & 1) * B + b) * kW;
-      const int k4 = 8 * wave + (lane & 7);
-      const int i1 = (ra0 + (lane >> 3)) * (kRA / 4) + k4;
-      const int i2 = ((ra0 + wave) * kRA + kQ) / 4 + lane;
-      const bool two = lane < kUW / 4;
-      float4 x1 = make_float4(0.f, 0.f, 0.f, 0.f), x2 = x1;
-      bool ok1 = false, ok2 = !two;
-      for (unsigned spins = 0;; ++spins) {
-        if (!ok1) x1 = ldc4(rRA, i1);
-        if (!ok2) x2 = ldc4(rRA, i2);
-        ok1 = tag_ok4(x1, want);
-        ok2 = ok2 || tag_ok4(x2, want);
-        if (!any_lane(!(ok1 && ok2)) || gave_up) break;
-        if (poll_give_up(spins, p.err)) { gave_up = true; break; }
-        __builtin_amdgcn_s_sleep(1);
-      }
-      const float4 q4 = make_float4(stride8_sum(x1.x), stride8_sum(x1.y), stride8_sum(x1.z),
-                                    stride8_sum(x1.w));
-      if (lane < 8) qsum4[k4] = q4;
-      if (two) reinterpret_cast<float4*>(hbuf)[(kUW / 4) * wave + lane] = x2;   // units 32 wave + 4 lane
-    } else {
+    // ============ 5. records A_t: wave jj stages record jj (query partial, h_t states)
+    {
       const unsigned want = lsb_tag(t);
       const int ra = (((t & 1) * B + b) * kW + wave) * kRA;
       const bool two = lane < kUW / 4;
@@ -793,7 +598,7 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
 #endif
       qst[wave][lane] = x1;
       if (two) reinterpret_cast<float4*>(hbuf)[(kUW / 4) * wave + lane] = x2;   // units 32 jj + 4 lane
-    }   // !RED
+    }
     tick(9);
     ev(10);
     lds_barrier();
@@ -804,14 +609,9 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
     if (4 * wave < nt) {
       const unsigned bit = lsb_tag(t);
       const int c = lane;
-      float4 q;
-      if constexpr (RED) {
-        q = qsum4[c];
-      } else {
-        q = qst[0][c];
+      float4 q = qst[0][c];
 #pragma unroll
-        for (int k = 1; k < kW; ++k) q = add4(q, qst[k][c]);
-      }
+      for (int k = 1; k < kW; ++k) q = add4(q, qst[k][c]);
       if (j == 0 && wave == 0) reinterpret_cast<float4*>(p.Q + ((int64_t)t * B + b) * kQ)[c] = q;
       const float4 v4 = *reinterpret_cast<const float4*>(&vcat[4 * c]);
       const bool d1 = c < kD1 / 4;
@@ -959,15 +759,14 @@ bool dec_attn_fwd8_eligible(const SatDecAttnFwd* a) {
 // Scratch: records A / B and the placement words live in the QP buffer of
 // sat_decoder_attention_scratch (2 B 32 256 floats >= 2 B 8 (288 + 320) + 256).
 int dec_attn_fwd8_launch(const SatDecAttnFwd* a, hipStream_t s) {
-  int dev = 0, cus = 0, per_cu = 0, per_cu2 = 0;
+  int dev = 0, cus = 0, per_cu = 0;
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, dec_attn_fwd8_kernel<true>, kTh, 0) != hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu2, dec_attn_fwd8_kernel<false>, kTh, 0) != hipSuccess) {
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, dec_attn_fwd8_kernel, kTh, 0) != hipSuccess) {
     set_error("sat_decoder_attention_fwd: device query failed");
     return SAT_ERR_HIP;
   }
-  SAT_CHECK_ARG((int64_t)cus * std::min(per_cu, per_cu2) >= kGmax * kW,
+  SAT_CHECK_ARG((int64_t)cus * per_cu >= kGmax * kW,
                 "sat_decoder_attention_fwd: fewer than 256 co-resident workgroups on this device");
   Fwd8P p;
   p.B = a->B; p.N = a->N; p.T = a->T;
@@ -990,12 +789,7 @@ int dec_attn_fwd8_launch(const SatDecAttnFwd* a, hipStream_t s) {
     set_error("sat_decoder_attention_fwd: scratch clear failed");
     return SAT_ERR_HIP;
   }
-  // RED needs wave 7 free of energy positions (ceil(N / 8) <= 28); SAT_FWD8_RED=1 selects it
-  // (A/B switch; the two-barrier staging stays the default until measured on hardware)
-  const char* red_env = getenv("SAT_FWD8_RED");
-  const bool red = p.P <= 28 && (red_env && red_env[0] == '1');
-  if (red) hipLaunchKernelGGL(dec_attn_fwd8_kernel<true>, dim3(kGmax * kW), dim3(kTh), 0, s, p);
-  else hipLaunchKernelGGL(dec_attn_fwd8_kernel<false>, dim3(kGmax * kW), dim3(kTh), 0, s, p);
+  hipLaunchKernelGGL(dec_attn_fwd8_kernel, dim3(kGmax * kW), dim3(kTh), 0, s, p);
   SAT_LAUNCH_CHECK("sat_decoder_attention_fwd");
   return SAT_OK;
 }

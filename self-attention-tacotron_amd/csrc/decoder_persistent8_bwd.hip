@@ -27,7 +27,6 @@
 // sat_decoder_attention_bwd_dq_parts).  Bounded spins as everywhere (persistent.h).
 #include "sat_common.h"
 #include "persistent.h"
-#include <cstdlib>
 
 namespace sat {
 namespace {
@@ -94,18 +93,6 @@ __device__ __forceinline__ void transpose_reduce4(float* v) {
   v[0] = group16_sum(v[0]);
 }
 
-// sum over lane bits 3..5 (one lane per producer record; decoder_persistent8.hip stride8_sum)
-__device__ __forceinline__ float stride8_sum(float v) {
-  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xF, 0xF, true));
-  auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  v = __uint_as_float(r[0]) + __uint_as_float(r[1]);
-  r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
-}
-
-// RED: the Q_t records reduced while staged (lane = (producer l >> 3, dq chunk 8 wave + (l & 7)),
-// summed in registers): one barrier instead of stage + barrier + wave 0's serial sum + barrier
-template <bool RED>
 __global__ void __launch_bounds__(kTh) dec_attn_bwd8_kernel(Bwd8P p) {
   __shared__ __attribute__((aligned(16))) float v1s[kPmax][kM1];
   __shared__ __attribute__((aligned(16))) float v2s[kPmax][kM2];
@@ -488,28 +475,7 @@ __global__ void __launch_bounds__(kTh) dec_attn_bwd8_kernel(Bwd8P p) {
     tick(9);
 
     // ===================== phase Z(t)
-    // ---- 1. records Q_t
-    if constexpr (RED) {
-      const int k4 = 8 * wave + (lane & 7);
-      const int i1 = ((((q & 1) * B + b) * kW + (lane >> 3)) * kRQ) / 4 + k4;
-      float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
-      for (unsigned spins = 0;; ++spins) {
-        x = ldc4(rRQ, i1);
-        if (!any_lane(!tag_ok4(x, bit)) || gave_up) break;
-        if (poll_give_up(spins, p.err)) { gave_up = true; break; }
-        __builtin_amdgcn_s_sleep(1);
-      }
-      const float4 a = make_float4(stride8_sum(x.x), stride8_sum(x.y), stride8_sum(x.z),
-                                   stride8_sum(x.w));
-      if (lane < 8) {
-        reinterpret_cast<float4*>(qb)[k4] = a;
-        if (j == 0) reinterpret_cast<float4*>(p.DQP + ((int64_t)t * B + b) * kQ)[k4] = a;
-      }
-      tick(10);
-      lds_barrier();
-      tick(11);
-    } else {
-    // (wave jj stages record jj's dq partial)
+    // ---- 1. records Q_t (wave jj stages record jj's dq partial)
     {
       const int rq = (((q & 1) * B + b) * kW + wave) * kRQ;
       float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -532,7 +498,6 @@ __global__ void __launch_bounds__(kTh) dec_attn_bwd8_kernel(Bwd8P p) {
     }
     lds_barrier();
     tick(11);
-    }   // !RED
     // ---- 2. the own units' reverse step: query term dq_t . Wq[unit] (wave w, units 4w..4w+3:
     //         row q of the wave holds unit q's sum), recurrent product from the R_{t+1} h rows,
     //         then the cell lane's pointwise reverse step (lstm.hip lstm_bwd_block)
@@ -652,15 +617,14 @@ bool dec_attn_bwd8_eligible(const SatDecAttnBwd* a) {
 // Scratch: records Q / R and the placement words live in the RDP buffer of
 // sat_decoder_attention_bwd_scratch (2 B 32 544 floats >= 2 B 8 (320 + 544) + 256).
 int dec_attn_bwd8_launch(const SatDecAttnBwd* a, hipStream_t s) {
-  int dev = 0, cus = 0, per_cu = 0, per_cu2 = 0;
+  int dev = 0, cus = 0, per_cu = 0;
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, dec_attn_bwd8_kernel<true>, kTh, 0) != hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu2, dec_attn_bwd8_kernel<false>, kTh, 0) != hipSuccess) {
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, dec_attn_bwd8_kernel, kTh, 0) != hipSuccess) {
     set_error("sat_decoder_attention_bwd: device query failed");
     return SAT_ERR_HIP;
   }
-  SAT_CHECK_ARG((int64_t)cus * std::min(per_cu, per_cu2) >= kGmax * kW,
+  SAT_CHECK_ARG((int64_t)cus * per_cu >= kGmax * kW,
                 "sat_decoder_attention_bwd: fewer than 256 co-resident workgroups on this device");
   Bwd8P p;
   p.B = a->B; p.N = a->N; p.T = a->T;
@@ -683,12 +647,7 @@ int dec_attn_bwd8_launch(const SatDecAttnBwd* a, hipStream_t s) {
     set_error("sat_decoder_attention_bwd: scratch clear failed");
     return SAT_ERR_HIP;
   }
-  // SAT_BWD8_RED=1: the Q records reduced at staging (A/B switch; off by default until measured)
-  const char* red_env = getenv("SAT_BWD8_RED");
-  if (red_env && red_env[0] == '1')
-    hipLaunchKernelGGL(dec_attn_bwd8_kernel<true>, dim3(kGmax * kW), dim3(kTh), 0, s, p);
-  else
-    hipLaunchKernelGGL(dec_attn_bwd8_kernel<false>, dim3(kGmax * kW), dim3(kTh), 0, s, p);
+  hipLaunchKernelGGL(dec_attn_bwd8_kernel, dim3(kGmax * kW), dim3(kTh), 0, s, p);
   SAT_LAUNCH_CHECK("sat_decoder_attention_bwd");
   return SAT_OK;
 }

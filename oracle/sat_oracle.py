@@ -172,17 +172,40 @@ def lstm_sequence(x, lengths, w, b, zc, zh, mc, mh, reverse: bool):
     return torch.stack(outs, dim=1)
 
 
-def encoder(ids, lengths, p, bufs, hp, masks, training):
-    """SelfAttentionCBHGEncoder.call (modules/module.py:425-438) -> (M1, M2, alignments)."""
+def encoder(ids, lengths, p, bufs, hp, masks, training, kinks=None):
+    """SelfAttentionCBHGEncoder.call (modules/module.py:425-438) -> (M1, M2, alignments).
+
+    ``kinks`` (tests only): the branch another implementation took at every piecewise-linear
+    point of the encoder front -- {"prenet{i}": relu gate, "bank": conv-bank relu gate,
+    "pool_first": max-pool window choice (out[n] takes x[n]), "proj1": relu gate} as 0/1
+    tensors.  The float64 arithmetic then follows the same sub-gradient branch, so a gradient
+    comparison measures rounding, not which side of a kink fp32 and fp64 landed on (a gate that
+    flips routes an element's whole gradient differently).  The forward values change only by
+    the flipped elements' distance from the kink (fp32 rounding)."""
     g = (lambda k: masks[k]) if masks is not None else (lambda k: None)
+    kk = kinks or {}
     x = p["embedding"][ids]                                           # ext Embedding
     for i in range(len(hp.encoder_prenet_out_units)):
-        x = prenet(x, p, f"encoder/prenet{i}", g(f"enc/prenet{i}"))
+        if f"prenet{i}" in kk:
+            x = dense(x, p, f"encoder/prenet{i}") * kk[f"prenet{i}"]
+            m = g(f"enc/prenet{i}")
+            x = x * m if m is not None else x
+        else:
+            x = prenet(x, p, f"encoder/prenet{i}", g(f"enc/prenet{i}"))
     inp = x
-    bank = [conv_bn(x, p, bufs, f"encoder/cbhg/conv_bank/K{k}", training, relu=True)
-            for k in range(1, hp.max_filter_width + 1)]               # module.py:78
-    y = maxpool2_same(torch.cat(bank, dim=-1))                        # :80
-    y = conv_bn(y, p, bufs, "encoder/cbhg/proj1", training, relu=True)   # :82
+    if "bank" in kk:
+        z = torch.cat([conv_bn(x, p, bufs, f"encoder/cbhg/conv_bank/K{k}", training, relu=False)
+                       for k in range(1, hp.max_filter_width + 1)], dim=-1) * kk["bank"]
+        nxt = torch.cat([z[:, 1:, :], z[:, -1:, :]], dim=1)
+        y = torch.where(kk["pool_first"].bool(), z, nxt)
+    else:
+        bank = [conv_bn(x, p, bufs, f"encoder/cbhg/conv_bank/K{k}", training, relu=True)
+                for k in range(1, hp.max_filter_width + 1)]           # module.py:78
+        y = maxpool2_same(torch.cat(bank, dim=-1))                    # :80
+    if "proj1" in kk:
+        y = conv_bn(y, p, bufs, "encoder/cbhg/proj1", training, relu=False) * kk["proj1"]
+    else:
+        y = conv_bn(y, p, bufs, "encoder/cbhg/proj1", training, relu=True)   # :82
     y = conv_bn(y, p, bufs, "encoder/cbhg/proj2", training, relu=False)  # :83
     y = y + inp                                                       # :86
     if "encoder/cbhg/adjustment/kernel" in p:                         # :88-89
@@ -413,11 +436,12 @@ def losses(mel, stop, targets, target_mask, done, done_mask):
 
 
 def model_forward(p: Dict[str, Tensor], bufs, hp, batch: Dict[str, Tensor],
-                  masks: Optional[Dict[str, Tensor]], training: bool, record=False):
+                  masks: Optional[Dict[str, Tensor]], training: bool, record=False, kinks=None):
     """model_fn TRAIN/EVAL-with-teacher forward (models/models.py:23-173).  Returns a dict with
-    mel [B,T,mels], stop [B,T',1], loss terms and intermediate tensors."""
+    mel [B,T,mels], stop [B,T',1], loss terms and intermediate tensors.  ``kinks``: see
+    ``encoder`` (tests only)."""
     m1, m2, enc_al = encoder(batch["source"], batch["source_length"], p, bufs, hp, masks,
-                             training)
+                             training, kinks=kinks)
     spk = None
     if hp.use_speaker_embedding and hp.speaker_embedd_to_prenet:
         spk = p["speaker_embedding"][batch["speaker_id"] - hp.speaker_embedding_offset]

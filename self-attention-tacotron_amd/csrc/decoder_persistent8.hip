@@ -370,9 +370,13 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
             const bool first = wave < kM1 / 64;    // wave-uniform: c1 dims (waves 0..3) or c2
             const float sc = first ? sc1 : sc2;
             const float* rf = reinterpret_cast<const float*>(&recs[0][2]) + tid;
-            float a = 0.f;
+            float a = 0.f, a2 = 0.f;      // two 4-deep chains (even / odd records)
 #pragma unroll
-            for (int k = 0; k < kW; ++k) a = fmaf(rf[k * kR4 * 4], rdl(sc, k), a);
+            for (int k = 0; k < kW; k += 2) {
+              a = fmaf(rf[k * kR4 * 4], rdl(sc, k), a);
+              a2 = fmaf(rf[(k + 1) * kR4 * 4], rdl(sc, k + 1), a2);
+            }
+            a += a2;
             a *= __builtin_amdgcn_rcpf(first ? A1 : Z2);
             cbuf[tid] = a;
             if (j == 0) p.REC0[((int64_t)t * B + b) * kK0 + tid] = a;
@@ -519,15 +523,18 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
       // column 32w + (l & 31), units 16 (l >> 5) .. + 15; halves folded, quads gathered
       {
         const int col = 32 * wave + (lane & 31), u0 = 16 * (lane >> 5);
-        float a = 0.f;
+        // four independent 4-deep chains (one per unit quad), summed pairwise: a 16-deep
+        // dependent chain put its FMA latency on the step's path
+        float ak[4];
 #pragma unroll
         for (int k4 = 0; k4 < 4; ++k4) {
           const float4 h4 = *reinterpret_cast<const float4*>(&hraw[u0 + 4 * k4]);
-          a = fmaf(h4.x, wqs[u0 + 4 * k4][col], a);
+          float a = h4.x * wqs[u0 + 4 * k4][col];
           a = fmaf(h4.y, wqs[u0 + 4 * k4 + 1][col], a);
           a = fmaf(h4.z, wqs[u0 + 4 * k4 + 2][col], a);
-          a = fmaf(h4.w, wqs[u0 + 4 * k4 + 3][col], a);
+          ak[k4] = fmaf(h4.w, wqs[u0 + 4 * k4 + 3][col], a);
         }
+        const float a = (ak[0] + ak[1]) + (ak[2] + ak[3]);
         const float4 q4 = quad_gather(fold32(a));
         const int ra = (((t & 1) * B + b) * kW + j) * kRA;
         if (lane < 32 && (lane & 3) == 0) stc4x(xl, rRA, ra / 4 + 8 * wave + (lane >> 2), tagf4(q4, bit));
@@ -693,23 +700,30 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
       const int rb = (((t & 1) * B + b) * kW + j) * kRB;
       const int col = lane & 31, r0 = 16 * (lane >> 5);
       const float* ws = &wsc[wave][0][r0];
-      float c = 0.f;
+      float ck[4];
 #pragma unroll
       for (int k4 = 0; k4 < 4; ++k4) {
         const float4 w4 = *reinterpret_cast<const float4*>(ws + 4 * k4);
-        c = fmaf(w4.x, v1s[r0 + 4 * k4][32 * wave + col], c);
+        float c = w4.x * v1s[r0 + 4 * k4][32 * wave + col];
         c = fmaf(w4.y, v1s[r0 + 4 * k4 + 1][32 * wave + col], c);
         c = fmaf(w4.z, v1s[r0 + 4 * k4 + 2][32 * wave + col], c);
-        c = fmaf(w4.w, v1s[r0 + 4 * k4 + 3][32 * wave + col], c);
+        ck[k4] = fmaf(w4.w, v1s[r0 + 4 * k4 + 3][32 * wave + col], c);
       }
+      const float c = (ck[0] + ck[1]) + (ck[2] + ck[3]);
       const float4 c4 = quad_gather(fold32(c));
       if (lane < 32 && (lane & 3) == 0)
         stc4x(xl, rRB, (rb + kRBctx) / 4 + 8 * wave + (lane >> 2), tagf4(c4, bit));
       if (wave == 0) {
         const float* ws2 = &wsc[0][1][r0];
-        float c2 = 0.f;
+        float c2k[4];
 #pragma unroll
-        for (int k = 0; k < 16; ++k) c2 = fmaf(ws2[k], v2s[r0 + k][col], c2);
+        for (int k4 = 0; k4 < 4; ++k4) {
+          float c = ws2[4 * k4] * v2s[r0 + 4 * k4][col];
+#pragma unroll
+          for (int k = 1; k < 4; ++k) c = fmaf(ws2[4 * k4 + k], v2s[r0 + 4 * k4 + k][col], c);
+          c2k[k4] = c;
+        }
+        const float c2 = (c2k[0] + c2k[1]) + (c2k[2] + c2k[3]);
         const float4 q4 = quad_gather(fold32(c2));
         if (lane < 32 && (lane & 3) == 0)
           stc4x(xl, rRB, (rb + kRBctx + kM1) / 4 + (lane >> 2), tagf4(q4, bit));

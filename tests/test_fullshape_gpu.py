@@ -38,7 +38,19 @@ def _report(name, **vals):
             f.write(json.dumps({"case": name, **vals}) + "\n")
 
 
-def _run(cuda, B, N, T, train, shape="max", seed=11, grads=False, preset="ljspeech"):
+def _gpu_kinks(sv, O):
+    """The HIP forward's branch at the encoder front's piecewise-linear points (prenet / conv
+    bank / proj1 ReLU gates, the max-pool window choice) for the oracle (``encoder(kinks=)``)."""
+    bank = sv["bank"]
+    nxt = torch.cat([bank[:, 1:], bank[:, -1:]], 1)
+    k = {"bank": bank > 0, "pool_first": bank >= nxt, "proj1": sv["p1"] > 0}
+    for i, x in enumerate(sv["enc_pre"][1:]):
+        k[f"prenet{i}"] = x > 0
+    return {n: v.double().cpu() for n, v in k.items()}
+
+
+def _run(cuda, B, N, T, train, shape="max", seed=11, grads=False, preset="ljspeech",
+         kinks=False):
     from sat_amd import data, engine, hparams, params
     from sat_amd.decoder import persistent_eligible
     from oracle import sat_oracle as O
@@ -60,7 +72,8 @@ def _run(cuda, B, N, T, train, shape="max", seed=11, grads=False, preset="ljspee
     p64 = {k: v.requires_grad_(grads) for k, v in O.to_torch(vals).items()}
     with torch.set_grad_enabled(grads):
         ref = O.model_forward(p64, O.to_torch(params.init_bn_buffers(hp)), hp, O.to_torch(b),
-                              None if mk is None else O.to_torch(mk), training=train)
+                              None if mk is None else O.to_torch(mk), training=train,
+                              kinks=_gpu_kinks(sv, O) if kinks else None)
         if grads:
             ref["loss"].backward()
     return hp, m, out, ref, p64, b
@@ -137,7 +150,15 @@ def test_c2_train_gradients_match_oracle(cuda):
     """The benched configuration itself: C2 (B=32, N=200, T=1000 -> 500 steps, every persistent
     grid on all 256 CUs, 32 hand-off groups over the 8 XCDs), train mode with injected dropout /
     zoneout masks: mel, stop and loss vs the float64 oracle, then every parameter gradient of
-    the BPTT vs float64 autograd (models/models.py:159-189)."""
-    hp, m, out, ref, p64, b = _run(cuda, 32, 200, 1000, True, seed=51, grads=True)
+    the BPTT vs float64 autograd (models/models.py:159-189).
+
+    At this size (6400 positions x 2048 conv-bank channels) a few of the encoder front's ReLU
+    gates and max-pool choices land on the other side of their kink in fp32 than in float64,
+    and each such flip routes that element's whole gradient differently: the conv-bank / prenet /
+    embedding gradients then differ by up to ~3e-2 of their max while every backward stage is
+    exact on its own inputs (profiles/r04_cbhg_bwd_stages.txt, tools/probes/enc_kinks.py).  The
+    oracle therefore takes the HIP forward's branch at those points (oracle ``encoder(kinks=)``:
+    the same sub-gradient), and the bar stays 2e-4 for every parameter."""
+    hp, m, out, ref, p64, b = _run(cuda, 32, 200, 1000, True, seed=51, grads=True, kinks=True)
     _compare_outputs("c2_train_outputs", out, ref, b)
     _compare_grads("c2_train_grad", m, p64, b)

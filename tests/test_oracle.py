@@ -177,6 +177,41 @@ def test_oracle_gradients_flow_everywhere():
     assert missing == []
 
 
+def test_oracle_kinks_from_its_own_forward_change_nothing():
+    """encoder(kinks=) with the gates / pool choices the float64 forward itself takes gives the
+    kink-free forward and gradients bit for bit (the option only fixes WHICH branch is taken at
+    a ReLU / max-pool kink; tests/test_fullshape_gpu.py feeds it the HIP forward's branches)."""
+    from sat_amd import hparams, params, data
+    hp = hparams.ljspeech_hparams()
+    vals = params.init_params(hp, seed=5)
+    bufs = O.to_torch(params.init_bn_buffers(hp))
+    b = O.to_torch(data.synthetic_batch(hp, 2, N=9, T=8, shape="ljs", seed=2))
+    m = O.to_torch(data.synthetic_masks(hp, 2, b["source"].shape[1], 4, seed=3))
+    # the float64 forward's own branches
+    x = O.to_torch(vals)["embedding"][b["source"]]
+    p0 = O.to_torch(vals)
+    kinks = {}
+    for i in range(len(hp.encoder_prenet_out_units)):
+        x = O.prenet(x, p0, f"encoder/prenet{i}", m[f"enc/prenet{i}"])
+        kinks[f"prenet{i}"] = (x > 0).double()
+    bank = torch.cat([O.conv_bn(x, p0, bufs, f"encoder/cbhg/conv_bank/K{k}", True, relu=True)
+                      for k in range(1, hp.max_filter_width + 1)], dim=-1)
+    nxt = torch.cat([bank[:, 1:], bank[:, -1:]], 1)
+    kinks["bank"], kinks["pool_first"] = (bank > 0).double(), (bank >= nxt).double()
+    kinks["proj1"] = (O.conv_bn(O.maxpool2_same(bank), p0, bufs, "encoder/cbhg/proj1", True,
+                                relu=True) > 0).double()
+    res = []
+    for kk in (None, kinks):
+        p = {k: v.clone().requires_grad_(True) for k, v in O.to_torch(vals).items()}
+        out = O.model_forward(p, bufs, hp, b, m, training=True, kinks=kk)
+        out["loss"].backward()
+        res.append((out["mel"].detach(), {k: v.grad for k, v in p.items()}))
+    (mel_a, g_a), (mel_b, g_b) = res
+    assert torch.equal(mel_a, mel_b)
+    for k in g_a:
+        assert torch.allclose(g_a[k], g_b[k], rtol=0, atol=1e-12 * float(g_a[k].abs().max()) + 1e-300), k
+
+
 @pytest.mark.parametrize("preset", ["ljspeech", "vctk"])
 def test_free_running_equals_teacher_forced_on_its_own_predictions(preset):
     """The PREDICT restatement (StopTokenBasedInferenceHelper feeding back the last predicted

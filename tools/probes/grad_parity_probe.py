@@ -30,13 +30,16 @@ for c in cases:
         g_ref = p.grad.numpy()
         scale = max(np.abs(g_ref).max(), 1e-4 * gmax)
         d = np.abs(grads[name].astype(np.float64) - g_ref)
-        rows.append((float(d.max() / scale), name, float(np.abs(g_ref).max()), float(d.mean() / scale)))
+        fro = float(np.sqrt((d ** 2).sum()) / max(np.sqrt((g_ref ** 2).sum()), 1e-30))
+        rows.append((float(d.max() / scale), name, float(np.abs(g_ref).max()), float(d.mean() / scale),
+                     fro))
     rows.sort(reverse=True)
     mel = out["mel"].double().cpu().numpy()
     print(f"== B={B} shape={shape} seed={seed}: loss {float(out['loss']):.9g} ref "
           f"{float(ref['loss']):.9g}, mel max {np.abs(mel - ref['mel'].detach().numpy()).max():.3e}, "
           f"gmax {gmax:.3e}", flush=True)
     for r in rows[:40]:
-        print(f"  {r[0]:.3e} (mean {r[3]:.2e}, |g|max {r[2]:.3e})  {r[1]}", flush=True)
+        print(f"  {r[0]:.3e} (mean {r[3]:.2e}, rel-Frobenius {r[4]:.2e}, |g|max {r[2]:.3e})  {r[1]}",
+              flush=True)
     del m, out, ref, p64
     torch.cuda.empty_cache()

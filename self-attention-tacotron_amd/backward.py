@@ -31,7 +31,9 @@ class Aux:
     must not hand its block to a later main-stream allocation while the branch may run)."""
 
     def __init__(self, device):
+        self.dev = device
         self.s = K.aux_stream(device)
+        self.used = [self.s]
         self.keep = []
 
     def run(self, fn, *tensors):
@@ -40,8 +42,15 @@ class Aux:
         with torch.cuda.stream(self.s):
             fn()
 
+    def switch(self):
+        """Later branches on a further stream, so they do not queue behind the branches issued
+        so far (the decoder's weight-gradient backlog)."""
+        self.s = K.aux_stream(self.dev, 1)
+        self.used.append(self.s)
+
     def join(self):
-        torch.cuda.current_stream().wait_stream(self.s)
+        for s in self.used:
+            torch.cuda.current_stream().wait_stream(s)
         self.keep.clear()
 
 
@@ -622,6 +631,8 @@ def model_backward(P, G, hp, d, sv, ws, attn_tile=32, pipe: Pipeline = SEQUENTIA
     lengths = sv["batch"]["source_length"]
     dm1 = K.seq_mask(dV1, lengths)
     dm2 = K.seq_mask(dV2, lengths)
+    if aux is not None and os.environ.get("SAT_AUX2") == "1":
+        aux.switch()      # A/B: the encoder's weight-gradient branches on their own stream
     encoder_bwd(P, G, hp, d, sv, dm1, dm2, lengths, masks, ws, aux=aux)
     if aux is not None:
         aux.join()                                    # every weight-gradient branch

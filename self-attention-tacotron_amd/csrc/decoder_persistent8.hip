@@ -265,9 +265,11 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
   };
   if ((tid0 >> 6) == 5) store_loc(0, tid0 & 63);   // f_0 from the initial state s_{-1}
 #if SAT_FWD8_TRACE
-  // per-wave event clocks of workgroup 0 over steps 100..107: prof[4096 + ...] (build with
+  // per-wave event clocks of workgroup 1 over steps 100..107: prof[4096 + ...] (build with
   // -DSAT_FWD8_TRACE=1; tools/probes/fwd8_profile.py prints them)
-  long long* evt = (p.prof && blockIdx.x == 0) ? p.prof + 256 * 16 : nullptr;
+  // (workgroup 1 = group 1's first: the per-wave stores must not perturb group 0, whose
+  // hand-off skew gevt measures)
+  long long* evt = (p.prof && blockIdx.x == 1) ? p.prof + 256 * 16 : nullptr;
   // group 0's eight workgroups, wave 0: {A published, A staged, B published, B staged} of steps
   // 100..107 at prof[256 * 16 + 8 * 8 * 20 + ((t - 100) * 8 + j) * 4 + k] (hand-off skew)
   long long* gevt = (p.prof && g == 0) ? p.prof + 256 * 16 + 8 * 8 * 20 + j * 4 : nullptr;
@@ -370,16 +372,14 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
             const bool first = wave < kM1 / 64;    // wave-uniform: c1 dims (waves 0..3) or c2
             const float sc = first ? sc1 : sc2;
             const float* rf = reinterpret_cast<const float*>(&recs[0][2]) + tid;
-            float a = 0.f, a2 = 0.f;      // two 4-deep chains (even / odd records)
+            float a = 0.f;
 #pragma unroll
-            for (int k = 0; k < kW; k += 2) {
-              a = fmaf(rf[k * kR4 * 4], rdl(sc, k), a);
-              a2 = fmaf(rf[(k + 1) * kR4 * 4], rdl(sc, k + 1), a2);
-            }
-            a += a2;
+            for (int k = 0; k < kW; ++k) a = fmaf(rf[k * kR4 * 4], rdl(sc, k), a);
             a *= __builtin_amdgcn_rcpf(first ? A1 : Z2);
             cbuf[tid] = a;
-            if (j == 0) p.REC0[((int64_t)t * B + b) * kK0 + tid] = a;
+            // the REC0 context row: every workgroup forms all 288 dims, each stores its own 36
+            // (the whole row from workgroup 0 alone put it a step-long offset behind its group)
+            if (tid / (kC / kW) == j) p.REC0[((int64_t)t * B + b) * kK0 + tid] = a;
           }
         } else {
           const unsigned bit = lsb_tag(t);
@@ -523,18 +523,15 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
       // column 32w + (l & 31), units 16 (l >> 5) .. + 15; halves folded, quads gathered
       {
         const int col = 32 * wave + (lane & 31), u0 = 16 * (lane >> 5);
-        // four independent 4-deep chains (one per unit quad), summed pairwise: a 16-deep
-        // dependent chain put its FMA latency on the step's path
-        float ak[4];
+        float a = 0.f;
 #pragma unroll
         for (int k4 = 0; k4 < 4; ++k4) {
           const float4 h4 = *reinterpret_cast<const float4*>(&hraw[u0 + 4 * k4]);
-          float a = h4.x * wqs[u0 + 4 * k4][col];
+          a = fmaf(h4.x, wqs[u0 + 4 * k4][col], a);
           a = fmaf(h4.y, wqs[u0 + 4 * k4 + 1][col], a);
           a = fmaf(h4.z, wqs[u0 + 4 * k4 + 2][col], a);
-          ak[k4] = fmaf(h4.w, wqs[u0 + 4 * k4 + 3][col], a);
+          a = fmaf(h4.w, wqs[u0 + 4 * k4 + 3][col], a);
         }
-        const float a = (ak[0] + ak[1]) + (ak[2] + ak[3]);
         const float4 q4 = quad_gather(fold32(a));
         const int ra = (((t & 1) * B + b) * kW + j) * kRA;
         if (lane < 32 && (lane & 3) == 0) stc4x(xl, rRA, ra / 4 + 8 * wave + (lane >> 2), tagf4(q4, bit));
@@ -619,7 +616,8 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
       float4 q = qst[0][c];
 #pragma unroll
       for (int k = 1; k < kW; ++k) q = add4(q, qst[k][c]);
-      if (j == 0 && wave == 0) reinterpret_cast<float4*>(p.Q + ((int64_t)t * B + b) * kQ)[c] = q;
+      // the Q row likewise: chunks 8j .. 8j+7 from workgroup j
+      if (wave == 0 && (c >> 3) == j) reinterpret_cast<float4*>(p.Q + ((int64_t)t * B + b) * kQ)[c] = q;
       const float4 v4 = *reinterpret_cast<const float4*>(&vcat[4 * c]);
       const bool d1 = c < kD1 / 4;
       float e[8];
@@ -700,30 +698,23 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
       const int rb = (((t & 1) * B + b) * kW + j) * kRB;
       const int col = lane & 31, r0 = 16 * (lane >> 5);
       const float* ws = &wsc[wave][0][r0];
-      float ck[4];
+      float c = 0.f;
 #pragma unroll
       for (int k4 = 0; k4 < 4; ++k4) {
         const float4 w4 = *reinterpret_cast<const float4*>(ws + 4 * k4);
-        float c = w4.x * v1s[r0 + 4 * k4][32 * wave + col];
+        c = fmaf(w4.x, v1s[r0 + 4 * k4][32 * wave + col], c);
         c = fmaf(w4.y, v1s[r0 + 4 * k4 + 1][32 * wave + col], c);
         c = fmaf(w4.z, v1s[r0 + 4 * k4 + 2][32 * wave + col], c);
-        ck[k4] = fmaf(w4.w, v1s[r0 + 4 * k4 + 3][32 * wave + col], c);
+        c = fmaf(w4.w, v1s[r0 + 4 * k4 + 3][32 * wave + col], c);
       }
-      const float c = (ck[0] + ck[1]) + (ck[2] + ck[3]);
       const float4 c4 = quad_gather(fold32(c));
       if (lane < 32 && (lane & 3) == 0)
         stc4x(xl, rRB, (rb + kRBctx) / 4 + 8 * wave + (lane >> 2), tagf4(c4, bit));
       if (wave == 0) {
         const float* ws2 = &wsc[0][1][r0];
-        float c2k[4];
+        float c2 = 0.f;
 #pragma unroll
-        for (int k4 = 0; k4 < 4; ++k4) {
-          float c = ws2[4 * k4] * v2s[r0 + 4 * k4][col];
-#pragma unroll
-          for (int k = 1; k < 4; ++k) c = fmaf(ws2[4 * k4 + k], v2s[r0 + 4 * k4 + k][col], c);
-          c2k[k4] = c;
-        }
-        const float c2 = (c2k[0] + c2k[1]) + (c2k[2] + c2k[3]);
+        for (int k = 0; k < 16; ++k) c2 = fmaf(ws2[k], v2s[r0 + k][col], c2);
         const float4 q4 = quad_gather(fold32(c2));
         if (lane < 32 && (lane & 3) == 0)
           stc4x(xl, rRB, (rb + kRBctx + kM1) / 4 + (lane >> 2), tagf4(q4, bit));

@@ -55,13 +55,15 @@ def _stream_scratch(device, tag: str, nbytes: int) -> int:
 _AUX = {}
 
 
-def aux_stream(device) -> torch.cuda.Stream:
+def aux_stream(device, which: int = 0) -> torch.cuda.Stream:
     """The step's second stream (independent branches beside the encoder, forward and backward),
     one per device, made on first use -- the eager warm-up before any graph capture; the GEMM
-    split-K and column-reduction scratch are keyed per stream already."""
-    s = _AUX.get(device.index)
+    split-K and column-reduction scratch are keyed per stream already.  ``which=1``: a third
+    stream (the encoder backward's weight-gradient branches, SAT_AUX2=1)."""
+    key = (device.index, which)
+    s = _AUX.get(key)
     if s is None:
-        s = _AUX[device.index] = torch.cuda.Stream(device=device)
+        s = _AUX[key] = torch.cuda.Stream(device=device)
     return s
 
 

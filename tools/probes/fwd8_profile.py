@@ -67,7 +67,7 @@ ev = prof[256 * 16:256 * 16 + 8 * 8 * 16].view(8, 8, 16).cpu().double() / 100.0 
 sp = prof[256 * 16 + 8 * 8 * 16:256 * 16 + 8 * 8 * 20].view(8, 8, 4).cpu().double() / 100.0  # [step][wave][B drain, B poll, A drain, A poll] us
 # (all zero unless libsat_hip was built with -DSAT_FWD8_TRACE=1)
 ev = ev - ev[:, 0:1, 0:1]                                          # vs wave 0's loop start
-print("per-wave event clocks of workgroup 0 (us after wave 0's step start, mean of steps 100..107)")
+print("per-wave event clocks of workgroup 1 (us after wave 0's step start, mean of steps 100..107)")
 print("  wave " + " ".join(f"{k:6d}" for k in range(16)))
 m = ev.mean(0)
 for w in range(8):
@@ -93,3 +93,10 @@ if float(gv.abs().sum()) > 0:
     for j in range(8):
         print(f"  wg {j}: A published {float(m[j, 0]):5.2f}  A staged {float(m[j, 1]):5.2f}  "
               f"B published {float(m[j, 2]):5.2f}  B staged {float(m[j, 3]):5.2f}")
+# per tile column j (mean over the groups): which segment makes one workgroup of a group slower
+print("segment clocks by workgroup j within the group (us/step, mean over groups)")
+print("  " + " ".join(f"{n[:10]:>10s}" for n in names[:15] if n != "-"))
+for jj in range(8):
+    rj = [g + 32 * jj for g in range(B)]
+    print(f"  j={jj} " + " ".join(f"{float(pr[rj, i].mean()) / Tp:10.3f}"
+                                  for i, n in enumerate(names[:15]) if n != "-"))

@@ -40,6 +40,14 @@
 #ifndef SAT_FWD8_HSTORE7
 #define SAT_FWD8_HSTORE7 1   // the cell's C0 / REC0 / H0RAW / G0 stores on wave 7 (A/B switch)
 #endif
+#ifndef SAT_FWD8_HMERGE
+// the h part of the gate sums inside the cell phase's dot (one dot, one transpose-reduce) rather
+// than a separate h-dot after publishing record B: 5.84 -> 5.78 us/step (three interleaved
+// rounds on one box).  The separate h-dot was meant to hide in B's latency, but the group's
+// last publisher (whichever workgroup it is) never waits -- every other record is already
+// there when it polls -- so its h-dot sat on the group's period (0: the old placement, A/B)
+#define SAT_FWD8_HMERGE 1
+#endif
 
 namespace sat {
 namespace {
@@ -456,6 +464,16 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
 #pragma unroll
       for (int q = 0; q < 8; ++q) acc[q] = f2{0.f, 0.f};
       if (t > 0) {
+#if SAT_FWD8_HMERGE
+        // h_{t-1} (staged with records A_{t-1}) and c_{t-1} in ONE dot and ONE transpose-reduce
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float xv = hbuf[64 * i + lane];
+          const f2 xx = {xv, xv};
+#pragma unroll
+          for (int q = 0; q < 8; ++q) acc[q] = __builtin_elementwise_fma(xx, w0[i][q], acc[q]);
+        }
+#endif
 #pragma unroll
         for (int i = 4; i < 8; ++i) {
           const float xv = cbuf[64 * (i - 4) + lane];
@@ -483,7 +501,11 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
       // lane holds column m = lane >> 2: activation of its gate (i, f, o sigmoid; j tanh via
       // 2 sigm(2x) - 1; forget_bias 1.0), then the cell lane (16q) gathers its unit's 4 gates
       const int gate = (lane >> 2) & 3;
+#if SAT_FWD8_HMERGE
+      const float pre = v[0] + xgn;
+#else
       const float pre = v[0] + gsum[wave][lane] + xgn;
+#endif
       const float sg = sigm_fast(gate == 1 ? 2.f * pre : pre + (gate == 2 ? 1.0f : 0.f));
       const float act = gate == 1 ? fmaf(2.f, sg, -1.f) : sg;
       const float gj = dpp_mov<0x104>(act);        // row_shl:4, 8, 12
@@ -730,7 +752,7 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
     tick(14);
     ev(15);
     // ============ 7. h part of step t+1's gate sums (h_t arrived with records A_t)
-    if (t + 1 < T) {
+    if (!SAT_FWD8_HMERGE && t + 1 < T) {
       f2 acc[8];
 #pragma unroll
       for (int q = 0; q < 8; ++q) acc[q] = f2{0.f, 0.f};

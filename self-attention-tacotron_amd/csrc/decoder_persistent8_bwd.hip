@@ -298,9 +298,7 @@ __global__ void __launch_bounds__(kTh) dec_attn_bwd8_kernel(Bwd8P p) {
       }
       if (tid < kC) {
         dcb[tid] = a;
-        // the RD row: every workgroup forms all 288 dims, each stores its own 36 (the whole
-        // row from workgroup 0 alone held it behind its group every step)
-        if (tid / (kC / kW) == j) p.RD[((int64_t)t * B + b) * kK0 + tid] = a;
+        if (j == 0) p.RD[((int64_t)t * B + b) * kK0 + tid] = a;
       }
       const float s = wave_sum_dpp(tid < kC ? a * y.cv : 0.f);   // waves 0-3: dc1.c1, 4: dc2.c2
       if (lane == 0) red[wave] = s;
@@ -496,7 +494,7 @@ __global__ void __launch_bounds__(kTh) dec_attn_bwd8_kernel(Bwd8P p) {
 #pragma unroll
       for (int w = 1; w < kW; ++w) a = add4(a, qz[w][lane]);
       reinterpret_cast<float4*>(qb)[lane] = a;
-      if ((lane >> 3) == j) reinterpret_cast<float4*>(p.DQP + ((int64_t)t * B + b) * kQ)[lane] = a;
+      if (j == 0) reinterpret_cast<float4*>(p.DQP + ((int64_t)t * B + b) * kQ)[lane] = a;
     }
     lds_barrier();
     tick(11);

@@ -666,6 +666,14 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
     } else {                                   // idle wave: its positions are padding
       const int r = 4 * wave + (lane & 3);
       if (lane < 4) eown[r] = -INFINITY; else if (lane < 8) e2own[r] = -INFINITY;
+      if (wave == 0 && (lane >> 3) == j) {
+        // no own positions (nt == 0, small N): the Q row's chunks 8j .. 8j+7 are still this
+        // workgroup's to store, summed in the same record order as the energy waves'
+        float4 q = qst[0][lane];
+#pragma unroll
+        for (int k = 1; k < kW; ++k) q = add4(q, qst[k][lane]);
+        reinterpret_cast<float4*>(p.Q + ((int64_t)t * B + b) * kQ)[lane] = q;
+      }
       if (wave == 7) {
         store_loc(t, lane);                    // the LOC history, off the critical path
         if (w7_stores && lane < kUW) {

@@ -486,8 +486,11 @@ def test_gemm_batched_b2(cuda):
     g = torch.Generator().manual_seed(12)
     nb, M, N, K1, K2 = 3, 70, 96, 64, 32
     A = torch.randn(nb, M, K1 + K2, generator=g)
-    B, B2 = torch.randn(nb, K1, N, generator=g), torch.randn(nb, K2, N, generator=g)
-    C = kernels.gemm(A.to(cuda), B.to(cuda), B2=B2.to(cuda))
+    # the second segment takes B's batch strides (SatGemmDesc has one b_sbatch): B2 is the
+    # leading K2 rows of a device buffer laid out like B
+    B, B2buf = torch.randn(nb, K1, N, generator=g), torch.randn(nb, K1, N, generator=g)
+    B2 = B2buf[:, :K2]
+    C = kernels.gemm(A.to(cuda), B.to(cuda), B2=B2buf.to(cuda)[:, :K2])
     ref = A.double() @ torch.cat([B, B2], 1).double()
     bound = 4e-7 * (A.double().abs() @ torch.cat([B, B2], 1).double().abs()) + 1e-7
     assert bool(((C.double().cpu() - ref).abs() <= bound).all())

@@ -76,7 +76,15 @@ typedef struct SatGemmDesc {
   float alpha, beta;
   const float* mul;
   int64_t mul_sm, mul_sbatch;
-  int32_t batch2, pad0;
+  /* tri (a hint; 0 = off): the causal self-attention's triangular structure, per batch matrix
+   * (row m = query position, column / reduction index = key position):
+   *   1: only the lower triangle of C is needed (column n <= row m): output tiles wholly above
+   *      the diagonal are skipped (C there is left unwritten);
+   *   2: A is lower-triangular (A[m][k] == 0 for k > m): each tile's reduction stops at its
+   *      last row;  3: A is upper-triangular (A[m][k] == 0 for k < m): it starts at its first.
+   * The skipped terms are exact zeros, so 2 / 3 give the same bits as the full product.
+   * Honoured by the LDS kernel; every other path computes the full product (also correct). */
+  int32_t batch2, tri;
   int64_t a_sbatch2, b_sbatch2, c_sbatch2, mul_sbatch2;
   const float* add;
   int64_t add_sm, add_sbatch;
@@ -747,11 +755,13 @@ int sat_copy3d(const float* src, int64_t s0, int64_t s1, float* dst, int64_t d0,
 
 /* ScaledDotProductAttentionMechanism softmax (modules/self_attention.py:45-65):
  * P = softmax(scale*S) per row of length L, causal (use_subsequent_mask) masks col > row%Lq,
- * Pd = P * mask (tf.layers.dropout on the probabilities).  Backward gives dS. */
+ * Pd = P * mask (tf.layers.dropout on the probabilities).  Backward gives dS; causal rows read
+ * P / dPd only up to the diagonal (dPd beyond it may be unwritten: SatGemmDesc.tri) and get
+ * dS = 0 there. */
 int sat_softmax_fwd(const float* S, float* P, float* Pd, const float* mask, int64_t R, int32_t L,
                     int32_t Lq, int32_t causal, float scale, void* stream);
 int sat_softmax_bwd(const float* P, const float* dPd, const float* mask, float* dS, int64_t R,
-                    int32_t L, float scale, void* stream);
+                    int32_t L, int32_t Lq, int32_t causal, float scale, void* stream);
 
 /* Loss of models/models.py:159-173: l1_weight * L1(mel, tgt; tmask) + sigmoid xent(stop, done;
  * dmask), tf.losses SUM_BY_NONZERO_WEIGHTS.  out[0..4] = loss, L1, BCE, counts; if dmel/dstop

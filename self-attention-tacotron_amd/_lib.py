@@ -37,7 +37,7 @@ class SatGemmDesc(ctypes.Structure):
         ("bias", ctypes.c_void_p), ("bias_sbatch", ctypes.c_int64),
         ("alpha", ctypes.c_float), ("beta", ctypes.c_float),
         ("mul", ctypes.c_void_p), ("mul_sm", ctypes.c_int64), ("mul_sbatch", ctypes.c_int64),
-        ("batch2", ctypes.c_int32), ("pad0", ctypes.c_int32),
+        ("batch2", ctypes.c_int32), ("tri", ctypes.c_int32),
         ("a_sbatch2", ctypes.c_int64), ("b_sbatch2", ctypes.c_int64),
         ("c_sbatch2", ctypes.c_int64), ("mul_sbatch2", ctypes.c_int64),
         ("add", ctypes.c_void_p), ("add_sm", ctypes.c_int64), ("add_sbatch", ctypes.c_int64),
@@ -233,7 +233,7 @@ SIGNATURES = {
     "sat_add": [_P, _P, _P, _I64, _P],
     "sat_copy3d": [_P, _I64, _I64, _P, _I64, _I64, _I32, _I32, _I32, _P],
     "sat_softmax_fwd": [_P, _P, _P, _P, _I64, _I32, _I32, _I32, _F, _P],
-    "sat_softmax_bwd": [_P, _P, _P, _P, _I64, _I32, _F, _P],
+    "sat_softmax_bwd": [_P, _P, _P, _P, _I64, _I32, _I32, _I32, _F, _P],
     "sat_loss_fwd_bwd": [_P, _P, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _F, _P, _P, _P, _P, _P],
 }
 

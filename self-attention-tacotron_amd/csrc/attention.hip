@@ -943,7 +943,9 @@ __device__ __forceinline__ void attn_pg_store(const SatAttnParamGrad& p, const f
 template <int SLOTS, int F>
 __device__ __forceinline__ void pg_recompute_body(const SatAttnParamGrad& p) {
   constexpr int FL = F > 0 ? F : 1;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // wave-uniform (scalar) position: the per-step history addresses of de1 / de2 / loc are then
+  // scalar and their loads go through the scalar cache instead of 64-bit VALU address math
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nq = (p.N + 3) / 4;
   const int b = blockIdx.x / nq, n = 4 * (blockIdx.x - b * nq) + wave;
   const int nn = min(n, p.N - 1);
@@ -952,7 +954,11 @@ __device__ __forceinline__ void pg_recompute_body(const SatAttnParamGrad& p) {
   const int64_t bn = (int64_t)b * p.N + nn;
   const int64_t TBN = (int64_t)p.B * p.N;
 
-  float4 kk[SLOTS], bb[SLOTS], vv[SLOTS], lw[SLOTS][FL];
+  // tanh(x) = 1 - 2 / (1 + 2^(kE x)), kE = 2 log2(e): K + b1 and W_loc are held pre-scaled by kE
+  // and q is scaled once per step, so the exponent argument costs no extra multiply per element
+  // (z agrees with tanh_fast to a few ulp; the forward's ZH is not read here)
+  constexpr float kE = 2.8853900817779268f;
+  float4 kk[SLOTS], vv[SLOTS], lw[SLOTS][FL];
   float4 adk[SLOTS], adv[SLOTS], adw[SLOTS][FL];
   bool m1[SLOTS], ok[SLOTS];
   const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -962,13 +968,17 @@ __device__ __forceinline__ void pg_recompute_body(const SatAttnParamGrad& p) {
     ok[s] = c < Q;
     m1[s] = c < Q1;
     const int c1 = min(c, Q1 - 1), c2 = min(max(c - Q1, 0), p.D2 / 4 - 1);
-    kk[s] = m1[s] ? reinterpret_cast<const float4*>(p.K1 + bn * p.D1)[c1]
-                  : reinterpret_cast<const float4*>(p.K2 + bn * p.D2)[c2];
-    bb[s] = (m1[s] && p.b1) ? reinterpret_cast<const float4*>(p.b1)[c1] : z4;
+    // the step-independent part of tanh's exponent argument, pre-scaled: exp(2x) = 2^(kE x)
+    const float4 k4 = m1[s] ? reinterpret_cast<const float4*>(p.K1 + bn * p.D1)[c1]
+                            : reinterpret_cast<const float4*>(p.K2 + bn * p.D2)[c2];
+    const float4 b4 = (m1[s] && p.b1) ? reinterpret_cast<const float4*>(p.b1)[c1] : z4;
+    kk[s] = make_float4(kE * (k4.x + b4.x), kE * (k4.y + b4.y), kE * (k4.z + b4.z), kE * (k4.w + b4.w));
     vv[s] = m1[s] ? reinterpret_cast<const float4*>(p.v1)[c1] : reinterpret_cast<const float4*>(p.v2)[c2];
 #pragma unroll
-    for (int f = 0; f < F; ++f)
-      lw[s][f] = m1[s] ? reinterpret_cast<const float4*>(p.locW + (int64_t)f * p.D1)[c1] : z4;
+    for (int f = 0; f < F; ++f) {
+      const float4 w4 = m1[s] ? reinterpret_cast<const float4*>(p.locW + (int64_t)f * p.D1)[c1] : z4;
+      lw[s][f] = make_float4(kE * w4.x, kE * w4.y, kE * w4.z, kE * w4.w);
+    }
     adk[s] = z4; adv[s] = z4;
 #pragma unroll
     for (int f = 0; f < FL; ++f) adw[s][f] = z4;
@@ -1013,8 +1023,8 @@ __device__ __forceinline__ void pg_recompute_body(const SatAttnParamGrad& p) {
       acw = fmaf(sv[u], dfv[u], acw);
 #pragma unroll
       for (int s = 0; s < SLOTS; ++s) {
-        float pre[4] = {kk[s].x + qv[u][s].x + bb[s].x, kk[s].y + qv[u][s].y + bb[s].y,
-                        kk[s].z + qv[u][s].z + bb[s].z, kk[s].w + qv[u][s].w + bb[s].w};
+        float pre[4] = {fmaf(kE, qv[u][s].x, kk[s].x), fmaf(kE, qv[u][s].y, kk[s].y),
+                        fmaf(kE, qv[u][s].z, kk[s].z), fmaf(kE, qv[u][s].w, kk[s].w)};
         if (m1[s]) {
 #pragma unroll
           for (int f = 0; f < F; ++f) {
@@ -1027,7 +1037,7 @@ __device__ __forceinline__ void pg_recompute_body(const SatAttnParamGrad& p) {
         const float vs[4] = {vv[s].x, vv[s].y, vv[s].z, vv[s].w};
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          z[k] = tanh_fast(pre[k]);
+          z[k] = 1.f - 2.f * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(pre[k]));
           dp[k] = e * vs[k] * (1.f - z[k] * z[k]);
         }
         adk[s].x += dp[0]; adk[s].y += dp[1]; adk[s].z += dp[2]; adk[s].w += dp[3];

@@ -591,22 +591,25 @@ __global__ void softmax_fwd_kernel(const float* __restrict__ S, float* __restric
   }
 }
 
-// dS = scale * P * (dP - sum_j dP_j P_j), dP = dPd * mask
+// dS = scale * P * (dP - sum_j dP_j P_j), dP = dPd * mask.  Causal rows read P / dPd only up to
+// the diagonal (beyond it P is zero and dPd may be unwritten: the score products skip the tiles
+// above it, SatGemmDesc.tri) and write dS = 0 there -- the same bits as the full row's terms.
 __global__ void softmax_bwd_kernel(const float* __restrict__ P, const float* __restrict__ dPd,
                                    const float* __restrict__ mask, float* __restrict__ dS, int64_t R,
-                                   int L, float scale) {
+                                   int L, int Lq, int causal, float scale) {
   const int lane = threadIdx.x & 63;
   const int64_t r = blockIdx.x * (int64_t)(blockDim.x >> 6) + (threadIdx.x >> 6);
   if (r >= R) return;
+  const int lim = causal ? min(L, (int)(r % Lq) + 1) : L;
   const float* p = P + r * L;
   const float* g = dPd + r * L;
   const float* m = mask ? mask + r * L : nullptr;
   float acc = 0.f;
-  for (int j = lane; j < L; j += 64) acc += (m ? g[j] * m[j] : g[j]) * p[j];
+  for (int j = lane; j < lim; j += 64) acc += (m ? g[j] * m[j] : g[j]) * p[j];
   acc = wave_sum(acc);
   for (int j = lane; j < L; j += 64) {
-    const float dp = m ? g[j] * m[j] : g[j];
-    dS[r * L + j] = scale * p[j] * (dp - acc);
+    const float dp = j < lim ? (m ? g[j] * m[j] : g[j]) : 0.f;
+    dS[r * L + j] = j < lim ? scale * p[j] * (dp - acc) : 0.f;
   }
 }
 
@@ -654,10 +657,11 @@ __global__ void softmax_fwd_reg_kernel(const float* __restrict__ S, float* __res
 template <int NC>
 __global__ void softmax_bwd_reg_kernel(const float* __restrict__ P, const float* __restrict__ dPd,
                                        const float* __restrict__ mask, float* __restrict__ dS,
-                                       int64_t R, int L, float scale) {
+                                       int64_t R, int L, int Lq, int causal, float scale) {
   const int lane = threadIdx.x & 63;
   const int64_t r = blockIdx.x * (int64_t)(blockDim.x >> 6) + (threadIdx.x >> 6);
   if (r >= R) return;
+  const int lim = causal ? min(L, (int)(r % Lq) + 1) : L;
   const float* p = P + r * L;
   const float* g = dPd + r * L;
   const float* m = mask ? mask + r * L : nullptr;
@@ -665,19 +669,19 @@ __global__ void softmax_bwd_reg_kernel(const float* __restrict__ P, const float*
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
     const int j = lane + 64 * c;
-    pv[c] = j < L ? p[j] : 0.f;
-    dp[c] = j < L ? (m ? g[j] * m[j] : g[j]) : 0.f;
+    pv[c] = j < lim ? p[j] : 0.f;
+    dp[c] = j < lim ? (m ? g[j] * m[j] : g[j]) : 0.f;
   }
   float acc = 0.f;
 #pragma unroll
   for (int c = 0; c < NC; ++c)
-    if (lane + 64 * c < L) acc += dp[c] * pv[c];
+    if (lane + 64 * c < lim) acc += dp[c] * pv[c];
   acc = wave_sum(acc);
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
     const int j = lane + 64 * c;
     if (j >= L) break;
-    dS[r * L + j] = scale * pv[c] * (dp[c] - acc);
+    dS[r * L + j] = j < lim ? scale * pv[c] * (dp[c] - acc) : 0.f;
   }
 }
 
@@ -1226,14 +1230,17 @@ extern "C" int sat_softmax_fwd(const float* S, float* P, float* Pd, const float*
 }
 
 extern "C" int sat_softmax_bwd(const float* P, const float* dPd, const float* mask, float* dS,
-                               int64_t R, int32_t L, float scale, void* stream) {
-  SAT_CHECK_ARG(P && dPd && dS && R >= 0 && L > 0, "sat_softmax_bwd: bad args");
+                               int64_t R, int32_t L, int32_t Lq, int32_t causal, float scale,
+                               void* stream) {
+  SAT_CHECK_ARG(P && dPd && dS && R >= 0 && L > 0 && (!causal || Lq > 0),
+                "sat_softmax_bwd: bad args");
   const dim3 g(ceil_div(R, 4)), b(256);
   hipStream_t s = as_stream(stream);
-  if (L <= 256) hipLaunchKernelGGL(softmax_bwd_reg_kernel<4>, g, b, 0, s, P, dPd, mask, dS, R, L, scale);
-  else if (L <= 512) hipLaunchKernelGGL(softmax_bwd_reg_kernel<8>, g, b, 0, s, P, dPd, mask, dS, R, L, scale);
-  else if (L <= 1024) hipLaunchKernelGGL(softmax_bwd_reg_kernel<16>, g, b, 0, s, P, dPd, mask, dS, R, L, scale);
-  else hipLaunchKernelGGL(softmax_bwd_kernel, g, b, 0, s, P, dPd, mask, dS, R, L, scale);
+  const int lq = Lq > 0 ? Lq : 1;
+  if (L <= 256) hipLaunchKernelGGL(softmax_bwd_reg_kernel<4>, g, b, 0, s, P, dPd, mask, dS, R, L, lq, causal, scale);
+  else if (L <= 512) hipLaunchKernelGGL(softmax_bwd_reg_kernel<8>, g, b, 0, s, P, dPd, mask, dS, R, L, lq, causal, scale);
+  else if (L <= 1024) hipLaunchKernelGGL(softmax_bwd_reg_kernel<16>, g, b, 0, s, P, dPd, mask, dS, R, L, lq, causal, scale);
+  else hipLaunchKernelGGL(softmax_bwd_kernel, g, b, 0, s, P, dPd, mask, dS, R, L, lq, causal, scale);
   SAT_LAUNCH_CHECK("sat_softmax_bwd");
   return SAT_OK;
 }

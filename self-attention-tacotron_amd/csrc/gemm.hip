@@ -47,6 +47,7 @@ struct GemmP {
   int splits, kchunk;          // split-K: grid.z = splits (batch == 1), partial slabs in ws
   float* ws;
   int remap;                   // XCD-aware tile order over the xy plane
+  int tri = 0;                 // SatGemmDesc.tri (causal structure hint, LDS kernel only)
   int probe;                   // sat_gemm_probe_mode: 1 skip DMA, 2 skip epilogue (probes only)
   // fused column sums of B (SatGemmDesc.colsum_out): the LDS kernel treats A as having one more
   // row of ones (index m_real = M - 1), whose output row goes to cs_out instead of C
@@ -685,8 +686,13 @@ __global__ void __launch_bounds__((64 * lds_waves<BM, BN>())) gemm_lds_kernel(Ge
       ac0 = m0 - atap * p.a_C;
     }
   }
-  const int kbeg = split * p.kchunk;
-  const int kend = min(Kt, kbeg + p.kchunk);
+  // causal structure (SatGemmDesc.tri): tiles wholly above the diagonal are not needed (1);
+  // a triangular A's zero K-tiles are not loaded (2: lower, 3: upper) -- exact zeros either way
+  if (p.tri == 1 && n0 >= m0 + BM) return;
+  int kbeg = split * p.kchunk;
+  int kend = min(Kt, kbeg + p.kchunk);
+  if (p.tri == 2) kend = min(kend, m0 + BM);
+  if (p.tri == 3) kbeg = max(kbeg, m0 / BK * BK);
   const float* zero = g_gemm_zero;
   const float* ones = g_gemm_ones;
 
@@ -1341,6 +1347,7 @@ extern "C" int sat_gemm(const SatGemmDesc* d, void* stream) {
   p.probe = t_probe;
   p.cs_out = nullptr;
   p.m_real = d->M;
+  p.tri = (d->tri >= 1 && d->tri <= 3) ? d->tri : 0;
   hipStream_t s = as_stream(stream);
   const int nb = d->batch * p.batch2;
   p.ws = reinterpret_cast<float*>(d->ws);

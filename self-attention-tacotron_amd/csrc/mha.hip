@@ -46,10 +46,12 @@ struct HeadOp {
   int64_t sb, sh;          // batch (utterance) and head strides
 };
 
+// tri: SatGemmDesc.tri when the attention is causal (triangular scores / probabilities)
 int head_gemm(int M, int N, int K, HeadOp a, HeadOp b, float* C, int64_t c_sm, int64_t c_sb,
-              int64_t c_sh, float alpha, const SatMha* d, hipStream_t s) {
+              int64_t c_sh, float alpha, const SatMha* d, hipStream_t s, int tri = 0) {
   SatGemmDesc g = dense_desc();
   g.M = M; g.N = N; g.K = K;
+  g.tri = d->causal ? tri : 0;
   g.batch = d->B; g.batch2 = d->H;
   g.A = a.p; g.a_sm = a.sr; g.a_sk = a.sc; g.a_sbatch = a.sb; g.a_sbatch2 = a.sh;
   g.B = b.p; g.b_sk = b.sr; g.b_sn = b.sc; g.b_sbatch = b.sb; g.b_sbatch2 = b.sh;
@@ -129,14 +131,16 @@ extern "C" int sat_mha_fwd(const SatMha* d, void* stream) {
     SAT_TRY(dense(d->x, d->Wv, d->bv, d->v, R, d->W, D, 0.f, d, s));
   }
   // S[b,h] = Q_h K_h^T                                               (self_attention.py:55)
+  // (causal: only the tiles on / below the diagonal; the softmax reads no further)
   SAT_TRY(head_gemm(L, L, dh, {d->q, D, 1, LD, dh}, {d->k, 1, D, LD, dh}, S, L, HLL, LL, 1.f, d,
-                    s));
+                    s, 1));
   float* Pd = d->probs_mask ? d->Pd : d->P;
   SAT_TRY(sat_softmax_fwd(S, d->P, d->probs_mask ? d->Pd : nullptr, d->probs_mask,
                           (int64_t)B * H * L, L, L, d->causal, 1.f / std::sqrt((float)dh), s));
   // O[b, :, h] = Pd[b,h] V_h  (heads written in place of the [B][L][D] concat)
+  // (causal: Pd is lower-triangular, each row tile's reduction stops at its last row)
   SAT_TRY(head_gemm(L, dh, L, {Pd, L, 1, HLL, LL}, {d->v, D, 1, LD, dh}, d->o, D, LD, dh, 1.f, d,
-                    s));
+                    s, 2));
   SAT_TRY(dense(d->o, d->Wo, d->bo, d->y, R, D, d->out_dim, 0.f, d, s));
   return SAT_OK;
 }
@@ -180,16 +184,18 @@ extern "C" int sat_mha_bwd(const SatMha* d, void* stream) {
   SAT_TRY(wgrad(d->o, D, d->dy, d->out_dim, d->dWo, d->dbo));
   SAT_TRY(dgrad(d->dy, d->out_dim, d->Wo, D, dO, 0.f));
   // dPd = dO_h V_h^T ;  dV_h = Pd^T dO_h
+  // (causal: dPd only on / below the diagonal; Pd^T upper-triangular)
   SAT_TRY(head_gemm(L, L, dh, {dO, D, 1, LD, dh}, {d->v, 1, D, LD, dh}, dPd, L, HLL, LL, 1.f, d,
-                    s));
-  SAT_TRY(head_gemm(L, dh, L, {Pd, 1, L, HLL, LL}, {dO, D, 1, LD, dh}, dV, D, LD, dh, 1.f, d, s));
-  SAT_TRY(sat_softmax_bwd(d->P, dPd, d->probs_mask, dS, (int64_t)B * H * L, L,
+                    s, 1));
+  SAT_TRY(head_gemm(L, dh, L, {Pd, 1, L, HLL, LL}, {dO, D, 1, LD, dh}, dV, D, LD, dh, 1.f, d, s,
+                    3));
+  SAT_TRY(sat_softmax_bwd(d->P, dPd, d->probs_mask, dS, (int64_t)B * H * L, L, L, d->causal,
                           1.f / std::sqrt((float)dh), s));
   // dQ_h = dS K_h ;  dK_h = dS^T Q_h
   SAT_TRY(head_gemm(L, dh, L, {dS, L, 1, HLL, LL}, {d->k, D, 1, LD, dh}, dQ, D, LD, dh, 1.f, d,
-                    s));
+                    s, 2));
   SAT_TRY(head_gemm(L, dh, L, {dS, 1, L, HLL, LL}, {d->q, D, 1, LD, dh}, dK, D, LD, dh, 1.f, d,
-                    s));
+                    s, 3));
   // input projections
   SAT_TRY(wgrad(d->x, Wi, dQ, D, d->dWq, d->dbq));
   SAT_TRY(wgrad(d->x, Wi, dK, D, d->dWk, d->dbk));

@@ -110,7 +110,7 @@ def _bstrides(t, nd):
 
 def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor = None, *, alpha=1.0, beta=0.0,
          bias=None, act=None, mul=None, add=None, colsum=None, A2=None, C2=None,
-         B2=None) -> torch.Tensor:
+         B2=None, tri=0) -> torch.Tensor:
     """C = act(alpha * A @ B + beta * C + bias) * mul + add.
 
     ``A2`` [M, K2] (2-D, row-contiguous like A): A is the two column blocks [A | A2] of one
@@ -119,6 +119,10 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor = None, *, alpha=1.0,
     and C2 (SatGemmDesc.C2: two outputs of one A over the column blocks of one B).
     ``B2`` [K2, N] (B's layout): B is the two row blocks [B ; B2] of one reduction; with ``A2``
     the launch computes A B + A2 B2 (SatGemmDesc.B2).
+
+    ``tri`` (SatGemmDesc.tri, a hint for a causal attention's per-batch square products): 1 only
+    the lower triangle of C is needed (tiles above the diagonal left unwritten); 2 / 3 A is
+    lower / upper triangular (its zero K-tiles are not loaded: same bits).
 
     ``colsum`` [N] (2-D, plain products only): also colsum = alpha * sum over rows of B + beta *
     colsum in the same launch (a dense layer's bias gradient next to its weight gradient).
@@ -198,6 +202,7 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor = None, *, alpha=1.0,
                 C.shape[1] + C2.shape[1] != N:
             raise ValueError("gemm: C2 must be [M, N - N1] beside a 2-D C [M, N1]")
         d.C2, d.c2_sm, d.n1 = _p(C2), C2.stride(0), C.shape[1]
+    d.tri = int(tri)
     _with_ws(d, C.device)
     _launch_gemm(d, "sat_gemm")
     return C
@@ -829,10 +834,10 @@ def softmax_fwd(S, P, Pd=None, mask=None, causal=False, scale=1.0):
               _stream())
 
 
-def softmax_bwd(P, dPd, dS, mask=None, scale=1.0):
+def softmax_bwd(P, dPd, dS, mask=None, scale=1.0, causal=False):
     L = P.shape[-1]
-    _lib.call("sat_softmax_bwd", _p(P), _p(dPd), _p(mask), _p(dS), P.numel() // L, L, scale,
-              _stream())
+    _lib.call("sat_softmax_bwd", _p(P), _p(dPd), _p(mask), _p(dS), P.numel() // L, L,
+              P.shape[-2], int(causal), scale, _stream())
 
 
 def loss_fwd_bwd(mel, tgt, tmask, stop, done, dmask, out, dmel=None, dstop=None, l1_weight=0.1):

@@ -494,3 +494,33 @@ def test_gemm_batched_b2(cuda):
     ref = A.double() @ torch.cat([B, B2], 1).double()
     bound = 4e-7 * (A.double().abs() @ torch.cat([B, B2], 1).double().abs()) + 1e-7
     assert bool(((C.double().cpu() - ref).abs() <= bound).all())
+
+
+# ---- causal structure hint (SatGemmDesc.tri): the decoder head's score / probability products
+@pytest.mark.parametrize("L,K", [(200, 128), (500, 128), (77, 40)])
+def test_gemm_tri(cuda, L, K):
+    """tri=1 writes every entry on / below the diagonal (above it C is left as it was); tri=2 / 3
+    with a lower / upper triangular A give the same bits as the full product."""
+    from sat_amd import kernels
+    g = torch.Generator().manual_seed(L + K)
+    nb = 3
+    A = torch.randn(nb, L, K, generator=g).to(cuda)
+    Bm = torch.randn(nb, K, L, generator=g).to(cuda)
+    C = torch.full((nb, L, L), float("nan"), device=cuda)
+    kernels.gemm(A, Bm, C, tri=1)
+    ref = kernels.gemm(A, Bm)
+    low = torch.ones(L, L, device=cuda).tril().bool()
+    assert bool((C[:, low] == ref[:, low]).all())
+    P = torch.randn(nb, L, L, generator=g).to(cuda)
+    V = torch.randn(nb, L, K, generator=g).to(cuda)
+    for tri, Pt in ((2, P.tril()), (3, P.triu())):
+        full = kernels.gemm(Pt, V)
+        part = kernels.gemm(Pt, V, tri=tri)
+        assert torch.equal(full, part), tri
+        # the transposed view (A_M layout) as the backward uses it: Pd^T dO / dS^T Q
+        Pl = P.tril()
+        full_t = kernels.gemm(Pl.transpose(1, 2), V)
+        part_t = kernels.gemm(Pl.transpose(1, 2), V, tri=3)
+        assert torch.equal(full_t, part_t)
+    ref64 = P.tril().double() @ V.double()
+    assert float((kernels.gemm(P.tril(), V, tri=2).double() - ref64).abs().max()) < 1e-3

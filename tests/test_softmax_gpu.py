@@ -25,7 +25,10 @@ def test_softmax_fwd_bwd(cuda, L, causal, dropout):
     md = mask.to(cuda) if dropout else None
     K.softmax_fwd(Sd, P, Pd, mask=md, causal=causal, scale=scale)
     dS = torch.empty_like(Sd)
-    K.softmax_bwd(P, dPd.to(cuda), dS, mask=md, scale=scale)
+    dPg = dPd.to(cuda)
+    if causal:    # above the diagonal dPd is never read (the score GEMM leaves it unwritten)
+        dPg.masked_fill_(torch.ones(Lq, L, device=cuda).triu(1).bool(), float("nan"))
+    K.softmax_bwd(P, dPg, dS, mask=md, scale=scale, causal=causal)
     torch.cuda.synchronize()
 
     x = S.double() * scale

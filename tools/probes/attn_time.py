@@ -1,4 +1,5 @@
-"""HIP-event time of the two attention-chain launches (sat_decoder_attention_fwd / _bwd) on the
+"""HIP-event time of the two attention-chain launches (sat_decoder_attention_fwd / _bwd) and the
+attention parameter-gradient pass (sat_attn_param_grads) on the
 training step's own buffers (B=32, N=200, T'=500, train mode) with whichever library is loaded
 (tools only; A/B two builds by running this twice, once with SAT_LIB_OVERRIDE=<other .so>).
 Also prints a checksum of the forward's histories and the BPTT outputs so two builds' results
@@ -19,7 +20,7 @@ from sat_amd import _lib, data, engine, hparams  # noqa: E402
 from sat_amd import kernels as K  # noqa: E402
 
 KW = {}
-for nm in ("decoder_attention_fwd", "decoder_attention_bwd"):
+for nm in ("decoder_attention_fwd", "decoder_attention_bwd", "attn_param_grads"):
     orig = getattr(K, nm)
 
     def rec(_o=orig, _n=nm, **kw):
@@ -55,11 +56,12 @@ def timed(nm, reps):
         torch.cuda.synchronize()
         if i:
             ts.append(e0.elapsed_time(e1) * 1e3)
-    assert int(kw["err"][0].item()) == 0
+    if "err" in kw:
+        assert int(kw["err"][0].item()) == 0
     return sorted(ts)
 
 
-for nm in ("decoder_attention_fwd", "decoder_attention_bwd"):
+for nm in ("decoder_attention_fwd", "decoder_attention_bwd", "attn_param_grads"):
     ts = timed(nm, reps)
     med = ts[len(ts) // 2]
     print(f"{os.path.basename(_lib.LIB_PATH)} {nm}: median {med:.1f} us/launch = {med / Tp:.3f} "
@@ -67,4 +69,6 @@ for nm in ("decoder_attention_fwd", "decoder_attention_bwd"):
 f, bw = KW["decoder_attention_fwd"], KW["decoder_attention_bwd"]
 sums = {k: float(f[k].double().sum()) for k in ("REC0", "Q", "AL1", "S2", "ZH")}
 sums.update({k: float(bw[k].double().sum()) for k in ("DG0", "DE1", "RD")})
+pg = KW["attn_param_grads"]
+sums.update({k: float(pg[k].double().sum()) for k in ("dK1", "dK2", "pg")})
 print("  checksums " + " ".join(f"{k}={v:.9e}" for k, v in sums.items()), flush=True)

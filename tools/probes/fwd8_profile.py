@@ -76,9 +76,10 @@ for k, nm in enumerate(["B own-store drain", "B poll (after drain)", "A own-stor
                         "A poll (after drain)"]):
     print(f"  {nm:22s} us per wave: " + " ".join(f"{float(sp[:, w, k].mean()):.2f}" for w in range(8)))
 pr = prof[:256 * 16].view(256, 16).cpu().double() / 100.0
-names = ["wait B records", "sync (staged)", "combine", "sync (c)", "c-dot + cell",
-         "sync (cell)", "q partial + publish A", "normalise", "loc + L", "wait A records",
-         "q sum (2 syncs)", "energies", "sync + stats", "sync + ctx + publish B", "h-dot", "-"]
+names = ["wait B records", "sync (staged)", "combine + normalise", "sync (c)",
+         "h+c dot + cell", "sync (cell)", "q partial + publish A", "-", "loc + L",
+         "wait A records", "sync (A staged)", "q sum + energies", "sync (energies)", "stats",
+         "ctx + publish B", "-"]
 rows = [g + 32 * j for g in range(B) for j in range(8)]
 for i, n in enumerate(names[:15]):
     col = pr[rows, i]

@@ -125,15 +125,17 @@ def test_c4_vctk_full_shape_matches_oracle(cuda, train):
 def _compare_grads(name, m, p64, b):
     grads = m.grads_dict()
     gmax = max(float(p.grad.abs().max()) for p in p64.values())
-    worst, bad = 0.0, []
-    for name, p in p64.items():
+    worst, worst_at, bad = 0.0, None, []
+    for pname, p in p64.items():
         g_ref = p.grad.numpy()
         scale = max(np.abs(g_ref).max(), 1e-4 * gmax)
-        err = float(np.abs(grads[name].astype(np.float64) - g_ref).max() / scale)
-        worst = max(worst, err)
+        err = float(np.abs(grads[pname].astype(np.float64) - g_ref).max() / scale)
+        if err > worst:
+            worst, worst_at = err, pname
         if not err <= 2e-4:
-            bad.append((name, err))
-    _report(name, worst_rel_grad_err=worst, steps=int(b["mel"].shape[1] // 2))
+            bad.append((pname, err))
+    _report(name, worst_rel_grad_err=worst, worst_param=worst_at, bar=2e-4,
+            steps=int(b["mel"].shape[1] // 2))
     assert not bad, bad
 
 

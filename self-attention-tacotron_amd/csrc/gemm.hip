@@ -1574,7 +1574,13 @@ extern "C" int sat_cbhg_convbank_bwd(const SatConvBank* d, void* stream) {
     p.B = d->W;
     p.C = d->dx; p.c_sm = d->dx_sm;
     p.beta = d->beta_dx;
-    const LdsPlan pl = plan_lds(p.M, p.N, p.K, 1, d->ws != nullptr, d->ws_bytes, 0, 0);
+    LdsPlan pl = plan_lds(p.M, p.N, p.K, 1, d->ws != nullptr, d->ws_bytes, 0, 0);
+    // measured at the C2 shape (tools/probes/convbank_bwd_probe.py): 128 x 128 tiles split 4
+    // ways 373 us, the cost model's choice 414 (odd splits 490+: their chunks straddle banks)
+    const int kc4 = (ceil_div(p.K, 4) + BK - 1) / BK * BK;
+    if (t_force_bm == 0 && d->C % 128 == 0 && p.M >= 4096 && d->ws != nullptr &&
+        (int64_t)ceil_div(p.K, kc4) * p.M * p.N * 4 <= d->ws_bytes)
+      pl = {128, 128, ceil_div(p.K, kc4), kc4};
     const int e = launch_lds_plan<2>(pl, A_IM2COL, B_FLIP, 1, p, s, "sat_cbhg_convbank_bwd(dX)");
     if (e != SAT_OK) return e;
   }

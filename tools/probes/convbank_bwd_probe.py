@@ -56,8 +56,8 @@ def both():
 
 
 fl = 2.0 * 6400 * 128 * 128 * 136
-for plan in ((0, 0, 0), (64, 64, 1), (64, 64, 2), (64, 64, 3), (64, 64, 4), (128, 64, 2),
-             (64, 128, 2), (128, 128, 4), (128, 128, 8)):
+print("both products on two streams, per forced plan (the plan applies to both):", flush=True)
+for plan in ((0, 0, 0), (64, 64, 3), (64, 128, 2)):
     lib.sat_gemm_force_plan(*plan)
     try:
         a, b = t_of(fdx), t_of(fdw)
@@ -67,4 +67,16 @@ for plan in ((0, 0, 0), (64, 64, 1), (64, 64, 2), (64, 64, 3), (64, 64, 4), (128
         continue
     print(f"plan {plan}: dX {a:7.1f} us ({fl / a / 1e6:5.1f} TF/s)  dW {b:7.1f} us "
           f"({fl / b / 1e6:5.1f} TF/s)  serial {a + b:7.1f}  two streams {c:7.1f}", flush=True)
+print("each product alone, per forced plan:", flush=True)
+for plan in ((128, 128, 1), (128, 128, 2), (128, 128, 3), (128, 128, 4), (128, 128, 6),
+             (128, 128, 8), (128, 64, 3), (128, 64, 4), (64, 128, 3), (64, 128, 4)):
+    lib.sat_gemm_force_plan(*plan)
+    row = []
+    for nm, f in (("dX", fdx), ("dW", fdw)):
+        try:
+            t = t_of(f)
+            row.append(f"{nm} {t:7.1f} us ({fl / t / 1e6:5.1f} TF/s)")
+        except Exception:  # noqa: BLE001
+            row.append(f"{nm} (plan refused)")
+    print(f"plan {plan}: " + "  ".join(row), flush=True)
 lib.sat_gemm_force_plan(0, 0, 0)

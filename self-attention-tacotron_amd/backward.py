@@ -42,6 +42,17 @@ class Aux:
         with torch.cuda.stream(self.s):
             fn()
 
+    def run_side(self, fn, *tensors):
+        """run a branch on a stream of its own (K.aux_stream index 2), forked here from the main
+        stream and joined with the others: it does not queue behind the aux backlog"""
+        s = K.aux_stream(self.dev, 2)
+        s.wait_stream(torch.cuda.current_stream())
+        if s not in self.used:
+            self.used.append(s)
+        self.keep.extend(tensors)
+        with torch.cuda.stream(s):
+            fn()
+
     def switch(self):
         """Later branches on a further stream, so they do not queue behind the branches issued
         so far (the decoder's weight-gradient backlog)."""
@@ -598,9 +609,15 @@ def encoder_bwd(P, G, hp, d, sv, dm1, dm2, lengths, masks, ws, aux: Aux = None):
         kern = [f"{n}/kernel" for n in names]
         # the weight-gradient branch forks BEFORE the dX product is issued: a branch waits for
         # everything the main stream has issued at its fork, so the other order serialises them
-        _wgrad(aux, lambda: K.conv_bank_bwd(inp, _contig_span(P, kern), dbank_pre, d.max_k, C,
-                                            dW=_contig_span(G, kern), beta_dw=1.0),
-               inp, dbank_pre)
+        # the weight-gradient product on a stream of its own (not behind the aux backlog): the
+        # graph then runs it beside the dX product instead of before it on the same queue
+        # (14.52 -> 14.47 ms/step, 6 interleaved pairs; SAT_BANK_DW_SIDE=0 restores the aux branch)
+        bank_dw = lambda: K.conv_bank_bwd(inp, _contig_span(P, kern), dbank_pre,  # noqa: E731
+                                          d.max_k, C, dW=_contig_span(G, kern), beta_dw=1.0)
+        if aux is not None and os.environ.get("SAT_BANK_DW_SIDE", "1") == "1":
+            aux.run_side(bank_dw, inp, dbank_pre)
+        else:
+            _wgrad(aux, bank_dw, inp, dbank_pre)
         K.conv_bank_bwd(inp, _contig_span(P, kern), dbank_pre, d.max_k, C, dx=dinp,
                         beta_dx=1.0)
     else:

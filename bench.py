@@ -54,6 +54,8 @@ def parse():
     ap.add_argument("--no-extra", action="store_true",
                     help="skip the C4 (VCTK training) and C5 (free-running inference) lines")
     ap.add_argument("--extra-steps", type=int, default=10)
+    ap.add_argument("--no-fallback", action="store_true",
+                    help="skip the B=64 per-step-path (persistent-ineligible) extra line")
     ap.add_argument("--no-roofline", action="store_true",
                     help="skip the attention-kernel probe (profiling runs of the step alone)")
     ap.add_argument("--cpu-baseline-batch", type=int, default=2)
@@ -124,21 +126,50 @@ def plumbing(args, world: int, rank: int) -> None:
 
 
 class _Recorder:
-    """Keeps the keyword arguments of the last sat_decoder_attention_fwd call (the graph-captured
-    training step's own buffers), so the probe can re-launch that exact kernel afterwards."""
+    """Keeps the keyword arguments of the last call of one persistent-kernel entry
+    (``kernels.decoder_attention_fwd`` / ``_bwd``: the graph-captured training step's own
+    buffers), so the probe can re-launch that exact kernel afterwards."""
 
-    def __init__(self):
+    def __init__(self, name):
         from sat_amd import kernels as K
-        self.K, self.orig, self.kw = K, K.decoder_attention_fwd, None
-        K.decoder_attention_fwd = self
+        self.K, self.name, self.orig, self.kw = K, name, getattr(K, name), None
+        setattr(K, name, self)
 
     def __call__(self, **kw):
         self.kw = dict(kw)
         self.orig(**kw)
 
 
+def _attn_fwd_step_bytes(kw, B, N):
+    """per decoder step 4 (549 B N + 67,191) bytes = K1/V1/K2/V2 + the two
+    alignment states of every utterance + the attention's own weights (query, location, v)
+    (d_q = U = 256 query rows: the query layers are [U, D1] and [U, D2])."""
+    D1, M1, D2, M2, F, KW, U = (int(kw[k]) for k in ("D1", "M1", "D2", "M2", "F", "KW", "U"))
+    return 4 * (B * N * (D1 + M1 + D2 + M2 + 5) + U * (D1 + D2)
+                + F * (KW + 1) + F * D1 + 2 * D1 + D2)
+
+
+def _attn_bwd_step_bytes(kw, B, N):
+    """The BPTT's per-step algorithmic bytes: the forward's 8(d) set
+    (memories, alignment states, attention weights) + the energy-tanh history it re-reads
+    (ZH, B N (D1 + D2)) + the energy / location-feature gradients it writes (DE1, DE2, DFH:
+    B N (2 + F))."""
+    D1, D2, F = (int(kw[k]) for k in ("D1", "D2", "F"))
+    return _attn_fwd_step_bytes(kw, B, N) + 4 * B * N * ((D1 + D2) + 2 + F)
+
+
+def _roof(bytes_launch, avg_s, T, reps, kernel, note, traffic=None, pmc_src=None):
+    achieved = bytes_launch / avg_s / 1e9
+    return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "traffic_source": pmc_src, "kernel": kernel, "bytes_per_launch": int(bytes_launch),
+            "attn_bytes_per_step": int(bytes_launch // T), "steps_per_launch": T,
+            "avg_launch_us": round(avg_s * 1e6, 1), "us_per_step": round(avg_s * 1e6 / T, 3),
+            "launches_timed": reps, "note": note}
+
+
 def attention_probe(rec, B, N, reps=6):
-    """Average duration of the persistent decoder attention kernel (dec_attn_fwd_kernel: all T'
+    """Average duration of the persistent decoder attention kernel (dec_attn_fwd8_kernel: all T'
     steps of attention RNN + query + dual-source attention in one launch), timed with HIP events
     on the stream it is launched on, re-launched on the training step's own buffers after the
     timed region; and its algorithmic bytes per launch (SURVEY.md 8(d) per-step attention bytes
@@ -158,44 +189,70 @@ def attention_probe(rec, B, N, reps=6):
     ev1.record(stream)
     torch.cuda.synchronize()
     avg_s = ev0.elapsed_time(ev1) / 1e3 / reps
-    D1, M1, D2, M2, F, KW, U = (int(kw[k]) for k in ("D1", "M1", "D2", "M2", "F", "KW", "U"))
-    f = 4  # fp32
-    # per decoder step 4 (549 B N + 67,191) bytes = K1/V1/K2/V2 + the two
-    # alignment states of every utterance + the attention's own weights (query, location, v)
-    # (d_q = U = 256 query rows: the query layers are [U, D1] and [U, D2])
-    attn_step = f * (B * N * (D1 + M1 + D2 + M2 + 5) + U * (D1 + D2)
-                     + F * (KW + 1) + F * D1 + 2 * D1 + D2)
-    bytes_launch = T * attn_step
-    achieved = bytes_launch / avg_s / 1e9
-    traffic, pmc_src = _pmc_traffic()
-    return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-            "kernel": "dec_attn_fwd8_kernel (sat_decoder_attention_fwd, persistent, T' steps)",
-            "bytes_per_launch": int(bytes_launch), "attn_bytes_per_step": int(attn_step),
-            "steps_per_launch": T, "avg_launch_us": round(avg_s * 1e6, 1),
-            "us_per_step": round(avg_s * 1e6 / T, 3), "launches_timed": reps,
-            "note": "achieved = SURVEY 8(d) ALGORITHMIC attention bytes (4(549 B N + 67191) per "
-                    "decoder step: K1/V1/K2/V2, alignment states, attention weights) x T' / "
-                    "HIP-event launch time on the launching stream; the kernel keeps K/V slices "
-                    "in LDS, so its real memory traffic (traffic = per-launch FETCH_SIZE + "
-                    f"WRITE_SIZE, {pmc_src}) is lower: it is bound by its in-kernel hand-off "
-                    "latency, not by HBM"}
+    traffic, pmc_src = _pmc_traffic("dec_attn_fwd", "decoder_persistent8.hip")
+    return _roof(T * _attn_fwd_step_bytes(kw, B, N), avg_s, T, reps,
+                 "dec_attn_fwd8_kernel (sat_decoder_attention_fwd, persistent, T' steps)",
+                 "achieved = SURVEY 8(d) ALGORITHMIC attention bytes (4(549 B N + 67191) per "
+                 "decoder step: K1/V1/K2/V2, alignment states, attention weights) x T' / "
+                 "HIP-event launch time on the launching stream; the kernel keeps K/V slices "
+                 "in LDS, so its real memory traffic (traffic = per-launch FETCH_SIZE + "
+                 "WRITE_SIZE of the PMC summary named in traffic_source) is lower: it is bound "
+                 "by its in-kernel hand-off latency, not by HBM", traffic, pmc_src)
 
 
-def _pmc_traffic():
-    """Per-launch memory-side bytes of the persistent attention kernel from the newest committed
-    PMC summary (profiles/rNN_dec_attn_fwd_pmc.json, made by tools/pmc_persistent.py +
-    tools/pmc_summary.py)."""
+def attention_bwd_probe(rec, B, N, reps=4):
+    """The same for the attention chain's BPTT (dec_attn_bwd8_kernel), re-launched on the
+    step's own buffers.  It accumulates into RD in place, so RD is restored between launches
+    and every launch is bracketed by its own HIP events (the restore is outside them)."""
+    kw = rec.kw
+    if kw is None:
+        return None
+    T = int(kw["T"])
+    rd = kw["RD"]
+    rd0 = rd.clone()
+    stream = torch.cuda.current_stream()
+    times = []
+    for i in range(reps + 1):
+        rd.copy_(rd0)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        rec.orig(**kw)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        if i:                                   # the first launch is a warm-up
+            times.append(e0.elapsed_time(e1) / 1e3)
+    rd.copy_(rd0)
+    avg_s = float(np.mean(times))
+    traffic, pmc_src = _pmc_traffic("dec_attn_bwd", "decoder_persistent8_bwd.hip")
+    return _roof(T * _attn_bwd_step_bytes(kw, B, N), avg_s, T, reps,
+                 "dec_attn_bwd8_kernel (sat_decoder_attention_bwd, persistent, T' reverse steps)",
+                 "achieved = the forward's 8(d) bytes + the ZH energy-tanh history re-read "
+                 "(B N (D1+D2) floats) + the DE1/DE2/DFH gradients written (B N (2+F)) per "
+                 "step, x T' / HIP-event time of one launch", traffic, pmc_src)
+
+
+def _pmc_traffic(kernel_tag: str, source: str):
+    """Per-launch memory-side bytes of a persistent attention kernel from the newest committed
+    PMC summary ``profiles/rNN_<kernel_tag>_pmc.json`` (tools/pmc_persistent.py +
+    tools/pmc_summary.py), with the summary's provenance: its file, the sha256 of the kernel
+    source it was measured on, and whether that equals the source of THIS tree (a stale summary
+    is reported as such, not as this build's traffic)."""
     import glob
-    files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles",
-                                          "r*_dec_attn_fwd_pmc.json")))
+    import hashlib
+    here = os.path.dirname(os.path.abspath(__file__))
+    files = sorted(glob.glob(os.path.join(here, "profiles", f"r*_{kernel_tag}_pmc.json")))
     if not files:
-        return None, "no PMC summary"
+        return None, {"file": None, "why": "no PMC summary committed"}
     try:
         d = json.load(open(files[-1]))
-        return int(d["hbm_bytes_per_launch"]), os.path.basename(files[-1])
+        src = os.path.join(here, "self-attention-tacotron_amd", "csrc", source)
+        now = hashlib.sha256(open(src, "rb").read()).hexdigest()[:16]
+        was = d.get("source_sha16")
+        return int(d["hbm_bytes_per_launch"]), {
+            "file": os.path.basename(files[-1]), "measured_on_source_sha16": was,
+            "current_source_sha16": now, "current": was == now}
     except (OSError, ValueError, KeyError):
-        return None, "unreadable PMC summary"
+        return None, {"file": os.path.basename(files[-1]), "why": "unreadable PMC summary"}
 
 
 def cpu_baseline(hp, args, B=None, steps=None):
@@ -269,6 +326,47 @@ def c4_vctk_training(args):
     return out
 
 
+def fallback_training(args, B=64, steps=3):
+    """The persistent-eligibility cliff, measured: a per-GPU batch the
+    one-launch decoder kernels cannot take (B=64 > 32: ceil(B/8) * ceil(N/32) > 32 groups)
+    runs the per-step launch path with a PersistentFallbackWarning.  Same step as the headline
+    (graphed, fwd + BPTT + Adam) at B=64; reported so the cost of leaving the eligible shapes
+    is a number, not a surprise."""
+    import warnings
+    from sat_amd import data, decoder, engine, hparams, params, train
+    hp = hparams.ljspeech_hparams()
+    N, T = args.chars, args.frames
+    why = decoder.persistent_ineligible_reason(params.resolve_dims(hp), B, N)
+    try:
+        m = engine.Tacotron(hp, "cuda", seed=4321)
+        b = data.synthetic_batch(hp, B, N=N, T=T, shape="max", seed=78)
+        batch = {k: torch.tensor(v).cuda() for k, v in b.items()}
+        tr = train.Trainer(m, B, N, T // hp.outputs_per_step, seed=98)
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore", decoder.PersistentFallbackWarning)
+            g = train.GraphedStep(tr, batch, warmup=1)
+        g.replay()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            g.replay()
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / steps
+        tr.check_health(wait=True)
+        out = {"value": round(B * T / dt, 1), "unit": "frames/s", "ms_per_step": round(1e3 * dt, 3),
+               "steps": steps}
+        del g, tr, m
+    except Exception as e:          # reported, never fatal to the headline line
+        out = {"error": f"{type(e).__name__}: {e}"[:300]}
+    torch.cuda.empty_cache()
+    out.update({"metric": f"teacher-forced mel frames/sec, LJSpeech batch={B} on 1 MI355X "
+                          "(per-step launch path: persistent decoder not eligible)",
+                "why_not_persistent": why,
+                "config": {"workload": "C2 step at a per-GPU batch outside the persistent "
+                                       "kernels' shapes", "batch": B, "chars": N, "mel_frames": T}})
+    return out
+
+
 def c5_free_running(args, B=8, steps=500):
     """C5 (BASELINE configs[4]): LJSpeech free-running inference, batch 8, 500 decoder steps
     (no early stop: min_iters = max_iters), the step loop captured as hipGraphs of 25 steps."""
@@ -321,7 +419,8 @@ def main():
     from sat_amd import data, dp, engine, hparams, train
     hp = hparams.ljspeech_hparams()
     B, N, T = args.batch, args.chars, args.frames
-    rec = _Recorder()
+    rec = _Recorder("decoder_attention_fwd")
+    rec_bwd = _Recorder("decoder_attention_bwd")
     model = engine.Tacotron(hp, "cuda", seed=1234, attn_tile=args.attn_tile,
                             pipeline_chunk=args.pipeline_chunk)
     dp.broadcast_params(model.params)   # identical initial weights on every replica
@@ -361,10 +460,13 @@ def main():
     frames = world * B * T * args.steps
     value = frames / dt
     roof = None if args.no_roofline else attention_probe(rec, B, N)
+    roof_bwd = None if args.no_roofline else attention_bwd_probe(rec_bwd, B, N)
     extra = {}
     if rank == 0 and world == 1 and not args.no_extra:
         extra["c4_vctk_training"] = c4_vctk_training(args)
         extra["c5_free_running"] = c5_free_running(args)
+        if not args.no_fallback:
+            extra["fallback_b64_per_step_path"] = fallback_training(args)
     if rank == 0:
         cpu = None if args.no_cpu_baseline else cpu_baseline(hp, args)
         cpu_c2 = (None if args.no_cpu_baseline or args.cpu_baseline_c2_steps <= 0
@@ -381,7 +483,7 @@ def main():
                        "decoder_steps": T // hp.outputs_per_step, "parallelism": f"dp{world}",
                        "hip_graph": not args.no_graph, "params": model.num_params},
             "median_ms_per_step": round(float(np.median(step_ms)), 3),
-            "roofline": roof, "cpu_baseline": cpu, "cpu_baseline_c2": cpu_c2, **extra,
+            "roofline": roof, "roofline_bptt": roof_bwd, "cpu_baseline": cpu, "cpu_baseline_c2": cpu_c2, **extra,
             "loss_first_timed": round(loss0, 5), "loss_last": round(loss1, 5),
         }
         print(json.dumps(line), flush=True)

@@ -35,8 +35,15 @@ extern "C" {
 #define SAT_ERR_HIP -2
 #define SAT_ERR_UNSUPPORTED -3
 
+/* Layout version of every struct / signature below: bumped whenever one changes, so a binding
+ * (or an A/B run loading an older build through SAT_LIB_OVERRIDE) can refuse a library whose
+ * structs it would misread.  5: round-5 layout (SatAttnParamGrad without zh, sat_softmax_bwd
+ * with Lq / causal). */
+#define SAT_ABI_VERSION 5
+
 /* ---------------------------------------------------------------- library */
 int sat_version(void);                         /* 100*major + minor */
+int sat_abi_version(void);                     /* SAT_ABI_VERSION the library was built with */
 const char* sat_last_error_string(void);
 int sat_device_arch(char* buf, int len);       /* gcnArchName of the current device */
 

@@ -229,6 +229,29 @@ def encoder(ids, lengths, p, bufs, hp, masks, training, kinks=None):
     return m1, s, aligns
 
 
+def encoder_front_branches(ids, p, bufs, hp, masks, training):
+    """The oracle's OWN branch at every kink ``encoder(kinks=)`` can be handed (tests only):
+    the same keys and the same definitions as the test's record of the HIP forward (prenet
+    outputs after dropout > 0, conv-bank ReLU outputs > 0, max-pool ``out[n] = x[n]`` choice on
+    the ReLU outputs, proj1 ReLU output > 0), so the two can be compared element by element and
+    the number of branches that fp32 and float64 take differently is bounded
+    (modules/module.py:77-83 front, ext PreNet)."""
+    g = (lambda k: masks[k]) if masks is not None else (lambda k: None)
+    x = p["embedding"][ids]
+    out = {}
+    for i in range(len(hp.encoder_prenet_out_units)):
+        x = prenet(x, p, f"encoder/prenet{i}", g(f"enc/prenet{i}"))
+        out[f"prenet{i}"] = x > 0
+    bank = torch.cat([conv_bn(x, p, bufs, f"encoder/cbhg/conv_bank/K{k}", training, relu=True)
+                      for k in range(1, hp.max_filter_width + 1)], dim=-1)
+    nxt = torch.cat([bank[:, 1:, :], bank[:, -1:, :]], dim=1)
+    out["bank"] = bank > 0
+    out["pool_first"] = bank >= nxt
+    y = conv_bn(torch.maximum(bank, nxt), p, bufs, "encoder/cbhg/proj1", training, relu=True)
+    out["proj1"] = y > 0
+    return {k: v.double() for k, v in out.items()}
+
+
 # ----------------------------------------------------------------------------- attention
 
 def seq_mask(lengths, n, dtype):

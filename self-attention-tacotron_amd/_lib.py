@@ -17,7 +17,14 @@ LIB_PATH = os.environ.get("SAT_LIB_OVERRIDE") or os.path.join(PKG_DIR, "libsat_h
 
 
 class SatLibraryError(RuntimeError):
-    pass
+    """A library call failed; ``rc`` is its SAT_ERR_* code (None when raised host-side)."""
+
+    def __init__(self, msg: str, rc: Optional[int] = None):
+        super().__init__(msg)
+        self.rc = rc
+
+
+SAT_ERR_UNSUPPORTED = -3
 
 
 class SatGemmDesc(ctypes.Structure):
@@ -176,6 +183,7 @@ SatAttnStep = _struct("SatAttnStep", """
 # name -> argtypes (restype is int for all but sat_last_error_string)
 SIGNATURES = {
     "sat_version": [],
+    "sat_abi_version": [],
     "sat_device_arch": [ctypes.c_char_p, _I32],
     "sat_gemm": [ctypes.POINTER(SatGemmDesc), _P],
     "sat_gemm_force_plan": [_I32, _I32, _I32],
@@ -264,6 +272,8 @@ RESTYPES = {"sat_workspace_colreduce": (ctypes.c_int64, [_I32, _I32]),
             "sat_tfrecord_index": (ctypes.c_int64, [_P, _I64, _I32, _P, _I64])}
 
 _lib: Optional[ctypes.CDLL] = None
+# include/sat_abi.h SAT_ABI_VERSION this binding's structs follow
+ABI_VERSION = 5
 
 
 def load(path: str = LIB_PATH) -> ctypes.CDLL:
@@ -273,6 +283,13 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     if not os.path.exists(path):
         raise SatLibraryError(f"{path} not found: run __graft_entry__.build() (make -C csrc)")
     lib = ctypes.CDLL(path)
+    # the structs / signatures below are bound with THIS binding's layout: refuse a library
+    # built against another (an older build loaded through SAT_LIB_OVERRIDE for an A/B would
+    # otherwise read past a struct that has since lost or gained fields)
+    got = lib.sat_abi_version() if hasattr(lib, "sat_abi_version") else None
+    if got != ABI_VERSION:
+        raise SatLibraryError(f"{path}: ABI version {got}, this binding needs {ABI_VERSION} "
+                              "(rebuild it: make -C self-attention-tacotron_amd/csrc)")
     for name, argtypes in SIGNATURES.items():
         if os.environ.get("SAT_LIB_OVERRIDE") and not hasattr(lib, name):
             continue     # an older build under A/B (tools/): entries added since stay unbound
@@ -322,7 +339,7 @@ def exported_symbols(path: str = LIB_PATH):
 def check(rc: int, what: str) -> None:
     if rc != 0:
         msg = load().sat_last_error_string().decode(errors="replace")
-        raise SatLibraryError(f"{what} failed (rc={rc}): {msg}")
+        raise SatLibraryError(f"{what} failed (rc={rc}): {msg}", rc)
 
 
 def call(name: str, *args) -> None:

@@ -1271,8 +1271,11 @@ static int launch_lds(const SatGemmDesc* d, GemmP& p, int nb, hipStream_t s) {
       (bm == B_FLIP && am != A_IM2COL))
     return 1;
   if (p.cs_out && am == A_M && p.m_real % 4 != 0) return 1;   // the ones chunk must start at m_real
-  const LdsPlan pl = plan_lds(p.M, d->N, d->K, nb, nb == 1 && d->ws != nullptr && !p.C2,
-                              d->ws_bytes, am == A_IM2COLT ? d->a_C : 0, 0);
+  // no split-K under a causal hint: the skipped tiles would leave their slab partials stale and
+  // the reduce would write them into C above the diagonal
+  const LdsPlan pl = plan_lds(p.M, d->N, d->K, nb,
+                              nb == 1 && d->ws != nullptr && !p.C2 && p.tri == 0, d->ws_bytes,
+                              am == A_IM2COLT ? d->a_C : 0, 0);
   if (pl.bm == 0) return 1;
   return launch_lds_plan<0>(pl, am, bm, nb, p, s, "sat_gemm");
 }
@@ -1348,6 +1351,10 @@ extern "C" int sat_gemm(const SatGemmDesc* d, void* stream) {
   p.cs_out = nullptr;
   p.m_real = d->M;
   p.tri = (d->tri >= 1 && d->tri <= 3) ? d->tri : 0;
+  // the causal hint is a plain-product option: the fused bias-gradient row, the segmented
+  // operands and the second output block would each see skipped tiles / K-ranges
+  SAT_CHECK_ARG(p.tri == 0 || (!d->colsum_out && !d->A2 && !d->B2 && !d->C2),
+                "sat_gemm: tri cannot be combined with colsum_out, A2 / B2 or C2");
   hipStream_t s = as_stream(stream);
   const int nb = d->batch * p.batch2;
   p.ws = reinterpret_cast<float*>(d->ws);

@@ -92,6 +92,8 @@ __global__ void counter_add_kernel(uint64_t* c, uint64_t inc) { c[0] += inc; }
 
 extern "C" int sat_version(void) { return 10; }
 
+extern "C" int sat_abi_version(void) { return SAT_ABI_VERSION; }
+
 extern "C" const char* sat_last_error_string(void) { return sat::g_err; }
 
 extern "C" int sat_device_arch(char* buf, int len) {

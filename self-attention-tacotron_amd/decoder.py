@@ -20,6 +20,7 @@ All state histories are kept (step-major ``[T'+1, B, .]``) for the hand-written 
 
 from __future__ import annotations
 
+import warnings
 from dataclasses import dataclass, field
 from typing import Dict, Optional
 
@@ -101,13 +102,54 @@ def decoder_inputs(P: Dict[str, torch.Tensor], hp, d: Dims, targets: torch.Tenso
     return {"xin": xin, "pres": pres, "X0": X0, "hist": None if hist is None else hist[1]}
 
 
+def persistent_ineligible_reason(d: Dims, B: int, N: int, attn_tile: int = 32) -> Optional[str]:
+    """Why sat_decoder_attention_fwd / sat_decoder_lstms_fwd (one launch for all T' steps) cannot
+    take this shape, or None when they can (the self-attention-tacotron configs: one utterance
+    per 8 workgroups for N <= 256, four per 32 otherwise, all of them resident on 256 CUs)."""
+    if not (d.att1 == "forward" and d.att2 == "additive"):
+        return f"attention kinds ({d.att1}, {d.att2}) are not (forward, additive)"
+    if attn_tile != 32:
+        return f"attn_tile {attn_tile} != 32"
+    dims = (d.att_rnn, d.m1, d.m2, d.d1, d.d2, d.loc_f, d.loc_k, d.dec)
+    if dims != (256, 256, 32, 224, 32, 5, 10, 256):
+        return f"layer widths {dims} differ from the compiled (256, 256, 32, 224, 32, 5, 10, 256)"
+    if not 0 < B <= 32:
+        return f"per-GPU batch {B} outside 1..32"
+    if ((B + 7) // 8) * ((N + 31) // 32) > 32:
+        return (f"ceil(B/8) * ceil(N/32) = {((B + 7) // 8) * ((N + 31) // 32)} > 32 groups of "
+                f"positions (B={B}, N={N}: more workgroups than CUs)")
+    return None
+
+
 def persistent_eligible(d: Dims, B: int, N: int, attn_tile: int = 32) -> bool:
     """Shapes sat_decoder_attention_fwd and sat_decoder_lstms_fwd are compiled for (the
     self-attention-tacotron configs)."""
-    return (d.att1 == "forward" and d.att2 == "additive" and attn_tile == 32 and
-            (d.att_rnn, d.m1, d.m2, d.d1, d.d2, d.loc_f, d.loc_k, d.dec) ==
-            (256, 256, 32, 224, 32, 5, 10, 256)
-            and 0 < B <= 32 and ((B + 7) // 8) * ((N + 31) // 32) <= 32)
+    return persistent_ineligible_reason(d, B, N, attn_tile) is None
+
+
+class PersistentFallbackWarning(RuntimeWarning):
+    """A training / eval shape left the one-launch persistent decoder for the per-step launch
+    path (several times slower per step; BASELINE.md section 3 lists the measured cost)."""
+
+
+_FALLBACK_WARNED = set()
+
+
+def use_persistent(d: Dims, B: int, N: int, attn_tile: int = 32, persistent: bool = True) -> bool:
+    """The decoder path for this shape.  ``persistent=True`` (the engine default) takes the
+    persistent kernels when eligible and otherwise WARNS once per (B, N) before falling back
+    to the per-step launches; ``persistent=False`` asks for the per-step path silently."""
+    if not persistent:
+        return False
+    why = persistent_ineligible_reason(d, B, N, attn_tile)
+    if why is None:
+        return True
+    if (B, N, why) not in _FALLBACK_WARNED:
+        _FALLBACK_WARNED.add((B, N, why))
+        warnings.warn(f"decoder falls back to the per-step launch path: {why} "
+                      f"(pass persistent_decoder=False to choose it explicitly)",
+                      PersistentFallbackWarning, stacklevel=3)
+    return False
 
 
 def decoder_forward(P: Dict[str, torch.Tensor], hp, d: Dims, m1: torch.Tensor, m2: torch.Tensor,
@@ -269,7 +311,7 @@ def decoder_forward(P: Dict[str, torch.Tensor], hp, d: Dims, m1: torch.Tensor, m
     def lstm2_desc(t):
         return _lstm_desc(X2, W2[Dd:], t, B, Dd, zc, zh, m2c, m2h, L2)
 
-    if persistent and persistent_eligible(d, B, N, attn_tile):
+    if use_persistent(d, B, N, attn_tile, persistent):
         if scratch is None:
             scratch = K.DecoderAttentionScratch(B, N, dev)
         # tanh of every energy pre-activation, kept for the persistent BPTT ([T', B, N, D1+D2]:

@@ -45,7 +45,7 @@ def allreduce_grads(flat: torch.Tensor, group=None) -> None:
 
 
 def exchange(arena: torch.Tensor, health: torch.Tensor, bn: torch.Tensor, tail: torch.Tensor,
-             group=None) -> None:
+             group=None, force: bool = False) -> None:
     """A replica's whole per-step exchange as ONE SUM all-reduce over the contiguous arena
     ``[gradients | bn | tail]`` (``bn`` and ``tail`` are views of it):
 
@@ -56,9 +56,12 @@ def exchange(arena: torch.Tensor, health: torch.Tensor, bn: torch.Tensor, tail: 
       rank or on none) and the code is exact when one rank failed.
 
     On device tensors the pack / unpack are the library's ``sat_exchange_pack/unpack``
-    launches; the host arithmetic below is the same restatement for the ``gloo`` CPU tests."""
+    launches; the host arithmetic below is the same restatement for the ``gloo`` CPU tests.
+
+    ``force`` runs the whole exchange (pack, collective, unpack) even in a one-rank group, where
+    it is the identity: the GPU tests drive the RCCL path that way on a one-GPU box."""
     w = world_size(group)
-    if w == 1:
+    if w == 1 and not (force and is_distributed(group)):
         return
     if arena.is_cuda:
         from . import _lib

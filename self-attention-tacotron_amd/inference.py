@@ -47,6 +47,7 @@ Every arithmetic op is a libsat_hip kernel; torch allocates, views and copies.
 from __future__ import annotations
 
 import math
+import warnings
 from typing import Dict, Optional
 
 import torch
@@ -228,9 +229,15 @@ class FreeRunningDecoder:
         try:
             self._run_persistent(pl, Tm)
         except _lib.SatLibraryError as e:
+            if e.rc != _lib.SAT_ERR_UNSUPPORTED:
+                raise
             return str(e)
         if int(pl.err.item()) != 0:
-            return "a hand-off timed out (the grid was not co-resident?)"
+            # not a refusal: the kernel started and a hand-off spin gave up -- a hang or a
+            # regression in the one-launch decode, never silently replaced
+            raise _lib.SatLibraryError("sat_decode_persistent: a hand-off timed out (error word "
+                                       f"{int(pl.err.item())}); the grid was not co-resident "
+                                       "or the kernel regressed")
         return None
 
     def _build(self, B: int, N: int, Tm: int) -> _Plan:
@@ -531,10 +538,12 @@ class FreeRunningDecoder:
             elif self.persistent:
                 raise _lib.SatLibraryError("sat_decode_persistent: " + why)
             else:
-                # persistent=None: the one-launch decode is not runnable here (too few
-                # co-resident workgroups on this device, or a hand-off timed out because
-                # another stream held CUs) -- this plan decodes with the per-step launches
-                # from now on, starting again from clean buffers
+                # persistent=None: the library refused the one-launch decode here
+                # (SAT_ERR_UNSUPPORTED: too few co-resident workgroups on this device) -- this
+                # plan decodes with the per-step launches from now on, starting again from
+                # clean buffers, and says so
+                warnings.warn("free-running decode falls back to per-step launches: " + why,
+                              RuntimeWarning, stacklevel=2)
                 pl.pk = None
                 pl.err.zero_()
                 prepare()

@@ -826,18 +826,29 @@ def axpby(x, y, a, b):
     return y
 
 
-def softmax_fwd(S, P, Pd=None, mask=None, causal=False, scale=1.0):
+def _causal_rows(x, Lq, causal, what):
+    """Rows per square matrix for the causal limit: explicit ``Lq``, else x's [.., Lq, L] shape
+    (a flattened 2-D [R, L] view cannot tell)."""
+    if Lq is not None:
+        return int(Lq)
+    if causal and x.dim() < 3:
+        raise ValueError(f"{what}: causal on a 2-D view needs Lq (rows per [Lq, L] matrix)")
+    return x.shape[-2]
+
+
+def softmax_fwd(S, P, Pd=None, mask=None, causal=False, scale=1.0, Lq=None):
     L = S.shape[-1]
-    Lq = S.shape[-2]
+    Lq = _causal_rows(S, Lq, causal, "softmax_fwd")
     R = S.numel() // L
     _lib.call("sat_softmax_fwd", _p(S), _p(P), _p(Pd), _p(mask), R, L, Lq, int(causal), scale,
               _stream())
 
 
-def softmax_bwd(P, dPd, dS, mask=None, scale=1.0, causal=False):
+def softmax_bwd(P, dPd, dS, mask=None, scale=1.0, causal=False, Lq=None):
     L = P.shape[-1]
+    Lq = _causal_rows(P, Lq, causal, "softmax_bwd")
     _lib.call("sat_softmax_bwd", _p(P), _p(dPd), _p(mask), _p(dS), P.numel() // L, L,
-              P.shape[-2], int(causal), scale, _stream())
+              Lq, int(causal), scale, _stream())
 
 
 def loss_fwd_bwd(mel, tgt, tmask, stop, done, dmask, out, dmel=None, dstop=None, l1_weight=0.1):

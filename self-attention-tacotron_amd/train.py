@@ -31,7 +31,7 @@ from .masks import mask_specs
 
 class Trainer:
     def __init__(self, model, B: int, N: int, Tp: int, seed: int = 1234,
-                 process_group=None):
+                 process_group=None, force_exchange: bool = False):
         self.m = model
         hp = model.hp
         dev = model.device
@@ -63,6 +63,8 @@ class Trainer:
         self.reshape(B, N, Tp)
         self.pg = process_group
         self.world = dp.world_size(process_group)
+        # run dp.exchange even in a one-rank group (tests of the RCCL path on one GPU)
+        self.force_exchange = force_exchange
         self.cfg.grad_scale = dp.grad_scale(process_group)
         self.last_loss = None
 
@@ -106,7 +108,8 @@ class Trainer:
         arena -- gradients (1/world folded into Adam), the BatchNorm moving statistics
         (averaged, so replicas never drift apart) and the health words (non-zero everywhere iff
         on some rank, so the guarded update is skipped on every rank or on none)."""
-        dp.exchange(self.m.exchange, self.m.health, self.m.bn.buf, self.m.health_tail, self.pg)
+        dp.exchange(self.m.exchange, self.m.health, self.m.bn.buf, self.m.health_tail, self.pg,
+                    force=self.force_exchange)
 
     def apply(self):
         """Guarded clip + Adam: skipped on the device when any health word of the step is set."""

@@ -31,6 +31,11 @@ def test_library_exports_every_header_symbol():
     assert not missing, missing
     lib = _lib.load()
     assert lib.sat_version() > 0
+    # the binding's struct layout == the header's == the library's
+    import re
+    hdr = open(_lib.HEADER_PATH).read()
+    assert int(re.search(r"#define SAT_ABI_VERSION (\d+)", hdr).group(1)) == _lib.ABI_VERSION
+    assert lib.sat_abi_version() == _lib.ABI_VERSION
     # host-only queries (no device touched)
     assert lib.sat_workspace_adam() > 0
     assert lib.sat_workspace_colreduce(1000, 256) > 0

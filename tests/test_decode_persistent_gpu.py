@@ -93,10 +93,11 @@ def test_one_launch_rerun_is_deterministic(cuda):
 
 
 def test_default_falls_back_when_one_launch_refused(cuda, monkeypatch):
-    """persistent=None: when the library refuses the one-launch decode at run time (e.g.
-    SAT_ERR_UNSUPPORTED on a device with too few co-resident workgroups) or a hand-off times out,
-    the run continues on the per-step launches from clean buffers and gives the launch path's
-    result; persistent=True raises instead."""
+    """persistent=None: when the library REFUSES the one-launch decode at run time
+    (SAT_ERR_UNSUPPORTED, e.g. a device with too few co-resident workgroups) the run continues
+    on the per-step launches from clean buffers with a warning and gives the launch path's
+    result; a hand-off timeout inside a launch that started is a hard error (it
+    would hide a regression), and persistent=True raises on a refusal too."""
     from sat_amd import _lib
     from sat_amd import kernels as K
     from sat_amd.inference import FreeRunningDecoder
@@ -106,16 +107,21 @@ def test_default_falls_back_when_one_launch_refused(cuda, monkeypatch):
     real = K.decode_persistent
 
     def refused(**kw):
-        raise _lib.SatLibraryError("sat_decode_persistent: fewer than 256 co-resident workgroups")
+        raise _lib.SatLibraryError("sat_decode_persistent: fewer than 256 co-resident workgroups",
+                                   _lib.SAT_ERR_UNSUPPORTED)
 
     def timed_out(**kw):
         real(**kw)
         kw["err"].fill_(1)
 
-    for fake in (refused, timed_out):
+    monkeypatch.setattr(K, "decode_persistent", timed_out)
+    with pytest.raises(_lib.SatLibraryError, match="timed out"):
+        FreeRunningDecoder(m, max_iters=T, min_iters=T).run(gb)
+    for fake in (refused,):
         monkeypatch.setattr(K, "decode_persistent", fake)
         dec = FreeRunningDecoder(m, max_iters=T, min_iters=T)
-        out = dec.run(gb)
+        with pytest.warns(RuntimeWarning, match="falls back to per-step launches"):
+            out = dec.run(gb)
         assert dec.last_path == "launches"
         assert out["steps"] == ref["steps"] == T
         assert torch.equal(out["mel"], ref["mel"])

@@ -49,6 +49,28 @@ def _gpu_kinks(sv, O):
     return {n: v.double().cpu() for n, v in k.items()}
 
 
+# at most this many of the encoder front's branch points may be decided differently by the
+# HIP forward (fp32) and the oracle (float64) per kind, before the oracle is handed the HIP's
+# branches (a systematic mask / max-pool bug must not be absorbed)
+KINK_FLIPS_MAX = 16
+
+
+def _bound_kink_flips(sv, O, p64, hp, b, mk, train):
+    """Count the branch points where the HIP forward's decision differs from the oracle's own
+    (float64, no substitution) and bound them; the counts go to the parity report."""
+    from sat_amd import params
+    ours = _gpu_kinks(sv, O)
+    with torch.no_grad():
+        theirs = O.encoder_front_branches(
+            O.to_torch(b)["source"], {k: v.detach() for k, v in p64.items()},
+            O.to_torch(params.init_bn_buffers(hp)), hp, None if mk is None else O.to_torch(mk),
+            train)
+    flips = {k: int((ours[k] != theirs[k]).sum()) for k in ours}
+    sizes = {k: int(ours[k].numel()) for k in ours}
+    _report("c2_train_kink_flips", flips=flips, sizes=sizes, bar=KINK_FLIPS_MAX)
+    assert all(v <= KINK_FLIPS_MAX for v in flips.values()), (flips, sizes)
+
+
 def _run(cuda, B, N, T, train, shape="max", seed=11, grads=False, preset="ljspeech",
          kinks=False):
     from sat_amd import data, engine, hparams, params
@@ -70,6 +92,8 @@ def _run(cuda, B, N, T, train, shape="max", seed=11, grads=False, preset="ljspee
     torch.cuda.synchronize()
     sv["dec"].tensors["attn_scratch"].check()
     p64 = {k: v.requires_grad_(grads) for k, v in O.to_torch(vals).items()}
+    if kinks:
+        _bound_kink_flips(sv, O, p64, hp, b, mk, train)
     with torch.set_grad_enabled(grads):
         ref = O.model_forward(p64, O.to_torch(params.init_bn_buffers(hp)), hp, O.to_torch(b),
                               None if mk is None else O.to_torch(mk), training=train,

@@ -524,3 +524,26 @@ def test_gemm_tri(cuda, L, K):
         assert torch.equal(full_t, part_t)
     ref64 = P.tril().double() @ V.double()
     assert float((kernels.gemm(P.tril(), V, tri=2).double() - ref64).abs().max()) < 1e-3
+
+
+def test_gemm_tri_batch1_long_k_never_splits(cuda):
+    """a batch-1 tri=1 product with K >= 512 (a split-K shape) must still leave the
+    tiles above the diagonal unwritten -- the planner takes no split under the hint -- and tri
+    with the fused bias-gradient row or segmented operands is refused."""
+    from sat_amd import _lib, kernels
+    g = torch.Generator().manual_seed(9)
+    L, K = 256, 1024
+    A = torch.randn(L, K, generator=g).to(cuda)
+    Bm = torch.randn(K, L, generator=g).to(cuda)
+    C = torch.full((L, L), float("nan"), device=cuda)
+    kernels.gemm(A, Bm, C, tri=1)
+    ref = A.double() @ Bm.double()          # (the untriangular product may split K: other bits)
+    low = torch.ones(L, L, device=cuda).tril().bool()
+    err = (C.double() - ref)[low].abs() / (A.abs().double() @ Bm.abs().double())[low]
+    assert float(err.max()) < 1e-6
+    assert bool(torch.isnan(C[:64, 128:]).all())            # wholly above the diagonal
+    with pytest.raises(_lib.SatLibraryError, match="tri cannot be combined"):
+        kernels.gemm(A, Bm, torch.empty(L, L, device=cuda), tri=1,
+                     colsum=torch.zeros(L, device=cuda))
+    with pytest.raises(_lib.SatLibraryError, match="tri cannot be combined"):
+        kernels.gemm(A[:, :512], Bm, torch.empty(L, L, device=cuda), tri=1, A2=A[:, 512:])

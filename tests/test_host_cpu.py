@@ -104,8 +104,9 @@ def test_synthetic_batch_contract(shape):
 
 def test_free_running_try_persistent_reports_why():
     """FreeRunningDecoder._try_persistent (the default decode's eligibility at run time): a
-    library refusal or a raised error word is reported, so run() can fall back to the per-step
-    launches (inference.py)."""
+    library REFUSAL (SAT_ERR_UNSUPPORTED) is reported, so run() falls back to the per-step
+    launches with a warning (inference.py); a raised error word (a hand-off timeout inside a
+    launch that started) or any other library error is a hard error."""
     import torch
     from sat_amd import _lib
     from sat_amd.inference import FreeRunningDecoder
@@ -117,11 +118,42 @@ def test_free_running_try_persistent_reports_why():
     dec = FreeRunningDecoder.__new__(FreeRunningDecoder)
 
     def refused(pl, Tm):
-        raise _lib.SatLibraryError("sat_decode_persistent: SAT_ERR_UNSUPPORTED")
+        raise _lib.SatLibraryError("sat_decode_persistent: SAT_ERR_UNSUPPORTED",
+                                   _lib.SAT_ERR_UNSUPPORTED)
+
+    def broken(pl, Tm):
+        raise _lib.SatLibraryError("sat_decode_persistent: launch failed", -2)
 
     dec._run_persistent = refused
     assert "UNSUPPORTED" in dec._try_persistent(Plan(), 5)
+    dec._run_persistent = broken
+    with pytest.raises(_lib.SatLibraryError, match="launch failed"):
+        dec._try_persistent(Plan(), 5)
     dec._run_persistent = lambda pl, Tm: pl.err.fill_(1)
-    assert "timed out" in dec._try_persistent(Plan(), 5)
+    with pytest.raises(_lib.SatLibraryError, match="timed out"):
+        dec._try_persistent(Plan(), 5)
     dec._run_persistent = lambda pl, Tm: None
     assert dec._try_persistent(Plan(), 5) is None
+
+
+def test_persistent_fallback_warns_once_with_reason():
+    """a training shape the one-launch persistent decoder cannot take
+    (here B=64 per GPU, and N=300 at B=32) warns once per shape, naming why, before the
+    per-step launch path runs; eligible shapes and an explicit persistent=False stay silent."""
+    import warnings
+    from sat_amd import decoder
+    d = params.resolve_dims(hparams.ljspeech_hparams())
+    decoder._FALLBACK_WARNED.clear()
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        assert decoder.use_persistent(d, 32, 200)
+        assert decoder.use_persistent(d, 8, 1024)
+        assert not decoder.use_persistent(d, 64, 200, persistent=False)
+        assert w == []
+        assert not decoder.use_persistent(d, 64, 200)
+        assert not decoder.use_persistent(d, 64, 200)            # once per shape
+        assert not decoder.use_persistent(d, 32, 300)
+    msgs = [str(x.message) for x in w if issubclass(x.category, decoder.PersistentFallbackWarning)]
+    assert len(msgs) == 2
+    assert "per-GPU batch 64" in msgs[0] and "B=32, N=300" in msgs[1]
+    assert decoder.persistent_ineligible_reason(d, 32, 256) is None

@@ -187,19 +187,8 @@ def test_oracle_kinks_from_its_own_forward_change_nothing():
     bufs = O.to_torch(params.init_bn_buffers(hp))
     b = O.to_torch(data.synthetic_batch(hp, 2, N=9, T=8, shape="ljs", seed=2))
     m = O.to_torch(data.synthetic_masks(hp, 2, b["source"].shape[1], 4, seed=3))
-    # the float64 forward's own branches
-    x = O.to_torch(vals)["embedding"][b["source"]]
-    p0 = O.to_torch(vals)
-    kinks = {}
-    for i in range(len(hp.encoder_prenet_out_units)):
-        x = O.prenet(x, p0, f"encoder/prenet{i}", m[f"enc/prenet{i}"])
-        kinks[f"prenet{i}"] = (x > 0).double()
-    bank = torch.cat([O.conv_bn(x, p0, bufs, f"encoder/cbhg/conv_bank/K{k}", True, relu=True)
-                      for k in range(1, hp.max_filter_width + 1)], dim=-1)
-    nxt = torch.cat([bank[:, 1:], bank[:, -1:]], 1)
-    kinks["bank"], kinks["pool_first"] = (bank > 0).double(), (bank >= nxt).double()
-    kinks["proj1"] = (O.conv_bn(O.maxpool2_same(bank), p0, bufs, "encoder/cbhg/proj1", True,
-                                relu=True) > 0).double()
+    # the float64 forward's own branches (the helper the C2 gradient test bounds flips with)
+    kinks = O.encoder_front_branches(b["source"], O.to_torch(vals), bufs, hp, m, True)
     res = []
     for kk in (None, kinks):
         p = {k: v.clone().requires_grad_(True) for k, v in O.to_torch(vals).items()}

@@ -1,4 +1,4 @@
-"""Drive the persistent decoder attention kernel (dec_attn_fwd_kernel) in the training
+"""Drive the persistent decoder attention kernels (dec_attn_fwd8 / bwd8) in the training
 configuration of the bench (B=32, N=200, T=1000, zoneout masks, energy-tanh history kept) for
 rocprofv3 PMC passes, one counter group per run:
 
@@ -30,9 +30,10 @@ def main(B=32, N=200, T=1000, passes=3):
           for k, v in data.synthetic_masks(hp, B, N, T // hp.outputs_per_step, seed=2).items()}
     for _ in range(passes):
         out, sv = m.forward(batch, mk, training=True)
+        m.backward(sv)               # the BPTT kernel (dec_attn_bwd8_kernel) too
         del out, sv
     torch.cuda.synchronize()
-    print("forward passes", passes)
+    print("forward + backward passes", passes)
 
 
 if __name__ == "__main__":

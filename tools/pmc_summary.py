@@ -6,8 +6,12 @@ bytes, with the gfx950 corrections of MI355X_MICROARCH.md (HBM section):
     widths are uncalibrated, so the doubled figure is an upper estimate for them);
   * WRITE_SIZE is exact for 16-B stores and is taken as is.
 
-    python3 tools/pmc_summary.py <fetch_dir> <write_dir> [kernel_regex]
+    python3 tools/pmc_summary.py <fetch_dir> <write_dir> [kernel_regex [kernel_source.hip]]
+
+With a kernel source file, the summary records its sha256 (first 16 hex digits) so bench.py can
+tell whether the committed traffic was measured on the tree it runs.
 """
+import hashlib
 import glob
 import json
 import re
@@ -47,10 +51,13 @@ def per_dispatch(path, counter, regex):
     return vals
 
 
-def main(fetch_dir, write_dir, regex="attn_energy_kernel"):
+def main(fetch_dir, write_dir, regex="attn_energy_kernel", source=None):
     f = per_dispatch(fetch_dir, "FETCH_SIZE", regex)
     w = per_dispatch(write_dir, "WRITE_SIZE", regex)
     out = {"kernel_regex": regex, "dispatches_fetch": len(f), "dispatches_write": len(w)}
+    if source:
+        out["source"] = source
+        out["source_sha16"] = hashlib.sha256(open(source, "rb").read()).hexdigest()[:16]
     if f and w:
         fk = sum(f) / len(f)
         wk = sum(w) / len(w)

@@ -184,10 +184,37 @@ typedef struct SatMha {
   int64_t scratch_bytes;
   void* gemm_ws;
   int64_t gemm_ws_bytes;
+  /* lse [B][H][L] (nullable): selects the fused causal attention (sat_flash_attn_fwd/bwd) for
+   * the score / softmax / context stage when causal, D / H == 128 and L % 4 == 0 -- the
+   * decoder head's shape.  The forward then writes lse instead of P / Pd (both may be NULL,
+   * nothing [L][L] is materialised) and the backward recomputes the probabilities from it. */
+  float* lse;
 } SatMha;
 int64_t sat_mha_scratch_bytes(int32_t B, int32_t L, int32_t D, int32_t H, int32_t out_dim);
 int sat_mha_fwd(const SatMha* d, void* stream);
 int sat_mha_bwd(const SatMha* d, void* stream);
+
+/* Fused causal scaled-dot-product attention (flash-style; the decoder head's mechanism,
+ * ScaledDotProductAttentionMechanism modules/self_attention.py:45-65 with
+ * use_subsequent_mask=True, built at modules/module.py:743-765): per (utterance b, head h)
+ * O_h = (softmax(Q_h K_h^T * scale + causal mask) * mask_h) V_h without materialising the
+ * [L][L] scores.  q, k, v, o, dout, dq, dk, dv are [B][L][ld] with head h in columns
+ * [h*128, h*128+128); mask [B][H][L][L] (dropout values, NULL = none); lse [B][H][L] the
+ * log2-domain row statistic the forward writes and the backward reads; delta [B][H][L]
+ * backward scratch.  dh = 128, causal = 1, L % 4 == 0, 16-byte aligned operands.
+ * scale <= 0 means 1/sqrt(128).  bwd WRITES dq, dk, dv. */
+typedef struct SatFlashAttn {
+  int32_t B, H, L, dh, causal;
+  float scale;
+  int64_t ld;
+  const float* q; const float* k; const float* v;
+  const float* mask;
+  float* o; float* lse;
+  const float* dout; float* delta;
+  float* dq; float* dk; float* dv;
+} SatFlashAttn;
+int sat_flash_attn_fwd(const SatFlashAttn* a, void* stream);
+int sat_flash_attn_bwd(const SatFlashAttn* a, void* stream);
 
 /* ---------------------------------------------------------------- CBHG conv bank
  * The K1..Kmax Conv1D(SAME) bank of ZoneoutCBHG (modules/module.py:77-80 over ext tacotron2

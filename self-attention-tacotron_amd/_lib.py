@@ -94,7 +94,11 @@ SatMha = _struct("SatMha", """
     i32:B i32:L i32:W i32:D i32:H i32:causal i32:out_dim i32:pad0 ptr:x ptr:Wq ptr:bq ptr:Wk
     ptr:bk ptr:Wv ptr:bv ptr:Wo ptr:bo ptr:probs_mask ptr:q ptr:k ptr:v ptr:P ptr:Pd ptr:o ptr:y
     ptr:dy ptr:dx ptr:dWq ptr:dbq ptr:dWk ptr:dbk ptr:dWv ptr:dbv ptr:dWo ptr:dbo ptr:scratch
-    i64:scratch_bytes ptr:gemm_ws i64:gemm_ws_bytes""")
+    i64:scratch_bytes ptr:gemm_ws i64:gemm_ws_bytes ptr:lse""")
+
+SatFlashAttn = _struct("SatFlashAttn", """
+    i32:B i32:H i32:L i32:dh i32:causal f32:scale i64:ld ptr:q ptr:k ptr:v ptr:mask ptr:o ptr:lse
+    ptr:dout ptr:delta ptr:dq ptr:dk ptr:dv""")
 
 class SatRngSegment(ctypes.Structure):      # mirrors include/sat_abi.h
     _fields_ = [("offset", ctypes.c_int64), ("n", ctypes.c_int64), ("stream_id", ctypes.c_uint64),
@@ -191,6 +195,8 @@ SIGNATURES = {
     "sat_cbhg_convbank_fwd": [ctypes.POINTER(SatConvBank), _P],
     "sat_mha_fwd": [ctypes.POINTER(SatMha), _P],
     "sat_mha_bwd": [ctypes.POINTER(SatMha), _P],
+    "sat_flash_attn_fwd": [ctypes.POINTER(SatFlashAttn), _P],
+    "sat_flash_attn_bwd": [ctypes.POINTER(SatFlashAttn), _P],
     "sat_cbhg_convbank_bwd": [ctypes.POINTER(SatConvBank), _P],
     "sat_rng_fill": [_P, _I64, _P, _U64, _F, _F, _P],
     "sat_rng_fill_segments": [_P, ctypes.POINTER(SatRngSegment), _I32, _P, _P],

@@ -40,6 +40,17 @@
 #ifndef SAT_FWD8_HSTORE7
 #define SAT_FWD8_HSTORE7 1   // the cell's C0 / REC0 / H0RAW / G0 stores on wave 7 (A/B switch)
 #endif
+#ifndef SAT_FWD8_OWNLDS
+// each workgroup stages its OWN records A_t / B_t from LDS (written when they are made) instead
+// of reading them back through L2: the group's last publisher then needs no round trip that
+// waits on its own stores, and its polls find the seven other records already there
+#define SAT_FWD8_OWNLDS 1
+#endif
+#ifndef SAT_FWD8_W7POLL
+// wave 7 (no energy positions when nt <= 28) polls the seven other A_t records while waves 0..6
+// form the location term, so the hand-off's round trip overlaps that work
+#define SAT_FWD8_W7POLL 1
+#endif
 #ifndef SAT_FWD8_HMERGE
 // the h part of the gate sums inside the cell phase's dot (one dot, one transpose-reduce) rather
 // than a separate h-dot after publishing record B: 5.84 -> 5.78 us/step (three interleaved
@@ -149,6 +160,7 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
   // wave 7 holds no energy positions when nt <= 28: it then stores the cell's histories in the
   // location-term phase (from LDS) instead of the cell lanes of every wave
   const bool w7_stores = SAT_FWD8_HSTORE7 && 4 * 7 >= nt;
+  const bool w7_poll = SAT_FWD8_OWNLDS && SAT_FWD8_W7POLL && 4 * 7 >= nt;
   const int64_t bN = (int64_t)b * N;
   const int len = (int)p.lengths[b];
   const float u = p.u;
@@ -325,7 +337,8 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
                                                                    : kRBal + hq - kPadL - kPadR);
       float4 x1 = make_float4(0.f, 0.f, 0.f, 0.f), x2 = x1;
       float hv = 0.f;
-      bool ok1 = false, ok2 = !two, ok3 = !hsrc;
+      const bool own = SAT_FWD8_OWNLDS && wave == j;     // staged from LDS when it was made
+      bool ok1 = own, ok2 = own || !two, ok3 = !hsrc;
 #if SAT_FWD8_TRACE
       // trace build: drain the wave's own earlier stores first, then time the poll alone
       const long long tq0 = wall_clock64();
@@ -352,9 +365,11 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
         }
       }
 #endif
-      recs[wave][2 + lane] = x1;
-      if (lane < kM2 / 4) recs[wave][2 + kM1 / 4 + lane] = x2;
-      else if (two) recs[wave][lane - kM2 / 4] = x2;
+      if (!own) {
+        recs[wave][2 + lane] = x1;
+        if (lane < kM2 / 4) recs[wave][2 + kM1 / 4 + lane] = x2;
+        else if (two) recs[wave][lane - kM2 / 4] = x2;
+      }
       if (hl) halo[hq] = hv;
       tick(0);
     ev(1);
@@ -556,9 +571,16 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
         }
         const float4 q4 = quad_gather(fold32(a));
         const int ra = (((t & 1) * B + b) * kW + j) * kRA;
-        if (lane < 32 && (lane & 3) == 0) stc4x(xl, rRA, ra / 4 + 8 * wave + (lane >> 2), tagf4(q4, bit));
-        if (wave == 1 && lane < kUW / 4)
-          stc4x(xl, rRA, (ra + kQ) / 4 + lane, *reinterpret_cast<const float4*>(&hst[4 * lane]));
+        if (lane < 32 && (lane & 3) == 0) {
+          const float4 qt = tagf4(q4, bit);
+          stc4x(xl, rRA, ra / 4 + 8 * wave + (lane >> 2), qt);
+          if (SAT_FWD8_OWNLDS) qst[j][8 * wave + (lane >> 2)] = qt;
+        }
+        if (wave == 1 && lane < kUW / 4) {
+          const float4 h4 = *reinterpret_cast<const float4*>(&hst[4 * lane]);
+          stc4x(xl, rRA, (ra + kQ) / 4 + lane, h4);
+          if (SAT_FWD8_OWNLDS) reinterpret_cast<float4*>(hbuf)[(kUW / 4) * j + lane] = h4;
+        }
       }
       tick(6);
     ev(7);
@@ -592,13 +614,54 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
     tick(8);
     ev(9);
 
-    // ============ 5. records A_t: wave jj stages record jj (query partial, h_t states)
-    {
+    // ============ 5. records A_t: wave jj stages record jj (query partial, h_t states); with
+    //                 w7_poll wave 7 alone stages the seven other records (it has no positions,
+    //                 so its poll's round trip runs beside waves 0..6's location term)
+    if (w7_poll) {
+      if (wave == 7) {
+        const unsigned want = lsb_tag(t);
+        constexpr int kRA4 = kRA / 4, kN4 = (kW - 1) * kRA4;     // 72 float4 per record, 504
+        float4 x[8];
+        bool ok[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          x[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+          ok[i] = lane + 64 * i >= kN4;
+        }
+        for (unsigned spins = 0;; ++spins) {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const int idx = lane + 64 * i, rec = idx / kRA4, off = idx - rec * kRA4;
+            const int jj = rec + (rec >= j ? 1 : 0);
+            if (!ok[i]) x[i] = ldc4(rRA, (((t & 1) * B + b) * kW + jj) * kRA4 + off);
+          }
+          bool all = true;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            ok[i] = ok[i] || tag_ok4(x[i], want);
+            all = all && ok[i];
+          }
+          if (!any_lane(!all) || gave_up) break;
+          if (poll_give_up(spins, p.err)) { gave_up = true; break; }
+          __builtin_amdgcn_s_sleep(1);
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int idx = lane + 64 * i, rec = idx / kRA4, off = idx - rec * kRA4;
+          const int jj = rec + (rec >= j ? 1 : 0);
+          if (idx < kN4) {
+            if (off < kQ / 4) qst[jj][off] = x[i];
+            else reinterpret_cast<float4*>(hbuf)[(kUW / 4) * jj + off - kQ / 4] = x[i];
+          }
+        }
+      }
+    } else {
       const unsigned want = lsb_tag(t);
       const int ra = (((t & 1) * B + b) * kW + wave) * kRA;
       const bool two = lane < kUW / 4;
       float4 x1 = make_float4(0.f, 0.f, 0.f, 0.f), x2 = x1;
-      bool ok1 = false, ok2 = !two;
+      const bool own = SAT_FWD8_OWNLDS && wave == j;
+      bool ok1 = own, ok2 = own || !two;
 #if SAT_FWD8_TRACE
       const long long tq0 = wall_clock64();
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -622,8 +685,10 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
         }
       }
 #endif
-      qst[wave][lane] = x1;
-      if (two) reinterpret_cast<float4*>(hbuf)[(kUW / 4) * wave + lane] = x2;   // units 32 jj + 4 lane
+      if (!own) {
+        qst[wave][lane] = x1;
+        if (two) reinterpret_cast<float4*>(hbuf)[(kUW / 4) * wave + lane] = x2;   // units 32 jj + 4 lane
+      }
     }
     tick(9);
     ev(10);
@@ -712,8 +777,10 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
         const float z2 = tagf(wave_sum_dpp(pe2), bit);
         if (lane == 0) {
           const int rb = (((t & 1) * B + b) * kW + j) * kRB;
-          stc4x(xl, rRB, rb / 4, make_float4(m1, z1, a1, m2));
-          stc4x(xl, rRB, rb / 4 + 1, tagf4(make_float4(z2, 0.f, 0.f, 0.f), bit));
+          const float4 s0 = make_float4(m1, z1, a1, m2), s1 = tagf4(make_float4(z2, 0.f, 0.f, 0.f), bit);
+          stc4x(xl, rRB, rb / 4, s0);
+          stc4x(xl, rRB, rb / 4 + 1, s1);
+          if (SAT_FWD8_OWNLDS) { recs[j][0] = s0; recs[j][1] = s1; }
         }
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // own-wave LDS copy is ready
@@ -738,16 +805,22 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
         c = fmaf(w4.w, v1s[r0 + 4 * k4 + 3][32 * wave + col], c);
       }
       const float4 c4 = quad_gather(fold32(c));
-      if (lane < 32 && (lane & 3) == 0)
-        stc4x(xl, rRB, (rb + kRBctx) / 4 + 8 * wave + (lane >> 2), tagf4(c4, bit));
+      if (lane < 32 && (lane & 3) == 0) {
+        const float4 ct = tagf4(c4, bit);
+        stc4x(xl, rRB, (rb + kRBctx) / 4 + 8 * wave + (lane >> 2), ct);
+        if (SAT_FWD8_OWNLDS) recs[j][2 + 8 * wave + (lane >> 2)] = ct;
+      }
       if (wave == 0) {
         const float* ws2 = &wsc[0][1][r0];
         float c2 = 0.f;
 #pragma unroll
         for (int k = 0; k < 16; ++k) c2 = fmaf(ws2[k], v2s[r0 + k][col], c2);
         const float4 q4 = quad_gather(fold32(c2));
-        if (lane < 32 && (lane & 3) == 0)
-          stc4x(xl, rRB, (rb + kRBctx + kM1) / 4 + (lane >> 2), tagf4(q4, bit));
+        if (lane < 32 && (lane & 3) == 0) {
+          const float4 ct = tagf4(q4, bit);
+          stc4x(xl, rRB, (rb + kRBctx + kM1) / 4 + (lane >> 2), ct);
+          if (SAT_FWD8_OWNLDS) recs[j][2 + kM1 / 4 + (lane >> 2)] = ct;
+        }
       } else if (wave == 1 && lane < kPadR + kPadL + 2) {
         const int q = lane;
         float v;

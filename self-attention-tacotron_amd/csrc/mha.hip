@@ -60,15 +60,34 @@ int head_gemm(int M, int N, int K, HeadOp a, HeadOp b, float* C, int64_t c_sm, i
   return sat_gemm(&g, s);
 }
 
+// the fused causal attention takes the decoder head's shape (dh = 128) when lse is given
+bool flash_ok(const SatMha* d) {
+  return d->lse && d->causal && d->D == 128 * d->H && d->L % 4 == 0 && aligned16(d->q) &&
+         aligned16(d->k) && aligned16(d->v) && aligned16(d->o) &&
+         (!d->probs_mask || aligned16(d->probs_mask));
+}
+
+SatFlashAttn flash_desc(const SatMha* d) {
+  SatFlashAttn fa;
+  std::memset(&fa, 0, sizeof(fa));
+  fa.B = d->B; fa.H = d->H; fa.L = d->L; fa.dh = 128; fa.causal = 1;
+  fa.scale = 1.f / std::sqrt(128.f);
+  fa.ld = d->D;
+  fa.q = d->q; fa.k = d->k; fa.v = d->v;
+  fa.mask = d->probs_mask;
+  fa.lse = d->lse;
+  return fa;
+}
+
 int check(const SatMha* d, bool bwd) {
   SAT_CHECK_ARG(d != nullptr, "sat_mha: null descriptor");
   SAT_CHECK_ARG(d->B > 0 && d->L > 0 && d->W > 0 && d->D > 0 && d->H > 0 && d->D % d->H == 0 &&
                     d->out_dim > 0,
                 "sat_mha: bad sizes (D must be a multiple of H)");
-  SAT_CHECK_ARG(d->x && d->Wq && d->Wk && d->Wv && d->Wo && d->q && d->k && d->v && d->P &&
-                    d->o,
-                "sat_mha: null tensor");
-  SAT_CHECK_ARG(!d->probs_mask || d->Pd, "sat_mha: a probability mask needs Pd");
+  SAT_CHECK_ARG(d->x && d->Wq && d->Wk && d->Wv && d->Wo && d->q && d->k && d->v &&
+                    (d->P || flash_ok(d)) && d->o,
+                "sat_mha: null tensor (P may be NULL only on the fused causal path)");
+  SAT_CHECK_ARG(!d->probs_mask || d->Pd || flash_ok(d), "sat_mha: a probability mask needs Pd");
   if (bwd) {
     SAT_CHECK_ARG(d->dy && d->dx && d->dWq && d->dWk && d->dWv && d->dWo,
                   "sat_mha_bwd: null gradient tensor");
@@ -130,6 +149,15 @@ extern "C" int sat_mha_fwd(const SatMha* d, void* stream) {
     SAT_TRY(dense(d->x, d->Wk, d->bk, d->k, R, d->W, D, 0.f, d, s));
     SAT_TRY(dense(d->x, d->Wv, d->bv, d->v, R, d->W, D, 0.f, d, s));
   }
+  if (flash_ok(d)) {
+    // scores, causal softmax, dropout and contexts fused per (utterance, head); nothing
+    // [L][L] is written (sat_flash_attn_fwd)
+    SatFlashAttn fa = flash_desc(d);
+    fa.o = d->o;
+    SAT_TRY(sat_flash_attn_fwd(&fa, s));
+    SAT_TRY(dense(d->o, d->Wo, d->bo, d->y, R, D, d->out_dim, 0.f, d, s));
+    return SAT_OK;
+  }
   // S[b,h] = Q_h K_h^T                                               (self_attention.py:55)
   // (causal: only the tiles on / below the diagonal; the softmax reads no further)
   SAT_TRY(head_gemm(L, L, dh, {d->q, D, 1, LD, dh}, {d->k, 1, D, LD, dh}, S, L, HLL, LL, 1.f, d,
@@ -183,6 +211,16 @@ extern "C" int sat_mha_bwd(const SatMha* d, void* stream) {
   // output projection
   SAT_TRY(wgrad(d->o, D, d->dy, d->out_dim, d->dWo, d->dbo));
   SAT_TRY(dgrad(d->dy, d->out_dim, d->Wo, D, dO, 0.f));
+  if (flash_ok(d)) {
+    // dQ, dK, dV of the fused causal attention, probabilities recomputed from lse
+    // (sat_flash_attn_bwd; delta in the unused score slab)
+    SatFlashAttn fa = flash_desc(d);
+    fa.o = d->o;
+    fa.dout = dO;
+    fa.delta = dPd;
+    fa.dq = dQ; fa.dk = dK; fa.dv = dV;
+    SAT_TRY(sat_flash_attn_bwd(&fa, s));
+  } else {
   // dPd = dO_h V_h^T ;  dV_h = Pd^T dO_h
   // (causal: dPd only on / below the diagonal; Pd^T upper-triangular)
   SAT_TRY(head_gemm(L, L, dh, {dO, D, 1, LD, dh}, {d->v, 1, D, LD, dh}, dPd, L, HLL, LL, 1.f, d,
@@ -196,6 +234,7 @@ extern "C" int sat_mha_bwd(const SatMha* d, void* stream) {
                     s, 2));
   SAT_TRY(head_gemm(L, dh, L, {dS, 1, L, HLL, LL}, {d->q, D, 1, LD, dh}, dK, D, LD, dh, 1.f, d,
                     s, 3));
+  }
   // input projections
   SAT_TRY(wgrad(d->x, Wi, dQ, D, d->dWq, d->dbq));
   SAT_TRY(wgrad(d->x, Wi, dK, D, d->dWk, d->dbk));

@@ -867,6 +867,30 @@ def transpose(x: torch.Tensor, out: torch.Tensor = None) -> torch.Tensor:
     return out
 
 
+# the fused causal attention (sat_flash_attn_fwd/bwd) for the decoder head's shape;
+# SAT_FLASH_ATTN=0 keeps the materialised scores (A/B and tests)
+FLASH_ATTN = os.environ.get("SAT_FLASH_ATTN", "1") != "0"
+
+
+def flash_attn_ok(causal: bool, dh: int, L: int) -> bool:
+    return FLASH_ATTN and causal and dh == 128 and L % 4 == 0
+
+
+def flash_attn(q, k, v, o, lse, heads: int, mask=None, dout=None, dq=None, dk=None, dv=None,
+               delta=None):
+    """sat_flash_attn_fwd (dout is None) / _bwd on [B, L, heads*128] row-major q/k/v/o (the
+    backward writes dq, dk, dv; ``delta`` [B, heads, L] scratch)."""
+    B, L, D = q.shape
+    a = _lib.SatFlashAttn()
+    a.B, a.H, a.L, a.dh, a.causal, a.scale, a.ld = B, heads, L, D // heads, 1, 0.0, q.stride(1)
+    a.q, a.k, a.v, a.mask, a.o, a.lse = _p(q), _p(k), _p(v), _p(mask), _p(o), _p(lse)
+    if dout is None:
+        _lib.check(_lib.load().sat_flash_attn_fwd(ctypes.byref(a), _stream()), "sat_flash_attn_fwd")
+        return
+    a.dout, a.delta, a.dq, a.dk, a.dv = _p(dout), _p(delta), _p(dq), _p(dk), _p(dv)
+    _lib.check(_lib.load().sat_flash_attn_bwd(ctypes.byref(a), _stream()), "sat_flash_attn_bwd")
+
+
 def mha_desc(x, Wq, bq, Wk, bk, Wv, bv, Wo, bo, heads: int, causal: bool, probs_mask, saved):
     """SatMha over x [B, L, W] with the forward's saved tensors (dict of q, k, v, P, Pd, o, y)."""
     B, L, W = x.shape
@@ -877,7 +901,7 @@ def mha_desc(x, Wq, bq, Wk, bk, Wv, bv, Wo, bo, heads: int, causal: bool, probs_
     d.x, d.Wq, d.bq, d.Wk, d.bk = _p(x), _p(Wq), _p(bq), _p(Wk), _p(bk)
     d.Wv, d.bv, d.Wo, d.bo = _p(Wv), _p(bv), _p(Wo), _p(bo)
     d.probs_mask = _p(probs_mask)
-    for f in ("q", "k", "v", "P", "Pd", "o", "y"):
+    for f in ("q", "k", "v", "P", "Pd", "o", "y", "lse"):
         setattr(d, f, _p(saved.get(f)))
     nbytes = int(_lib.load().sat_mha_scratch_bytes(B, L, d.D, heads, d.out_dim))
     scratch = torch.empty(nbytes, dtype=torch.uint8, device=x.device)

@@ -85,10 +85,17 @@ def mha_fwd(x: torch.Tensor, P, scope: str, heads: int, causal: bool,
     out = P[f"{scope}/output_projection/kernel"].shape[1]
     dev = x.device
     qkv = torch.empty(3, B, L, model, device=dev)     # one buffer: a single batched Q/K/V product
-    s = dict(x=x, q=qkv[0], k=qkv[1], v=qkv[2], P=torch.empty(B, heads, L, L, device=dev),
-             o=torch.empty(B, L, model, device=dev), y=torch.empty(B, L, out, device=dev),
-             mask=probs_mask, heads=heads, dh=model // heads, causal=causal, scope=scope)
-    s["Pd"] = torch.empty_like(s["P"]) if probs_mask is not None else s["P"]
+    s = dict(x=x, q=qkv[0], k=qkv[1], v=qkv[2], o=torch.empty(B, L, model, device=dev),
+             y=torch.empty(B, L, out, device=dev), mask=probs_mask, heads=heads,
+             dh=model // heads, causal=causal, scope=scope)
+    if K.flash_attn_ok(causal, model // heads, L):
+        # the decoder head (causal, dh = 128): scores, softmax, dropout and contexts fused per
+        # (utterance, head) -- only the row statistic is kept for the backward
+        s["lse"] = torch.empty(B, heads, L, device=dev)
+        s["P"] = s["Pd"] = None
+    else:
+        s["P"] = torch.empty(B, heads, L, L, device=dev)
+        s["Pd"] = torch.empty_like(s["P"]) if probs_mask is not None else s["P"]
     d, _ = K.mha_desc(x, *(P[f"{scope}/{n}_projection/{t}"] for n in ("query", "key", "value",
                                                                         "output")
                            for t in ("kernel", "bias")), heads, causal, probs_mask, s)

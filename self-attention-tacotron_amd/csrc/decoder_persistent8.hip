@@ -40,16 +40,12 @@
 #ifndef SAT_FWD8_HSTORE7
 #define SAT_FWD8_HSTORE7 1   // the cell's C0 / REC0 / H0RAW / G0 stores on wave 7 (A/B switch)
 #endif
-#ifndef SAT_FWD8_OWNLDS
-// each workgroup stages its OWN records A_t / B_t from LDS (written when they are made) instead
-// of reading them back through L2: the group's last publisher then needs no round trip that
-// waits on its own stores, and its polls find the seven other records already there
-#define SAT_FWD8_OWNLDS 1
-#endif
-#ifndef SAT_FWD8_W7POLL
-// wave 7 (no energy positions when nt <= 28) polls the seven other A_t records while waves 0..6
-// form the location term, so the hand-off's round trip overlaps that work
-#define SAT_FWD8_W7POLL 1
+#ifndef SAT_FWD8_ESCALE
+// the energies' tanh argument pre-scaled: K + b1 + convb W_loc and the folded location weights
+// held x 2 log2(e) in LDS, so tanh(a + q) = 1 - 2 / (1 + exp2(fma(q, 2 log2 e, a'))) takes one
+// fma where the plain form took an add and a multiply (16 per lane per step): 5.65 -> 5.58 us
+// per step over three interleaved rounds on one box (profiles/r05_fwd8_ab.txt)
+#define SAT_FWD8_ESCALE 1
 #endif
 #ifndef SAT_FWD8_HMERGE
 // the h part of the gate sums inside the cell phase's dot (one dot, one transpose-reduce) rather
@@ -78,6 +74,7 @@ constexpr int kRA = kQ + kUW;          // record A floats
 constexpr int kRB = 320;               // record B floats (307 used)
 constexpr int kRBctx = 8, kRBeh = kRBctx + kC, kRBet = kRBeh + kPadR, kRBal = kRBet + kPadL;
 constexpr int kR4 = 2 + kC / 4;        // staged record B: 2 statistics float4 + 72 context float4
+constexpr float kTwoLog2e = 2.8853900817779268f;   // 2 log2(e)
 static_assert(kRBal + 2 <= kRB && kK0 == 544 && kQ == 256 && kD1 % 16 == 0, "layout");
 
 struct Fwd8P {
@@ -160,7 +157,6 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
   // wave 7 holds no energy positions when nt <= 28: it then stores the cell's histories in the
   // location-term phase (from LDS) instead of the cell lanes of every wave
   const bool w7_stores = SAT_FWD8_HSTORE7 && 4 * 7 >= nt;
-  const bool w7_poll = SAT_FWD8_OWNLDS && SAT_FWD8_W7POLL && 4 * 7 >= nt;
   const int64_t bN = (int64_t)b * N;
   const int len = (int)p.lengths[b];
   const float u = p.u;
@@ -202,8 +198,9 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
 #pragma unroll
       for (int f = 0; f < kF; ++f) lb = fmaf(p.convb[f], p.locW[f * kD1 + c], lb);
     }
-    kc[r][c] = r >= nt ? 0.f : c < kD1 ? p.K1[(bN + n0 + r) * kD1 + c] + p.b1[c] + lb
-                                       : p.K2[(bN + n0 + r) * kD2 + (c - kD1)];
+    const float kv = r >= nt ? 0.f : c < kD1 ? p.K1[(bN + n0 + r) * kD1 + c] + p.b1[c] + lb
+                                            : p.K2[(bN + n0 + r) * kD2 + (c - kD1)];
+    kc[r][c] = SAT_FWD8_ESCALE ? kv * kTwoLog2e : kv;
   }
   for (int i = tid0; i < kKW * kQ; i += kTh) {
     const int k = i / kQ, c = i - k * kQ;
@@ -212,7 +209,7 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
 #pragma unroll
       for (int f = 0; f < kF; ++f) a = fmaf(p.convW[k * kF + f], p.locW[f * kD1 + c], a);
     }
-    cwl[k][c] = a;
+    cwl[k][c] = SAT_FWD8_ESCALE ? a * kTwoLog2e : a;
   }
   for (int i = tid0; i < kPmax * kM1 / 4; i += kTh) {
     const int r = i / (kM1 / 4), c4 = i - r * (kM1 / 4);
@@ -337,8 +334,7 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
                                                                    : kRBal + hq - kPadL - kPadR);
       float4 x1 = make_float4(0.f, 0.f, 0.f, 0.f), x2 = x1;
       float hv = 0.f;
-      const bool own = SAT_FWD8_OWNLDS && wave == j;     // staged from LDS when it was made
-      bool ok1 = own, ok2 = own || !two, ok3 = !hsrc;
+      bool ok1 = false, ok2 = !two, ok3 = !hsrc;
 #if SAT_FWD8_TRACE
       // trace build: drain the wave's own earlier stores first, then time the poll alone
       const long long tq0 = wall_clock64();
@@ -365,11 +361,9 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
         }
       }
 #endif
-      if (!own) {
-        recs[wave][2 + lane] = x1;
-        if (lane < kM2 / 4) recs[wave][2 + kM1 / 4 + lane] = x2;
-        else if (two) recs[wave][lane - kM2 / 4] = x2;
-      }
+      recs[wave][2 + lane] = x1;
+      if (lane < kM2 / 4) recs[wave][2 + kM1 / 4 + lane] = x2;
+      else if (two) recs[wave][lane - kM2 / 4] = x2;
       if (hl) halo[hq] = hv;
       tick(0);
     ev(1);
@@ -571,16 +565,9 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
         }
         const float4 q4 = quad_gather(fold32(a));
         const int ra = (((t & 1) * B + b) * kW + j) * kRA;
-        if (lane < 32 && (lane & 3) == 0) {
-          const float4 qt = tagf4(q4, bit);
-          stc4x(xl, rRA, ra / 4 + 8 * wave + (lane >> 2), qt);
-          if (SAT_FWD8_OWNLDS) qst[j][8 * wave + (lane >> 2)] = qt;
-        }
-        if (wave == 1 && lane < kUW / 4) {
-          const float4 h4 = *reinterpret_cast<const float4*>(&hst[4 * lane]);
-          stc4x(xl, rRA, (ra + kQ) / 4 + lane, h4);
-          if (SAT_FWD8_OWNLDS) reinterpret_cast<float4*>(hbuf)[(kUW / 4) * j + lane] = h4;
-        }
+        if (lane < 32 && (lane & 3) == 0) stc4x(xl, rRA, ra / 4 + 8 * wave + (lane >> 2), tagf4(q4, bit));
+        if (wave == 1 && lane < kUW / 4)
+          stc4x(xl, rRA, (ra + kQ) / 4 + lane, *reinterpret_cast<const float4*>(&hst[4 * lane]));
       }
       tick(6);
     ev(7);
@@ -614,54 +601,13 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
     tick(8);
     ev(9);
 
-    // ============ 5. records A_t: wave jj stages record jj (query partial, h_t states); with
-    //                 w7_poll wave 7 alone stages the seven other records (it has no positions,
-    //                 so its poll's round trip runs beside waves 0..6's location term)
-    if (w7_poll) {
-      if (wave == 7) {
-        const unsigned want = lsb_tag(t);
-        constexpr int kRA4 = kRA / 4, kN4 = (kW - 1) * kRA4;     // 72 float4 per record, 504
-        float4 x[8];
-        bool ok[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          x[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-          ok[i] = lane + 64 * i >= kN4;
-        }
-        for (unsigned spins = 0;; ++spins) {
-#pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            const int idx = lane + 64 * i, rec = idx / kRA4, off = idx - rec * kRA4;
-            const int jj = rec + (rec >= j ? 1 : 0);
-            if (!ok[i]) x[i] = ldc4(rRA, (((t & 1) * B + b) * kW + jj) * kRA4 + off);
-          }
-          bool all = true;
-#pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            ok[i] = ok[i] || tag_ok4(x[i], want);
-            all = all && ok[i];
-          }
-          if (!any_lane(!all) || gave_up) break;
-          if (poll_give_up(spins, p.err)) { gave_up = true; break; }
-          __builtin_amdgcn_s_sleep(1);
-        }
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const int idx = lane + 64 * i, rec = idx / kRA4, off = idx - rec * kRA4;
-          const int jj = rec + (rec >= j ? 1 : 0);
-          if (idx < kN4) {
-            if (off < kQ / 4) qst[jj][off] = x[i];
-            else reinterpret_cast<float4*>(hbuf)[(kUW / 4) * jj + off - kQ / 4] = x[i];
-          }
-        }
-      }
-    } else {
+    // ============ 5. records A_t: wave jj stages record jj (query partial, h_t states)
+    {
       const unsigned want = lsb_tag(t);
       const int ra = (((t & 1) * B + b) * kW + wave) * kRA;
       const bool two = lane < kUW / 4;
       float4 x1 = make_float4(0.f, 0.f, 0.f, 0.f), x2 = x1;
-      const bool own = SAT_FWD8_OWNLDS && wave == j;
-      bool ok1 = own, ok2 = own || !two;
+      bool ok1 = false, ok2 = !two;
 #if SAT_FWD8_TRACE
       const long long tq0 = wall_clock64();
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -685,10 +631,8 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
         }
       }
 #endif
-      if (!own) {
-        qst[wave][lane] = x1;
-        if (two) reinterpret_cast<float4*>(hbuf)[(kUW / 4) * wave + lane] = x2;   // units 32 jj + 4 lane
-      }
+      qst[wave][lane] = x1;
+      if (two) reinterpret_cast<float4*>(hbuf)[(kUW / 4) * wave + lane] = x2;   // units 32 jj + 4 lane
     }
     tick(9);
     ev(10);
@@ -711,8 +655,16 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int r = 4 * wave + i;
+#if SAT_FWD8_ESCALE
+        auto tz = [](float a2, float qv) {        // tanh(a + q) from a' = 2 log2(e) a
+          return fmaf(-2.f, __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(fmaf(qv, kTwoLog2e, a2))), 1.f);
+        };
+        const float4 z = make_float4(tz(Lr[i].x, q.x), tz(Lr[i].y, q.y), tz(Lr[i].z, q.z),
+                                     tz(Lr[i].w, q.w));
+#else
         const float4 z = make_float4(tanh_fast(Lr[i].x + q.x), tanh_fast(Lr[i].y + q.y),
                                      tanh_fast(Lr[i].z + q.z), tanh_fast(Lr[i].w + q.w));
+#endif
         float a = v4.x * z.x;
         a = fmaf(v4.y, z.y, a); a = fmaf(v4.z, z.z, a); a = fmaf(v4.w, z.w, a);
         e[i] = d1 ? a : 0.f;
@@ -777,10 +729,8 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
         const float z2 = tagf(wave_sum_dpp(pe2), bit);
         if (lane == 0) {
           const int rb = (((t & 1) * B + b) * kW + j) * kRB;
-          const float4 s0 = make_float4(m1, z1, a1, m2), s1 = tagf4(make_float4(z2, 0.f, 0.f, 0.f), bit);
-          stc4x(xl, rRB, rb / 4, s0);
-          stc4x(xl, rRB, rb / 4 + 1, s1);
-          if (SAT_FWD8_OWNLDS) { recs[j][0] = s0; recs[j][1] = s1; }
+          stc4x(xl, rRB, rb / 4, make_float4(m1, z1, a1, m2));
+          stc4x(xl, rRB, rb / 4 + 1, tagf4(make_float4(z2, 0.f, 0.f, 0.f), bit));
         }
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // own-wave LDS copy is ready
@@ -805,22 +755,16 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
         c = fmaf(w4.w, v1s[r0 + 4 * k4 + 3][32 * wave + col], c);
       }
       const float4 c4 = quad_gather(fold32(c));
-      if (lane < 32 && (lane & 3) == 0) {
-        const float4 ct = tagf4(c4, bit);
-        stc4x(xl, rRB, (rb + kRBctx) / 4 + 8 * wave + (lane >> 2), ct);
-        if (SAT_FWD8_OWNLDS) recs[j][2 + 8 * wave + (lane >> 2)] = ct;
-      }
+      if (lane < 32 && (lane & 3) == 0)
+        stc4x(xl, rRB, (rb + kRBctx) / 4 + 8 * wave + (lane >> 2), tagf4(c4, bit));
       if (wave == 0) {
         const float* ws2 = &wsc[0][1][r0];
         float c2 = 0.f;
 #pragma unroll
         for (int k = 0; k < 16; ++k) c2 = fmaf(ws2[k], v2s[r0 + k][col], c2);
         const float4 q4 = quad_gather(fold32(c2));
-        if (lane < 32 && (lane & 3) == 0) {
-          const float4 ct = tagf4(q4, bit);
-          stc4x(xl, rRB, (rb + kRBctx + kM1) / 4 + (lane >> 2), ct);
-          if (SAT_FWD8_OWNLDS) recs[j][2 + kM1 / 4 + (lane >> 2)] = ct;
-        }
+        if (lane < 32 && (lane & 3) == 0)
+          stc4x(xl, rRB, (rb + kRBctx + kM1) / 4 + (lane >> 2), tagf4(q4, bit));
       } else if (wave == 1 && lane < kPadR + kPadL + 2) {
         const int q = lane;
         float v;

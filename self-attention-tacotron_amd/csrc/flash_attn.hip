@@ -20,8 +20,9 @@
 //    and the shortest last, so the two co-resident workgroups of a CU carry equal work.
 //
 // Forward stores O and the row statistic lse = max + log2(sum) (log2 domain of the scaled
-// scores); the backward recomputes P from it: dQ kernel (query-owned, also forms
-// delta = rowsum(dO * O), the softmax-backward row term) then dK / dV kernel (key-owned).
+// scores); the backward recomputes P from it: a small pass forms delta = rowsum(dO * O) (the
+// softmax-backward row term), then ONE launch runs both roles -- dQ (query-owned rows) and
+// dK / dV (key-owned rows).
 // Numerics: fp32 throughout; the online softmax and the per-tile split of the 128-long dot
 // products change the summation order against the materialised path (sat_softmax_fwd + GEMMs),
 // not the precision.
@@ -208,13 +209,32 @@ __global__ void __launch_bounds__(256) flash_fwd_kernel(FlashP p) {
   }
 }
 
-// ---------------------------------------------------------------- backward: dQ (+ delta)
-// dS = scale * P * (dPd * mask - delta), delta_q = sum_j Pd_qj dPd_qj = dO_q . O_q
-__global__ void __launch_bounds__(256) flash_bwd_dq_kernel(FlashP p) {
-  __shared__ __attribute__((aligned(16))) float ks[2][ST * RS];
-  __shared__ __attribute__((aligned(16))) float vs[2][ST * RS];
-  const int nbh = p.B * p.H, bh = blockIdx.x % nbh;
-  const int qb = block_order(blockIdx.x / nbh, p.nblk, true);
+// ---------------------------------------------------------------- backward: delta
+// delta_q = sum_j Pd_qj dPd_qj = dO_q . O_q per (utterance, head, query), the softmax-backward
+// row term both backward roles read (same lane layout as the roles: lane (n, g) sums head
+// columns [32 g, 32 g + 32) of row q0 + n, then the 4-group sum)
+__global__ void __launch_bounds__(256) flash_delta_kernel(FlashP p) {
+  const int nbh = p.B * p.H, bh = blockIdx.x % nbh, qb = blockIdx.x / nbh;
+  const int b = bh / p.H, h = bh % p.H, L = p.L;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, n = lane & 15, g = lane >> 4;
+  const int qi = qb * 64 + 16 * w + n;
+  const bool qok = qi < L;
+  const int64_t roff = (int64_t)b * L * p.ld + h * FD + (int64_t)qi * p.ld + 32 * g;
+  float dor[32], orr[32];
+  load_row32(dor, p.dout + roff, qok);
+  load_row32(orr, p.o + roff, qok);
+  float part = 0.f;
+#pragma unroll
+  for (int s = 0; s < 32; ++s) part = fmaf(dor[s], orr[s], part);
+  const float dl = grp4_sum(part);
+  if (qok && g == 0) p.delta[(int64_t)bh * L + qi] = dl;
+}
+
+// ---------------------------------------------------------------- backward: dQ
+// dS = scale * P * (dPd * mask - delta)
+__device__ __forceinline__ void flash_bwd_dq(const FlashP& p, int bh, int qb, float* smem) {
+  float (*ks)[ST * RS] = reinterpret_cast<float (*)[ST * RS]>(smem);
+  float (*vs)[ST * RS] = reinterpret_cast<float (*)[ST * RS]>(smem + 2 * ST * RS);
   const int b = bh / p.H, h = bh % p.H, L = p.L;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, n = lane & 15, g = lane >> 4;
   const int Q0 = qb * 64, q0 = Q0 + 16 * w, qi = q0 + n;
@@ -227,17 +247,8 @@ __global__ void __launch_bounds__(256) flash_bwd_dq_kernel(FlashP p) {
   float qr[32], dor[32];
   load_row32(qr, p.q + roff, qok);
   load_row32(dor, p.dout + roff, qok);
-  float dl;
-  {
-    float orr[32];
-    load_row32(orr, p.o + roff, qok);
-    float part = 0.f;
-#pragma unroll
-    for (int s = 0; s < 32; ++s) part = fmaf(dor[s], orr[s], part);
-    dl = grp4_sum(part);
-  }
+  const float dl = qok ? p.delta[(int64_t)bh * L + qi] : 0.f;
   const float ls = qok ? p.lse[(int64_t)bh * L + qi] : 0.f;
-  if (qok && g == 0) p.delta[(int64_t)bh * L + qi] = dl;
   f32x4 acc[8];
 #pragma unroll
   for (int t = 0; t < 8; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -280,12 +291,11 @@ __global__ void __launch_bounds__(256) flash_bwd_dq_kernel(FlashP p) {
 }
 
 // ---------------------------------------------------------------- backward: dK, dV
-__global__ void __launch_bounds__(256, 2) flash_bwd_dkdv_kernel(FlashP p) {
-  __shared__ __attribute__((aligned(16))) float qs[2][ST * RS];
-  __shared__ __attribute__((aligned(16))) float gs[2][ST * RS];
-  __shared__ float lss[2][ST], dls[2][ST];
-  const int nbh = p.B * p.H, bh = blockIdx.x % nbh;
-  const int kb = block_order(blockIdx.x / nbh, p.nblk, false);
+__device__ __forceinline__ void flash_bwd_dkdv(const FlashP& p, int bh, int kb, float* smem) {
+  float (*qs)[ST * RS] = reinterpret_cast<float (*)[ST * RS]>(smem);
+  float (*gs)[ST * RS] = reinterpret_cast<float (*)[ST * RS]>(smem + 2 * ST * RS);
+  float (*lss)[ST] = reinterpret_cast<float (*)[ST]>(smem + 4 * ST * RS);
+  float (*dls)[ST] = reinterpret_cast<float (*)[ST]>(smem + 4 * ST * RS + 2 * ST);
   const int b = bh / p.H, h = bh % p.H, L = p.L;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, n = lane & 15, g = lane >> 4;
   const int K0 = kb * 64, k0 = K0 + 16 * w, kj = k0 + n;
@@ -371,6 +381,17 @@ __global__ void __launch_bounds__(256, 2) flash_bwd_dkdv_kernel(FlashP p) {
   }
 }
 
+// Both backward roles in ONE launch (they are independent once delta is known): workgroup
+// index -> (row-block rank, role, utterance x head), rank-major, so the longest blocks of both
+// roles are dispatched first and the shortest fill the slots they leave
+__global__ void __launch_bounds__(256, 2) flash_bwd_kernel(FlashP p) {
+  __shared__ __attribute__((aligned(16))) float smem[4 * ST * RS + 4 * ST];
+  const int nbh = p.B * p.H, rank = blockIdx.x / (2 * nbh), within = blockIdx.x - rank * 2 * nbh;
+  const int bh = within % nbh;
+  if (within < nbh) flash_bwd_dkdv(p, bh, block_order(rank, p.nblk, false), smem);
+  else flash_bwd_dq(p, bh, block_order(rank, p.nblk, true), smem);
+}
+
 int check(const SatFlashAttn* a, bool bwd) {
   SAT_CHECK_ARG(a != nullptr, "sat_flash_attn: null descriptor");
   SAT_CHECK_ARG(a->B > 0 && a->H > 0 && a->L > 0 && a->dh == FD && a->causal == 1 && a->L % 4 == 0 &&
@@ -416,9 +437,9 @@ extern "C" int sat_flash_attn_bwd(const SatFlashAttn* a, void* stream) {
   if (const int rc = check(a, true)) return rc;
   const FlashP p = params(a);
   hipStream_t s = as_stream(stream);
-  hipLaunchKernelGGL(flash_bwd_dq_kernel, dim3(p.B * p.H * p.nblk), dim3(256), 0, s, p);
-  SAT_LAUNCH_CHECK("sat_flash_attn_bwd (dQ)");
-  hipLaunchKernelGGL(flash_bwd_dkdv_kernel, dim3(p.B * p.H * p.nblk), dim3(256), 0, s, p);
-  SAT_LAUNCH_CHECK("sat_flash_attn_bwd (dK, dV)");
+  hipLaunchKernelGGL(flash_delta_kernel, dim3(p.B * p.H * p.nblk), dim3(256), 0, s, p);
+  SAT_LAUNCH_CHECK("sat_flash_attn_bwd (delta)");
+  hipLaunchKernelGGL(flash_bwd_kernel, dim3(2 * p.B * p.H * p.nblk), dim3(256), 0, s, p);
+  SAT_LAUNCH_CHECK("sat_flash_attn_bwd (dQ, dK, dV)");
   return SAT_OK;
 }

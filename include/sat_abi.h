@@ -38,8 +38,8 @@ extern "C" {
 /* Layout version of every struct / signature below: bumped whenever one changes, so a binding
  * (or an A/B run loading an older build through SAT_LIB_OVERRIDE) can refuse a library whose
  * structs it would misread.  5: round-5 layout (SatAttnParamGrad without zh, sat_softmax_bwd
- * with Lq / causal). */
-#define SAT_ABI_VERSION 5
+ * with Lq / causal, SatMha.lse); 6: SatMha.wgrad_stream / wgrad_ws. */
+#define SAT_ABI_VERSION 6
 
 /* ---------------------------------------------------------------- library */
 int sat_version(void);                         /* 100*major + minor */
@@ -184,25 +184,36 @@ typedef struct SatMha {
   int64_t scratch_bytes;
   void* gemm_ws;
   int64_t gemm_ws_bytes;
-  /* lse [B][H][L] (nullable): selects the fused causal attention (sat_flash_attn_fwd/bwd) for
-   * the score / softmax / context stage when causal, D / H == 128 and L % 4 == 0 -- the
-   * decoder head's shape.  The forward then writes lse instead of P / Pd (both may be NULL,
-   * nothing [L][L] is materialised) and the backward recomputes the probabilities from it. */
+  /* lse [B][H][L] (nullable): selects the fused attention (sat_flash_attn_fwd/bwd) for the
+   * score / softmax / context stage on its two shapes -- causal with D / H == 128 and
+   * L % 4 == 0 (the decoder head), or D / H in {8, 16, 32} with L <= 256, causal or not (the
+   * encoder's self-attention).  The forward then writes lse instead of P / Pd (both may be
+   * NULL, nothing [L][L] is materialised) and the backward recomputes the probabilities. */
   float* lse;
+  /* wgrad_stream (nullable, a hipStream_t as void*): the backward forks the four projection
+   * weight gradients onto it (dWo / dbo at entry, dWq..dbv once dQ / dK / dV exist) with its
+   * own split-K scratch wgrad_ws, and the caller's stream joins it before sat_mha_bwd returns --
+   * nothing downstream reads them, so they leave the input-gradient chain. */
+  void* wgrad_stream;
+  void* wgrad_ws;
+  int64_t wgrad_ws_bytes;
 } SatMha;
 int64_t sat_mha_scratch_bytes(int32_t B, int32_t L, int32_t D, int32_t H, int32_t out_dim);
 int sat_mha_fwd(const SatMha* d, void* stream);
 int sat_mha_bwd(const SatMha* d, void* stream);
 
-/* Fused causal scaled-dot-product attention (flash-style; the decoder head's mechanism,
- * ScaledDotProductAttentionMechanism modules/self_attention.py:45-65 with
- * use_subsequent_mask=True, built at modules/module.py:743-765): per (utterance b, head h)
- * O_h = (softmax(Q_h K_h^T * scale + causal mask) * mask_h) V_h without materialising the
+/* Fused scaled-dot-product attention (flash-style; ScaledDotProductAttentionMechanism,
+ * modules/self_attention.py:45-65): per (utterance b, head h)
+ * O_h = (softmax(Q_h K_h^T * scale [+ causal mask]) * mask_h) V_h without materialising the
  * [L][L] scores.  q, k, v, o, dout, dq, dk, dv are [B][L][ld] with head h in columns
- * [h*128, h*128+128); mask [B][H][L][L] (dropout values, NULL = none); lse [B][H][L] the
+ * [h*dh, h*dh+dh); mask [B][H][L][L] (dropout values, NULL = none); lse [B][H][L] the
  * log2-domain row statistic the forward writes and the backward reads; delta [B][H][L]
- * backward scratch.  dh = 128, causal = 1, L % 4 == 0, 16-byte aligned operands.
- * scale <= 0 means 1/sqrt(128).  bwd WRITES dq, dk, dv. */
+ * backward scratch (dh = 128 only).  Two shapes:
+ *   dh = 128, causal = 1, L % 4 == 0 -- the decoder head (use_subsequent_mask=True,
+ *     modules/module.py:743-765), MFMA tiles streaming the other operand through LDS;
+ *   dh in {8, 16, 32}, causal 0 or 1, L <= 256, (2 L dh + 2 L) * 4 <= 64 KB -- the encoder's
+ *     self-attention (modules/module.py:425-438), one (utterance, head) per workgroup's LDS.
+ * 16-byte aligned operands, ld % 4 == 0.  scale <= 0 means 1/sqrt(dh).  bwd WRITES dq, dk, dv. */
 typedef struct SatFlashAttn {
   int32_t B, H, L, dh, causal;
   float scale;

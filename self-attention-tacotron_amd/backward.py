@@ -91,8 +91,14 @@ def lin_bwd(x, dy, W, dW, db, ws, dx=None, beta_dx=0.0, need_dx=True, aux=None):
     return dx
 
 
-def mha_bwd(P, G, scope, s, dy, ws):
-    """Backward of model.mha_fwd: ONE sat_mha_bwd call.  Returns dx [B, L, W]."""
+# the projections' weight gradients of a multi-head attention backward on a stream of their own
+# (SatMha.wgrad_stream; joined inside sat_mha_bwd); SAT_MHA_WGRAD_SIDE=0 keeps them inline (A/B)
+MHA_WGRAD_SIDE = os.environ.get("SAT_MHA_WGRAD_SIDE", "1") == "1"
+
+
+def mha_bwd(P, G, scope, s, dy, ws, side=False):
+    """Backward of model.mha_fwd: ONE sat_mha_bwd call.  Returns dx [B, L, W].  ``side``: fork
+    the four projection weight gradients onto K.aux_stream(dev, 3) inside the call."""
     names = [f"{scope}/{n}_projection/{t}" for n in ("query", "key", "value", "output")
              for t in ("kernel", "bias")]
     d, _scratch = K.mha_desc(s["x"], *(P[n] for n in names), s["heads"], s["causal"], s["mask"], s)
@@ -100,6 +106,11 @@ def mha_bwd(P, G, scope, s, dy, ws):
     dyc = K.contiguous(dy)
     d.dy, d.dx = dyc.data_ptr(), dx.data_ptr()
     d.dWq, d.dbq, d.dWk, d.dbk, d.dWv, d.dbv, d.dWo, d.dbo = (G[n].data_ptr() for n in names)
+    if side and MHA_WGRAD_SIDE and dy.is_cuda:
+        st = K.aux_stream(dy.device, 3)
+        with torch.cuda.stream(st):
+            wws = K._gemm_ws(dy.device)
+        d.wgrad_stream, d.wgrad_ws, d.wgrad_ws_bytes = st.cuda_stream, wws.data_ptr(), wws.numel()
     K.mha_bwd(d)
     return dx
 
@@ -110,7 +121,7 @@ def sa_transformer_bwd(P, G, scope, s, dz, ws, aux=None):
     K.act_bwd(dz, s["u"], du, "tanh")
     dy = lin_bwd(s["y"], du, P[f"{scope}/transform/kernel"], G[f"{scope}/transform/kernel"],
                  G[f"{scope}/transform/bias"], ws, aux=aux)
-    dx = mha_bwd(P, G, f"{scope}/mha", s, dy, ws)
+    dx = mha_bwd(P, G, f"{scope}/mha", s, dy, ws, side=aux is not None)
     K.axpby(dz, dx, 1.0, 1.0)                                        # residual
     return dx
 

@@ -47,6 +47,13 @@
 // per step over three interleaved rounds on one box (profiles/r05_fwd8_ab.txt)
 #define SAT_FWD8_ESCALE 1
 #endif
+#ifndef SAT_FWD8_POLL1
+// the hand-off polls' first attempt branch-free: every lane issues its loads (clamped in-record
+// addresses for lanes without one), the tags are checked, and only a miss enters the retry
+// loop -- the first attempt succeeds on the critical path (trace: 0 spins), where the loop's
+// per-load exec-mask branches were ~30 branches + 150 scalar instructions of the staging phase
+#define SAT_FWD8_POLL1 1
+#endif
 #ifndef SAT_FWD8_HMERGE
 // the h part of the gate sums inside the cell phase's dot (one dot, one transpose-reduce) rather
 // than a separate h-dot after publishing record B: 5.84 -> 5.78 us/step (three interleaved
@@ -341,16 +348,29 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const long long tq1 = wall_clock64();
 #endif
-      for (unsigned spins = 0;; ++spins) {
-        if (!ok1) x1 = ldc4(rRB, (rec + kRBctx) / 4 + lane);
-        if (!ok2) x2 = ldc4(rRB, i2);
-        if (!ok3) hv = ldc(rRB, hsrc ? hw : 0);
+      bool retry = true;
+      if (SAT_FWD8_POLL1) {
+        x1 = ldc4(rRB, (rec + kRBctx) / 4 + lane);
+        x2 = ldc4(rRB, i2);                    // (lanes >= 10: in-record words, unused)
+        const float h0 = ldc(rRB, hsrc ? hw : 0);
+        hv = hsrc ? h0 : 0.f;                  // an absent neighbour's halo words stay 0
         ok1 = tag_ok4(x1, want);
         ok2 = ok2 || tag_ok4(x2, want);
         ok3 = ok3 || tag_ok(hv, want);
-        if (!any_lane(!(ok1 && ok2 && ok3)) || gave_up) break;
-        if (poll_give_up(spins, p.err)) { gave_up = true; break; }
-        __builtin_amdgcn_s_sleep(1);
+        retry = any_lane(!(ok1 && ok2 && ok3)) && !gave_up;
+      }
+      if (retry) {
+        for (unsigned spins = 0;; ++spins) {
+          if (!ok1) x1 = ldc4(rRB, (rec + kRBctx) / 4 + lane);
+          if (!ok2) x2 = ldc4(rRB, i2);
+          if (!ok3) hv = ldc(rRB, hsrc ? hw : 0);
+          ok1 = tag_ok4(x1, want);
+          ok2 = ok2 || tag_ok4(x2, want);
+          ok3 = ok3 || tag_ok(hv, want);
+          if (!any_lane(!(ok1 && ok2 && ok3)) || gave_up) break;
+          if (poll_give_up(spins, p.err)) { gave_up = true; break; }
+          __builtin_amdgcn_s_sleep(1);
+        }
       }
 #if SAT_FWD8_TRACE
       {
@@ -613,14 +633,24 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const long long tq1 = wall_clock64();
 #endif
-      for (unsigned spins = 0;; ++spins) {
-        if (!ok1) x1 = ldc4(rRA, ra / 4 + lane);
-        if (!ok2) x2 = ldc4(rRA, (ra + kQ) / 4 + lane);
+      bool retry = true;
+      if (SAT_FWD8_POLL1) {
+        x1 = ldc4(rRA, ra / 4 + lane);
+        x2 = ldc4(rRA, (ra + kQ) / 4 + (two ? lane : 0));
         ok1 = tag_ok4(x1, want);
         ok2 = ok2 || tag_ok4(x2, want);
-        if (!any_lane(!(ok1 && ok2)) || gave_up) break;
-        if (poll_give_up(spins, p.err)) { gave_up = true; break; }
-        __builtin_amdgcn_s_sleep(1);
+        retry = any_lane(!(ok1 && ok2)) && !gave_up;
+      }
+      if (retry) {
+        for (unsigned spins = 0;; ++spins) {
+          if (!ok1) x1 = ldc4(rRA, ra / 4 + lane);
+          if (!ok2) x2 = ldc4(rRA, (ra + kQ) / 4 + lane);
+          ok1 = tag_ok4(x1, want);
+          ok2 = ok2 || tag_ok4(x2, want);
+          if (!any_lane(!(ok1 && ok2)) || gave_up) break;
+          if (poll_give_up(spins, p.err)) { gave_up = true; break; }
+          __builtin_amdgcn_s_sleep(1);
+        }
       }
 #if SAT_FWD8_TRACE
       {

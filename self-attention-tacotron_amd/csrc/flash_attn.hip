@@ -40,6 +40,7 @@ using f32x4 = __attribute__((ext_vector_type(4))) float;
 
 struct FlashP {
   int B, H, L, nblk;          // nblk = ceil(L / 64) row blocks per (utterance, head)
+  int causal;                 // (the dh = 128 kernels are causal only)
   float c;                    // scale * log2(e): exponent factor of the raw scores
   float scale;                // 1 / sqrt(dh)
   int64_t ld;                 // row stride of q, k, v, o, dout, dq, dk, dv ([B][L][ld], head h at h*128)
@@ -392,8 +393,237 @@ __global__ void __launch_bounds__(256, 2) flash_bwd_kernel(FlashP p) {
   else flash_bwd_dq(p, bh, block_order(rank, p.nblk, true), smem);
 }
 
+// ---------------------------------------------------------------- narrow heads
+// The encoder's self-attention (SelfAttentionCBHGEncoder, modules/module.py:425-438: 2 heads of
+// 16 over the L = N <= 256 source positions, no causal mask, dropout on the probabilities): the
+// whole (utterance, head) fits one workgroup's LDS, and its 200 x 200 x 16 products are far too
+// small for MFMA tiles (the materialised path spends a chain of ~12 launches and four [L][L]
+// tensors on it).  A workgroup = 64 rows, 4 lanes per row, lane g4 of a row takes the keys (or
+// queries) g4, g4 + 4, ...; the other operand's rows of the (utterance, head) sit in LDS.
+//  * forward: pass 1 streams the scaled scores into a running (max, sum) per lane, the 4 lanes
+//    combine them into lse; pass 2 recomputes each score, P = 2^(s - lse), and accumulates
+//    O = sum_j P mask V_j -- no per-row score array, so the kernel holds ~3 DH registers;
+//  * backward, two roles in one launch: dQ (query-owned rows: dQ_i = scale sum_j dS_ij K_j) and
+//    dK / dV (key-owned rows: dV_j = sum_i Pd_ij dO_i, dK_j = scale sum_i dS_ij Q_i) with
+//    dS = P (mask dPd - delta), delta_i = dO_i . O_i formed where it is needed (no extra pass).
+// Same lse / delta conventions as the dh = 128 kernels above (log2 domain of the scaled scores).
+constexpr int kNarrowMaxL = 256;
+
+__device__ __forceinline__ float row4_max(float x) {
+  x = fmaxf(x, __shfl_xor(x, 1, 64));
+  return fmaxf(x, __shfl_xor(x, 2, 64));
+}
+__device__ __forceinline__ float row4_sum(float x) {
+  x += __shfl_xor(x, 1, 64);
+  return x + __shfl_xor(x, 2, 64);
+}
+// running (max, sum of 2^(s - max)) of two lanes merged; an empty lane has max = -inf
+__device__ __forceinline__ void lse_merge(float& m, float& z, float m2, float z2) {
+  const float mn = fmaxf(m, m2);
+  if (mn == -INFINITY) return;
+  z = (m == -INFINITY ? 0.f : z * exp2f(m - mn)) + (m2 == -INFINITY ? 0.f : z2 * exp2f(m2 - mn));
+  m = mn;
+}
+
+template <int DH>
+__device__ __forceinline__ void load_head_row(float (&r)[DH], const float* src, float mul) {
+#pragma unroll
+  for (int c = 0; c < DH / 4; ++c) {
+    const float4 x = reinterpret_cast<const float4*>(src)[c];
+    r[4 * c] = mul * x.x; r[4 * c + 1] = mul * x.y; r[4 * c + 2] = mul * x.z; r[4 * c + 3] = mul * x.w;
+  }
+}
+template <int DH>
+__device__ __forceinline__ float dot_lds(const float (&r)[DH], const float* row) {
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < DH / 4; ++c) {
+    const float4 x = reinterpret_cast<const float4*>(row)[c];
+    s = fmaf(r[4 * c], x.x, s); s = fmaf(r[4 * c + 1], x.y, s);
+    s = fmaf(r[4 * c + 2], x.z, s); s = fmaf(r[4 * c + 3], x.w, s);
+  }
+  return s;
+}
+template <int DH>
+__device__ __forceinline__ void axpy_lds(float (&acc)[DH], float w, const float* row) {
+#pragma unroll
+  for (int c = 0; c < DH / 4; ++c) {
+    const float4 x = reinterpret_cast<const float4*>(row)[c];
+    acc[4 * c] = fmaf(w, x.x, acc[4 * c]); acc[4 * c + 1] = fmaf(w, x.y, acc[4 * c + 1]);
+    acc[4 * c + 2] = fmaf(w, x.z, acc[4 * c + 2]); acc[4 * c + 3] = fmaf(w, x.w, acc[4 * c + 3]);
+  }
+}
+// the row's 4 lanes sum their partial vectors; lane g4 stores its quarter (DH / 4 columns)
+template <int DH>
+__device__ __forceinline__ void store_row4(float (&acc)[DH], float* dst, float mul, int g4, bool live) {
+#pragma unroll
+  for (int d = 0; d < DH; ++d) acc[d] = row4_sum(acc[d]);
+  if (!live) return;
+#pragma unroll
+  for (int d = 0; d < DH; ++d)
+    if (d / (DH / 4) == g4) dst[d] = mul * acc[d];
+}
+// the (utterance, head) rows of two [B][L][ld] operands into LDS [L][DH] each
+template <int DH>
+__device__ __forceinline__ void stage_head(float* sa, float* sb, const float* a, const float* b,
+                                           int64_t ld, int L) {
+  for (int idx = threadIdx.x; idx < L * (DH / 4); idx += blockDim.x) {
+    const int r = idx / (DH / 4), c = idx - r * (DH / 4);
+    reinterpret_cast<float4*>(sa)[idx] = *reinterpret_cast<const float4*>(a + r * ld + 4 * c);
+    reinterpret_cast<float4*>(sb)[idx] = *reinterpret_cast<const float4*>(b + r * ld + 4 * c);
+  }
+}
+
+template <int DH>
+__global__ void __launch_bounds__(256) narrow_fwd_kernel(FlashP p) {
+  extern __shared__ __attribute__((aligned(16))) float nsm[];
+  const int L = p.L;
+  float* Ks = nsm;
+  float* Vs = nsm + L * DH;
+  const int bh = blockIdx.x / p.nblk, blk = blockIdx.x - bh * p.nblk;
+  const int b = bh / p.H, h = bh - b * p.H;
+  const int64_t base = (int64_t)b * L * p.ld + h * DH;
+  stage_head<DH>(Ks, Vs, p.k + base, p.v + base, p.ld, L);
+  const int g4 = threadIdx.x & 3, i = blk * 64 + (threadIdx.x >> 2);
+  const bool live = i < L;
+  const int ii = live ? i : L - 1;
+  float q[DH];
+  load_head_row<DH>(q, p.q + base + ii * p.ld, p.c);
+  __syncthreads();
+  const int lim = p.causal ? ii + 1 : L;
+  float m = -INFINITY, z = 0.f;
+  for (int j = g4; j < lim; j += 4) {
+    const float s = dot_lds<DH>(q, Ks + j * DH);
+    if (s > m) { z = z * exp2f(m - s) + 1.f; m = s; }
+    else z += exp2f(s - m);
+  }
+  lse_merge(m, z, __shfl_xor(m, 1, 64), __shfl_xor(z, 1, 64));
+  lse_merge(m, z, __shfl_xor(m, 2, 64), __shfl_xor(z, 2, 64));
+  const float lse = m + log2f(z);
+  const float* mrow = p.mask ? p.mask + ((int64_t)bh * L + ii) * L : nullptr;
+  float acc[DH];
+#pragma unroll
+  for (int d = 0; d < DH; ++d) acc[d] = 0.f;
+  for (int j = g4; j < lim; j += 4) {
+    float w = exp2f(dot_lds<DH>(q, Ks + j * DH) - lse);
+    if (mrow) w *= mrow[j];
+    axpy_lds<DH>(acc, w, Vs + j * DH);
+  }
+  store_row4<DH>(acc, p.o + base + ii * p.ld, 1.f, g4, live);
+  if (live && g4 == 0) p.lse[(int64_t)bh * L + i] = lse;
+}
+
+// dQ role: 64 query rows; K, V of the (utterance, head) in LDS
+template <int DH>
+__device__ __forceinline__ void narrow_bwd_dq(const FlashP& p, int bh, int blk, float* sm) {
+  const int L = p.L;
+  float* Ks = sm;
+  float* Vs = sm + L * DH;
+  const int b = bh / p.H, h = bh - b * p.H;
+  const int64_t base = (int64_t)b * L * p.ld + h * DH;
+  stage_head<DH>(Ks, Vs, p.k + base, p.v + base, p.ld, L);
+  const int g4 = threadIdx.x & 3, i = blk * 64 + (threadIdx.x >> 2);
+  const bool live = i < L;
+  const int ii = live ? i : L - 1;
+  const int64_t row = base + ii * p.ld;
+  float q[DH], dO[DH], o[DH];
+  load_head_row<DH>(q, p.q + row, p.c);
+  load_head_row<DH>(dO, p.dout + row, 1.f);
+  load_head_row<DH>(o, p.o + row, 1.f);
+  float delta = 0.f;
+#pragma unroll
+  for (int d = 0; d < DH; ++d) delta = fmaf(dO[d], o[d], delta);
+  const float lse = p.lse[(int64_t)bh * L + ii];
+  const float* mrow = p.mask ? p.mask + ((int64_t)bh * L + ii) * L : nullptr;
+  __syncthreads();
+  const int lim = p.causal ? ii + 1 : L;
+  float acc[DH];
+#pragma unroll
+  for (int d = 0; d < DH; ++d) acc[d] = 0.f;
+  for (int j = g4; j < lim; j += 4) {
+    const float P = exp2f(dot_lds<DH>(q, Ks + j * DH) - lse);
+    const float dpd = dot_lds<DH>(dO, Vs + j * DH);
+    const float mk = mrow ? mrow[j] : 1.f;
+    axpy_lds<DH>(acc, P * (mk * dpd - delta), Ks + j * DH);
+  }
+  store_row4<DH>(acc, p.dq + row, p.scale, g4, live);
+}
+
+// dK / dV role: 64 key rows; Q, dO, lse and delta of every query row in LDS
+template <int DH>
+__device__ __forceinline__ void narrow_bwd_dkdv(const FlashP& p, int bh, int blk, float* sm) {
+  const int L = p.L;
+  float* Qs = sm;
+  float* Gs = sm + L * DH;
+  float* ls = sm + 2 * L * DH;
+  float* dl = ls + L;
+  const int b = bh / p.H, h = bh - b * p.H;
+  const int64_t base = (int64_t)b * L * p.ld + h * DH;
+  stage_head<DH>(Qs, Gs, p.q + base, p.dout + base, p.ld, L);
+  for (int r = threadIdx.x; r < L; r += blockDim.x) {
+    const float* go = p.dout + base + r * p.ld;
+    const float* oo = p.o + base + r * p.ld;
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < DH / 4; ++c) {
+      const float4 x = reinterpret_cast<const float4*>(go)[c], y = reinterpret_cast<const float4*>(oo)[c];
+      s = fmaf(x.x, y.x, s); s = fmaf(x.y, y.y, s); s = fmaf(x.z, y.z, s); s = fmaf(x.w, y.w, s);
+    }
+    dl[r] = s;
+    ls[r] = p.lse[(int64_t)bh * L + r];
+  }
+  const int g4 = threadIdx.x & 3, j = blk * 64 + (threadIdx.x >> 2);
+  const bool live = j < L;
+  const int jj = live ? j : L - 1;
+  const int64_t row = base + jj * p.ld;
+  float k[DH], v[DH];
+  load_head_row<DH>(k, p.k + row, p.c);
+  load_head_row<DH>(v, p.v + row, 1.f);
+  __syncthreads();
+  const float* mcol = p.mask ? p.mask + (int64_t)bh * L * L + jj : nullptr;
+  float dk[DH], dv[DH];
+#pragma unroll
+  for (int d = 0; d < DH; ++d) { dk[d] = 0.f; dv[d] = 0.f; }
+  for (int i = (p.causal ? jj : 0) + g4; i < L; i += 4) {
+    const float P = exp2f(dot_lds<DH>(k, Qs + i * DH) - ls[i]);
+    const float mk = mcol ? mcol[(int64_t)i * L] : 1.f;
+    const float dpd = dot_lds<DH>(v, Gs + i * DH);
+    axpy_lds<DH>(dv, P * mk, Gs + i * DH);
+    axpy_lds<DH>(dk, P * (mk * dpd - dl[i]), Qs + i * DH);
+  }
+  store_row4<DH>(dk, p.dk + row, p.scale, g4, live);
+  store_row4<DH>(dv, p.dv + row, 1.f, g4, live);
+}
+
+template <int DH>
+__global__ void __launch_bounds__(256) narrow_bwd_kernel(FlashP p) {
+  extern __shared__ __attribute__((aligned(16))) float nsm[];
+  const int nbh = p.B * p.H, role = blockIdx.x / (nbh * p.nblk);
+  const int w = blockIdx.x - role * nbh * p.nblk, bh = w / p.nblk, blk = w - bh * p.nblk;
+  if (role == 0) narrow_bwd_dkdv<DH>(p, bh, blk, nsm);
+  else narrow_bwd_dq<DH>(p, bh, blk, nsm);
+}
+
+bool narrow(const SatFlashAttn* a) { return a->dh != FD; }
+size_t narrow_lds(const SatFlashAttn* a) { return (2 * (size_t)a->L * a->dh + 2 * a->L) * sizeof(float); }
+
 int check(const SatFlashAttn* a, bool bwd) {
   SAT_CHECK_ARG(a != nullptr, "sat_flash_attn: null descriptor");
+  if (narrow(a)) {
+    SAT_CHECK_ARG(a->B > 0 && a->H > 0 && a->L > 0 && a->L <= kNarrowMaxL &&
+                      (a->dh == 8 || a->dh == 16 || a->dh == 32) && (a->causal == 0 || a->causal == 1) &&
+                      a->ld >= (int64_t)a->H * a->dh && a->ld % 4 == 0 && narrow_lds(a) <= 65536,
+                  "sat_flash_attn: narrow heads need dh in {8, 16, 32}, L <= 256, ld >= H * dh, "
+                  "ld %% 4 == 0 and (2 L dh + 2 L) * 4 <= 64 KB");
+    SAT_CHECK_ARG(a->q && a->k && a->v && a->o && a->lse, "sat_flash_attn: null q / k / v / o / lse");
+    SAT_CHECK_ARG(aligned16(a->q) && aligned16(a->k) && aligned16(a->v) && aligned16(a->o),
+                  "sat_flash_attn: operands must be 16-byte aligned");
+    if (bwd)
+      SAT_CHECK_ARG(a->dout && a->dq && a->dk && a->dv && aligned16(a->dout) && aligned16(a->dq) &&
+                        aligned16(a->dk) && aligned16(a->dv),
+                    "sat_flash_attn_bwd: null or unaligned dout / dq / dk / dv");
+    return SAT_OK;
+  }
   SAT_CHECK_ARG(a->B > 0 && a->H > 0 && a->L > 0 && a->dh == FD && a->causal == 1 && a->L % 4 == 0 &&
                     a->ld >= (int64_t)a->H * FD && a->ld % 4 == 0,
                 "sat_flash_attn: needs dh == 128, causal, L %% 4 == 0, ld >= H * 128, ld %% 4 == 0");
@@ -411,7 +641,8 @@ int check(const SatFlashAttn* a, bool bwd) {
 FlashP params(const SatFlashAttn* a) {
   FlashP p;
   p.B = a->B; p.H = a->H; p.L = a->L; p.nblk = (a->L + 63) / 64;
-  p.scale = a->scale > 0.f ? a->scale : 1.f / std::sqrt((float)FD);
+  p.causal = a->causal;
+  p.scale = a->scale > 0.f ? a->scale : 1.f / std::sqrt((float)a->dh);
   p.c = p.scale * kLog2e;
   p.ld = a->ld;
   p.q = a->q; p.k = a->k; p.v = a->v; p.mask = a->mask;
@@ -428,6 +659,16 @@ using namespace sat;
 extern "C" int sat_flash_attn_fwd(const SatFlashAttn* a, void* stream) {
   if (const int rc = check(a, false)) return rc;
   const FlashP p = params(a);
+  if (narrow(a)) {
+    const dim3 g(p.B * p.H * p.nblk);
+    const size_t shm = narrow_lds(a);
+    hipStream_t s = as_stream(stream);
+    if (a->dh == 8) hipLaunchKernelGGL(narrow_fwd_kernel<8>, g, dim3(256), shm, s, p);
+    else if (a->dh == 16) hipLaunchKernelGGL(narrow_fwd_kernel<16>, g, dim3(256), shm, s, p);
+    else hipLaunchKernelGGL(narrow_fwd_kernel<32>, g, dim3(256), shm, s, p);
+    SAT_LAUNCH_CHECK("sat_flash_attn_fwd (narrow)");
+    return SAT_OK;
+  }
   hipLaunchKernelGGL(flash_fwd_kernel, dim3(p.B * p.H * p.nblk), dim3(256), 0, as_stream(stream), p);
   SAT_LAUNCH_CHECK("sat_flash_attn_fwd");
   return SAT_OK;
@@ -437,6 +678,15 @@ extern "C" int sat_flash_attn_bwd(const SatFlashAttn* a, void* stream) {
   if (const int rc = check(a, true)) return rc;
   const FlashP p = params(a);
   hipStream_t s = as_stream(stream);
+  if (narrow(a)) {
+    const dim3 g(2 * p.B * p.H * p.nblk);
+    const size_t shm = narrow_lds(a);
+    if (a->dh == 8) hipLaunchKernelGGL(narrow_bwd_kernel<8>, g, dim3(256), shm, s, p);
+    else if (a->dh == 16) hipLaunchKernelGGL(narrow_bwd_kernel<16>, g, dim3(256), shm, s, p);
+    else hipLaunchKernelGGL(narrow_bwd_kernel<32>, g, dim3(256), shm, s, p);
+    SAT_LAUNCH_CHECK("sat_flash_attn_bwd (narrow)");
+    return SAT_OK;
+  }
   hipLaunchKernelGGL(flash_delta_kernel, dim3(p.B * p.H * p.nblk), dim3(256), 0, s, p);
   SAT_LAUNCH_CHECK("sat_flash_attn_bwd (delta)");
   hipLaunchKernelGGL(flash_bwd_kernel, dim3(2 * p.B * p.H * p.nblk), dim3(256), 0, s, p);

@@ -60,18 +60,35 @@ int head_gemm(int M, int N, int K, HeadOp a, HeadOp b, float* C, int64_t c_sm, i
   return sat_gemm(&g, s);
 }
 
-// the fused causal attention takes the decoder head's shape (dh = 128) when lse is given
+// three fork / join events per host thread (created once; recording them inside a stream
+// capture adds the edges to the graph)
+hipEvent_t* mha_events() {
+  static thread_local hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+  static thread_local bool ok = false;
+  if (!ok) {
+    for (auto& e : ev)
+      if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
+    ok = true;
+  }
+  return ev;
+}
+
+// the fused attention takes its two shapes when lse is given: the decoder head's (causal,
+// dh = 128) and the encoder's narrow heads (dh <= 32, L <= 256; sat_flash_attn_fwd)
 bool flash_ok(const SatMha* d) {
-  return d->lse && d->causal && d->D == 128 * d->H && d->L % 4 == 0 && aligned16(d->q) &&
-         aligned16(d->k) && aligned16(d->v) && aligned16(d->o) &&
-         (!d->probs_mask || aligned16(d->probs_mask));
+  const int dh = d->D / d->H;
+  const bool wide = d->causal && dh == 128 && d->L % 4 == 0;
+  const bool narrow = (dh == 8 || dh == 16 || dh == 32) && d->L <= 256 && d->D % 4 == 0 &&
+                      (2LL * d->L * dh + 2LL * d->L) * 4 <= 65536;
+  return d->lse && (wide || narrow) && aligned16(d->q) && aligned16(d->k) && aligned16(d->v) &&
+         aligned16(d->o) && (!d->probs_mask || aligned16(d->probs_mask));
 }
 
 SatFlashAttn flash_desc(const SatMha* d) {
   SatFlashAttn fa;
   std::memset(&fa, 0, sizeof(fa));
-  fa.B = d->B; fa.H = d->H; fa.L = d->L; fa.dh = 128; fa.causal = 1;
-  fa.scale = 1.f / std::sqrt(128.f);
+  fa.B = d->B; fa.H = d->H; fa.L = d->L; fa.dh = d->D / d->H; fa.causal = d->causal ? 1 : 0;
+  fa.scale = 1.f / std::sqrt((float)fa.dh);
   fa.ld = d->D;
   fa.q = d->q; fa.k = d->k; fa.v = d->v;
   fa.mask = d->probs_mask;
@@ -188,15 +205,36 @@ extern "C" int sat_mha_bwd(const SatMha* d, void* stream) {
   float* dPd = reinterpret_cast<float*>(p + 4 * act);
   float* dS = reinterpret_cast<float*>(p + 4 * act + score);
   const float* Pd = d->probs_mask ? d->Pd : d->P;
+  // the projections' weight gradients on their own stream when the caller gives one (forked
+  // by events, joined before returning; its own split-K scratch)
+  hipStream_t sw = s;
+  void* wws = d->gemm_ws;
+  int64_t wwsb = d->gemm_ws_bytes;
+  hipEvent_t* ev = nullptr;
+  if (d->wgrad_stream && as_stream(d->wgrad_stream) != s) {
+    ev = mha_events();
+    SAT_CHECK_ARG(ev != nullptr, "sat_mha_bwd: event creation failed");
+    sw = as_stream(d->wgrad_stream);
+    wws = d->wgrad_ws;
+    wwsb = d->wgrad_ws_bytes;
+  }
+  auto fork = [&](int i) -> int {
+    if (!ev) return SAT_OK;
+    if (hipEventRecord(ev[i], s) != hipSuccess || hipStreamWaitEvent(sw, ev[i], 0) != hipSuccess) {
+      set_error("sat_mha_bwd: stream fork failed");
+      return SAT_ERR_HIP;
+    }
+    return SAT_OK;
+  };
   auto wgrad = [&](const float* X, int K, const float* dY, int N, float* dW, float* db) -> int {
     SatGemmDesc g = dense_desc();   // dW += X^T dY
     g.M = K; g.N = N; g.K = R;
     g.A = X; g.a_sm = 1; g.a_sk = K;
     g.B = dY; g.b_sk = N; g.b_sn = 1;
     g.C = dW; g.c_sm = N; g.beta = 1.f;
-    g.ws = d->gemm_ws; g.ws_bytes = d->gemm_ws_bytes;
+    g.ws = wws; g.ws_bytes = wwsb;
     g.colsum_out = db;                // db += colsum(dY) in the same launch
-    SAT_TRY(sat_gemm(&g, s));
+    SAT_TRY(sat_gemm(&g, sw));
     return SAT_OK;
   };
   auto dgrad = [&](const float* dY, int N, const float* W, int K, float* dX, float beta) {
@@ -209,6 +247,7 @@ extern "C" int sat_mha_bwd(const SatMha* d, void* stream) {
     return sat_gemm(&g, s);
   };
   // output projection
+  SAT_TRY(fork(0));
   SAT_TRY(wgrad(d->o, D, d->dy, d->out_dim, d->dWo, d->dbo));
   SAT_TRY(dgrad(d->dy, d->out_dim, d->Wo, D, dO, 0.f));
   if (flash_ok(d)) {
@@ -236,6 +275,7 @@ extern "C" int sat_mha_bwd(const SatMha* d, void* stream) {
                     s, 3));
   }
   // input projections
+  SAT_TRY(fork(1));
   SAT_TRY(wgrad(d->x, Wi, dQ, D, d->dWq, d->dbq));
   SAT_TRY(wgrad(d->x, Wi, dK, D, d->dWk, d->dbk));
   SAT_TRY(wgrad(d->x, Wi, dV, D, d->dWv, d->dbv));
@@ -255,5 +295,11 @@ extern "C" int sat_mha_bwd(const SatMha* d, void* stream) {
     SAT_TRY(dgrad(dK, D, d->Wk, Wi, d->dx, 1.f));
   }
   SAT_TRY(dgrad(dV, D, d->Wv, Wi, d->dx, 1.f));
+  if (ev) {   // join: the caller's stream waits for the weight-gradient branch
+    if (hipEventRecord(ev[2], sw) != hipSuccess || hipStreamWaitEvent(s, ev[2], 0) != hipSuccess) {
+      set_error("sat_mha_bwd: stream join failed");
+      return SAT_ERR_HIP;
+    }
+  }
   return SAT_OK;
 }

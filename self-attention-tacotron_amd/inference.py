@@ -507,7 +507,7 @@ class FreeRunningDecoder:
             raise ValueError(f"forced alignments must be [B={B}, T', N={N}], got "
                              f"{tuple(self.forced[0].shape)}")
         pl = self._plan(B, N, Tm)
-        sv = {}
+        sv = {"keep_probs": True}      # the encoder self-alignments are an output here
         # the encoder BiLSTM as one launch (encoder_lstm.hip) like the training step's
         m1, m2 = encoder_fwd(P, m.bn, hp, d, ids, lengths, None, False, m.ws, sv,
                              persistent=m.persistent_decoder)

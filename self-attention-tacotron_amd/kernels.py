@@ -870,19 +870,28 @@ def transpose(x: torch.Tensor, out: torch.Tensor = None) -> torch.Tensor:
 # the fused causal attention (sat_flash_attn_fwd/bwd) for the decoder head's shape;
 # SAT_FLASH_ATTN=0 keeps the materialised scores (A/B and tests)
 FLASH_ATTN = os.environ.get("SAT_FLASH_ATTN", "1") != "0"
+# SAT_FLASH_NARROW=0 keeps the encoder's narrow heads on the materialised path (A/B)
+FLASH_NARROW = os.environ.get("SAT_FLASH_NARROW", "1") != "0"
 
 
 def flash_attn_ok(causal: bool, dh: int, L: int) -> bool:
-    return FLASH_ATTN and causal and dh == 128 and L % 4 == 0
+    """the fused attention's two shapes: the decoder head (causal, dh = 128) and narrow heads
+    (dh in {8, 16, 32}, L <= 256, causal or not: the encoder's self-attention)"""
+    if not FLASH_ATTN:
+        return False
+    if causal and dh == 128 and L % 4 == 0:
+        return True
+    return FLASH_NARROW and dh in (8, 16, 32) and L <= 256 and (2 * L * dh + 2 * L) * 4 <= 65536
 
 
 def flash_attn(q, k, v, o, lse, heads: int, mask=None, dout=None, dq=None, dk=None, dv=None,
-               delta=None):
-    """sat_flash_attn_fwd (dout is None) / _bwd on [B, L, heads*128] row-major q/k/v/o (the
-    backward writes dq, dk, dv; ``delta`` [B, heads, L] scratch)."""
+               delta=None, causal: bool = True):
+    """sat_flash_attn_fwd (dout is None) / _bwd on [B, L, heads*dh] row-major q/k/v/o (the
+    backward writes dq, dk, dv; ``delta`` [B, heads, L] scratch, dh = 128 only)."""
     B, L, D = q.shape
     a = _lib.SatFlashAttn()
-    a.B, a.H, a.L, a.dh, a.causal, a.scale, a.ld = B, heads, L, D // heads, 1, 0.0, q.stride(1)
+    a.B, a.H, a.L, a.dh, a.scale, a.ld = B, heads, L, D // heads, 0.0, q.stride(1)
+    a.causal = 1 if causal else 0
     a.q, a.k, a.v, a.mask, a.o, a.lse = _p(q), _p(k), _p(v), _p(mask), _p(o), _p(lse)
     if dout is None:
         _lib.check(_lib.load().sat_flash_attn_fwd(ctypes.byref(a), _stream()), "sat_flash_attn_fwd")

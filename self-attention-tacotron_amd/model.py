@@ -88,9 +88,10 @@ def mha_fwd(x: torch.Tensor, P, scope: str, heads: int, causal: bool,
     s = dict(x=x, q=qkv[0], k=qkv[1], v=qkv[2], o=torch.empty(B, L, model, device=dev),
              y=torch.empty(B, L, out, device=dev), mask=probs_mask, heads=heads,
              dh=model // heads, causal=causal, scope=scope)
-    if K.flash_attn_ok(causal, model // heads, L):
-        # the decoder head (causal, dh = 128): scores, softmax, dropout and contexts fused per
-        # (utterance, head) -- only the row statistic is kept for the backward
+    if K.flash_attn_ok(causal, model // heads, L) and not sv.get("keep_probs"):
+        # the decoder head (causal, dh = 128) and the encoder's narrow heads: scores, softmax,
+        # dropout and contexts fused per (utterance, head) -- only the row statistic is kept for
+        # the backward (sv["keep_probs"]: the caller wants P itself, e.g. inference alignments)
         s["lse"] = torch.empty(B, heads, L, device=dev)
         s["P"] = s["Pd"] = None
     else:

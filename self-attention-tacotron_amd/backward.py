@@ -93,7 +93,7 @@ def lin_bwd(x, dy, W, dW, db, ws, dx=None, beta_dx=0.0, need_dx=True, aux=None):
 
 # the projections' weight gradients of a multi-head attention backward on a stream of their own
 # (SatMha.wgrad_stream; joined inside sat_mha_bwd); SAT_MHA_WGRAD_SIDE=0 keeps them inline (A/B)
-MHA_WGRAD_SIDE = os.environ.get("SAT_MHA_WGRAD_SIDE", "1") == "1"
+MHA_WGRAD_SIDE = os.environ.get("SAT_MHA_WGRAD_SIDE", "0") == "1"
 
 
 def mha_bwd(P, G, scope, s, dy, ws, side=False):

@@ -22,6 +22,27 @@ namespace sat {
 namespace {
 
 using f32x16 = __attribute__((ext_vector_type(16))) float;
+using f4v = __attribute__((ext_vector_type(4))) float;
+using f2v = __attribute__((ext_vector_type(2))) float;
+
+// One operand's MFMA fragments of a K-tile (16 steps x S sub-tiles of 32) in the register shape
+// its LDS reads produce, so the two sets carried around the K loop stay whole register tuples:
+// K-major images are read 4 steps at a time (ds_read_b128), M/N-major ones one step at a time,
+// and the compiler pairs the two sub-tiles of a step (ds_read2_b32) when S = 2 or two steps
+// (ds_read2st64_b32) when S = 1.  (Scalar [16][S] arrays made it re-assemble the loop-carried
+// set with up to 36 v_mov per K-tile, each behind a wait on the reads just issued.)
+template <int S, bool KM>
+struct Frag {
+  f4v v[S][4];
+  __device__ __forceinline__ float get(int i, int t) const { return v[i][t >> 2][t & 3]; }
+  __device__ __forceinline__ void set(int i, int t, float x) { v[i][t >> 2][t & 3] = x; }
+};
+template <>
+struct Frag<2, false> {
+  f2v v[16];
+  __device__ __forceinline__ float get(int i, int t) const { return v[t][i]; }
+  __device__ __forceinline__ void set(int i, int t, float x) { v[t][i] = x; }
+};
 
 constexpr int BK = 32;
 
@@ -604,6 +625,8 @@ __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 __device__ __forceinline__ void raw_barrier() { asm volatile("s_barrier" ::: "memory"); }
+// s_waitcnt simm16 of gfx9 with only lgkmcnt(0): vmcnt 63 ([3:0] | [15:14]), expcnt 7 ([6:4])
+constexpr int kLgkm0 = 0xC07F;
 
 // One global_load_lds_dwordx4: 16 bytes per lane into LDS at lds_off + 16 * lane.  Issued from
 // inline asm so the compiler does not track it: its own wait insertion would otherwise put a
@@ -860,8 +883,10 @@ __global__ void __launch_bounds__((64 * lds_waves<BM, BN>())) gemm_lds_kernel(Ge
 
   const int li = lane & 31, lh = lane >> 5;
   const int swz = (li >> 1) & 7;     // K-major read swizzle of this lane's rows
-  // fragments of one K-tile: step t = 4 jj + i takes k = 8 jj + 4 h + i (both operands)
-  auto read_frags = [&](int stage, float (&a)[16][SM], float (&b)[16][SN]) {
+  // fragments of one K-tile: step t = 4 jj + i takes k = 8 jj + 4 h + i (both operands; Frag)
+  using FA = Frag<SM, AKM>;
+  using FB = Frag<SN, BKM>;
+  auto read_frags = [&](int stage, FA& a, FB& b) {
     const float* la = lds + stage * ST_SZ;
     const float* lb = la + A_SZ;
     if constexpr (AKM) {
@@ -869,43 +894,39 @@ __global__ void __launch_bounds__((64 * lds_waves<BM, BN>())) gemm_lds_kernel(Ge
       for (int i = 0; i < SM; ++i)
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) {
-          const float4 v = *reinterpret_cast<const float4*>(
-              la + (wm + i * 32 + li) * BK + 4 * ((2 * jj + lh) ^ swz));
-          a[4 * jj][i] = v.x; a[4 * jj + 1][i] = v.y; a[4 * jj + 2][i] = v.z; a[4 * jj + 3][i] = v.w;
+          a.v[i][jj] = *reinterpret_cast<const f4v*>(la + (wm + i * 32 + li) * BK + 4 * ((2 * jj + lh) ^ swz));
         }
     } else {
 #pragma unroll
       for (int t = 0; t < 16; ++t)
 #pragma unroll
         for (int i = 0; i < SM; ++i)
-          a[t][i] = la[(8 * (t >> 2) + 4 * lh + (t & 3)) * BM + wm + i * 32 + li];
+          a.set(i, t, la[(8 * (t >> 2) + 4 * lh + (t & 3)) * BM + wm + i * 32 + li]);
     }
     if constexpr (BKM) {
 #pragma unroll
       for (int j = 0; j < SN; ++j)
 #pragma unroll
         for (int jj = 0; jj < 4; ++jj) {
-          const float4 v = *reinterpret_cast<const float4*>(
-              lb + (wn + j * 32 + li) * BK + 4 * ((2 * jj + lh) ^ swz));
-          b[4 * jj][j] = v.x; b[4 * jj + 1][j] = v.y; b[4 * jj + 2][j] = v.z; b[4 * jj + 3][j] = v.w;
+          b.v[j][jj] = *reinterpret_cast<const f4v*>(lb + (wn + j * 32 + li) * BK + 4 * ((2 * jj + lh) ^ swz));
         }
     } else {
 #pragma unroll
       for (int t = 0; t < 16; ++t)
 #pragma unroll
         for (int j = 0; j < SN; ++j)
-          b[t][j] = lb[(8 * (t >> 2) + 4 * lh + (t & 3)) * BN + wn + j * 32 + li];
+          b.set(j, t, lb[(8 * (t >> 2) + 4 * lh + (t & 3)) * BN + wn + j * 32 + li]);
     }
   };
-  auto mfma_steps = [&](int t0, int t1, const float (&a)[16][SM], const float (&b)[16][SN]) {
+  auto mfma_steps = [&](int t0, int t1, const FA& a, const FB& b) {
 #pragma unroll
     for (int t = t0; t < t1; ++t)
 #pragma unroll
       for (int i = 0; i < SM; ++i)
 #pragma unroll
         for (int j = 0; j < SN; ++j)
-          acc[t % NC][i][j] =
-              __builtin_amdgcn_mfma_f32_32x32x2f32(a[t][i], b[t][j], acc[t % NC][i][j], 0, 0, 0);
+          acc[t % NC][i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(
+              a.get(i, t), b.get(j, t), acc[t % NC][i][j], 0, 0, 0);
   };
 
   // Schedule per K-tile kt (fragments of kt already in registers): issue the DMA of kt+2 into
@@ -914,7 +935,8 @@ __global__ void __launch_bounds__((64 * lds_waves<BM, BN>())) gemm_lds_kernel(Ge
   // the next issue overwrites); read kt+1's fragments into the other register set while
   // MFMA steps 8-15 of kt run.  Two register sets alternate, so the loop is unrolled by 2.
   const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
-  float fa0[16][SM], fb0[16][SN], fa1[16][SM], fb1[16][SN];
+  FA fa0, fa1;
+  FB fb0, fb1;
   if (nk > 0) {
     issue(0, kbeg);
     if (nk > 1) issue(1, kbeg + BK);
@@ -922,11 +944,15 @@ __global__ void __launch_bounds__((64 * lds_waves<BM, BN>())) gemm_lds_kernel(Ge
     raw_barrier();
     read_frags(0, fa0, fb0);
   }
-  auto tile = [&](int kt, int stage, const float (&ca)[16][SM], const float (&cb)[16][SN],
-                  float (&na)[16][SM], float (&nb)[16][SN]) {
+  auto tile = [&](int kt, int stage, const FA& ca, const FB& cb, FA& na, FB& nb) {
     const bool more2 = kt + 2 < nk;
     if (more2) issue(stage == 0 ? 2 : stage - 1, kbeg + (kt + 2) * BK);
     mfma_steps(0, 8, ca, cb);
+    // every fragment read of this K-tile has landed by now (issued a half K-tile ago); saying so
+    // with the compiler-visible form of s_waitcnt lgkmcnt(0), on both paths, stops it from
+    // making MFMA steps 8-15 wait behind the next tile's 16 reads (the in-order lgkmcnt cannot
+    // single out the older reads those steps use)
+    __builtin_amdgcn_s_waitcnt(kLgkm0);
     if (kt + 1 < nk) {
       if (more2) wait_vmcnt<LPT>(); else wait_vmcnt<0>();
       raw_barrier();

@@ -38,8 +38,8 @@ extern "C" {
 /* Layout version of every struct / signature below: bumped whenever one changes, so a binding
  * (or an A/B run loading an older build through SAT_LIB_OVERRIDE) can refuse a library whose
  * structs it would misread.  5: round-5 layout (SatAttnParamGrad without zh, sat_softmax_bwd
- * with Lq / causal, SatMha.lse); 6: SatMha.wgrad_stream / wgrad_ws. */
-#define SAT_ABI_VERSION 6
+ * with Lq / causal, SatMha.lse); 6: SatMha.wgrad_stream / wgrad_ws; 7: SatAttnParamGrad.tsplit. */
+#define SAT_ABI_VERSION 7
 
 /* ---------------------------------------------------------------- library */
 int sat_version(void);                         /* 100*major + minor */
@@ -508,7 +508,10 @@ int sat_attn_step_bwd(const SatAttnStepBwd* args, void* stream);
  * b*N + n).  Writes dK1 [B][N][D1], dK2 [B][N][D2] (overwritten) and one partial row per
  * workgroup, pg [sat_attn_param_grad_rows(B, N)][pg_stride] =
  * [dv1 D1 | dW_loc F*D1 | dconvW KW*F | dconvb F | dv2 D2] (F = KW = 0 when !att1_forward),
- * to be column-summed. */
+ * to be column-summed.  tsplit = k > 1 splits the T steps into k ranges run by separate
+ * workgroups (the one-wave-per-position grid otherwise leaves its last residency round almost
+ * empty): dK1 / dK2 are then [k][B][N][D] scratch whose slab 0 holds the gradient on return,
+ * and pg has k * sat_attn_param_grad_rows(B, N) rows (0 or 1: no split). */
 typedef struct SatAttnParamGrad {
   int32_t T, B, N, D1, D2, F, KW, att1_forward;
   const float* K1; const float* K2;
@@ -520,6 +523,7 @@ typedef struct SatAttnParamGrad {
   const float* df;
   float* dK1; float* dK2;
   float* pg; int64_t pg_stride;
+  int32_t tsplit;
 } SatAttnParamGrad;
 
 int sat_attn_pg_stride(int32_t D1, int32_t D2, int32_t F, int32_t KW);

@@ -126,7 +126,8 @@ SatAttnStepBwd = _struct("SatAttnStepBwd", """
 SatAttnParamGrad = _struct("SatAttnParamGrad", """
     i32:T i32:B i32:N i32:D1 i32:D2 i32:F i32:KW i32:att1_forward ptr:K1 ptr:K2
     ptr:q i64:q_tstride i64:q_bstride ptr:b1 ptr:v1 ptr:locW ptr:v2 ptr:loc
-    ptr:s_prev i64:s_tstride ptr:de1 ptr:de2 ptr:df ptr:dK1 ptr:dK2 ptr:pg i64:pg_stride""")
+    ptr:s_prev i64:s_tstride ptr:de1 ptr:de2 ptr:df ptr:dK1 ptr:dK2 ptr:pg i64:pg_stride
+    i32:tsplit""")
 
 SatDecAttnFwd = _struct("SatDecAttnFwd", """
     i32:B i32:N i32:T i32:U i32:M1 i32:M2 i32:D1 i32:D2 i32:F i32:KW f32:u f32:zc f32:zh
@@ -280,7 +281,7 @@ RESTYPES = {"sat_workspace_colreduce": (ctypes.c_int64, [_I32, _I32]),
 
 _lib: Optional[ctypes.CDLL] = None
 # include/sat_abi.h SAT_ABI_VERSION this binding's structs follow
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 
 def load(path: str = LIB_PATH) -> ctypes.CDLL:

@@ -91,6 +91,11 @@ def lin_bwd(x, dy, W, dW, db, ws, dx=None, beta_dx=0.0, need_dx=True, aux=None):
     return dx
 
 
+# the attention parameter pass's T steps in PG_TSPLIT ranges per position (sat_attn_param_grads
+# tsplit): 1600 one-position workgroups at 3 waves per SIMD leave the third residency round
+# nearly empty; SAT_PG_TSPLIT=1 is the unsplit A/B arm
+PG_TSPLIT = int(os.environ.get("SAT_PG_TSPLIT", "3"))
+
 # the projections' weight gradients of a multi-head attention backward on a stream of their own
 # (SatMha.wgrad_stream; joined inside sat_mha_bwd); SAT_MHA_WGRAD_SIDE=0 keeps them inline (A/B)
 MHA_WGRAD_SIDE = os.environ.get("SAT_MHA_WGRAD_SIDE", "0") == "1"
@@ -425,9 +430,11 @@ def decoder_bwd(P, G, hp, d, dsv, dH2, masks, ws, attn_tile=32, pipe: Pipeline =
     #      sum of its per-workgroup partial rows
     F, KW = (d.loc_f, d.loc_k) if fwd else (0, 0)
     pgs = K.pg_stride(D1, D2, F, KW)
-    PG = torch.empty(K.attn_param_grad_rows(B, N), pgs, **f32)
-    dK1 = torch.empty(B, N, D1, **f32)
-    dK2 = torch.empty(B, N, D2, **f32)
+    ts = PG_TSPLIT
+    PG = torch.empty(ts * K.attn_param_grad_rows(B, N), pgs, **f32)
+    dK1s = torch.empty(ts, B, N, D1, **f32)       # slab 0 holds the gradient on return
+    dK2s = torch.empty(ts, B, N, D2, **f32)
+    dK1, dK2 = dK1s[0], dK2s[0]
     Qh = S["Q"]
     K.attn_param_grads(
         T=Tp, B=B, N=N, D1=D1, D2=D2, F=F, KW=KW, att1_forward=1 if fwd else 0,
@@ -436,7 +443,8 @@ def decoder_bwd(P, G, hp, d, dsv, dH2, masks, ws, attn_tile=32, pipe: Pipeline =
         v1=P[f"{a1}/attention_variable"] if fwd else P[f"{a1}/attention_v"],
         locW=P[f"{a1}/location_layer/kernel"] if fwd else None, v2=P[f"{a2}/attention_v"],
         loc=S["LOC"] if fwd else None, s_prev=S["S1"], s_tstride=S["S1"].stride(0),
-        de1=DE1, de2=DE2, df=DFH if fwd else None, dK1=dK1, dK2=dK2, pg=PG, pg_stride=pgs)
+        de1=DE1, de2=DE2, df=DFH if fwd else None, dK1=dK1s, dK2=dK2s, pg=PG, pg_stride=pgs,
+        tsplit=ts)
     if late:
         fork_wgrad()
     if fwd:

@@ -947,7 +947,11 @@ __device__ __forceinline__ void pg_recompute_body(const SatAttnParamGrad& p) {
   // scalar and their loads go through the scalar cache instead of 64-bit VALU address math
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nq = (p.N + 3) / 4;
-  const int b = blockIdx.x / nq, n = 4 * (blockIdx.x - b * nq) + wave;
+  // part `part` of the tsplit step ranges: workgroup index = part * (B * nq) + b * nq + n / 4
+  const int rows = p.B * nq, part = blockIdx.x / rows, wgi = blockIdx.x - part * rows;
+  const int ts = max(p.tsplit, 1);
+  const int t_lo = (int)((int64_t)p.T * part / ts), t_hi = (int)((int64_t)p.T * (part + 1) / ts);
+  const int b = wgi / nq, n = 4 * (wgi - b * nq) + wave;
   const int nn = min(n, p.N - 1);
   const int Q1 = p.D1 / 4, Q = Q1 + p.D2 / 4;
   const int padl = (p.KW - 1) / 2;
@@ -990,13 +994,13 @@ __device__ __forceinline__ void pg_recompute_body(const SatAttnParamGrad& p) {
   // the step loop is latency-bound (a handful of dependent loads per step): issue the loads of
   // kU steps at once, then do their arithmetic
   constexpr int kU = 4;
-  for (int t0 = 0; t0 < p.T; t0 += kU) {
+  for (int t0 = t_lo; t0 < t_hi; t0 += kU) {
     float e1s[kU], e2s[kU], fls[kU][FL], sv[kU], dfv[kU];
     float4 qv[kU][SLOTS];
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
-      const int t = min(t0 + u, p.T - 1);
-      const bool on = t0 + u < p.T;
+      const int t = min(t0 + u, t_hi - 1);
+      const bool on = t0 + u < t_hi;
       const int64_t tb = (int64_t)t * TBN + bn;
       e1s[u] = on ? p.de1[tb] : 0.f;       // a step past T contributes exactly zero
       e2s[u] = on ? p.de2[tb] : 0.f;
@@ -1062,9 +1066,11 @@ __device__ __forceinline__ void attn_pg_store(const SatAttnParamGrad& p, const f
                                               const float4 (*adw)[F > 0 ? F : 1], float acw) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int nq = (p.N + 3) / 4;
-  const int b = blockIdx.x / nq, n = 4 * (blockIdx.x - b * nq) + wave;
+  const int rows = p.B * nq, part = blockIdx.x / rows, wgi = blockIdx.x - part * rows;
+  const int b = wgi / nq, n = 4 * (wgi - b * nq) + wave;
   const bool live = n < p.N;
-  const int64_t bn = (int64_t)b * p.N + min(n, p.N - 1);
+  // part k of a step-split launch writes its dK partial into slab k (summed by the entry point)
+  const int64_t bn = (int64_t)b * p.N + min(n, p.N - 1) + (int64_t)part * p.B * p.N;
   const int Q1 = p.D1 / 4, Q = Q1 + p.D2 / 4;
   const int nconv = F > 0 ? p.KW * F : 0;
   bool ok[SLOTS], m1[SLOTS];
@@ -1149,8 +1155,27 @@ extern "C" int sat_attn_pg_stride(int32_t D1, int32_t D2, int32_t F, int32_t KW)
 
 extern "C" int sat_attn_param_grad_rows(int32_t B, int32_t N) { return B * ((N + 3) / 4); }
 
+namespace sat {
+namespace {
+// dK[0] = dK[0] + dK[1] + ... + dK[k-1] over the slabs of a step-split launch (fixed order)
+__global__ void __launch_bounds__(256) pg_slab_sum_kernel(float4* dK, int64_t n4, int k) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    float4 a = dK[i];
+    for (int s = 1; s < k; ++s) {
+      const float4 v = dK[s * n4 + i];
+      a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+    }
+    dK[i] = a;
+  }
+}
+}  // namespace
+}  // namespace sat
+
 extern "C" int sat_attn_param_grads(const SatAttnParamGrad* a, void* stream) {
   SAT_CHECK_ARG(a && a->T > 0 && a->B > 0 && a->N > 0, "sat_attn_param_grads: bad sizes");
+  SAT_CHECK_ARG(a->tsplit >= 0 && a->tsplit <= 8 && std::max(1, a->tsplit) <= a->T,
+                "sat_attn_param_grads: tsplit in 0..8 and <= T");
   SAT_CHECK_ARG(a->D1 % 4 == 0 && a->D2 % 4 == 0 && a->D1 > 0 && a->D2 > 0 &&
                 (a->D1 + a->D2) / 4 <= 128, "sat_attn_param_grads: D1, D2 multiples of 4, D1+D2 <= 512");
   const int F = a->att1_forward ? a->F : 0, KW = a->att1_forward ? a->KW : 0;
@@ -1173,7 +1198,8 @@ extern "C" int sat_attn_param_grads(const SatAttnParamGrad* a, void* stream) {
   SatAttnParamGrad p = *a;
   p.F = F; p.KW = KW;
   const int slots = ((a->D1 + a->D2) / 4 + 63) / 64;
-  const dim3 grid(sat_attn_param_grad_rows(a->B, a->N));
+  const int ts = std::max(1, a->tsplit);
+  const dim3 grid(ts * sat_attn_param_grad_rows(a->B, a->N));
   const size_t shm = 4 * (size_t)a->pg_stride * sizeof(float);
   hipStream_t s = as_stream(stream);
   if (slots == 1 && F == 5) hipLaunchKernelGGL((attn_param_grad_kernel<1, 5>), grid, dim3(256), shm, s, p);
@@ -1181,6 +1207,14 @@ extern "C" int sat_attn_param_grads(const SatAttnParamGrad* a, void* stream) {
   else if (F == 0) hipLaunchKernelGGL((attn_param_grad_kernel<2, 0>), grid, dim3(256), shm, s, p);
   else hipLaunchKernelGGL((attn_param_grad_kernel<2, 8>), grid, dim3(256), shm, s, p);
   SAT_LAUNCH_CHECK("sat_attn_param_grads");
+  if (ts > 1) {
+    const int64_t n1 = (int64_t)a->B * a->N * a->D1 / 4, n2 = (int64_t)a->B * a->N * a->D2 / 4;
+    hipLaunchKernelGGL(pg_slab_sum_kernel, dim3((unsigned)std::min<int64_t>((n1 + 255) / 256, 2048)),
+                       dim3(256), 0, s, reinterpret_cast<float4*>(a->dK1), n1, ts);
+    hipLaunchKernelGGL(pg_slab_sum_kernel, dim3((unsigned)std::min<int64_t>((n2 + 255) / 256, 2048)),
+                       dim3(256), 0, s, reinterpret_cast<float4*>(a->dK2), n2, ts);
+    SAT_LAUNCH_CHECK("sat_attn_param_grads (dK slabs)");
+  }
   return SAT_OK;
 }
 

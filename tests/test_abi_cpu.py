@@ -139,3 +139,17 @@ def test_attn_param_grads_rejects_uncompiled_location_widths():
     rc = lib.sat_attn_param_grads(ctypes.byref(d), None)
     assert rc != 0
     assert b"location features" in lib.sat_last_error_string()
+
+
+def test_attn_param_grads_rejects_bad_step_split():
+    """tsplit outside 0..8, or above T (an empty step range), is refused before device work."""
+    if not _lib_built():
+        pytest.skip("libsat_hip.so not built")
+    lib = _lib.load()
+    for T, ts in ((4, 9), (3, 4), (8, -1)):
+        d = _lib.SatAttnParamGrad()
+        d.T, d.B, d.N, d.D1, d.D2, d.F, d.KW, d.att1_forward = T, 2, 9, 224, 32, 5, 10, 1
+        d.tsplit = ts
+        rc = lib.sat_attn_param_grads(ctypes.byref(d), None)
+        assert rc != 0
+        assert b"tsplit" in lib.sat_last_error_string()

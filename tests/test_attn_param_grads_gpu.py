@@ -37,24 +37,29 @@ def _reference(c, D1, F, KW):
     return out, z1, z2
 
 
-@pytest.mark.parametrize("T,B,N", [(7, 2, 13), (33, 3, 200), (500, 2, 61)])
-def test_attn_param_grads(cuda, T, B, N):
+@pytest.mark.parametrize("T,B,N,ts", [(7, 2, 13, 1), (33, 3, 200, 1), (500, 2, 61, 1),
+                                      (7, 2, 13, 3), (33, 3, 200, 2), (500, 2, 61, 4),
+                                      (5, 1, 9, 5)])
+def test_attn_param_grads(cuda, T, B, N, ts):
+    """sat_attn_param_grads against float64 autograd, unsplit and with the T steps split into
+    ts ranges (tsplit; T = ts: one step per range)."""
     from sat_amd import kernels as K
     D1, D2, F, KW = 224, 32, 5, 10
     c = _case(T, B, N, D1, D2, F, KW, seed=T + N)
     ref, _, _ = _reference(c, D1, F, KW)
     dv = {k: v.to(cuda).contiguous() for k, v in c.items()}
     pgs = K.pg_stride(D1, D2, F, KW)
-    PG = torch.full((K.attn_param_grad_rows(B, N), pgs), float("nan"), device=cuda)
-    dK1 = torch.empty(B, N, D1, device=cuda)
-    dK2 = torch.empty(B, N, D2, device=cuda)
+    PG = torch.full((ts * K.attn_param_grad_rows(B, N), pgs), float("nan"), device=cuda)
+    dK1s = torch.full((ts, B, N, D1), float("nan"), device=cuda)
+    dK2s = torch.full((ts, B, N, D2), float("nan"), device=cuda)
+    dK1, dK2 = dK1s[0], dK2s[0]
     q = dv["q"]
     K.attn_param_grads(
         T=T, B=B, N=N, D1=D1, D2=D2, F=F, KW=KW, att1_forward=1, K1=dv["K1"], K2=dv["K2"],
         q=q, q_tstride=q.stride(0), q_bstride=q.stride(1), b1=dv["b1"], v1=dv["v1"],
         locW=dv["locW"], v2=dv["v2"], loc=dv["loc"], s_prev=dv["s_prev"],
         s_tstride=dv["s_prev"].stride(0), de1=dv["de1"], de2=dv["de2"], df=dv["df"],
-        dK1=dK1, dK2=dK2, pg=PG, pg_stride=pgs)
+        dK1=dK1s, dK2=dK2s, pg=PG, pg_stride=pgs, tsplit=ts)
     torch.cuda.synchronize()
     pg = PG.double().cpu().sum(0)
     o = 0

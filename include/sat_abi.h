@@ -38,8 +38,9 @@ extern "C" {
 /* Layout version of every struct / signature below: bumped whenever one changes, so a binding
  * (or an A/B run loading an older build through SAT_LIB_OVERRIDE) can refuse a library whose
  * structs it would misread.  5: round-5 layout (SatAttnParamGrad without zh, sat_softmax_bwd
- * with Lq / causal, SatMha.lse); 6: SatMha.wgrad_stream / wgrad_ws; 7: SatAttnParamGrad.tsplit. */
-#define SAT_ABI_VERSION 7
+ * with Lq / causal, SatMha.lse); 6: SatMha.wgrad_stream / wgrad_ws; 7: SatAttnParamGrad.tsplit; 8: SatMha without
+ * wgrad_stream / wgrad_ws (deferred weight gradients: sat_mha_bwd_wgrad). */
+#define SAT_ABI_VERSION 8
 
 /* ---------------------------------------------------------------- library */
 int sat_version(void);                         /* 100*major + minor */
@@ -190,17 +191,16 @@ typedef struct SatMha {
    * encoder's self-attention).  The forward then writes lse instead of P / Pd (both may be
    * NULL, nothing [L][L] is materialised) and the backward recomputes the probabilities. */
   float* lse;
-  /* wgrad_stream (nullable, a hipStream_t as void*): the backward forks the four projection
-   * weight gradients onto it (dWo / dbo at entry, dWq..dbv once dQ / dK / dV exist) with its
-   * own split-K scratch wgrad_ws, and the caller's stream joins it before sat_mha_bwd returns --
-   * nothing downstream reads them, so they leave the input-gradient chain. */
-  void* wgrad_stream;
-  void* wgrad_ws;
-  int64_t wgrad_ws_bytes;
 } SatMha;
 int64_t sat_mha_scratch_bytes(int32_t B, int32_t L, int32_t D, int32_t H, int32_t out_dim);
 int sat_mha_fwd(const SatMha* d, void* stream);
+/* dWq / dWk / dWv / dWo all NULL: the weight and bias gradients are deferred -- sat_mha_bwd
+ * writes dx only and leaves dO, dQ, dK, dV in the scratch; sat_mha_bwd_wgrad (same descriptor
+ * with the gradient pointers, same scratch, after sat_mha_bwd on any stream ordered after it)
+ * accumulates them.  Nothing downstream of the input gradient reads them, so a caller can run
+ * them beside the dx chain. */
 int sat_mha_bwd(const SatMha* d, void* stream);
+int sat_mha_bwd_wgrad(const SatMha* d, void* stream);
 
 /* Fused scaled-dot-product attention (flash-style; ScaledDotProductAttentionMechanism,
  * modules/self_attention.py:45-65): per (utterance b, head h)

@@ -94,8 +94,7 @@ SatMha = _struct("SatMha", """
     i32:B i32:L i32:W i32:D i32:H i32:causal i32:out_dim i32:pad0 ptr:x ptr:Wq ptr:bq ptr:Wk
     ptr:bk ptr:Wv ptr:bv ptr:Wo ptr:bo ptr:probs_mask ptr:q ptr:k ptr:v ptr:P ptr:Pd ptr:o ptr:y
     ptr:dy ptr:dx ptr:dWq ptr:dbq ptr:dWk ptr:dbk ptr:dWv ptr:dbv ptr:dWo ptr:dbo ptr:scratch
-    i64:scratch_bytes ptr:gemm_ws i64:gemm_ws_bytes ptr:lse ptr:wgrad_stream ptr:wgrad_ws
-    i64:wgrad_ws_bytes""")
+    i64:scratch_bytes ptr:gemm_ws i64:gemm_ws_bytes ptr:lse""")
 
 SatFlashAttn = _struct("SatFlashAttn", """
     i32:B i32:H i32:L i32:dh i32:causal f32:scale i64:ld ptr:q ptr:k ptr:v ptr:mask ptr:o ptr:lse
@@ -197,6 +196,7 @@ SIGNATURES = {
     "sat_cbhg_convbank_fwd": [ctypes.POINTER(SatConvBank), _P],
     "sat_mha_fwd": [ctypes.POINTER(SatMha), _P],
     "sat_mha_bwd": [ctypes.POINTER(SatMha), _P],
+    "sat_mha_bwd_wgrad": [ctypes.POINTER(SatMha), _P],
     "sat_flash_attn_fwd": [ctypes.POINTER(SatFlashAttn), _P],
     "sat_flash_attn_bwd": [ctypes.POINTER(SatFlashAttn), _P],
     "sat_cbhg_convbank_bwd": [ctypes.POINTER(SatConvBank), _P],
@@ -281,7 +281,7 @@ RESTYPES = {"sat_workspace_colreduce": (ctypes.c_int64, [_I32, _I32]),
 
 _lib: Optional[ctypes.CDLL] = None
 # include/sat_abi.h SAT_ABI_VERSION this binding's structs follow
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 
 def load(path: str = LIB_PATH) -> ctypes.CDLL:

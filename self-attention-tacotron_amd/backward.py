@@ -96,27 +96,37 @@ def lin_bwd(x, dy, W, dW, db, ws, dx=None, beta_dx=0.0, need_dx=True, aux=None):
 # nearly empty; SAT_PG_TSPLIT=1 is the unsplit A/B arm
 PG_TSPLIT = int(os.environ.get("SAT_PG_TSPLIT", "3"))
 
-# the projections' weight gradients of a multi-head attention backward on a stream of their own
-# (SatMha.wgrad_stream; joined inside sat_mha_bwd); SAT_MHA_WGRAD_SIDE=0 keeps them inline (A/B)
-MHA_WGRAD_SIDE = os.environ.get("SAT_MHA_WGRAD_SIDE", "0") == "1"
+# SAT_MHA_WGRAD_AUX=1 runs a multi-head attention's four weight gradients on the aux stream
+# (sat_mha_bwd_wgrad after a weight-deferred sat_mha_bwd).  Off: measured +0.45 ms/step for both
+# hops (the tail's aux branch is the longer one already) and neutral for the decoder head alone
+# (profiles/r05n_mha_wgrad_aux_ab.txt) -- the LSTM stack's BPTT waits for the aux join anyway.
+MHA_WGRAD_AUX = os.environ.get("SAT_MHA_WGRAD_AUX", "0") == "1"
 
 
-def mha_bwd(P, G, scope, s, dy, ws, side=False):
-    """Backward of model.mha_fwd: ONE sat_mha_bwd call.  Returns dx [B, L, W].  ``side``: fork
-    the four projection weight gradients onto K.aux_stream(dev, 3) inside the call."""
+def mha_bwd(P, G, scope, s, dy, ws, aux=None):
+    """Backward of model.mha_fwd: ONE sat_mha_bwd call.  Returns dx [B, L, W].  With ``aux`` the
+    four weight gradients are deferred to sat_mha_bwd_wgrad on the aux stream."""
     names = [f"{scope}/{n}_projection/{t}" for n in ("query", "key", "value", "output")
              for t in ("kernel", "bias")]
-    d, _scratch = K.mha_desc(s["x"], *(P[n] for n in names), s["heads"], s["causal"], s["mask"], s)
+    d, scratch = K.mha_desc(s["x"], *(P[n] for n in names), s["heads"], s["causal"], s["mask"], s)
     dx = torch.empty_like(s["x"])
     dyc = K.contiguous(dy)
     d.dy, d.dx = dyc.data_ptr(), dx.data_ptr()
-    d.dWq, d.dbq, d.dWk, d.dbk, d.dWv, d.dbv, d.dWo, d.dbo = (G[n].data_ptr() for n in names)
-    if side and MHA_WGRAD_SIDE and dy.is_cuda:
-        st = K.aux_stream(dy.device, 3)
-        with torch.cuda.stream(st):
-            wws = K._gemm_ws(dy.device)
-        d.wgrad_stream, d.wgrad_ws, d.wgrad_ws_bytes = st.cuda_stream, wws.data_ptr(), wws.numel()
+    grads = [G[n].data_ptr() for n in names]
+    defer = aux is not None and MHA_WGRAD_AUX and dy.is_cuda
+    if not defer:
+        d.dWq, d.dbq, d.dWk, d.dbk, d.dWv, d.dbv, d.dWo, d.dbo = grads
     K.mha_bwd(d)
+    if defer:
+        dw = type(d).from_buffer_copy(d)
+        dw.dWq, dw.dbq, dw.dWk, dw.dbk, dw.dWv, dw.dbv, dw.dWo, dw.dbo = grads
+
+        def wgrad():
+            wsb = K._gemm_ws(dy.device)        # the aux stream's own split-K scratch
+            dw.gemm_ws, dw.gemm_ws_bytes = wsb.data_ptr(), wsb.numel()
+            K.mha_bwd_wgrad(dw)
+        # the branch reads x, o, dy and the scratch's dQ / dK / dV: referenced until the join
+        aux.run(wgrad, scratch, dyc, s["x"], s["o"])
     return dx
 
 
@@ -126,7 +136,7 @@ def sa_transformer_bwd(P, G, scope, s, dz, ws, aux=None):
     K.act_bwd(dz, s["u"], du, "tanh")
     dy = lin_bwd(s["y"], du, P[f"{scope}/transform/kernel"], G[f"{scope}/transform/kernel"],
                  G[f"{scope}/transform/bias"], ws, aux=aux)
-    dx = mha_bwd(P, G, f"{scope}/mha", s, dy, ws, side=aux is not None)
+    dx = mha_bwd(P, G, f"{scope}/mha", s, dy, ws, aux=aux)
     K.axpby(dz, dx, 1.0, 1.0)                                        # residual
     return dx
 

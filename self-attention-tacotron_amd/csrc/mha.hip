@@ -60,19 +60,6 @@ int head_gemm(int M, int N, int K, HeadOp a, HeadOp b, float* C, int64_t c_sm, i
   return sat_gemm(&g, s);
 }
 
-// three fork / join events per host thread (created once; recording them inside a stream
-// capture adds the edges to the graph)
-hipEvent_t* mha_events() {
-  static thread_local hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
-  static thread_local bool ok = false;
-  if (!ok) {
-    for (auto& e : ev)
-      if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
-    ok = true;
-  }
-  return ev;
-}
-
 // the fused attention takes its two shapes when lse is given: the decoder head's (causal,
 // dh = 128) and the encoder's narrow heads (dh <= 32, L <= 256; sat_flash_attn_fwd)
 bool flash_ok(const SatMha* d) {
@@ -106,8 +93,10 @@ int check(const SatMha* d, bool bwd) {
                 "sat_mha: null tensor (P may be NULL only on the fused causal path)");
   SAT_CHECK_ARG(!d->probs_mask || d->Pd || flash_ok(d), "sat_mha: a probability mask needs Pd");
   if (bwd) {
-    SAT_CHECK_ARG(d->dy && d->dx && d->dWq && d->dWk && d->dWv && d->dWo,
-                  "sat_mha_bwd: null gradient tensor");
+    const bool all = d->dWq && d->dWk && d->dWv && d->dWo;
+    const bool none = !d->dWq && !d->dWk && !d->dWv && !d->dWo;
+    SAT_CHECK_ARG(d->dy && d->dx && (all || none),
+                  "sat_mha_bwd: null gradient tensor (the four weight gradients: all or none)");
     SAT_CHECK_ARG(d->scratch && d->scratch_bytes >= sat_mha_scratch_bytes(d->B, d->L, d->D, d->H,
                                                                           d->out_dim),
                   "sat_mha_bwd: scratch smaller than sat_mha_scratch_bytes()");
@@ -190,53 +179,66 @@ extern "C" int sat_mha_fwd(const SatMha* d, void* stream) {
   return SAT_OK;
 }
 
-// Gradients of sat_mha_fwd: parameter gradients ACCUMULATE (+=), dx is written.
+namespace sat {
+namespace {
+// the backward's scratch: dO, dQ, dK, dV [B L D], then dPd, dS [B H L L] (score slabs)
+struct MhaBwdScratch {
+  float *dO, *dQ, *dK, *dV, *dPd, *dS;
+};
+MhaBwdScratch bwd_scratch(const SatMha* d) {
+  char* p = static_cast<char*>(d->scratch);
+  const int64_t act = align_up((int64_t)d->B * d->L * d->D * 4);
+  const int64_t score = align_up((int64_t)d->H * d->L * d->L * d->B * 4);
+  return {reinterpret_cast<float*>(p), reinterpret_cast<float*>(p + act),
+          reinterpret_cast<float*>(p + 2 * act), reinterpret_cast<float*>(p + 3 * act),
+          reinterpret_cast<float*>(p + 4 * act), reinterpret_cast<float*>(p + 4 * act + score)};
+}
+// dW += X^T dY with db += colsum(dY) in the same launch
+int mha_wgrad(const SatMha* d, const float* X, int K, const float* dY, int N, float* dW, float* db,
+              hipStream_t s) {
+  SatGemmDesc g = dense_desc();
+  g.M = K; g.N = N; g.K = d->B * d->L;
+  g.A = X; g.a_sm = 1; g.a_sk = K;
+  g.B = dY; g.b_sk = N; g.b_sn = 1;
+  g.C = dW; g.c_sm = N; g.beta = 1.f;
+  g.ws = d->gemm_ws; g.ws_bytes = d->gemm_ws_bytes;
+  g.colsum_out = db;
+  return sat_gemm(&g, s);
+}
+}  // namespace
+}  // namespace sat
+
+// The four projections' weight / bias gradients (ACCUMULATE) from the dO, dQ, dK, dV a
+// weight-deferred sat_mha_bwd left in the scratch.
+extern "C" int sat_mha_bwd_wgrad(const SatMha* d, void* stream) {
+  SAT_TRY(check(d, true));
+  SAT_CHECK_ARG(d->dWq && d->dWk && d->dWv && d->dWo, "sat_mha_bwd_wgrad: null weight gradient");
+  hipStream_t s = as_stream(stream);
+  const MhaBwdScratch sc = bwd_scratch(d);
+  SAT_TRY(mha_wgrad(d, d->o, d->D, d->dy, d->out_dim, d->dWo, d->dbo, s));
+  SAT_TRY(mha_wgrad(d, d->x, d->W, sc.dQ, d->D, d->dWq, d->dbq, s));
+  SAT_TRY(mha_wgrad(d, d->x, d->W, sc.dK, d->D, d->dWk, d->dbk, s));
+  SAT_TRY(mha_wgrad(d, d->x, d->W, sc.dV, d->D, d->dWv, d->dbv, s));
+  return SAT_OK;
+}
+
+// Gradients of sat_mha_fwd: parameter gradients ACCUMULATE (+=), dx is written.  With all four
+// weight gradients NULL the weight / bias gradients are deferred to sat_mha_bwd_wgrad (same
+// descriptor and scratch, e.g. on a stream of the caller's that runs beside the dx chain).
 extern "C" int sat_mha_bwd(const SatMha* d, void* stream) {
   SAT_TRY(check(d, true));
   hipStream_t s = as_stream(stream);
   const int B = d->B, L = d->L, D = d->D, H = d->H, dh = D / H, R = B * L, Wi = d->W;
   const int64_t LD = (int64_t)L * D, LL = (int64_t)L * L, HLL = H * LL;
-  char* p = static_cast<char*>(d->scratch);
-  const int64_t act = align_up((int64_t)B * L * D * 4), score = align_up(HLL * B * 4);
-  float* dO = reinterpret_cast<float*>(p);
-  float* dQ = reinterpret_cast<float*>(p + act);
-  float* dK = reinterpret_cast<float*>(p + 2 * act);
-  float* dV = reinterpret_cast<float*>(p + 3 * act);
-  float* dPd = reinterpret_cast<float*>(p + 4 * act);
-  float* dS = reinterpret_cast<float*>(p + 4 * act + score);
+  const MhaBwdScratch sc = bwd_scratch(d);
+  float* dO = sc.dO;
+  float* dQ = sc.dQ;
+  float* dK = sc.dK;
+  float* dV = sc.dV;
+  float* dPd = sc.dPd;
+  float* dS = sc.dS;
   const float* Pd = d->probs_mask ? d->Pd : d->P;
-  // the projections' weight gradients on their own stream when the caller gives one (forked
-  // by events, joined before returning; its own split-K scratch)
-  hipStream_t sw = s;
-  void* wws = d->gemm_ws;
-  int64_t wwsb = d->gemm_ws_bytes;
-  hipEvent_t* ev = nullptr;
-  if (d->wgrad_stream && as_stream(d->wgrad_stream) != s) {
-    ev = mha_events();
-    SAT_CHECK_ARG(ev != nullptr, "sat_mha_bwd: event creation failed");
-    sw = as_stream(d->wgrad_stream);
-    wws = d->wgrad_ws;
-    wwsb = d->wgrad_ws_bytes;
-  }
-  auto fork = [&](int i) -> int {
-    if (!ev) return SAT_OK;
-    if (hipEventRecord(ev[i], s) != hipSuccess || hipStreamWaitEvent(sw, ev[i], 0) != hipSuccess) {
-      set_error("sat_mha_bwd: stream fork failed");
-      return SAT_ERR_HIP;
-    }
-    return SAT_OK;
-  };
-  auto wgrad = [&](const float* X, int K, const float* dY, int N, float* dW, float* db) -> int {
-    SatGemmDesc g = dense_desc();   // dW += X^T dY
-    g.M = K; g.N = N; g.K = R;
-    g.A = X; g.a_sm = 1; g.a_sk = K;
-    g.B = dY; g.b_sk = N; g.b_sn = 1;
-    g.C = dW; g.c_sm = N; g.beta = 1.f;
-    g.ws = wws; g.ws_bytes = wwsb;
-    g.colsum_out = db;                // db += colsum(dY) in the same launch
-    SAT_TRY(sat_gemm(&g, sw));
-    return SAT_OK;
-  };
+  const bool wg = d->dWq != nullptr;    // weight gradients here (else deferred)
   auto dgrad = [&](const float* dY, int N, const float* W, int K, float* dX, float beta) {
     SatGemmDesc g = dense_desc();   // dX (=|+=) dY W^T
     g.M = R; g.N = K; g.K = N;
@@ -247,8 +249,7 @@ extern "C" int sat_mha_bwd(const SatMha* d, void* stream) {
     return sat_gemm(&g, s);
   };
   // output projection
-  SAT_TRY(fork(0));
-  SAT_TRY(wgrad(d->o, D, d->dy, d->out_dim, d->dWo, d->dbo));
+  if (wg) SAT_TRY(mha_wgrad(d, d->o, D, d->dy, d->out_dim, d->dWo, d->dbo, s));
   SAT_TRY(dgrad(d->dy, d->out_dim, d->Wo, D, dO, 0.f));
   if (flash_ok(d)) {
     // dQ, dK, dV of the fused causal attention, probabilities recomputed from lse
@@ -275,10 +276,11 @@ extern "C" int sat_mha_bwd(const SatMha* d, void* stream) {
                     s, 3));
   }
   // input projections
-  SAT_TRY(fork(1));
-  SAT_TRY(wgrad(d->x, Wi, dQ, D, d->dWq, d->dbq));
-  SAT_TRY(wgrad(d->x, Wi, dK, D, d->dWk, d->dbk));
-  SAT_TRY(wgrad(d->x, Wi, dV, D, d->dWv, d->dbv));
+  if (wg) {
+    SAT_TRY(mha_wgrad(d, d->x, Wi, dQ, D, d->dWq, d->dbq, s));
+    SAT_TRY(mha_wgrad(d, d->x, Wi, dK, D, d->dWk, d->dbk, s));
+    SAT_TRY(mha_wgrad(d, d->x, Wi, dV, D, d->dWv, d->dbv, s));
+  }
   if (D % 32 == 0 && aligned16(d->Wq) && aligned16(d->Wk) && aligned16(dQ) && aligned16(dK)) {
     // dx = dQ Wq^T + dK Wk^T as ONE reduction (two-segment operands), then += dV Wv^T
     SatGemmDesc g = dense_desc();
@@ -295,11 +297,5 @@ extern "C" int sat_mha_bwd(const SatMha* d, void* stream) {
     SAT_TRY(dgrad(dK, D, d->Wk, Wi, d->dx, 1.f));
   }
   SAT_TRY(dgrad(dV, D, d->Wv, Wi, d->dx, 1.f));
-  if (ev) {   // join: the caller's stream waits for the weight-gradient branch
-    if (hipEventRecord(ev[2], sw) != hipSuccess || hipStreamWaitEvent(s, ev[2], 0) != hipSuccess) {
-      set_error("sat_mha_bwd: stream join failed");
-      return SAT_ERR_HIP;
-    }
-  }
   return SAT_OK;
 }

@@ -926,3 +926,8 @@ def mha_fwd(d):
 
 def mha_bwd(d):
     _lib.check(_lib.load().sat_mha_bwd(ctypes.byref(d), _stream()), "sat_mha_bwd")
+
+
+def mha_bwd_wgrad(d):
+    """the four projections' weight / bias gradients a weight-deferred mha_bwd left for later"""
+    _lib.check(_lib.load().sat_mha_bwd_wgrad(ctypes.byref(d), _stream()), "sat_mha_bwd_wgrad")

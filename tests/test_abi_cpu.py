@@ -153,3 +153,23 @@ def test_attn_param_grads_rejects_bad_step_split():
         rc = lib.sat_attn_param_grads(ctypes.byref(d), None)
         assert rc != 0
         assert b"tsplit" in lib.sat_last_error_string()
+
+
+def test_mha_bwd_weight_gradients_all_or_none():
+    """sat_mha_bwd refuses a descriptor with only some of the four weight gradients set (all of
+    them: inline; none: deferred to sat_mha_bwd_wgrad), before any device work."""
+    if not _lib_built():
+        pytest.skip("libsat_hip.so not built")
+    lib = _lib.load()
+    d = _lib.SatMha()
+    d.B, d.L, d.W, d.D, d.H, d.out_dim, d.causal = 2, 8, 16, 16, 2, 16, 0
+    fake = ctypes.c_void_p(16)
+    for f in ("x", "Wq", "Wk", "Wv", "Wo", "q", "k", "v", "P", "o", "dy", "dx", "scratch"):
+        setattr(d, f, fake)
+    d.scratch_bytes = 1 << 30
+    d.dWq = fake                      # only one of four
+    rc = lib.sat_mha_bwd(ctypes.byref(d), None)
+    assert rc != 0
+    assert b"all or none" in lib.sat_last_error_string()
+    rc = lib.sat_mha_bwd_wgrad(ctypes.byref(_lib.SatMha()), None)
+    assert rc != 0

@@ -241,3 +241,50 @@ def test_narrow_flash_equals_materialised_path_closely(cuda):
     gmax = max(float(G2[n].abs().max()) for n in names)
     for n in names:
         assert float((G1[n] - G2[n]).abs().max()) <= 1e-5 * gmax, n
+
+
+@pytest.mark.parametrize("flash", [True, False])
+def test_deferred_weight_gradients_equal_inline(cuda, flash):
+    """sat_mha_bwd with the four weight gradients NULL (dx only) followed by sat_mha_bwd_wgrad on
+    the same scratch gives bitwise the inline call's dx and parameter gradients (the decoder
+    head's shape through the fused attention, and the materialised path)."""
+    from sat_amd import kernels
+    B, L, W, D, H, out = 2, 96, 64, 256, 2, 64
+    g = torch.Generator().manual_seed(21)
+    P, names = {}, []
+    for nm, (i, o) in {"query": (W, D), "key": (W, D), "value": (W, D), "output": (D, out)}.items():
+        P[f"m/{nm}_projection/kernel"] = (torch.randn(i, o, generator=g) / i ** 0.5).to(cuda)
+        P[f"m/{nm}_projection/bias"] = (0.1 * torch.randn(o, generator=g)).to(cuda)
+        names += [f"m/{nm}_projection/kernel", f"m/{nm}_projection/bias"]
+    x = torch.randn(B, L, W, generator=g).to(cuda)
+    md = ((torch.rand(B, H, L, L, generator=g) < 0.9).float() / 0.9).to(cuda)
+    dy = torch.randn(B, L, out, generator=g).to(cuda)
+    res = []
+    for deferred in (False, True):
+        s = dict(x=x, q=torch.empty(B, L, D, device=cuda), k=torch.empty(B, L, D, device=cuda),
+                 v=torch.empty(B, L, D, device=cuda), o=torch.empty(B, L, D, device=cuda),
+                 y=torch.empty(B, L, out, device=cuda))
+        if flash:
+            s["lse"] = torch.empty(B, H, L, device=cuda)
+        else:
+            s["P"] = torch.empty(B, H, L, L, device=cuda)
+            s["Pd"] = torch.empty_like(s["P"])
+        G = {n: torch.zeros_like(P[n]) for n in names}
+        d, scratch = kernels.mha_desc(x, *(P[n] for n in names), H, True, md, s)
+        kernels.mha_fwd(d)
+        dx = torch.empty_like(x)
+        d.dy, d.dx = dy.data_ptr(), dx.data_ptr()
+        grads = [G[n].data_ptr() for n in names]
+        if deferred:
+            kernels.mha_bwd(d)
+            d.dWq, d.dbq, d.dWk, d.dbk, d.dWv, d.dbv, d.dWo, d.dbo = grads
+            kernels.mha_bwd_wgrad(d)
+        else:
+            d.dWq, d.dbq, d.dWk, d.dbk, d.dWv, d.dbv, d.dWo, d.dbo = grads
+            kernels.mha_bwd(d)
+        torch.cuda.synchronize()
+        res.append((dx, G))
+    (dx1, G1), (dx2, G2) = res
+    assert torch.equal(dx1, dx2)
+    for n in names:
+        assert torch.equal(G1[n], G2[n]), n

@@ -34,4 +34,4 @@ for name, p in p64.items():
     err = np.abs(grads[name].astype(np.float64) - g_ref).max() / scale
     if err > 2e-4:
         print(f"{name:60s} {err:.3e}")
-print("done", os.environ.get("SAT_MHA_WGRAD_SIDE"), os.environ.get("SAT_LIB_OVERRIDE", "in-tree"))
+print("done", os.environ.get("SAT_MHA_WGRAD_AUX"), os.environ.get("SAT_LIB_OVERRIDE", "in-tree"))

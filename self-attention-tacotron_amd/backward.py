@@ -606,9 +606,25 @@ def encoder_bwd(P, G, hp, d, sv, dm1, dm2, lengths, masks, ws, aux: Aux = None):
     K.bn_bwd(dy.view(-1, C2), sv["p2_pre"].view(-1, C2), None, dp2.view(-1, C2), s2["mean"],
              s2["var"], s2["gamma"], G["encoder/cbhg/proj2/bn/gamma"],
              G["encoder/cbhg/proj2/bn/beta"], ws, training=training)
-    _wgrad(aux, lambda: (K.conv1d_dw(sv["p1"], dp2, G["encoder/cbhg/proj2/kernel"], beta=1.0),
-                         K.colsum(dp2.view(-1, C2), G["encoder/cbhg/proj2/bias"], ws)),
-           sv["p1"], dp2)
+    # the two projections' weight gradients run after the conv bank's weight gradient on its
+    # side stream instead of forking here, where they held the CUs the dX chain's short BN /
+    # max-pool launches wait for (a 96 us column-sum finish behind a 127 us GEMM):
+    # 14.03 -> 13.99 ms/step, 3 interleaved rounds (profiles/r05q_tail_ab.txt);
+    # SAT_PROJ_DW_BANK=0 forks them here again
+    proj_later = (aux is not None and bank_fused(d, inp)
+                  and os.environ.get("SAT_BANK_DW_SIDE", "1") == "1"
+                  and os.environ.get("SAT_PROJ_DW_BANK", "1") == "1")
+    later = []
+
+    def proj_wgrad(fn, *tensors):
+        if proj_later:
+            later.append(fn)
+            aux.keep.extend(tensors)
+        else:
+            _wgrad(aux, fn, *tensors)
+    proj_wgrad(lambda: (K.conv1d_dw(sv["p1"], dp2, G["encoder/cbhg/proj2/kernel"], beta=1.0),
+                        K.colsum(dp2.view(-1, C2), G["encoder/cbhg/proj2/bias"], ws)),
+               sv["p1"], dp2)
     dp1 = K.conv1d_dx(dp2, P["encoder/cbhg/proj2/kernel"])
     # proj1: p1 = relu(BN(p1_pre))
     C1 = d.proj1
@@ -618,9 +634,9 @@ def encoder_bwd(P, G, hp, d, sv, dm1, dm2, lengths, masks, ws, aux: Aux = None):
              dp1_pre.view(-1, C1), s1["mean"], s1["var"], s1["gamma"],
              G["encoder/cbhg/proj1/bn/gamma"], G["encoder/cbhg/proj1/bn/beta"], ws,
              training=training)
-    _wgrad(aux, lambda: (K.conv1d_dw(sv["mp"], dp1_pre, G["encoder/cbhg/proj1/kernel"], beta=1.0),
-                         K.colsum(dp1_pre.view(-1, C1), G["encoder/cbhg/proj1/bias"], ws)),
-           sv["mp"], dp1_pre)
+    proj_wgrad(lambda: (K.conv1d_dw(sv["mp"], dp1_pre, G["encoder/cbhg/proj1/kernel"], beta=1.0),
+                        K.colsum(dp1_pre.view(-1, C1), G["encoder/cbhg/proj1/bias"], ws)),
+               sv["mp"], dp1_pre)
     dmp = K.conv1d_dx(dp1_pre, P["encoder/cbhg/proj1/kernel"])
     # max-pool, conv bank BN (one launch over the concatenated channels), conv bank
     dbank = torch.empty_like(dmp)
@@ -653,7 +669,8 @@ def encoder_bwd(P, G, hp, d, sv, dm1, dm2, lengths, masks, ws, aux: Aux = None):
         bank_dw = lambda: K.conv_bank_bwd(inp, _contig_span(P, kern), dbank_pre,  # noqa: E731
                                           d.max_k, C, dW=_contig_span(G, kern), beta_dw=1.0)
         if aux is not None and os.environ.get("SAT_BANK_DW_SIDE", "1") == "1":
-            aux.run_side((lambda: (bank_bias(), bank_dw())) if bias_side else bank_dw,
+            side = (lambda: (bank_bias(), bank_dw())) if bias_side else bank_dw
+            aux.run_side((lambda: (side(), [f() for f in later])) if later else side,
                          inp, dbank_pre)
         else:
             _wgrad(aux, bank_dw, inp, dbank_pre)

@@ -1592,7 +1592,16 @@ extern "C" int sat_cbhg_convbank_bwd(const SatConvBank* d, void* stream) {
     p.B = d->y; p.b_sk = d->y_sm; p.b_sn = 1;
     p.C = d->dW; p.c_sm = d->Co;
     p.beta = d->beta_dw;
-    const LdsPlan pl = plan_lds(p.M, p.N, p.K, 1, d->ws != nullptr, d->ws_bytes, d->C, 0);
+    LdsPlan pl = plan_lds(p.M, p.N, p.K, 1, d->ws != nullptr, d->ws_bytes, d->C, 0);
+    // a dW-only call is the caller running it beside the dX product on another stream (the
+    // training step): measured as that pair at the C2 shape (tools/probes/bank_dw_plans.py),
+    // 128 x 128 tiles split 2 take 640 us with dX against 728 for the cost model's choice, whose
+    // larger grid crowds the dX product out (alone they are 494 / 368 us, so a call doing both
+    // products serially keeps the cost model); the step 13.99 -> 13.91 ms (profiles/r05q_tail_ab.txt)
+    const int kc2 = (ceil_div(p.K, 2) + BK - 1) / BK * BK;
+    if (t_force_bm == 0 && !d->dx && d->C % 128 == 0 && p.K >= 4096 && d->ws != nullptr &&
+        (int64_t)ceil_div(p.K, kc2) * p.M * p.N * 4 <= d->ws_bytes)
+      pl = {128, 128, ceil_div(p.K, kc2), kc2};
     const int e = launch_lds_plan<3>(pl, A_IM2COLT, B_N, 1, p, s, "sat_cbhg_convbank_bwd(dW)");
     if (e != SAT_OK) return e;
   }

@@ -153,6 +153,14 @@ def test_conv_bank_matches_per_conv_oracle(cuda, max_k, C, Co, S, L):
     assert _rel(dxd, x.grad + dx0.double()) < 2e-6
     dW_ref = torch.cat([w.grad.reshape(-1) for w in Ws]) + dW0.double()
     assert _rel(dWd, dW_ref) < 2e-6
+    # the training step's split calls (dW alone beside dX on another stream: at the C2 shape
+    # the dW-only call takes its own measured plan, 128 x 128 tiles split 2)
+    dWs = dW0.to(cuda)
+    kernels.conv_bank_bwd(xd, Wb, dy.float().to(cuda), max_k, Co, dW=dWs, beta_dw=1.0)
+    assert _rel(dWs, dW_ref) < 2e-6
+    dxs = dx0.to(cuda)
+    kernels.conv_bank_bwd(xd, Wb, dy.float().to(cuda), max_k, Co, dx=dxs, beta_dx=1.0)
+    assert torch.equal(dxs, dxd)
 
 
 # ---- forced plans: every tile shape incl. the 8-wave 128 x 128 variant, with and without split-K

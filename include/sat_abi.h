@@ -100,7 +100,8 @@ typedef struct SatGemmDesc {
   int64_t ws_bytes;
   /* optional: also colsum_out[n] = alpha * sum_k B[k][n] + beta * colsum_out[n] in the same
    * launch (the bias gradient of a weight-gradient product dW = X^T dY, db = 1^T dY); needs a
-   * batch-1 product without bias / act / mul / add.  NULL = off. */
+   * product without bias / act / mul / add and batch2 == 1; with batch > 1, batch b's sums go
+   * to colsum_out + b * bias_sbatch (bias_sbatch is otherwise unused here).  NULL = off. */
   float* colsum_out;
   /* optional second A segment: A's columns k >= k1 come from A2 (row stride a2_sm), i.e.
    * C = A[:, :k1] B[:k1] + A2 B[k1:] as ONE reduction (two inputs of one layer that live in

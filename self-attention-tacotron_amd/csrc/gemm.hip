@@ -65,7 +65,9 @@ struct GemmP {
   int64_t a_sbatch2, b_sbatch2, c_sbatch2, mul_sbatch2;
   const float* add;
   int64_t add_sm, add_sbatch;
-  int splits, kchunk;          // split-K: grid.z = splits (batch == 1), partial slabs in ws
+  int splits, kchunk;          // split-K: grid.z = nb x splits (LDS kernel; the register kernel
+                               // splits batch-1 products only), partial slabs in ws
+  int nb = 1;                  // batch x batch2 (the split-K reduce walks every batch's slabs)
   float* ws;
   int remap;                   // XCD-aware tile order over the xy plane
   int tri = 0;                 // SatGemmDesc.tri (causal structure hint, LDS kernel only)
@@ -74,6 +76,7 @@ struct GemmP {
   // row of ones (index m_real = M - 1), whose output row goes to cs_out instead of C
   float* cs_out;
   int m_real;
+  int64_t cs_sbatch = 0;       // batch stride of cs_out (SatGemmDesc.bias_sbatch; batch2 == 1)
   int grp_co;                  // conv-bank launches: output channels per conv (GRP > 0)
   // second A segment (SatGemmDesc.A2, dense K-contiguous A only): columns k >= k1 of A come
   // from A2 (row stride a2_sm), i.e. C = A[:, :k1] B[:k1] + A2 B[k1:] in one product
@@ -430,11 +433,11 @@ __global__ void __launch_bounds__(64 * GM * GN) gemm_kernel(GemmP p) {
 // split-K finish: sum S slabs in order, then the same epilogue as gemm_kernel (batch == 1).
 // Four consecutive outputs per thread (16-byte slab loads when N % 4 == 0) and four slab loads
 // in flight per trip: the pass is latency-bound, not bandwidth-bound, at these sizes.
-__device__ __forceinline__ float* out_ptr(const GemmP& p, float* C, int row, int col) {
-  return (p.cs_out && row == p.m_real) ? p.cs_out + col : C + (int64_t)row * p.c_sm + col;
+__device__ __forceinline__ float* out_ptr(const GemmP& p, float* C, float* cs, int row, int col) {
+  return (cs && row == p.m_real) ? cs + col : C + (int64_t)row * p.c_sm + col;
 }
-__device__ __forceinline__ float splitk_epilogue(const GemmP& p, int row, int col, float s) {
-  float* dst = out_ptr(p, p.C, row, col);
+__device__ __forceinline__ float splitk_epilogue(const GemmP& p, const float* dst, int row,
+                                                 int col, float s) {
   float v = p.alpha * s;
   if (p.beta != 0.f) v += p.beta * (*dst);
   v = apply_act(v + (p.bias ? p.bias[col] : 0.f), p.act);
@@ -442,41 +445,56 @@ __device__ __forceinline__ float splitk_epilogue(const GemmP& p, int row, int co
   if (p.add) v += p.add[(int64_t)row * p.add_sm + col];
   return v;
 }
+// batch b of a split-K launch: its output block (batched splits carry no bias / mul / add:
+// launch_lds plans them only without)
+__device__ __forceinline__ float* batch_c(const GemmP& p, int b) {
+  const int bz = b / p.batch2, bz2 = b - bz * p.batch2;
+  return p.C + bz * p.c_sbatch + bz2 * p.c_sbatch2;
+}
 __global__ void __launch_bounds__(256) gemm_splitk_reduce(GemmP p) {
   const int64_t total = (int64_t)p.M * p.N;
   if ((p.N & 3) == 0) {
     const int64_t total4 = total >> 2;
     const float4* ws4 = reinterpret_cast<const float4*>(p.ws);
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total4;
-         i += (int64_t)gridDim.x * blockDim.x) {
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < p.nb * total4;
+         e += (int64_t)gridDim.x * blockDim.x) {
+      const int b = (int)(e / total4);
+      const int64_t i = e - b * total4;
+      const float4* src = ws4 + (int64_t)b * p.splits * total4 + i;
       float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
       int k = 0;
       for (; k + 4 <= p.splits; k += 4) {
         float4 v[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) v[q] = ws4[(int64_t)(k + q) * total4 + i];
+        for (int q = 0; q < 4; ++q) v[q] = src[(int64_t)(k + q) * total4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) { a.x += v[q].x; a.y += v[q].y; a.z += v[q].z; a.w += v[q].w; }
       }
       for (; k < p.splits; ++k) {
-        const float4 v = ws4[(int64_t)k * total4 + i];
+        const float4 v = src[(int64_t)k * total4];
         a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
       }
       const int row = (int)((4 * i) / p.N), col = (int)(4 * i - (int64_t)row * p.N);
-      float* dst = out_ptr(p, p.C, row, col);
-      dst[0] = splitk_epilogue(p, row, col, a.x);
-      dst[1] = splitk_epilogue(p, row, col + 1, a.y);
-      dst[2] = splitk_epilogue(p, row, col + 2, a.z);
-      dst[3] = splitk_epilogue(p, row, col + 3, a.w);
+      float* dst = out_ptr(p, batch_c(p, b), p.cs_out ? p.cs_out + b * p.cs_sbatch : nullptr,
+                           row, col);
+      dst[0] = splitk_epilogue(p, dst, row, col, a.x);
+      dst[1] = splitk_epilogue(p, dst + 1, row, col + 1, a.y);
+      dst[2] = splitk_epilogue(p, dst + 2, row, col + 2, a.z);
+      dst[3] = splitk_epilogue(p, dst + 3, row, col + 3, a.w);
     }
     return;
   }
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
-       i += (int64_t)gridDim.x * blockDim.x) {
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < p.nb * total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int b = (int)(e / total);
+    const int64_t i = e - b * total;
     const int row = (int)(i / p.N), col = (int)(i - (int64_t)row * p.N);
+    const float* src = p.ws + (int64_t)b * p.splits * total + i;
     float s = 0.f;
-    for (int k = 0; k < p.splits; ++k) s += p.ws[(int64_t)k * total + i];
-    *out_ptr(p, p.C, row, col) = splitk_epilogue(p, row, col, s);
+    for (int k = 0; k < p.splits; ++k) s += src[(int64_t)k * total];
+    float* dst = out_ptr(p, batch_c(p, b), p.cs_out ? p.cs_out + b * p.cs_sbatch : nullptr, row,
+                         col);
+    *dst = splitk_epilogue(p, dst, row, col, s);
   }
 }
 
@@ -582,7 +600,10 @@ __global__ void __launch_bounds__(256) gemm_n1_kernel(GemmP p, int vec) {
     for (int k = lane; k < p.K; k += 64) s += a[k] * p.B[(int64_t)k * p.b_sk];
   }
   s = wave_sum(s);
-  if (lane == 0) p.C[(int64_t)row * p.c_sm] = splitk_epilogue(p, row, 0, s);
+  if (lane == 0) {
+    float* dst = p.C + (int64_t)row * p.c_sm;
+    *dst = splitk_epilogue(p, dst, row, 0, s);
+  }
 }
 // K == 1: the outer product C = epilogue(alpha a b^T), one thread per output element
 __global__ void __launch_bounds__(256) gemm_k1_kernel(GemmP p) {
@@ -590,7 +611,8 @@ __global__ void __launch_bounds__(256) gemm_k1_kernel(GemmP p) {
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
     const int row = i / p.N, col = i - row * p.N;
     const float s = p.A[(int64_t)row * p.a_sm] * p.B[(int64_t)col * p.b_sn];
-    p.C[(int64_t)row * p.c_sm + col] = splitk_epilogue(p, row, col, s);
+    float* dst = p.C + (int64_t)row * p.c_sm + col;
+    *dst = splitk_epilogue(p, dst, row, col, s);
   }
 }
 
@@ -677,9 +699,10 @@ __global__ void __launch_bounds__((64 * lds_waves<BM, BN>())) gemm_lds_kernel(Ge
     ty = t / gridDim.x;
     tx = t - ty * gridDim.x;
   }
-  int bz, bz2, split;
-  if (p.splits > 1) { bz = 0; bz2 = 0; split = blockIdx.z; }
-  else { bz = blockIdx.z / p.batch2; bz2 = blockIdx.z - bz * p.batch2; split = 0; }
+  // grid.z = batch index x splits + split (split-K) or the batch index
+  const int bb = p.splits > 1 ? (int)blockIdx.z / p.splits : (int)blockIdx.z;
+  const int split = p.splits > 1 ? (int)blockIdx.z - bb * p.splits : 0;
+  const int bz = bb / p.batch2, bz2 = bb - bz * p.batch2;
   // conv-bank forward: column blocks have different reductions ((g + 1) * C); the dispatcher
   // deals workgroup i to XCD i % 8, so rotate the column index by the row index to give every
   // XCD the same mix of kernel widths, longest first within a row
@@ -993,7 +1016,7 @@ __global__ void __launch_bounds__((64 * lds_waves<BM, BN>())) gemm_lds_kernel(Ge
   // Whole tiles with a plain epilogue (the common case) take a branch-free store loop.
   const bool full = (m0 + BM <= p.M) && (n0 + BN <= p.N);
   if (p.splits > 1) {
-    float* slab = p.ws + (int64_t)split * p.M * p.N;
+    float* slab = p.ws + (int64_t)blockIdx.z * p.M * p.N;    // slab (batch, split)
 #pragma unroll
     for (int i = 0; i < SM; ++i)
 #pragma unroll
@@ -1046,7 +1069,8 @@ __global__ void __launch_bounds__((64 * lds_waves<BM, BN>())) gemm_lds_kernel(Ge
       for (int r = 0; r < 16; ++r) {
         const int row = m0 + wm + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
         if (row >= p.M) continue;
-        float* dst = (p.cs_out && row == p.m_real) ? p.cs_out + col : C + (int64_t)row * cs + col;
+        float* dst = (p.cs_out && row == p.m_real) ? p.cs_out + bb * p.cs_sbatch + col
+                                                   : C + (int64_t)row * cs + col;
         float v = p.alpha * acc[0][i][j][r];
         if (p.beta != 0.f) v += p.beta * (*dst);
         v = apply_act(v + bv, p.act);
@@ -1159,7 +1183,7 @@ static bool gemm_skinny_enabled() {
 }
 
 static void launch_splitk_reduce(const GemmP& p, hipStream_t s) {
-  const int64_t total = (int64_t)p.M * p.N;
+  const int64_t total = (int64_t)p.M * p.N * p.nb;
   const int64_t work = (p.N % 4 == 0) ? total / 4 : total;
   const int blocks = (int)std::min<int64_t>((work + 255) / 256, 2048);
   hipLaunchKernelGGL(gemm_splitk_reduce, dim3(blocks), dim3(256), 0, s, p);
@@ -1195,7 +1219,7 @@ static LdsPlan plan_lds(int M, int N, int K, int nb, bool can_split, int64_t ws_
   struct Cand { int bm, bn, occ; };
   // (ties go to the first: two 128x64 workgroups per CU overlap each other's epilogue)
   static const Cand cands[4] = {{128, 64, 2}, {64, 128, 2}, {128, 128, 1}, {64, 64, 3}};
-  can_split = can_split && nb == 1 && K >= 512;
+  can_split = can_split && K >= 512;
   double best = 1e30;
   LdsPlan pl{0, 0, 1, K};
   for (int c = 0; c < 4; ++c) {
@@ -1207,7 +1231,7 @@ static LdsPlan plan_lds(int M, int N, int K, int nb, bool can_split, int64_t ws_
     for (int S = 1; S <= smax; S = (S < 4 ? S + 1 : S * 2)) {
       const int kc = (ceil_div(K, S) + BK - 1) / BK * BK;
       const int Se = ceil_div(K, kc);
-      if (Se > 1 && (int64_t)Se * M * N * 4 > ws_bytes) break;
+      if (Se > 1 && (int64_t)Se * nb * M * N * 4 > ws_bytes) break;
       const int64_t tiles = base * Se;
       const int64_t per_cu = (tiles + 255) / 256;
       // MFMA efficiency vs resident waves x 32x32 sub-tiles per wave (probe: gemm_sweep.py)
@@ -1226,7 +1250,7 @@ static LdsPlan plan_lds(int M, int N, int K, int nb, bool can_split, int64_t ws_
     int bs = can_split ? t_force_s : 1;
     const int kc = (ceil_div(K, bs) + BK - 1) / BK * BK;
     bs = ceil_div(K, kc);
-    if (bs > 1 && (int64_t)bs * M * N * 4 > ws_bytes) return LdsPlan{0, 0, 1, K};
+    if (bs > 1 && (int64_t)bs * nb * M * N * 4 > ws_bytes) return LdsPlan{0, 0, 1, K};
     pl = {t_force_bm, t_force_bn, bs, bs > 1 ? kc : K};
   }
   return pl;
@@ -1255,7 +1279,8 @@ static int launch_lds_plan(const LdsPlan& pl, int am, int bm, int nb, GemmP& p, 
   p.splits = pl.splits;
   p.kchunk = pl.kchunk;
   p.remap = (GRP == 0 && gx * gy >= 16) ? 1 : 0;
-  const dim3 grid(gx, gy, pl.splits > 1 ? pl.splits : nb);
+  p.nb = nb;
+  const dim3 grid(gx, gy, pl.splits > 1 ? pl.splits * nb : nb);
   hipError_t e;
   if (pl.bm == 128 && pl.bn == 128) e = launch_lds_grp<128, 128, GRP>(am, bm, grid, s, p);
   else if (pl.bm == 128) e = launch_lds_grp<128, 64, GRP>(am, bm, grid, s, p);
@@ -1299,8 +1324,10 @@ static int launch_lds(const SatGemmDesc* d, GemmP& p, int nb, hipStream_t s) {
   if (p.cs_out && am == A_M && p.m_real % 4 != 0) return 1;   // the ones chunk must start at m_real
   // no split-K under a causal hint: the skipped tiles would leave their slab partials stale and
   // the reduce would write them into C above the diagonal
-  const LdsPlan pl = plan_lds(p.M, d->N, d->K, nb,
-                              nb == 1 && d->ws != nullptr && !p.C2 && p.tri == 0, d->ws_bytes,
+  // (a batched split-K: the reduce's epilogue has no per-batch bias / mul / add)
+  const bool split_ok = (nb == 1 || (!p.bias && !p.mul && !p.add)) && d->ws != nullptr &&
+                        !p.C2 && p.tri == 0;
+  const LdsPlan pl = plan_lds(p.M, d->N, d->K, nb, split_ok, d->ws_bytes,
                               am == A_IM2COLT ? d->a_C : 0, 0);
   if (pl.bm == 0) return 1;
   return launch_lds_plan<0>(pl, am, bm, nb, p, s, "sat_gemm");
@@ -1416,16 +1443,30 @@ extern "C" int sat_gemm(const SatGemmDesc* d, void* stream) {
   if (d->colsum_out) {
     // C = alpha A B + beta C and colsum_out = alpha 1^T B + beta colsum_out (the bias gradient of
     // a weight-gradient product) in ONE launch: A gets a row of ones
-    SAT_CHECK_ARG(nb == 1 && d->a_mode == 0 && d->b_mode == 0 && !d->bias && d->act == 0 &&
+    SAT_CHECK_ARG(p.batch2 == 1 && d->a_mode == 0 && d->b_mode == 0 && !d->bias && d->act == 0 &&
                       !d->mul && !d->add,
-                  "sat_gemm: colsum_out needs a plain batch-1 product (no bias/act/mul/add)");
+                  "sat_gemm: colsum_out needs a plain product with batch2 == 1 (no bias/act/mul/add)");
     if (gemm_lds_enabled()) {
       p.cs_out = d->colsum_out;
+      p.cs_sbatch = d->bias_sbatch;     // batch b's sums at colsum_out + b * bias_sbatch
+      p.bias_sbatch = 0;
       p.M = d->M + 1;
       const int r = launch_lds(d, p, nb, s);
       if (r != 1) return r;
       p.cs_out = nullptr;
       p.M = d->M;
+    }
+    if (nb > 1) {   // not vector-loadable: one batch-1 product per batch
+      for (int b = 0; b < nb; ++b) {
+        SatGemmDesc d1 = *d;
+        d1.batch = 1;
+        d1.A = d->A + b * d->a_sbatch; d1.B = d->B + b * d->b_sbatch; d1.C = d->C + b * d->c_sbatch;
+        d1.colsum_out = d->colsum_out + b * d->bias_sbatch;
+        d1.a_sbatch = d1.b_sbatch = d1.c_sbatch = d1.bias_sbatch = 0;
+        const int rc = sat_gemm(&d1, stream);
+        if (rc != SAT_OK) return rc;
+      }
+      return SAT_OK;
     }
     // operands not vector-loadable: the product, then the column sums as a separate reduction
     SatGemmDesc d2 = *d;

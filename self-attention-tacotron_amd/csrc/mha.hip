@@ -205,6 +205,31 @@ int mha_wgrad(const SatMha* d, const float* X, int K, const float* dY, int N, fl
   g.colsum_out = db;
   return sat_gemm(&g, s);
 }
+// the three input projections' dW += x^T dQ|dK|dV, db += colsum: ONE batched product (A = x
+// shared, batch stride 0; split-K over the three batches' slabs) when the gradients, their
+// biases and dQ / dK / dV are equally spaced (the gradient arena mirrors the parameter arena:
+// query / key / value kernel + bias back to back; dQ, dK, dV are consecutive scratch slabs)
+int mha_wgrad_qkv(const SatMha* d, const float* dQ, const float* dK, const float* dV,
+                  hipStream_t s) {
+  const int64_t sw = d->dWk - d->dWq, so = dK - dQ;
+  const bool nob = !d->dbq && !d->dbk && !d->dbv;
+  const bool eqb = d->dbq && d->dbk && d->dbv && d->dbk - d->dbq == d->dbv - d->dbk;
+  if (sw == d->dWv - d->dWk && so == dV - dK && (nob || eqb)) {
+    SatGemmDesc g = dense_desc();
+    g.M = d->W; g.N = d->D; g.K = d->B * d->L;
+    g.batch = 3;
+    g.A = d->x; g.a_sm = 1; g.a_sk = d->W; g.a_sbatch = 0;
+    g.B = dQ; g.b_sk = d->D; g.b_sn = 1; g.b_sbatch = so;
+    g.C = d->dWq; g.c_sm = d->D; g.c_sbatch = sw; g.beta = 1.f;
+    g.colsum_out = d->dbq;
+    g.bias_sbatch = eqb ? d->dbk - d->dbq : 0;   // the batches' column sums, bias_sbatch apart
+    g.ws = d->gemm_ws; g.ws_bytes = d->gemm_ws_bytes;
+    return sat_gemm(&g, s);
+  }
+  SAT_TRY(mha_wgrad(d, d->x, d->W, dQ, d->D, d->dWq, d->dbq, s));
+  SAT_TRY(mha_wgrad(d, d->x, d->W, dK, d->D, d->dWk, d->dbk, s));
+  return mha_wgrad(d, d->x, d->W, dV, d->D, d->dWv, d->dbv, s);
+}
 }  // namespace
 }  // namespace sat
 
@@ -216,10 +241,7 @@ extern "C" int sat_mha_bwd_wgrad(const SatMha* d, void* stream) {
   hipStream_t s = as_stream(stream);
   const MhaBwdScratch sc = bwd_scratch(d);
   SAT_TRY(mha_wgrad(d, d->o, d->D, d->dy, d->out_dim, d->dWo, d->dbo, s));
-  SAT_TRY(mha_wgrad(d, d->x, d->W, sc.dQ, d->D, d->dWq, d->dbq, s));
-  SAT_TRY(mha_wgrad(d, d->x, d->W, sc.dK, d->D, d->dWk, d->dbk, s));
-  SAT_TRY(mha_wgrad(d, d->x, d->W, sc.dV, d->D, d->dWv, d->dbv, s));
-  return SAT_OK;
+  return mha_wgrad_qkv(d, sc.dQ, sc.dK, sc.dV, s);
 }
 
 // Gradients of sat_mha_fwd: parameter gradients ACCUMULATE (+=), dx is written.  With all four
@@ -276,11 +298,7 @@ extern "C" int sat_mha_bwd(const SatMha* d, void* stream) {
                     s, 3));
   }
   // input projections
-  if (wg) {
-    SAT_TRY(mha_wgrad(d, d->x, Wi, dQ, D, d->dWq, d->dbq, s));
-    SAT_TRY(mha_wgrad(d, d->x, Wi, dK, D, d->dWk, d->dbk, s));
-    SAT_TRY(mha_wgrad(d, d->x, Wi, dV, D, d->dWv, d->dbv, s));
-  }
+  if (wg) SAT_TRY(mha_wgrad_qkv(d, dQ, dK, dV, s));
   if (D % 32 == 0 && aligned16(d->Wq) && aligned16(d->Wk) && aligned16(dQ) && aligned16(dK)) {
     // dx = dQ Wq^T + dK Wk^T as ONE reduction (two-segment operands), then += dV Wv^T
     SatGemmDesc g = dense_desc();

@@ -125,7 +125,8 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor = None, *, alpha=1.0,
     lower / upper triangular (its zero K-tiles are not loaded: same bits).
 
     ``colsum`` [N] (2-D, plain products only): also colsum = alpha * sum over rows of B + beta *
-    colsum in the same launch (a dense layer's bias gradient next to its weight gradient).
+    colsum in the same launch (a dense layer's bias gradient next to its weight gradient); with
+    one batch dim, [batch, N]: one row per batch.
 
     A [.., M, K], B [.., K, N] with up to two leading batch dims (any strides: pass ``x.t()`` /
     ``x.transpose(-1, -2)`` views for transposed operands); C gets the broadcast batch shape.
@@ -188,7 +189,11 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor = None, *, alpha=1.0,
         d.add_sbatch = add.stride(0) if add.dim() == 3 else 0
     if colsum is not None:
         _f32(colsum, "colsum")
-        if colsum.numel() != N or not colsum.is_contiguous():
+        if nd == 1 and colsum.dim() == 2:       # one [N] row per batch (bias_sbatch apart)
+            if tuple(colsum.shape) != (nb, N) or colsum.stride(1) != 1:
+                raise ValueError("gemm: a batched colsum must be [batch, N] with unit stride")
+            d.bias_sbatch = colsum.stride(0)
+        elif colsum.numel() != N or not colsum.is_contiguous():
             raise ValueError("gemm: colsum must be a contiguous [N] tensor")
         d.colsum_out = _p(colsum)
     if A2 is not None:

@@ -263,6 +263,38 @@ def test_gemm_colsum_fused(cuda, M, N, K, ta, split, alpha):
     assert bool(((s.double().cpu() - rs).abs() <= bs).all()), float(((s.double().cpu() - rs).abs() / bs).max())
 
 
+@pytest.mark.parametrize("plan", [(0, 0, 0), (64, 64, 4), (128, 64, 3), (128, 128, 2), (64, 64, 1)])
+@pytest.mark.parametrize("ta", [True, False])
+def test_gemm_batched_split_colsum(cuda, plan, ta):
+    """a batch of weight-gradient products over one shared X (A batch stride 0: the MHA's three
+    input projections) with per-batch fused column sums, split-K over the batches' slabs"""
+    from sat_amd import _lib, kernels
+    g = torch.Generator().manual_seed(sum(plan) + ta)
+    nb, M, N, K = 3, 256, 192, 4000
+    X = torch.randn(K, M, generator=g) if ta else torch.randn(M, K, generator=g)
+    B = torch.randn(nb, K, N, generator=g)
+    C0 = torch.randn(nb, M, N, generator=g)
+    s0 = torch.randn(nb, N, generator=g)
+    C, s = C0.to(cuda), s0.to(cuda)
+    Xd = X.to(cuda)
+    A = (Xd.t() if ta else Xd).unsqueeze(0).expand(nb, M, K)
+    lib = _lib.load()
+    lib.sat_gemm_force_plan(*plan)
+    try:
+        kernels.gemm(A, B.to(cuda), C, alpha=-0.5, beta=1.0, colsum=s)
+        torch.cuda.synchronize()
+    finally:
+        lib.sat_gemm_force_plan(0, 0, 0)
+    Al = (X.t() if ta else X).double()
+    for b in range(nb):
+        ref = -0.5 * (Al @ B[b].double()) + C0[b].double()
+        bound = 6e-7 * (0.5 * (Al.abs() @ B[b].double().abs()) + C0[b].double().abs()) + 1e-7
+        assert bool(((C[b].double().cpu() - ref).abs() <= bound).all()), b
+        rs = -0.5 * B[b].double().sum(0) + s0[b].double()
+        bs = 6e-7 * (0.5 * B[b].double().abs().sum(0) + s0[b].double().abs()) + 1e-7
+        assert bool(((s[b].double().cpu() - rs).abs() <= bs).all()), b
+
+
 def test_gemm_colsum_fused_strided_b(cuda):
     """the attention query-layer shape: B is one tile of a [T'B, tiles, D1+D2] partial arena"""
     from sat_amd import kernels

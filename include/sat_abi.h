@@ -101,7 +101,8 @@ typedef struct SatGemmDesc {
   /* optional: also colsum_out[n] = alpha * sum_k B[k][n] + beta * colsum_out[n] in the same
    * launch (the bias gradient of a weight-gradient product dW = X^T dY, db = 1^T dY); needs a
    * product without bias / act / mul / add and batch2 == 1; with batch > 1, batch b's sums go
-   * to colsum_out + b * bias_sbatch (bias_sbatch is otherwise unused here).  NULL = off. */
+   * to colsum_out + b * bias_sbatch (bias_sbatch is otherwise unused here; 0: batch 0's sums
+   * only -- the batches of a shared B, b_sbatch == 0, have the same sums).  NULL = off. */
   float* colsum_out;
   /* optional second A segment: A's columns k >= k1 come from A2 (row stride a2_sm), i.e.
    * C = A[:, :k1] B[:k1] + A2 B[k1:] as ONE reduction (two inputs of one layer that live in
@@ -266,6 +267,11 @@ int sat_gemm_force_plan(int32_t bm, int32_t bn, int32_t splits);
 /* Speed-of-light probe (tools/probes/gemm_sol.py): mode bit 0 skips the LDS kernel's operand
  * DMA, bit 1 its epilogue stores (results are then garbage); 0 = normal.  Calling thread only. */
 int sat_gemm_probe_mode(int32_t mode);
+/* Scheduling hint: cap the workgroups of the calling thread's subsequent sat_gemm launches at
+ * about `cap` by limiting their split-K factor (0 = no cap).  For products issued on a side
+ * stream beside a latency-bound chain, whose short launches otherwise wait for the side
+ * product's workgroups to drain. */
+int sat_gemm_set_wg_cap(int32_t cap);
 /* Skinny product C = alpha * A . Bt^T + beta * C, A [M][K], Bt [N][K] rows contiguous in K
  * (16-B aligned, K % 4 == 0): the per-step gradient of the attention contexts through the
  * attention RNN's input weights (M = batch). */

@@ -39,7 +39,7 @@ class Aux:
     def run(self, fn, *tensors):
         self.s.wait_stream(torch.cuda.current_stream())
         self.keep.extend(tensors)
-        with torch.cuda.stream(self.s):
+        with torch.cuda.stream(self.s), K.gemm_wg_cap(AUX_WG_CAP):
             fn()
 
     def run_side(self, fn, *tensors):
@@ -95,6 +95,12 @@ def lin_bwd(x, dy, W, dW, db, ws, dx=None, beta_dx=0.0, need_dx=True, aux=None):
 # tsplit): 1600 one-position workgroups at 3 waves per SIMD leave the third residency round
 # nearly empty; SAT_PG_TSPLIT=1 is the unsplit A/B arm
 PG_TSPLIT = int(os.environ.get("SAT_PG_TSPLIT", "3"))
+# SAT_WGRAD_BATCH=1: the decoder LSTM kernels' weight-gradient blocks as one batched launch per
+# kernel -- measured slower (13.80 -> 13.96 ms/step: its larger grid crowds out the encoder
+# backward's short launches beside it; profiles/r05r_wgrad_batch_ab.txt)
+WGRAD_BATCH = os.environ.get("SAT_WGRAD_BATCH", "0") == "1"
+# workgroup cap of the aux branches' GEMMs (sat_gemm_set_wg_cap; 0 = none)
+AUX_WG_CAP = int(os.environ.get("SAT_AUX_WG_CAP", "0"))
 
 # SAT_MHA_WGRAD_AUX=1 runs a multi-head attention's four weight gradients on the aux stream
 # (sat_mha_bwd_wgrad after a weight-deferred sat_mha_bwd).  Off: measured +0.45 ms/step for both
@@ -393,20 +399,34 @@ def decoder_bwd(P, G, hp, d, dsv, dH2, masks, ws, attn_tile=32, pipe: Pipeline =
         if aux is not None:
             aux.s.wait_stream(torch.cuda.current_stream())
             aux.keep.extend([DG0, DG1, DG2, DQP, S])
-        with torch.cuda.stream(aux_s):
+        with torch.cuda.stream(aux_s), K.gemm_wg_cap(AUX_WG_CAP if aux is not None else 0):
             dec_wgrad()
 
     def dec_wgrad():
         # LSTM weight gradients: one GEMM per weight block over all steps
         DG2f = DG2.view(Tp * B, 4 * Dd)
         DG1f = DG1.view(Tp * B, 4 * Dd)
-        K.gemm(S["H2S"][:Tp].reshape(Tp * B, Dd).t(), DG2f, dW2[Dd:], beta=1.0)
-        K.gemm(S["H1RAW"].view(Tp * B, Dd).t(), DG2f, dW2[:Dd], beta=1.0,
-               colsum=G["decoder/lstm2/bias"])                     # + the bias gradient
-        K.gemm(S["H1S"][:Tp].reshape(Tp * B, Dd).t(), DG1f, dW1[A + M1 + M2:], beta=1.0,
-               colsum=G["decoder/lstm1/bias"])
+        h2s = S["H2S"][:Tp].reshape(Tp * B, Dd)
+        h1raw = S["H1RAW"].view(Tp * B, Dd)
+        h1s = S["H1S"][:Tp].reshape(Tp * B, Dd)
+        h0raw = S["H0RAW"].view(Tp * B, A)
+        if WGRAD_BATCH:
+            # (A/B only, WGRAD_BATCH above)
+            K.gemm_wgrad_batch([h1raw, h2s], DG2f, [dW2[:Dd], dW2[Dd:]],
+                               colsum=G["decoder/lstm2/bias"])
+            if A == Dd:
+                K.gemm_wgrad_batch([h1s, h0raw], DG1f, [dW1[A + M1 + M2:], dW1[:A]],
+                                   colsum=G["decoder/lstm1/bias"])
+            else:
+                K.gemm(h1s.t(), DG1f, dW1[A + M1 + M2:], beta=1.0, colsum=G["decoder/lstm1/bias"])
+                K.gemm(h0raw.t(), DG1f, dW1[:A], beta=1.0)
+        else:
+            K.gemm(h2s.t(), DG2f, dW2[Dd:], beta=1.0)
+            K.gemm(h1raw.t(), DG2f, dW2[:Dd], beta=1.0,
+                   colsum=G["decoder/lstm2/bias"])                 # + the bias gradient
+            K.gemm(h1s.t(), DG1f, dW1[A + M1 + M2:], beta=1.0, colsum=G["decoder/lstm1/bias"])
+            K.gemm(h0raw.t(), DG1f, dW1[:A], beta=1.0)
         ctx_all = S["REC0"][1:].reshape(Tp * B, R0)[:, :M1 + M2]
-        K.gemm(S["H0RAW"].view(Tp * B, A).t(), DG1f, dW1[:A], beta=1.0)
         K.gemm(ctx_all.t(), DG1f, dW1[A:A + M1 + M2], beta=1.0)
 
         DG0f = DG0.view(Tp * B, 4 * A)

@@ -76,7 +76,8 @@ struct GemmP {
   // row of ones (index m_real = M - 1), whose output row goes to cs_out instead of C
   float* cs_out;
   int m_real;
-  int64_t cs_sbatch = 0;       // batch stride of cs_out (SatGemmDesc.bias_sbatch; batch2 == 1)
+  int64_t cs_sbatch = 0;       // batch stride of cs_out (SatGemmDesc.bias_sbatch; batch2 == 1);
+                               // 0 with batch > 1: batch 0's sums only (a B shared by the batches)
   int grp_co;                  // conv-bank launches: output channels per conv (GRP > 0)
   // second A segment (SatGemmDesc.A2, dense K-contiguous A only): columns k >= k1 of A come
   // from A2 (row stride a2_sm), i.e. C = A[:, :k1] B[:k1] + A2 B[k1:] in one product
@@ -430,11 +431,17 @@ __global__ void __launch_bounds__(64 * GM * GN) gemm_kernel(GemmP p) {
     }
 }
 
-// split-K finish: sum S slabs in order, then the same epilogue as gemm_kernel (batch == 1).
+// split-K finish: sum each batch's S slabs in order, then the same epilogue as gemm_kernel.
 // Four consecutive outputs per thread (16-byte slab loads when N % 4 == 0) and four slab loads
 // in flight per trip: the pass is latency-bound, not bandwidth-bound, at these sizes.
+// batch b's column-sum row (null: batch b > 0 of a shared-B product writes none)
+__device__ __forceinline__ float* batch_cs(const GemmP& p, int b) {
+  return (!p.cs_out || (b > 0 && p.cs_sbatch == 0)) ? nullptr : p.cs_out + b * p.cs_sbatch;
+}
+// null: the column-sum row of a batch that writes none
 __device__ __forceinline__ float* out_ptr(const GemmP& p, float* C, float* cs, int row, int col) {
-  return (cs && row == p.m_real) ? cs + col : C + (int64_t)row * p.c_sm + col;
+  if (p.cs_out && row == p.m_real) return cs ? cs + col : nullptr;
+  return C + (int64_t)row * p.c_sm + col;
 }
 __device__ __forceinline__ float splitk_epilogue(const GemmP& p, const float* dst, int row,
                                                  int col, float s) {
@@ -475,8 +482,8 @@ __global__ void __launch_bounds__(256) gemm_splitk_reduce(GemmP p) {
         a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
       }
       const int row = (int)((4 * i) / p.N), col = (int)(4 * i - (int64_t)row * p.N);
-      float* dst = out_ptr(p, batch_c(p, b), p.cs_out ? p.cs_out + b * p.cs_sbatch : nullptr,
-                           row, col);
+      float* dst = out_ptr(p, batch_c(p, b), batch_cs(p, b), row, col);
+      if (!dst) continue;
       dst[0] = splitk_epilogue(p, dst, row, col, a.x);
       dst[1] = splitk_epilogue(p, dst + 1, row, col + 1, a.y);
       dst[2] = splitk_epilogue(p, dst + 2, row, col + 2, a.z);
@@ -492,8 +499,8 @@ __global__ void __launch_bounds__(256) gemm_splitk_reduce(GemmP p) {
     const float* src = p.ws + (int64_t)b * p.splits * total + i;
     float s = 0.f;
     for (int k = 0; k < p.splits; ++k) s += src[(int64_t)k * total];
-    float* dst = out_ptr(p, batch_c(p, b), p.cs_out ? p.cs_out + b * p.cs_sbatch : nullptr, row,
-                         col);
+    float* dst = out_ptr(p, batch_c(p, b), batch_cs(p, b), row, col);
+    if (!dst) continue;
     *dst = splitk_epilogue(p, dst, row, col, s);
   }
 }
@@ -605,6 +612,30 @@ __global__ void __launch_bounds__(256) gemm_n1_kernel(GemmP p, int vec) {
     *dst = splitk_epilogue(p, dst, row, 0, s);
   }
 }
+// N == 1 with a column-contiguous A (a_sm == 1: A = X^T, the stop-token layer's weight
+// gradient dw = X^T dstop, 256 x 1 x 16000): workgroup (column block, K slice) = 64 columns x
+// 4 row groups, coalesced along m; the K slices' partials go to split-K slabs [split][M] and
+// gemm_splitk_reduce applies the epilogue.  The fused column sum (cs_out) is row m_real of a
+// virtual ones column of X.  Replaces a register-kernel tile launch (28 us + 25 us reduce).
+__global__ void __launch_bounds__(256) gemm_tn1_kernel(GemmP p) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int m = blockIdx.x * 64 + lane, split = blockIdx.y;
+  const int kbeg = split * p.kchunk, kend = min(p.K, kbeg + p.kchunk);
+  float acc = 0.f;
+  if (m < p.M) {
+    const bool ones = p.cs_out && m == p.m_real;
+    for (int k = kbeg + g; k < kend; k += 4) {
+      const float x = ones ? 1.f : p.A[(int64_t)k * p.a_sk + m];
+      acc += x * p.B[(int64_t)k * p.b_sk];
+    }
+  }
+  red[g][lane] = acc;
+  __syncthreads();
+  if (g == 0 && m < p.M)
+    p.ws[(int64_t)split * p.M + m] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+}
+
 // K == 1: the outer product C = epilogue(alpha a b^T), one thread per output element
 __global__ void __launch_bounds__(256) gemm_k1_kernel(GemmP p) {
   const int total = p.M * p.N;
@@ -1069,8 +1100,14 @@ __global__ void __launch_bounds__((64 * lds_waves<BM, BN>())) gemm_lds_kernel(Ge
       for (int r = 0; r < 16; ++r) {
         const int row = m0 + wm + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
         if (row >= p.M) continue;
-        float* dst = (p.cs_out && row == p.m_real) ? p.cs_out + bb * p.cs_sbatch + col
-                                                   : C + (int64_t)row * cs + col;
+        float* dst;
+        if (p.cs_out && row == p.m_real) {
+          float* cso = batch_cs(p, bb);
+          if (!cso) continue;
+          dst = cso + col;
+        } else {
+          dst = C + (int64_t)row * cs + col;
+        }
         float v = p.alpha * acc[0][i][j][r];
         if (p.beta != 0.f) v += p.beta * (*dst);
         v = apply_act(v + bv, p.act);
@@ -1151,7 +1188,12 @@ static hipError_t launch_tiles(int am, int bm, dim3 grid, hipStream_t s, const G
 
 // Tuning hook for probes (tools/probes/gemm_sweep.py): a forced tile / split-K plan for the
 // calling thread's next launches on the LDS kernel (bm = 0 restores the cost model).
-static thread_local int t_force_bm = 0, t_force_bn = 0, t_force_s = 0, t_probe = 0;
+static thread_local int t_force_bm = 0, t_force_bn = 0, t_force_s = 0, t_probe = 0, t_wg_cap = 0;
+extern "C" int sat_gemm_set_wg_cap(int32_t cap) {
+  SAT_CHECK_ARG(cap >= 0, "sat_gemm_set_wg_cap: negative cap");
+  t_wg_cap = cap;
+  return SAT_OK;
+}
 extern "C" int sat_gemm_probe_mode(int32_t m) {
   SAT_CHECK_ARG(m >= 0 && m <= 3, "sat_gemm_probe_mode: bad mode");
   t_probe = m;
@@ -1233,6 +1275,7 @@ static LdsPlan plan_lds(int M, int N, int K, int nb, bool can_split, int64_t ws_
       const int Se = ceil_div(K, kc);
       if (Se > 1 && (int64_t)Se * nb * M * N * 4 > ws_bytes) break;
       const int64_t tiles = base * Se;
+      if (Se > 1 && t_wg_cap > 0 && tiles > t_wg_cap) break;   // sat_gemm_set_wg_cap
       const int64_t per_cu = (tiles + 255) / 256;
       // MFMA efficiency vs resident waves x 32x32 sub-tiles per wave (probe: gemm_sweep.py)
       const int conc = (int)std::min<int64_t>(cd.occ, per_cu);
@@ -1440,6 +1483,26 @@ extern "C" int sat_gemm(const SatGemmDesc* d, void* stream) {
     SAT_CHECK_ARG(r != 1, "sat_gemm: segmented operands are not vector-loadable");
     return r;
   }
+  if (nb == 1 && d->a_mode == 0 && d->b_mode == 0 && !t_probe && d->N == 1 && d->a_sm == 1 &&
+      d->M >= 64 && d->K >= 1024 && !d->bias && d->act == 0 && !d->mul && !d->add && d->ws) {
+    // N == 1 weight gradient (gemm_tn1_kernel): K slices of >= 256 rows, partials reduced by
+    // gemm_splitk_reduce with the usual epilogue (and the fused column sum as row m_real)
+    const int Mx = d->M + (d->colsum_out ? 1 : 0);
+    int S = std::min(64, d->K / 256);
+    while (S > 1 && (int64_t)S * Mx * 4 > d->ws_bytes) --S;
+    if (S > 1) {
+      p.cs_out = d->colsum_out;
+      p.cs_sbatch = 0;
+      p.M = Mx;
+      p.kchunk = ceil_div(d->K, S);
+      p.splits = ceil_div(d->K, p.kchunk);
+      hipLaunchKernelGGL(gemm_tn1_kernel, dim3(ceil_div(Mx, 64), p.splits), dim3(256), 0, s, p);
+      SAT_LAUNCH_CHECK("sat_gemm (N == 1, transposed A)");
+      launch_splitk_reduce(p, s);
+      SAT_LAUNCH_CHECK("sat_gemm (N == 1 reduce)");
+      return SAT_OK;
+    }
+  }
   if (d->colsum_out) {
     // C = alpha A B + beta C and colsum_out = alpha 1^T B + beta colsum_out (the bias gradient of
     // a weight-gradient product) in ONE launch: A gets a row of ones
@@ -1461,7 +1524,7 @@ extern "C" int sat_gemm(const SatGemmDesc* d, void* stream) {
         SatGemmDesc d1 = *d;
         d1.batch = 1;
         d1.A = d->A + b * d->a_sbatch; d1.B = d->B + b * d->b_sbatch; d1.C = d->C + b * d->c_sbatch;
-        d1.colsum_out = d->colsum_out + b * d->bias_sbatch;
+        d1.colsum_out = (b > 0 && d->bias_sbatch == 0) ? nullptr : d->colsum_out + b * d->bias_sbatch;
         d1.a_sbatch = d1.b_sbatch = d1.c_sbatch = d1.bias_sbatch = 0;
         const int rc = sat_gemm(&d1, stream);
         if (rc != SAT_OK) return rc;
@@ -1539,7 +1602,8 @@ extern "C" int sat_gemm(const SatGemmDesc* d, void* stream) {
   p.kchunk = d->K;
   p.ws = reinterpret_cast<float*>(d->ws);
   if (nb == 1 && tiles < 160 && d->K >= 512 && d->ws != nullptr) {
-    int S = std::min<int>(std::max(1, 384 / tiles), std::max(1, d->K / 256));
+    int S = std::min<int>(std::max(1, (t_wg_cap > 0 ? std::min(384, t_wg_cap) : 384) / tiles),
+                          std::max(1, d->K / 256));
     S = std::min(S, 64);
     while (S > 1 && (int64_t)S * d->M * d->N * 4 > d->ws_bytes) --S;
     if (S > 1) {

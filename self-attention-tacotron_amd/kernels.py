@@ -213,6 +213,62 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor = None, *, alpha=1.0,
     return C
 
 
+def gemm_wgrad_batch(Xs, dY: torch.Tensor, dWs, colsum=None, beta=1.0):
+    """dW_b = X_b^T dY + beta dW_b for every b as ONE batched launch (split-K over the batches'
+    slabs): the weight gradients of layers that share the output gradient dY [K, N] (the blocks
+    of one LSTM kernel).  Xs: 2-D [K, M] views of one shape and strides, equally spaced in
+    memory (any buffers); dWs: [M, N] row-contiguous, equally spaced.  ``colsum`` [N]: also
+    colsum = sum over rows of dY + beta colsum, once (SatGemmDesc.colsum_out, bias_sbatch 0)."""
+    nb = len(Xs)
+    X0, W0 = Xs[0], dWs[0]
+    for t in list(Xs) + [dY] + list(dWs):
+        _f32(t, "gemm_wgrad_batch operand")
+    K_, M = X0.shape
+    N = dY.shape[1]
+    sx = (Xs[1].data_ptr() - X0.data_ptr()) // 4 if nb > 1 else 0
+    sw = (dWs[1].data_ptr() - W0.data_ptr()) // 4 if nb > 1 else 0
+    for b in range(nb):
+        X, W = Xs[b], dWs[b]
+        if (tuple(X.shape) != (K_, M) or X.stride() != X0.stride() or
+                X.data_ptr() - X0.data_ptr() != 4 * b * sx or tuple(W.shape) != (M, N) or
+                W.stride() != W0.stride() or W.stride(1) != 1 or
+                W.data_ptr() - W0.data_ptr() != 4 * b * sw or dY.shape[0] != K_):
+            raise ValueError("gemm_wgrad_batch: operands must share shape / strides and be "
+                             "equally spaced")
+    d = _lib.SatGemmDesc()
+    d.M, d.N, d.K, d.batch, d.batch2 = M, N, K_, nb, 1
+    d.A, d.a_sm, d.a_sk, d.a_sbatch = _p(X0), X0.stride(1), X0.stride(0), sx
+    d.B, d.b_sk, d.b_sn, d.b_sbatch = _p(dY), dY.stride(0), dY.stride(1), 0
+    d.C, d.c_sm, d.c_sbatch = _p(W0), W0.stride(0), sw
+    d.alpha, d.beta = 1.0, beta
+    d.batch2 = 1
+    if colsum is not None:
+        _f32(colsum, "colsum")
+        if colsum.numel() != N or not colsum.is_contiguous():
+            raise ValueError("gemm_wgrad_batch: colsum must be a contiguous [N] tensor")
+        d.colsum_out = _p(colsum)
+    _with_ws(d, dY.device)
+    _launch_gemm(d, "sat_gemm")
+
+
+class gemm_wg_cap:
+    """``with gemm_wg_cap(n):`` the sat_gemm launches issued inside plan at most about n
+    workgroups (split-K limited; sat_gemm_set_wg_cap); 0 = no cap."""
+
+    def __init__(self, cap: int):
+        self.cap = int(cap)
+
+    def __enter__(self):
+        if self.cap:
+            _lib.check(_lib.load().sat_gemm_set_wg_cap(self.cap), "sat_gemm_set_wg_cap")
+        return self
+
+    def __exit__(self, *exc):
+        if self.cap:
+            _lib.load().sat_gemm_set_wg_cap(0)
+        return False
+
+
 def rowdot(A: torch.Tensor, Bt: torch.Tensor, C: torch.Tensor, alpha=1.0, beta=0.0):
     """C = alpha * A @ Bt^T + beta * C  (A [M, K], Bt [N, K] row-contiguous)."""
     M, Kd = A.shape

@@ -295,6 +295,64 @@ def test_gemm_batched_split_colsum(cuda, plan, ta):
         assert bool(((s[b].double().cpu() - rs).abs() <= bs).all()), b
 
 
+@pytest.mark.parametrize("plan", [(0, 0, 0), (64, 64, 4), (128, 128, 2), (64, 64, 1)])
+def test_gemm_wgrad_batch_shared_b(cuda, plan):
+    """kernels.gemm_wgrad_batch: two X blocks (strided views of two buffers, equally spaced by
+    construction) against one dY, the two dW blocks of one kernel, the bias column sum once
+    (bias_sbatch 0: batch 0 only) -- the decoder LSTM kernels' weight gradients"""
+    from sat_amd import _lib, kernels
+    g = torch.Generator().manual_seed(sum(plan) + 5)
+    K_, M, N = 3000, 256, 1024
+    arena = torch.randn(2, K_, M + 32, generator=g).to(cuda)       # padded rows, like H2S views
+    Xs = [arena[0, :, :M], arena[1, :, :M]]
+    dY = torch.randn(K_, N, generator=g)
+    W0 = torch.randn(2 * M, N, generator=g)
+    s0 = torch.randn(N, generator=g)
+    W, s = W0.to(cuda), s0.to(cuda)
+    lib = _lib.load()
+    lib.sat_gemm_force_plan(*plan)
+    try:
+        kernels.gemm_wgrad_batch(Xs, dY.to(cuda), [W[:M], W[M:]], colsum=s)
+        torch.cuda.synchronize()
+    finally:
+        lib.sat_gemm_force_plan(0, 0, 0)
+    Xh = arena.double().cpu()
+    for b in range(2):
+        ref = Xh[b, :, :M].t() @ dY.double() + W0[b * M:(b + 1) * M].double()
+        bound = 6e-7 * ((Xh[b, :, :M].abs().t() @ dY.double().abs()) +
+                        W0[b * M:(b + 1) * M].double().abs()) + 1e-7
+        assert bool(((W[b * M:(b + 1) * M].double().cpu() - ref).abs() <= bound).all()), b
+    rs = dY.double().sum(0) + s0.double()
+    assert bool(((s.double().cpu() - rs).abs() <= 6e-7 * (dY.double().abs().sum(0) +
+                                                          s0.double().abs()) + 1e-7).all())
+    with pytest.raises(ValueError):
+        kernels.gemm_wgrad_batch([Xs[0], Xs[1][:, :M - 4]], dY.to(cuda), [W[:M], W[M:]])
+
+
+@pytest.mark.parametrize("M,K", [(256, 16000), (100, 3000), (64, 1024)])
+@pytest.mark.parametrize("with_colsum", [True, False])
+def test_gemm_n1_transposed_a(cuda, M, K, with_colsum):
+    """N == 1 weight gradient dw = X^T dy (+ the bias sum) on gemm_tn1_kernel + the split-K
+    reduce: alpha / beta / colsum against float64"""
+    from sat_amd import kernels
+    g = torch.Generator().manual_seed(M + K)
+    X = torch.randn(K, M, generator=g)
+    dy = torch.randn(K, 1, generator=g)
+    w0 = torch.randn(M, 1, generator=g)
+    s0 = torch.randn(1, generator=g)
+    w, s = w0.to(cuda), s0.to(cuda)
+    kernels.gemm(X.to(cuda).t(), dy.to(cuda), w, alpha=-0.5, beta=1.0,
+                 colsum=s if with_colsum else None)
+    torch.cuda.synchronize()
+    ref = -0.5 * (X.double().t() @ dy.double()) + w0.double()
+    bound = 6e-7 * (0.5 * (X.double().abs().t() @ dy.double().abs()) + w0.double().abs()) + 1e-7
+    assert bool(((w.double().cpu() - ref).abs() <= bound).all())
+    if with_colsum:
+        rs = -0.5 * dy.double().sum() + s0.double()
+        assert abs(float(s.double().cpu()[0] - rs[0])) <= 6e-7 * (0.5 * float(dy.abs().sum()) +
+                                                                abs(float(s0[0]))) + 1e-7
+
+
 def test_gemm_colsum_fused_strided_b(cuda):
     """the attention query-layer shape: B is one tile of a [T'B, tiles, D1+D2] partial arena"""
     from sat_amd import kernels

@@ -267,11 +267,6 @@ int sat_gemm_force_plan(int32_t bm, int32_t bn, int32_t splits);
 /* Speed-of-light probe (tools/probes/gemm_sol.py): mode bit 0 skips the LDS kernel's operand
  * DMA, bit 1 its epilogue stores (results are then garbage); 0 = normal.  Calling thread only. */
 int sat_gemm_probe_mode(int32_t mode);
-/* Scheduling hint: cap the workgroups of the calling thread's subsequent sat_gemm launches at
- * about `cap` by limiting their split-K factor (0 = no cap).  For products issued on a side
- * stream beside a latency-bound chain, whose short launches otherwise wait for the side
- * product's workgroups to drain. */
-int sat_gemm_set_wg_cap(int32_t cap);
 /* Skinny product C = alpha * A . Bt^T + beta * C, A [M][K], Bt [N][K] rows contiguous in K
  * (16-B aligned, K % 4 == 0): the per-step gradient of the attention contexts through the
  * attention RNN's input weights (M = batch). */

@@ -193,7 +193,6 @@ SIGNATURES = {
     "sat_gemm": [ctypes.POINTER(SatGemmDesc), _P],
     "sat_gemm_force_plan": [_I32, _I32, _I32],
     "sat_gemm_probe_mode": [_I32],
-    "sat_gemm_set_wg_cap": [_I32],
     "sat_cbhg_convbank_fwd": [ctypes.POINTER(SatConvBank), _P],
     "sat_mha_fwd": [ctypes.POINTER(SatMha), _P],
     "sat_mha_bwd": [ctypes.POINTER(SatMha), _P],

@@ -39,7 +39,7 @@ class Aux:
     def run(self, fn, *tensors):
         self.s.wait_stream(torch.cuda.current_stream())
         self.keep.extend(tensors)
-        with torch.cuda.stream(self.s), K.gemm_wg_cap(AUX_WG_CAP):
+        with torch.cuda.stream(self.s):
             fn()
 
     def run_side(self, fn, *tensors):
@@ -99,8 +99,6 @@ PG_TSPLIT = int(os.environ.get("SAT_PG_TSPLIT", "3"))
 # kernel -- measured slower (13.80 -> 13.96 ms/step: its larger grid crowds out the encoder
 # backward's short launches beside it; profiles/r05r_wgrad_batch_ab.txt)
 WGRAD_BATCH = os.environ.get("SAT_WGRAD_BATCH", "0") == "1"
-# workgroup cap of the aux branches' GEMMs (sat_gemm_set_wg_cap; 0 = none)
-AUX_WG_CAP = int(os.environ.get("SAT_AUX_WG_CAP", "0"))
 
 # SAT_MHA_WGRAD_AUX=1 runs a multi-head attention's four weight gradients on the aux stream
 # (sat_mha_bwd_wgrad after a weight-deferred sat_mha_bwd).  Off: measured +0.45 ms/step for both
@@ -399,7 +397,7 @@ def decoder_bwd(P, G, hp, d, dsv, dH2, masks, ws, attn_tile=32, pipe: Pipeline =
         if aux is not None:
             aux.s.wait_stream(torch.cuda.current_stream())
             aux.keep.extend([DG0, DG1, DG2, DQP, S])
-        with torch.cuda.stream(aux_s), K.gemm_wg_cap(AUX_WG_CAP if aux is not None else 0):
+        with torch.cuda.stream(aux_s):
             dec_wgrad()
 
     def dec_wgrad():

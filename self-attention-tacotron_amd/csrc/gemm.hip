@@ -1188,12 +1188,7 @@ static hipError_t launch_tiles(int am, int bm, dim3 grid, hipStream_t s, const G
 
 // Tuning hook for probes (tools/probes/gemm_sweep.py): a forced tile / split-K plan for the
 // calling thread's next launches on the LDS kernel (bm = 0 restores the cost model).
-static thread_local int t_force_bm = 0, t_force_bn = 0, t_force_s = 0, t_probe = 0, t_wg_cap = 0;
-extern "C" int sat_gemm_set_wg_cap(int32_t cap) {
-  SAT_CHECK_ARG(cap >= 0, "sat_gemm_set_wg_cap: negative cap");
-  t_wg_cap = cap;
-  return SAT_OK;
-}
+static thread_local int t_force_bm = 0, t_force_bn = 0, t_force_s = 0, t_probe = 0;
 extern "C" int sat_gemm_probe_mode(int32_t m) {
   SAT_CHECK_ARG(m >= 0 && m <= 3, "sat_gemm_probe_mode: bad mode");
   t_probe = m;
@@ -1275,7 +1270,6 @@ static LdsPlan plan_lds(int M, int N, int K, int nb, bool can_split, int64_t ws_
       const int Se = ceil_div(K, kc);
       if (Se > 1 && (int64_t)Se * nb * M * N * 4 > ws_bytes) break;
       const int64_t tiles = base * Se;
-      if (Se > 1 && t_wg_cap > 0 && tiles > t_wg_cap) break;   // sat_gemm_set_wg_cap
       const int64_t per_cu = (tiles + 255) / 256;
       // MFMA efficiency vs resident waves x 32x32 sub-tiles per wave (probe: gemm_sweep.py)
       const int conc = (int)std::min<int64_t>(cd.occ, per_cu);
@@ -1602,8 +1596,7 @@ extern "C" int sat_gemm(const SatGemmDesc* d, void* stream) {
   p.kchunk = d->K;
   p.ws = reinterpret_cast<float*>(d->ws);
   if (nb == 1 && tiles < 160 && d->K >= 512 && d->ws != nullptr) {
-    int S = std::min<int>(std::max(1, (t_wg_cap > 0 ? std::min(384, t_wg_cap) : 384) / tiles),
-                          std::max(1, d->K / 256));
+    int S = std::min<int>(std::max(1, 384 / tiles), std::max(1, d->K / 256));
     S = std::min(S, 64);
     while (S > 1 && (int64_t)S * d->M * d->N * 4 > d->ws_bytes) --S;
     if (S > 1) {

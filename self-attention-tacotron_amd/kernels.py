@@ -251,24 +251,6 @@ def gemm_wgrad_batch(Xs, dY: torch.Tensor, dWs, colsum=None, beta=1.0):
     _launch_gemm(d, "sat_gemm")
 
 
-class gemm_wg_cap:
-    """``with gemm_wg_cap(n):`` the sat_gemm launches issued inside plan at most about n
-    workgroups (split-K limited; sat_gemm_set_wg_cap); 0 = no cap."""
-
-    def __init__(self, cap: int):
-        self.cap = int(cap)
-
-    def __enter__(self):
-        if self.cap:
-            _lib.check(_lib.load().sat_gemm_set_wg_cap(self.cap), "sat_gemm_set_wg_cap")
-        return self
-
-    def __exit__(self, *exc):
-        if self.cap:
-            _lib.load().sat_gemm_set_wg_cap(0)
-        return False
-
-
 def rowdot(A: torch.Tensor, Bt: torch.Tensor, C: torch.Tensor, alpha=1.0, beta=0.0):
     """C = alpha * A @ Bt^T + beta * C  (A [M, K], Bt [N, K] row-contiguous)."""
     M, Kd = A.shape

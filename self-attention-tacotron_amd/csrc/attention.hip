@@ -962,30 +962,43 @@ __device__ __forceinline__ void pg_recompute_body(const SatAttnParamGrad& p) {
   // and q is scaled once per step, so the exponent argument costs no extra multiply per element
   // (z agrees with tanh_fast to a few ulp; the forward's ZH is not read here)
   constexpr float kE = 2.8853900817779268f;
-  float4 kk[SLOTS], vv[SLOTS], lw[SLOTS][FL];
-  float4 adk[SLOTS], adv[SLOTS], adw[SLOTS][FL];
-  bool m1[SLOTS], ok[SLOTS];
+  // Factored step arithmetic: with r = 1 / (1 + 2^(kE x)), z = tanh(x) = 1 - 2 r and
+  // 1 - z^2 = 4 r (1 - r) = 4 g, so per element and step only g, e g, e r and the F products
+  // (f e) g are accumulated, in packed pairs; the step-independent factors 4 v (dK, dW_loc) and
+  // sum_t e - 2 (.) (dv) are applied once after the loop.  (The per-element form spent ~25 % of
+  // its VALU slots on register moves feeding the packed FMAs: 268 -> 227 VALU instructions per
+  // 4 steps, 607 -> 471 us per launch, profiles/r05u_pg_factored_ab.txt.  Strength-reducing the
+  // per-step history addresses as well moved 54 SALU instructions onto 16 more VALU ones: 510 us.)
+  using f2 = __attribute__((ext_vector_type(2))) float;
+  f2 kk[SLOTS][2], lw[SLOTS][FL][2];
+  float4 vv[SLOTS];
+  f2 aG[SLOTS][2], aR[SLOTS][2], aW[SLOTS][FL][2];
+  float esum[SLOTS];
+  bool m1[SLOTS];
   const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  const f2 z2 = {0.f, 0.f};
 #pragma unroll
   for (int s = 0; s < SLOTS; ++s) {
     const int c = lane + 64 * s;
-    ok[s] = c < Q;
     m1[s] = c < Q1;
     const int c1 = min(c, Q1 - 1), c2 = min(max(c - Q1, 0), p.D2 / 4 - 1);
     // the step-independent part of tanh's exponent argument, pre-scaled: exp(2x) = 2^(kE x)
     const float4 k4 = m1[s] ? reinterpret_cast<const float4*>(p.K1 + bn * p.D1)[c1]
                             : reinterpret_cast<const float4*>(p.K2 + bn * p.D2)[c2];
     const float4 b4 = (m1[s] && p.b1) ? reinterpret_cast<const float4*>(p.b1)[c1] : z4;
-    kk[s] = make_float4(kE * (k4.x + b4.x), kE * (k4.y + b4.y), kE * (k4.z + b4.z), kE * (k4.w + b4.w));
+    kk[s][0] = f2{kE * (k4.x + b4.x), kE * (k4.y + b4.y)};
+    kk[s][1] = f2{kE * (k4.z + b4.z), kE * (k4.w + b4.w)};
     vv[s] = m1[s] ? reinterpret_cast<const float4*>(p.v1)[c1] : reinterpret_cast<const float4*>(p.v2)[c2];
 #pragma unroll
     for (int f = 0; f < F; ++f) {
       const float4 w4 = m1[s] ? reinterpret_cast<const float4*>(p.locW + (int64_t)f * p.D1)[c1] : z4;
-      lw[s][f] = make_float4(kE * w4.x, kE * w4.y, kE * w4.z, kE * w4.w);
+      lw[s][f][0] = f2{kE * w4.x, kE * w4.y};
+      lw[s][f][1] = f2{kE * w4.z, kE * w4.w};
     }
-    adk[s] = z4; adv[s] = z4;
+    aG[s][0] = aG[s][1] = aR[s][0] = aR[s][1] = z2;
 #pragma unroll
-    for (int f = 0; f < FL; ++f) adw[s][f] = z4;
+    for (int f = 0; f < FL; ++f) aW[s][f][0] = aW[s][f][1] = z2;
+    esum[s] = 0.f;
   }
   // location-conv roles: lane < KW*F owns (j, f) of convW, the next F lanes own convb
   const int nconv = F > 0 ? p.KW * F : 0;
@@ -994,6 +1007,7 @@ __device__ __forceinline__ void pg_recompute_body(const SatAttnParamGrad& p) {
   // the step loop is latency-bound (a handful of dependent loads per step): issue the loads of
   // kU steps at once, then do their arithmetic
   constexpr int kU = 4;
+  const f2 kE2 = {kE, kE};
   for (int t0 = t_lo; t0 < t_hi; t0 += kU) {
     float e1s[kU], e2s[kU], fls[kU][FL], sv[kU], dfv[kU];
     float4 qv[kU][SLOTS];
@@ -1027,33 +1041,45 @@ __device__ __forceinline__ void pg_recompute_body(const SatAttnParamGrad& p) {
       acw = fmaf(sv[u], dfv[u], acw);
 #pragma unroll
       for (int s = 0; s < SLOTS; ++s) {
-        float pre[4] = {fmaf(kE, qv[u][s].x, kk[s].x), fmaf(kE, qv[u][s].y, kk[s].y),
-                        fmaf(kE, qv[u][s].z, kk[s].z), fmaf(kE, qv[u][s].w, kk[s].w)};
-        if (m1[s]) {
-#pragma unroll
-          for (int f = 0; f < F; ++f) {
-            pre[0] = fmaf(fls[u][f], lw[s][f].x, pre[0]); pre[1] = fmaf(fls[u][f], lw[s][f].y, pre[1]);
-            pre[2] = fmaf(fls[u][f], lw[s][f].z, pre[2]); pre[3] = fmaf(fls[u][f], lw[s][f].w, pre[3]);
-          }
-        }
-        const float e = m1[s] ? e1s[u] : e2s[u];
-        float z[4], dp[4];
-        const float vs[4] = {vv[s].x, vv[s].y, vv[s].z, vv[s].w};
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          z[k] = 1.f - 2.f * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(pre[k]));
-          dp[k] = e * vs[k] * (1.f - z[k] * z[k]);
-        }
-        adk[s].x += dp[0]; adk[s].y += dp[1]; adk[s].z += dp[2]; adk[s].w += dp[3];
-        adv[s].x = fmaf(e, z[0], adv[s].x); adv[s].y = fmaf(e, z[1], adv[s].y);
-        adv[s].z = fmaf(e, z[2], adv[s].z); adv[s].w = fmaf(e, z[3], adv[s].w);
+        f2 pr[2] = {__builtin_elementwise_fma(kE2, f2{qv[u][s].x, qv[u][s].y}, kk[s][0]),
+                    __builtin_elementwise_fma(kE2, f2{qv[u][s].z, qv[u][s].w}, kk[s][1])};
 #pragma unroll
         for (int f = 0; f < F; ++f) {
-          adw[s][f].x = fmaf(fls[u][f], dp[0], adw[s][f].x); adw[s][f].y = fmaf(fls[u][f], dp[1], adw[s][f].y);
-          adw[s][f].z = fmaf(fls[u][f], dp[2], adw[s][f].z); adw[s][f].w = fmaf(fls[u][f], dp[3], adw[s][f].w);
+          const f2 fl = {fls[u][f], fls[u][f]};
+          pr[0] = __builtin_elementwise_fma(fl, lw[s][f][0], pr[0]);
+          pr[1] = __builtin_elementwise_fma(fl, lw[s][f][1], pr[1]);
+        }
+        const float e = m1[s] ? e1s[u] : e2s[u];
+        esum[s] += e;
+        const f2 ee = {e, e};
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const f2 r = {__builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(pr[h].x)),
+                        __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(pr[h].y))};
+          const f2 g = __builtin_elementwise_fma(-r, r, r);          // r (1 - r)
+          aG[s][h] = __builtin_elementwise_fma(ee, g, aG[s][h]);
+          aR[s][h] = __builtin_elementwise_fma(ee, r, aR[s][h]);
+#pragma unroll
+          for (int f = 0; f < F; ++f) {
+            const float fe = fls[u][f] * e;
+            aW[s][f][h] = __builtin_elementwise_fma(f2{fe, fe}, g, aW[s][f][h]);
+          }
         }
       }
     }
+  }
+  // the step-independent factors: dK = 4 v sum e g, dv = sum e - 2 sum e r, dW_loc = 4 v sum f e g
+  float4 adk[SLOTS], adv[SLOTS], adw[SLOTS][FL];
+#pragma unroll
+  for (int s = 0; s < SLOTS; ++s) {
+    const float4 v4 = make_float4(4.f * vv[s].x, 4.f * vv[s].y, 4.f * vv[s].z, 4.f * vv[s].w);
+    adk[s] = make_float4(v4.x * aG[s][0].x, v4.y * aG[s][0].y, v4.z * aG[s][1].x, v4.w * aG[s][1].y);
+    adv[s] = make_float4(fmaf(-2.f, aR[s][0].x, esum[s]), fmaf(-2.f, aR[s][0].y, esum[s]),
+                         fmaf(-2.f, aR[s][1].x, esum[s]), fmaf(-2.f, aR[s][1].y, esum[s]));
+#pragma unroll
+    for (int f = 0; f < FL; ++f)
+      adw[s][f] = make_float4(v4.x * aW[s][f][0].x, v4.y * aW[s][f][0].y, v4.z * aW[s][f][1].x,
+                              v4.w * aW[s][f][1].y);
   }
   attn_pg_store<SLOTS, F>(p, adk, adv, adw, acw);
 }

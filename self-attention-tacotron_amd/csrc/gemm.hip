@@ -734,10 +734,17 @@ __global__ void __launch_bounds__((64 * lds_waves<BM, BN>())) gemm_lds_kernel(Ge
   const int bb = p.splits > 1 ? (int)blockIdx.z / p.splits : (int)blockIdx.z;
   const int split = p.splits > 1 ? (int)blockIdx.z - bb * p.splits : 0;
   const int bz = bb / p.batch2, bz2 = bb - bz * p.batch2;
-  // conv-bank forward: column blocks have different reductions ((g + 1) * C); the dispatcher
-  // deals workgroup i to XCD i % 8, so rotate the column index by the row index to give every
-  // XCD the same mix of kernel widths, longest first within a row
-  if constexpr (GRP == 1) tx = gridDim.x - 1 - (int)((blockIdx.x + blockIdx.y) % gridDim.x);
+  // conv-bank forward: column blocks have different reductions ((g + 1) * C), so the tiles go
+  // out longest-first (every row tile of the widest bank, then the next, ...): the greedy
+  // dispatcher then ends the launch on the short tiles.  A row-major order with a per-row
+  // rotation left long tiles among the last dispatched (a list-scheduling model of the C2 shape:
+  // makespan 160 vs 121 units for a 116 lower bound).  Consecutive workgroups still land on
+  // different XCDs (the dispatcher deals workgroup i to XCD i % 8).
+  if constexpr (GRP == 1) {
+    const int i = blockIdx.y * gridDim.x + blockIdx.x, c = i / gridDim.y;
+    tx = gridDim.x - 1 - c;
+    ty = i - c * gridDim.y;
+  }
   const int m0 = ty * BM, n0 = tx * BN;
   const float* A = p.A + bz * p.a_sbatch + bz2 * p.a_sbatch2;
   const float* B = p.B + bz * p.b_sbatch + bz2 * p.b_sbatch2;
@@ -1668,6 +1675,7 @@ extern "C" int sat_cbhg_convbank_fwd(const SatConvBank* d, void* stream) {
   // plan on the mean reduction; no split (3,200 tiles at the C2 shape already fill the chip)
   LdsPlan pl = plan_lds(p.M, p.N, (d->max_k + 1) * d->C / 2, 1, false, 0, 0, d->Co);
   // measured at the C2 shape (tools/probes/conv_sol.py): 64x128 352 us, 64x64 384, 128x* 405
+  // (row-major dispatch; longest-first dispatch, gemm_lds_kernel, takes 64x128 to 282 us)
   if (t_force_bm == 0 && d->Co % 128 == 0) pl = {64, 128, 1, p.K};
   LdsPlan fixed = pl;
   fixed.splits = 1;

@@ -773,6 +773,12 @@ int sat_colsum_scatter(const float* x, int64_t ldx, int32_t M, int32_t C,
 /* MaxPooling1D(pool 2, stride 1, SAME) over [B][N][C] (modules/module.py:54,80) and its
  * gradient (first index wins ties, as TF MaxPoolGrad). */
 int sat_maxpool2(const float* x, float* y, int32_t B, int32_t N, int32_t C, void* stream);
+/* y = BN(x) (+ReLU) as sat_bn_apply over the [B*N][C] rows (contiguous, no residual) AND
+ * mp = sat_maxpool2(y) in one pass: the CBHG conv bank's BN and max-pool
+ * (modules/module.py:79-80); bit-identical to the two calls. */
+int sat_bn_apply_maxpool2(const float* x, float* y, float* mp, int32_t B, int32_t N, int32_t C,
+                          const float* mean, const float* var, float eps, const float* gamma,
+                          const float* beta, int32_t relu, void* stream);
 int sat_maxpool2_bwd(const float* x, const float* dy, float* dx, int32_t B, int32_t N, int32_t C,
                      void* stream);
 

@@ -239,6 +239,7 @@ SIGNATURES = {
     "sat_colsum_scatter": [_P, _I64, _I32, _I32, ctypes.POINTER(SatColSegment), _I32, _F, _P,
                            _P],
     "sat_maxpool2": [_P, _P, _I32, _I32, _I32, _P],
+    "sat_bn_apply_maxpool2": [_P, _P, _P, _I32, _I32, _I32, _P, _P, _F, _P, _P, _I32, _P],
     "sat_maxpool2_bwd": [_P, _P, _P, _I32, _I32, _I32, _P],
     "sat_highway_fwd": [_P, _P, _P, _P, _I64, _P],
     "sat_highway_act_fwd": [_P, _P, _P, _P, _I64, _P],

@@ -267,6 +267,15 @@ __global__ void bn_apply_kernel(const float* __restrict__ x, int64_t ldx, float*
 // float4 variants of the two BN element passes (C and every leading dimension % 4 == 0,
 // 16-byte aligned, M*C < 2^31): 32-bit row arithmetic once per four channels and 16-byte
 // accesses; per element the same expressions as the scalar kernels (bit-identical)
+// one BN(+ReLU) output element (shared by bn_apply4_kernel and bn_apply_pool4c_kernel so the two
+// produce the same bits)
+__device__ __forceinline__ float bn_val(float x, float g, float m, float v, float b, float eps,
+                                        int relu) {
+  float o = g * (x - m) * rsqrtf(v + eps) + b;
+  if (relu) o = fmaxf(o, 0.f);
+  return o;
+}
+
 __global__ void bn_apply4_kernel(const float* __restrict__ x, int ldx, float* __restrict__ y,
                                  int ldy, int M, int C, const float* __restrict__ mean,
                                  const float* __restrict__ var, float eps,
@@ -288,8 +297,7 @@ __global__ void bn_apply4_kernel(const float* __restrict__ x, int ldx, float* __
     float o[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      float v = gs[k] * (xs[k] - ms[k]) * rsqrtf(vs[k] + eps) + bs[k];
-      if (relu) v = fmaxf(v, 0.f);
+      float v = bn_val(xs[k], gs[k], ms[k], vs[k], bs[k], eps, relu);
       if (res) v += rs[k];
       o[k] = v;
     }
@@ -484,6 +492,49 @@ __global__ void maxpool_fwd4c_kernel(const float4* __restrict__ x, float4* __res
                                           : a;
   }
 }
+// BN(+ReLU) apply and the stride-1 width-2 max-pool over time in one pass (the CBHG conv bank,
+// modules/module.py:79-80): a thread owns kMpL consecutive positions of one (utterance, float4
+// column) as in maxpool_fwd4c_kernel, forms the BN outputs of positions n0 .. n0 + kMpL once
+// (the next chunk's first one again), writes y (kept for the backward) and the pooled output.
+__global__ void bn_apply_pool4c_kernel(const float4* __restrict__ x, float4* __restrict__ y,
+                                       float4* __restrict__ mp, int N, int C4, int nchunk,
+                                       int total, const float4* __restrict__ mean,
+                                       const float4* __restrict__ var, float eps,
+                                       const float4* __restrict__ gamma,
+                                       const float4* __restrict__ beta, int relu) {
+  const int tid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (tid >= total) return;
+  const int c = tid % C4;
+  const int rest = tid / C4;
+  const int ch = rest % nchunk, b = rest / nchunk;
+  const int n0 = ch * kMpL;
+  const int64_t base = (int64_t)b * N * C4 + c;
+  const float4 mu = mean[c], va = var[c], ga = gamma[c], be = beta[c];
+  float4 xv[kMpL + 1];
+#pragma unroll
+  for (int k = 0; k < kMpL + 1; ++k) {        // positions n0 + k (clamped)
+    const int n = min(n0 + k, N - 1);
+    xv[k] = x[base + (int64_t)n * C4];
+  }
+  float4 yv[kMpL + 1];
+#pragma unroll
+  for (int k = 0; k < kMpL + 1; ++k)
+    yv[k] = make_float4(bn_val(xv[k].x, ga.x, mu.x, va.x, be.x, eps, relu),
+                        bn_val(xv[k].y, ga.y, mu.y, va.y, be.y, eps, relu),
+                        bn_val(xv[k].z, ga.z, mu.z, va.z, be.z, eps, relu),
+                        bn_val(xv[k].w, ga.w, mu.w, va.w, be.w, eps, relu));
+#pragma unroll
+  for (int k = 0; k < kMpL; ++k) {
+    const int n = n0 + k;
+    if (n >= N) break;
+    const float4 a = yv[k], b2 = yv[k + 1];
+    y[base + (int64_t)n * C4] = a;
+    mp[base + (int64_t)n * C4] = n + 1 < N ? make_float4(fmaxf(a.x, b2.x), fmaxf(a.y, b2.y),
+                                                         fmaxf(a.z, b2.z), fmaxf(a.w, b2.w))
+                                           : a;
+  }
+}
+
 __global__ void maxpool_bwd4_kernel(const float4* __restrict__ x, const float4* __restrict__ dy,
                                     float4* __restrict__ dx, unsigned N, unsigned C4,
                                     unsigned total4) {
@@ -1135,6 +1186,31 @@ extern "C" int sat_maxpool2(const float* x, float* y, int32_t B, int32_t N, int3
                        as_stream(stream), x, y, B, N, C);
   SAT_LAUNCH_CHECK("sat_maxpool2");
   return SAT_OK;
+}
+
+extern "C" int sat_bn_apply_maxpool2(const float* x, float* y, float* mp, int32_t B, int32_t N,
+                                     int32_t C, const float* mean, const float* var, float eps,
+                                     const float* gamma, const float* beta, int32_t relu,
+                                     void* stream) {
+  SAT_CHECK_ARG(x && y && mp && mean && var && gamma && beta && B > 0 && N > 0 && C > 0,
+                "sat_bn_apply_maxpool2: bad args");
+  const int64_t total = (int64_t)B * N * C;
+  if (C % 4 == 0 && total < (1LL << 31) && aligned16(x) && aligned16(y) && aligned16(mp) &&
+      aligned16(mean) && aligned16(var) && aligned16(gamma) && aligned16(beta)) {
+    const int64_t nthreads = (int64_t)B * ((N + kMpL - 1) / kMpL) * (C / 4);
+    hipLaunchKernelGGL(bn_apply_pool4c_kernel, dim3(ceil_div(nthreads, 256)), dim3(256), 0,
+                       as_stream(stream), reinterpret_cast<const float4*>(x),
+                       reinterpret_cast<float4*>(y), reinterpret_cast<float4*>(mp), N, C / 4,
+                       (N + kMpL - 1) / kMpL, (int)nthreads,
+                       reinterpret_cast<const float4*>(mean), reinterpret_cast<const float4*>(var),
+                       eps, reinterpret_cast<const float4*>(gamma),
+                       reinterpret_cast<const float4*>(beta), relu);
+    SAT_LAUNCH_CHECK("sat_bn_apply_maxpool2");
+    return SAT_OK;
+  }
+  const int r = sat_bn_apply(x, C, y, C, B * N, C, mean, var, eps, gamma, beta, relu, nullptr, 0,
+                             stream);
+  return r != SAT_OK ? r : sat_maxpool2(y, mp, B, N, C, stream);
 }
 
 extern "C" int sat_maxpool2_bwd(const float* x, const float* dy, float* dx, int32_t B, int32_t N,

@@ -820,6 +820,15 @@ def maxpool2(x, y):
     return y
 
 
+def bn_apply_maxpool2(x, y, mp, mean, var, gamma, beta, relu=True, eps=1e-3):
+    """y = BN(x) (+ReLU) and mp = maxpool2(y) in one pass (x, y, mp [B, N, C] contiguous):
+    bit-identical to bn_apply + maxpool2 (sat_bn_apply_maxpool2)."""
+    B, N, C = x.shape
+    _lib.call("sat_bn_apply_maxpool2", _p(x), _p(y), _p(mp), B, N, C, _p(mean), _p(var), eps,
+              _p(gamma), _p(beta), int(relu), _stream())
+    return mp
+
+
 def maxpool2_bwd(x, dy, dx):
     B, N, C = x.shape
     _lib.call("sat_maxpool2_bwd", _p(x), _p(dy), _p(dx), B, N, C, _stream())

@@ -12,6 +12,7 @@ except the attention energies which the backward recomputes to avoid a [T', B, N
 from __future__ import annotations
 
 import math
+import os
 from typing import Dict, List, Optional, Tuple
 
 import numpy as np
@@ -152,10 +153,13 @@ def encoder_fwd(P, bn: BNState, hp, d: PR.Dims, ids, lengths, masks, training, w
     bank = torch.empty_like(bank_pre)
     gam = _contig_span(P, [f"{n}/bn/gamma" for n in names])
     bet = _contig_span(P, [f"{n}/bn/beta" for n in names])
-    st_bank = _bn(bank_pre.view(-1, KC), bank.view(-1, KC), gam, bet, bn, f"{names[0]}/bn", KC, True,
-                  training, ws)
     mp = torch.empty_like(bank)
-    K.maxpool2(bank, mp)                                              # module.py:80
+    # BN + ReLU and the max-pool (module.py:79-80) in one pass over the bank
+    fused = os.environ.get("SAT_BANK_POOL_FUSED", "1") == "1"       # 0: two launches (A/B)
+    st_bank = _bn(bank_pre.view(-1, KC), bank.view(-1, KC), gam, bet, bn, f"{names[0]}/bn", KC, True,
+                  training, ws, pool=(bank_pre, bank, mp) if fused else None)
+    if not fused:
+        K.maxpool2(bank, mp)                                          # module.py:80
     p1_pre = K.conv1d(mp, P["encoder/cbhg/proj1/kernel"], P["encoder/cbhg/proj1/bias"])
     p1 = torch.empty_like(p1_pre)
     st_p1 = _bn(p1_pre.view(-1, d.proj1), p1.view(-1, d.proj1), P["encoder/cbhg/proj1/bn/gamma"],
@@ -260,7 +264,8 @@ def encoder_fwd(P, bn: BNState, hp, d: PR.Dims, ids, lengths, masks, training, w
     return m1, x
 
 
-def _bn(x2, y2, gamma, beta, bn: BNState, scope, C, relu, training, ws, res=None):
+def _bn(x2, y2, gamma, beta, bn: BNState, scope, C, relu, training, ws, res=None, pool=None):
+    """``pool`` = (x3, y3, mp3): also the max-pool of the output into mp3, fused (no ``res``)."""
     dev = x2.device
     if training:
         mean = torch.empty(C, device=dev)
@@ -269,7 +274,10 @@ def _bn(x2, y2, gamma, beta, bn: BNState, scope, C, relu, training, ws, res=None
         K.bn_stats(x2, mean, var, ws, mm, mv, momentum=0.99)
     else:
         mean, var = bn.span(scope, C)
-    K.bn_apply(x2, y2, mean, var, gamma, beta, relu=relu, res=res)
+    if pool is not None:
+        K.bn_apply_maxpool2(*pool, mean, var, gamma, beta, relu=relu)
+    else:
+        K.bn_apply(x2, y2, mean, var, gamma, beta, relu=relu, res=res)
     return dict(mean=mean, var=var, gamma=gamma, beta=beta)
 
 

@@ -80,6 +80,29 @@ def test_maxpool2_fwd_bwd(cuda, B, N, C):
     assert torch.equal(dx.cpu(), dxr)
 
 
+@pytest.mark.parametrize("B,N,C", [(32, 200, 2048), (3, 17, 2048), (2, 1, 128), (4, 9, 7),
+                                   (16, 203, 256)])
+@pytest.mark.parametrize("relu", [True, False])
+def test_bn_apply_maxpool2_fused(cuda, B, N, C, relu):
+    """sat_bn_apply_maxpool2 (the conv bank's BN + max-pool in one pass, ragged last chunk and
+    the two-launch fallback at C % 4 != 0) == sat_bn_apply then sat_maxpool2, bitwise"""
+    from sat_amd import kernels as K
+    g = torch.Generator().manual_seed(B * N + C + relu)
+    x = (torch.randn(B, N, C, generator=g) * 2).to(cuda)
+    mean = torch.randn(C, generator=g).to(cuda)
+    var = torch.rand(C, generator=g).to(cuda) + 0.1
+    gam = torch.randn(C, generator=g).to(cuda)
+    bet = torch.randn(C, generator=g).to(cuda)
+    y1 = torch.empty_like(x)
+    K.bn_apply(x.view(-1, C), y1.view(-1, C), mean, var, gam, bet, relu=relu)
+    mp1 = K.maxpool2(y1, torch.empty_like(x))
+    y2, mp2 = torch.empty_like(x), torch.empty_like(x)
+    K.bn_apply_maxpool2(x, y2, mp2, mean, var, gam, bet, relu=relu)
+    torch.cuda.synchronize()
+    assert torch.equal(y1, y2)
+    assert torch.equal(mp1, mp2)
+
+
 @pytest.mark.parametrize("R,D,V,offset", [(6400, 512, 70, 0), (37, 300, 5, 3), (1, 512, 4, 0),
                                           (1100, 64, 1, 0), (8192, 256, 9, 0), (9000, 64, 3, 0)])
 def test_embedding_bwd_row_order(cuda, R, D, V, offset):

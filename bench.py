@@ -240,19 +240,43 @@ def _pmc_traffic(kernel_tag: str, source: str):
     import glob
     import hashlib
     here = os.path.dirname(os.path.abspath(__file__))
-    files = sorted(glob.glob(os.path.join(here, "profiles", f"r*_{kernel_tag}_pmc.json")))
+    import re
+    files = glob.glob(os.path.join(here, "profiles", f"r*_{kernel_tag}_pmc.json"))
     if not files:
         return None, {"file": None, "why": "no PMC summary committed"}
+
+    def tag_key(path):
+        # round tags are r<round><letters>: r05 < r05a < r05z < r05aa < r05ab < r06 (the
+        # letters count like a spreadsheet column; a plain string sort puts r05y after r05ab)
+        m = re.match(r"r(\d+)([a-z]*)_", os.path.basename(path))
+        if not m:
+            return (-1, -1)
+        col = 0
+        for ch in m.group(2):
+            col = col * 26 + (ord(ch) - 96)
+        return (int(m.group(1)), col)
+
+    src = os.path.join(here, "self-attention-tacotron_amd", "csrc", source)
     try:
-        d = json.load(open(files[-1]))
-        src = os.path.join(here, "self-attention-tacotron_amd", "csrc", source)
         now = hashlib.sha256(open(src, "rb").read()).hexdigest()[:16]
-        was = d.get("source_sha16")
-        return int(d["hbm_bytes_per_launch"]), {
-            "file": os.path.basename(files[-1]), "measured_on_source_sha16": was,
-            "current_source_sha16": now, "current": was == now}
-    except (OSError, ValueError, KeyError):
-        return None, {"file": os.path.basename(files[-1]), "why": "unreadable PMC summary"}
+    except OSError:
+        now = None
+    summaries = []
+    for f in files:
+        try:
+            d = json.load(open(f))
+            summaries.append((tag_key(f), f, d, int(d["hbm_bytes_per_launch"])))
+        except (OSError, ValueError, KeyError):
+            continue
+    if not summaries:
+        return None, {"file": os.path.basename(max(files, key=tag_key)),
+                      "why": "unreadable PMC summary"}
+    # the newest summary measured on THIS tree's kernel source; else the newest one (stale)
+    cur = [x for x in summaries if x[2].get("source_sha16") == now]
+    _, f, d, nbytes = max(cur or summaries, key=lambda x: x[0])
+    was = d.get("source_sha16")
+    return nbytes, {"file": os.path.basename(f), "measured_on_source_sha16": was,
+                    "current_source_sha16": now, "current": was == now}
 
 
 def cpu_baseline(hp, args, B=None, steps=None):

@@ -195,6 +195,10 @@ typedef struct SatMha {
   float* lse;
 } SatMha;
 int64_t sat_mha_scratch_bytes(int32_t B, int32_t L, int32_t D, int32_t H, int32_t out_dim);
+/* the same for a descriptor that takes the fused attention (sat_flash_attn_*: lse set, the
+ * head shapes of sat_flash_attn_fwd, 16-byte-aligned q / k / v / o / probs_mask): dO, dQ, dK,
+ * dV [B][L][D] and the row term [B][H][L], no [B][H][L][L] slab */
+int64_t sat_mha_scratch_bytes_fused(int32_t B, int32_t L, int32_t D, int32_t H, int32_t out_dim);
 int sat_mha_fwd(const SatMha* d, void* stream);
 /* dWq / dWk / dWv / dWo all NULL: the weight and bias gradients are deferred -- sat_mha_bwd
  * writes dx only and leaves dO, dQ, dK, dV in the scratch; sat_mha_bwd_wgrad (same descriptor

@@ -268,6 +268,7 @@ RESTYPES = {"sat_workspace_colreduce": (ctypes.c_int64, [_I32, _I32]),
             "sat_workspace_adam": (ctypes.c_int64, []),
             "sat_workspace_loss": (ctypes.c_int64, []),
             "sat_mha_scratch_bytes": (ctypes.c_int64, [_I32, _I32, _I32, _I32, _I32]),
+            "sat_mha_scratch_bytes_fused": (ctypes.c_int64, [_I32, _I32, _I32, _I32, _I32]),
             "sat_workspace_size": (ctypes.c_int64, [ctypes.c_void_p]),
             "sat_decoder_attention_scratch": (ctypes.c_int64, [_I32, _I32, _P, _P, _P]),
             "sat_decoder_attention_bwd_scratch": (ctypes.c_int64, [_I32, _I32, _P, _P]),
@@ -299,9 +300,8 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     if got != ABI_VERSION:
         raise SatLibraryError(f"{path}: ABI version {got}, this binding needs {ABI_VERSION} "
                               "(rebuild it: make -C self-attention-tacotron_amd/csrc)")
+    # (an A/B build loaded through SAT_LIB_OVERRIDE must therefore carry this ABI version too)
     for name, argtypes in SIGNATURES.items():
-        if os.environ.get("SAT_LIB_OVERRIDE") and not hasattr(lib, name):
-            continue     # an older build under A/B (tools/): entries added since stay unbound
         fn = getattr(lib, name)
         fn.argtypes = argtypes
         fn.restype = ctypes.c_int

@@ -458,7 +458,7 @@ def decoder_bwd(P, G, hp, d, dsv, dH2, masks, ws, attn_tile=32, pipe: Pipeline =
     #      sum of its per-workgroup partial rows
     F, KW = (d.loc_f, d.loc_k) if fwd else (0, 0)
     pgs = K.pg_stride(D1, D2, F, KW)
-    ts = PG_TSPLIT
+    ts = max(1, min(PG_TSPLIT, Tp, 8))     # the library takes 1 <= tsplit <= min(T', 8)
     PG = torch.empty(ts * K.attn_param_grad_rows(B, N), pgs, **f32)
     dK1s = torch.empty(ts, B, N, D1, **f32)       # slab 0 holds the gradient on return
     dK2s = torch.empty(ts, B, N, D2, **f32)

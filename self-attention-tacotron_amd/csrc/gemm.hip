@@ -1510,6 +1510,11 @@ extern "C" int sat_gemm(const SatGemmDesc* d, void* stream) {
     SAT_CHECK_ARG(p.batch2 == 1 && d->a_mode == 0 && d->b_mode == 0 && !d->bias && d->act == 0 &&
                       !d->mul && !d->add,
                   "sat_gemm: colsum_out needs a plain product with batch2 == 1 (no bias/act/mul/add)");
+    // bias_sbatch == 0 means "batch 0's sums only", which is right only when every batch reads
+    // the same B; with a batch-strided B the other batches' sums would be dropped silently
+    SAT_CHECK_ARG(nb <= 1 || d->bias_sbatch != 0 || d->b_sbatch == 0,
+                  "sat_gemm: colsum_out of a batched product with a batch-strided B needs "
+                  "bias_sbatch (one [N] row per batch)");
     if (gemm_lds_enabled()) {
       p.cs_out = d->colsum_out;
       p.cs_sbatch = d->bias_sbatch;     // batch b's sums at colsum_out + b * bias_sbatch

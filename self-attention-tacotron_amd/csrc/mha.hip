@@ -71,6 +71,14 @@ bool flash_ok(const SatMha* d) {
          aligned16(d->o) && (!d->probs_mask || aligned16(d->probs_mask));
 }
 
+// scratch the descriptor's path needs: the fused path keeps only dO, dQ, dK, dV and the
+// [B][H][L] row term delta (in the first score slab's place); the materialised path the two
+// [B][H][L][L] score slabs as well
+int64_t scratch_need(const SatMha* d) {
+  return flash_ok(d) ? sat_mha_scratch_bytes_fused(d->B, d->L, d->D, d->H, d->out_dim)
+                     : sat_mha_scratch_bytes(d->B, d->L, d->D, d->H, d->out_dim);
+}
+
 SatFlashAttn flash_desc(const SatMha* d) {
   SatFlashAttn fa;
   std::memset(&fa, 0, sizeof(fa));
@@ -97,13 +105,13 @@ int check(const SatMha* d, bool bwd) {
     const bool none = !d->dWq && !d->dWk && !d->dWv && !d->dWo;
     SAT_CHECK_ARG(d->dy && d->dx && (all || none),
                   "sat_mha_bwd: null gradient tensor (the four weight gradients: all or none)");
-    SAT_CHECK_ARG(d->scratch && d->scratch_bytes >= sat_mha_scratch_bytes(d->B, d->L, d->D, d->H,
-                                                                          d->out_dim),
-                  "sat_mha_bwd: scratch smaller than sat_mha_scratch_bytes()");
+    SAT_CHECK_ARG(d->scratch && d->scratch_bytes >= scratch_need(d),
+                  "sat_mha_bwd: scratch smaller than sat_mha_scratch_bytes() "
+                  "(sat_mha_scratch_bytes_fused() on the fused path)");
   } else {
-    SAT_CHECK_ARG(d->y && d->scratch &&
-                      d->scratch_bytes >= sat_mha_scratch_bytes(d->B, d->L, d->D, d->H, d->out_dim),
-                  "sat_mha_fwd: needs y and scratch of sat_mha_scratch_bytes()");
+    SAT_CHECK_ARG(d->y && d->scratch && d->scratch_bytes >= scratch_need(d),
+                  "sat_mha_fwd: needs y and scratch of sat_mha_scratch_bytes() "
+                  "(sat_mha_scratch_bytes_fused() on the fused path)");
   }
   return SAT_OK;
 }
@@ -126,6 +134,15 @@ extern "C" int64_t sat_mha_scratch_bytes(int32_t B, int32_t L, int32_t D, int32_
   // backward: dO, dQ, dK, dV [B L D], dPd, dS [B H L L], column-sum scratch; the forward uses
   // the first score slab for the raw scores
   return 4 * align_up(act) + 2 * align_up(score) + align_up(cs);
+}
+
+// the fused attention's (flash_ok) share of that: dO, dQ, dK, dV and delta [B][H][L] -- no
+// O(L^2) slab in either direction
+extern "C" int64_t sat_mha_scratch_bytes_fused(int32_t B, int32_t L, int32_t D, int32_t H,
+                                               int32_t out_dim) {
+  (void)out_dim;
+  const int64_t act = (int64_t)B * L * D * 4, delta = (int64_t)B * H * L * 4;
+  return 4 * align_up(act) + align_up(delta);
 }
 
 // y = Wo . concat_h(softmax(Q_h K_h^T / sqrt(dh)) [* mask] V_h) + bo,  Q/K/V = x W + b

@@ -195,6 +195,10 @@ def gemm(A: torch.Tensor, B: torch.Tensor, C: torch.Tensor = None, *, alpha=1.0,
             d.bias_sbatch = colsum.stride(0)
         elif colsum.numel() != N or not colsum.is_contiguous():
             raise ValueError("gemm: colsum must be a contiguous [N] tensor")
+        elif nb > 1 and d.b_sbatch != 0:
+            # one [N] row with a batched B would keep batch 0's column sums only
+            raise ValueError("gemm: a batched product with a batch-strided B needs a "
+                             "[batch, N] colsum")
         d.colsum_out = _p(colsum)
     if A2 is not None:
         d.A2, d.a2_sm, d.k1 = _p(A2), A2.stride(-2), k1
@@ -964,7 +968,11 @@ def mha_desc(x, Wq, bq, Wk, bk, Wv, bv, Wo, bo, heads: int, causal: bool, probs_
     d.probs_mask = _p(probs_mask)
     for f in ("q", "k", "v", "P", "Pd", "o", "y", "lse"):
         setattr(d, f, _p(saved.get(f)))
-    nbytes = int(_lib.load().sat_mha_scratch_bytes(B, L, d.D, heads, d.out_dim))
+    # the fused path (saved["lse"]: model.mha_fwd chose it under the library's flash_ok rule)
+    # needs no [B][H][L][L] score slab in either direction
+    size = (_lib.load().sat_mha_scratch_bytes_fused if saved.get("lse") is not None
+            else _lib.load().sat_mha_scratch_bytes)
+    nbytes = int(size(B, L, d.D, heads, d.out_dim))
     scratch = torch.empty(nbytes, dtype=torch.uint8, device=x.device)
     d.scratch, d.scratch_bytes = scratch.data_ptr(), nbytes
     ws = _gemm_ws(x.device)

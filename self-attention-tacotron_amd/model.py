@@ -89,7 +89,10 @@ def mha_fwd(x: torch.Tensor, P, scope: str, heads: int, causal: bool,
     s = dict(x=x, q=qkv[0], k=qkv[1], v=qkv[2], o=torch.empty(B, L, model, device=dev),
              y=torch.empty(B, L, out, device=dev), mask=probs_mask, heads=heads,
              dh=model // heads, causal=causal, scope=scope)
-    if K.flash_attn_ok(causal, model // heads, L) and not sv.get("keep_probs"):
+    # the same rule as the library's flash_ok (csrc/mha.hip): 16-byte operands, the probability
+    # mask included (a mask view at an unaligned arena offset takes the materialised path)
+    aligned = all(t is None or t.data_ptr() % 16 == 0 for t in (probs_mask, *qkv))
+    if aligned and K.flash_attn_ok(causal, model // heads, L) and not sv.get("keep_probs"):
         # the decoder head (causal, dh = 128) and the encoder's narrow heads: scores, softmax,
         # dropout and contexts fused per (utterance, head) -- only the row statistic is kept for
         # the backward (sv["keep_probs"]: the caller wants P itself, e.g. inference alignments)

@@ -73,7 +73,13 @@ class Trainer:
         if self.shape == (B, N, Tp):
             return
         self.specs = mask_specs(self.hp, B, N, Tp)
-        need = sum(int(np.prod(s.shape)) for s in self.specs)
+        # every mask starts on a 256-byte boundary (64 floats): the fused attention kernels take
+        # 16-byte-aligned operands only, and a segment packed right behind an odd-sized one
+        # (e.g. B * N odd) would otherwise start misaligned.  Each segment's draw depends only
+        # on its own stream id and index, so the padding changes no mask value.
+        def up(n: int) -> int:
+            return (n + 63) // 64 * 64
+        need = sum(up(int(np.prod(s.shape))) for s in self.specs)
         if need > self._mask_arena.numel():
             self._mask_arena = torch.empty(need, device=self.m.device)
         self.masks: Dict[str, torch.Tensor] = {}
@@ -85,7 +91,7 @@ class Trainer:
             keep = 1.0 - s.rate
             on = 1.0 / keep if s.kind == "dropout" else 1.0
             segs.append((off, n, i + 1, keep, on))
-            off += n
+            off += up(n)
         self._mask_segs = K.rng_segments(segs)
         self.shape = (B, N, Tp)
 

@@ -124,3 +124,21 @@ def test_model_fn_memory_flat_over_shapes(cuda):
     assert len(shapes) >= 6
     assert torch.cuda.memory_allocated() <= base + (1 << 20)
     assert len(model.engine._scratch) == 1
+
+
+def test_odd_rows_fused_attention_with_dropout(cuda):
+    """B * N odd with T' % 4 == 0 and dropout on (advisor r5): every mask view starts on a
+    16-byte boundary, so Python's and the library's fused-attention rules agree and the
+    training step takes the fused path without a refusal; the step is finite and replays."""
+    from sat_amd import train
+    hp, m, batch, tr = _setup(cuda, B=1, N=13, T=16, seed=5)
+    assert (batch["source"].shape[1] * 1) % 2 == 1 and (batch["mel"].shape[1] // 2) % 4 == 0
+    tr.reshape(1, batch["source"].shape[1], batch["mel"].shape[1] // 2)
+    assert all(v.data_ptr() % 16 == 0 for v in tr.masks.values())
+    tr.forward_backward(batch)
+    torch.cuda.synchronize()
+    sv = tr.last_saved
+    fused = [k for k, s in sv.items() if isinstance(s, dict) and s.get("lse") is not None]
+    assert fused, "no multi-head attention took the fused path"
+    assert np.isfinite(float(tr.last_loss.item()))
+    assert torch.isfinite(m.grads).all()

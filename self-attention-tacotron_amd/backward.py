@@ -42,10 +42,11 @@ class Aux:
         with torch.cuda.stream(self.s):
             fn()
 
-    def run_side(self, fn, *tensors):
-        """run a branch on a stream of its own (K.aux_stream index 2), forked here from the main
-        stream and joined with the others: it does not queue behind the aux backlog"""
-        s = K.aux_stream(self.dev, 2)
+    def run_side(self, fn, *tensors, which: int = 2):
+        """run a branch on a stream of its own (K.aux_stream index 2, or ``which``), forked here
+        from the main stream and joined with the others: it does not queue behind the aux
+        backlog"""
+        s = K.aux_stream(self.dev, which)
         s.wait_stream(torch.cuda.current_stream())
         if s not in self.used:
             self.used.append(s)
@@ -632,6 +633,9 @@ def encoder_bwd(P, G, hp, d, sv, dm1, dm2, lengths, masks, ws, aux: Aux = None):
     proj_later = (aux is not None and bank_fused(d, inp)
                   and os.environ.get("SAT_BANK_DW_SIDE", "1") == "1"
                   and os.environ.get("SAT_PROJ_DW_BANK", "1") == "1")
+    # SAT_PROJ_DW_SIDE2=1: those two products on a third side stream forked with the bank's
+    # (beside the bank dX and dW products) instead of queued behind the bank dW
+    proj_side2 = proj_later and os.environ.get("SAT_PROJ_DW_SIDE2", "0") == "1"
     later = []
 
     def proj_wgrad(fn, *tensors):
@@ -688,8 +692,12 @@ def encoder_bwd(P, G, hp, d, sv, dm1, dm2, lengths, masks, ws, aux: Aux = None):
                                           d.max_k, C, dW=_contig_span(G, kern), beta_dw=1.0)
         if aux is not None and os.environ.get("SAT_BANK_DW_SIDE", "1") == "1":
             side = (lambda: (bank_bias(), bank_dw())) if bias_side else bank_dw
-            aux.run_side((lambda: (side(), [f() for f in later])) if later else side,
-                         inp, dbank_pre)
+            if proj_side2 and later:
+                aux.run_side(side, inp, dbank_pre)
+                aux.run_side(lambda: [f() for f in later], which=3)
+            else:
+                aux.run_side((lambda: (side(), [f() for f in later])) if later else side,
+                             inp, dbank_pre)
         else:
             _wgrad(aux, bank_dw, inp, dbank_pre)
         K.conv_bank_bwd(inp, _contig_span(P, kern), dbank_pre, d.max_k, C, dx=dinp,
@@ -711,8 +719,16 @@ def encoder_bwd(P, G, hp, d, sv, dm1, dm2, lengths, masks, ws, aux: Aux = None):
     K.embedding_bwd(dx, sv["batch"]["source"], G["embedding"])
 
 
-def model_backward(P, G, hp, d, sv, ws, attn_tile=32, pipe: Pipeline = SEQUENTIAL):
-    """Accumulate dL/dparams of model_forward's loss into G (caller zeroes G)."""
+def model_backward(P, G, hp, d, sv, ws, attn_tile=32, pipe: Pipeline = SEQUENTIAL,
+                   on_decoder_grads=None):
+    """Accumulate dL/dparams of model_forward's loss into G (caller zeroes G).
+
+    ``on_decoder_grads(streams)``: called once every decoder-side gradient (the speaker
+    embedding, prenets, attention RNN and mechanisms, LSTM stack, head, projections -- the
+    arena's tail behind the encoder, ``Tacotron.decoder_grad_span``) has been ISSUED, before the
+    encoder's backward starts; ``streams`` are the streams that carry that work (the caller
+    waits on them, e.g. to all-reduce that bucket beside the encoder backward).  The encoder
+    backward writes only encoder / embedding rows (``encoder_bwd``)."""
     masks = sv["masks"]
     aux = Aux(sv["Z"].device) if sv["Z"].is_cuda else None
     dH2 = head_bwd(P, G, hp, d, sv, ws, aux=aux)
@@ -723,6 +739,9 @@ def model_backward(P, G, hp, d, sv, ws, attn_tile=32, pipe: Pipeline = SEQUENTIA
     lengths = sv["batch"]["source_length"]
     dm1 = K.seq_mask(dV1, lengths)
     dm2 = K.seq_mask(dV2, lengths)
+    if on_decoder_grads is not None:
+        on_decoder_grads([torch.cuda.current_stream()] + (list(aux.used) if aux is not None
+                                                          else []))
     if aux is not None and os.environ.get("SAT_AUX2") == "1":
         aux.switch()      # A/B: the encoder's weight-gradient branches on their own stream
     encoder_bwd(P, G, hp, d, sv, dm1, dm2, lengths, masks, ws, aux=aux)

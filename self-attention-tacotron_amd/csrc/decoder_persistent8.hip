@@ -11,8 +11,7 @@
 // per step.  Here group g = utterance g owns 8 workgroups (blockIdx = g + 32 j, one XCD under
 // the observed round-robin placement); workgroup j holds
 //   * LSTM units [32j, 32j+32): their 128 gate columns x 512 inputs in registers (128 per lane
-//     at 512 threads: lane l holds h rows 4l..4l+3 and c1 rows 4l..4l+3; the 32 c2 rows in
-//     LDS), and their 32 query rows (32 KB) in LDS;
+//     at 512 threads; the 32 c2 rows in LDS), and their 32 query rows (32 KB) in LDS;
 //   * memory positions [jP, jP+P), P = max(5, ceil(N/8)) <= 32: K1/V1/K2/V2 rows in LDS.
 // Per decoder step two 8-producer hand-offs of ~1.2 KB records, both data-tagged (every word
 // carries the step parity in its mantissa LSB, persistent.h lsb_tag):
@@ -20,11 +19,11 @@
 //   record B_t = {tile statistics (m1, z1, a1, m2, z2), unnormalised partial contexts (288),
 //                 the tile's first 5 / last 4 energies and last 2 alignments (the halos the
 //                 neighbours' location convolution and alignment recursion need)}.
-// Iteration t:  [B_{t-1}: staged; every lane combines the c_{t-1} dims its dot reads] -> LSTM
-// step t -> publish A_t -> [normalise s_{t-1}, alpha_{t-1} on the own positions, location
-// features, query-independent part of the energies -- all in the shadow of A_t's latency] ->
-// [A_t: q_t, h_t] -> energies, tile statistics, partial contexts -> publish B_t.
-// Four workgroup barriers per step: B staged, cell done, A staged, energies done.
+// Iteration t:  [B_{t-1}: combine c_{t-1}] -> LSTM step t (h part of the dot done at the end of
+// iteration t-1) -> publish A_t -> [normalise s_{t-1}, alpha_{t-1} on the own positions,
+// location features, query-independent part of the energies -- all in the shadow of A_t's
+// latency] -> [A_t: q_t, h_t] -> energies, tile statistics, partial contexts -> publish B_t ->
+// h part of step t+1's gate sums.
 // Consistency rule: every value that crosses a workgroup boundary is tagged when it is made and
 // its maker uses the tagged value too, so all readers (and the histories) see identical bits.
 // Every spin is bounded (persistent.h poll_give_up): a timeout raises err[0], later polls give
@@ -35,13 +34,34 @@
 #ifndef SAT_FWD8_TRACE
 #define SAT_FWD8_TRACE 0
 #endif
-// Settled variants (measured rounds 3-5), no longer switchable: the
-// normalise window's and the cell's history stores on wave 7, the energies' tanh argument
-// pre-scaled by 2 log2(e) (5.65 -> 5.58 us/step), the hand-off polls' first attempt branch-free
-// (5.44 -> 5.33), the h part of the gate sums inside the cell phase's dot (5.84 -> 5.78).
-// Round 6: the context combine moved into the lanes of the LSTM dot (section 2 of the loop) and
-// the normalise of step t-1 into the shadow of record A_t (section 4): one workgroup barrier and
-// one dependent phase fewer per step.
+#ifndef SAT_FWD8_NORM3
+#define SAT_FWD8_NORM3 1     // the normalise window's history stores on wave 7 (A/B switch)
+#endif
+#ifndef SAT_FWD8_HSTORE7
+#define SAT_FWD8_HSTORE7 1   // the cell's C0 / REC0 / H0RAW / G0 stores on wave 7 (A/B switch)
+#endif
+#ifndef SAT_FWD8_ESCALE
+// the energies' tanh argument pre-scaled: K + b1 + convb W_loc and the folded location weights
+// held x 2 log2(e) in LDS, so tanh(a + q) = 1 - 2 / (1 + exp2(fma(q, 2 log2 e, a'))) takes one
+// fma where the plain form took an add and a multiply (16 per lane per step): 5.65 -> 5.58 us
+// per step over three interleaved rounds on one box (profiles/r05_fwd8_ab.txt)
+#define SAT_FWD8_ESCALE 1
+#endif
+#ifndef SAT_FWD8_POLL1
+// the hand-off polls' first attempt branch-free: every lane issues its loads (clamped in-record
+// addresses for lanes without one), the tags are checked, and only a miss enters the retry
+// loop -- the first attempt succeeds on the critical path (trace: 0 spins), where the loop's
+// per-load exec-mask branches were ~30 branches + 150 scalar instructions of the staging phase
+#define SAT_FWD8_POLL1 1
+#endif
+#ifndef SAT_FWD8_HMERGE
+// the h part of the gate sums inside the cell phase's dot (one dot, one transpose-reduce) rather
+// than a separate h-dot after publishing record B: 5.84 -> 5.78 us/step (three interleaved
+// rounds on one box).  The separate h-dot was meant to hide in B's latency, but the group's
+// last publisher (whichever workgroup it is) never waits -- every other record is already
+// there when it polls -- so its h-dot sat on the group's period (0: the old placement, A/B)
+#define SAT_FWD8_HMERGE 1
+#endif
 
 namespace sat {
 namespace {
@@ -119,18 +139,20 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
   __shared__ float cw[kKW * kF + kF];
   // per step
   __shared__ __attribute__((aligned(16))) float hbuf[kU];        // h_t states (next LSTM input)
+  __shared__ __attribute__((aligned(16))) float cbuf[kC];        // c_{t-1}
   __shared__ __attribute__((aligned(16))) float4 qst[kW][64];    // staged query partials
   __shared__ __attribute__((aligned(16))) float4 recs[kW][kR4];  // staged records B_{t-1}
   __shared__ __attribute__((aligned(16))) float hst[kUW];        // own units' h_t (tagged)
   __shared__ __attribute__((aligned(16))) float hraw[kUW];       // own units' raw outputs
   __shared__ float cown[kUW];                                    // own units' c_t
   __shared__ __attribute__((aligned(16))) float4 gown[kUW];      // own units' gates (i, j, f, o)
+  __shared__ float gsum[8][64];             // h part of the gate sums (transpose-reduced)
   __shared__ float halo[12];                // e_{t-1} left 4 | right 5 ; alpha_{t-2} at n0-2, n0-1
   __shared__ float eown[kPmax], e2own[kPmax];
   __shared__ float alf[2][kPmax + 1];       // alf[t & 1][k] = alpha_{t-1} at n0 - 1 + k
   __shared__ float sp[kPmax + kKW];         // s_{t-1} on n0-4 .. n0+nt+4
   __shared__ __attribute__((aligned(16))) float wsc[8][2][kPmax];     // per-wave alignment weights
-  __shared__ long long tp[16];              // optional segment clocks of thread 0 (trace build)
+  __shared__ long long tp[16];              // optional segment clocks of thread 0
 
   const int tid0 = threadIdx.x;
   const int g = blockIdx.x % kGmax, j = blockIdx.x / kGmax;
@@ -140,8 +162,8 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
   const int n0 = j * P, nt = max(0, min(P, N - n0));
   const bool has_left = j > 0, has_right = j + 1 < kW && n0 + P < N;
   // wave 7 holds no energy positions when nt <= 28: it then stores the cell's histories in the
-  // energies phase (from LDS) instead of the cell lanes of every wave
-  const bool w7_stores = 4 * 7 >= nt;
+  // location-term phase (from LDS) instead of the cell lanes of every wave
+  const bool w7_stores = SAT_FWD8_HSTORE7 && 4 * 7 >= nt;
   const int64_t bN = (int64_t)b * N;
   const int len = (int)p.lengths[b];
   const float u = p.u;
@@ -149,15 +171,14 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
 
   // ---------------- prologue
   // LSTM: wave w owns gate columns 128j + 16w + m (m < 16: unit 32j + 4w + m/4, gate m%4);
-  // lane owns input rows 4 lane + i of h (chunk i < 4) and of c1 (chunk 4 + i): both are read
-  // as ONE float4 per lane (h from the staged A records, c1 combined in the lane itself from
-  // the staged B records); the 32 c2 rows sit in LDS (wc2).  W0r rows are [c1 | c2 | h].
+  // lane owns input rows: chunk i < 4 -> h row 64i + lane, 4 <= i < 8 -> c1 row 64(i-4) +
+  // lane; the 32 c2 rows sit in LDS (wc2).  W0r rows are [c1 | c2 | h].
   f2 w0[8][8];
   {
     const int lane = tid0 & 63, wave = tid0 >> 6;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      const int r = i < 4 ? kC + 4 * lane + i : 4 * lane + (i - 4);
+      const int r = i < 4 ? kC + 64 * i + lane : 64 * (i - 4) + lane;
       const float4* src = reinterpret_cast<const float4*>(p.W0r + (int64_t)r * (4 * kU) +
                                                           128 * j + 16 * wave);
 #pragma unroll
@@ -186,7 +207,7 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
     }
     const float kv = r >= nt ? 0.f : c < kD1 ? p.K1[(bN + n0 + r) * kD1 + c] + p.b1[c] + lb
                                             : p.K2[(bN + n0 + r) * kD2 + (c - kD1)];
-    kc[r][c] = kv * kTwoLog2e;
+    kc[r][c] = SAT_FWD8_ESCALE ? kv * kTwoLog2e : kv;
   }
   for (int i = tid0; i < kKW * kQ; i += kTh) {
     const int k = i / kQ, c = i - k * kQ;
@@ -195,7 +216,7 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
 #pragma unroll
       for (int f = 0; f < kF; ++f) a = fmaf(p.convW[k * kF + f], p.locW[f * kD1 + c], a);
     }
-    cwl[k][c] = a * kTwoLog2e;
+    cwl[k][c] = SAT_FWD8_ESCALE ? a * kTwoLog2e : a;
   }
   for (int i = tid0; i < kPmax * kM1 / 4; i += kTh) {
     const int r = i / (kM1 / 4), c4 = i - r * (kM1 / 4);
@@ -211,6 +232,7 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
   if (tid0 < kF) cw[kKW * kF + tid0] = p.convb[tid0];
   if (tid0 < kU) hbuf[tid0] = 0.f;                                  // h_{-1}
   if (tid0 < 16) tp[tid0] = 0;
+  gsum[tid0 >> 6][tid0 & 63] = 0.f;          // h_{-1} = 0: no h part at step 0
   // initial state rows (host): s_{-1} on the conv window, alpha_{-1} on n0-1 .. n0+nt-1
   // (tagged with step 0's bit: they travel in record B_0)
   if (tid0 < nt + kKW - 1) {
@@ -240,7 +262,7 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
 
   const bool xl = (p.flags & 1) ? xcd_local_group(p.XID, g, kGmax, kW, p.err) : false;
 
-#if SAT_FWD8_TRACE
+#if SAT_FWD8_TRACE || SAT_SEGMENT_CLOCKS
   long long t0 = p.prof ? wall_clock64() : 0;
   auto tick = [&](int seg) {
     if (p.prof && tid0 == 0) {
@@ -250,7 +272,7 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
     }
   };
 #else
-  auto tick = [](int) {};                   // production build: no clock reads, no flag tests
+  auto tick = [](int) {};   // production build: no clock reads and no per-phase flag tests
 #endif
   bool gave_up = false;
   // location features f_t of the own positions from s_{t-1} in sp (the BPTT's LOC history;
@@ -270,18 +292,14 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
     }
   };
   if ((tid0 >> 6) == 5) store_loc(0, tid0 & 63);   // f_0 from the initial state s_{-1}
-  // e_{t-1}(n) on the window around the own positions, -inf where masked (the own energies of
-  // step t-1 in eown until the energies phase of step t rewrites them; the neighbours' in halo)
-  auto e_at = [&](int n) -> float {
-    if (n < 0 || n >= len) return -INFINITY;
-    if (n < n0) return halo[n - n0 + kPadL];
-    if (n < n0 + nt) return eown[n - n0];
-    return halo[kPadL + (n - n0 - nt)];
-  };
 #if SAT_FWD8_TRACE
   // per-wave event clocks of workgroup 1 over steps 100..107: prof[4096 + ...] (build with
   // -DSAT_FWD8_TRACE=1; tools/probes/fwd8_profile.py prints them)
+  // (workgroup 1 = group 1's first: the per-wave stores must not perturb group 0, whose
+  // hand-off skew gevt measures)
   long long* evt = (p.prof && blockIdx.x == 1) ? p.prof + 256 * 16 : nullptr;
+  // group 0's eight workgroups, wave 0: {A published, A staged, B published, B staged} of steps
+  // 100..107 at prof[256 * 16 + 8 * 8 * 20 + ((t - 100) * 8 + j) * 4 + k] (hand-off skew)
   long long* gevt = (p.prof && g == 0) ? p.prof + 256 * 16 + 8 * 8 * 20 + j * 4 : nullptr;
 #endif
 
@@ -299,6 +317,7 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
       if (evt && t >= 100 && t < 108 && lane == 0) evt[((t - 100) * 8 + wave) * 16 + k] = wall_clock64();
       if (gevt && t >= 100 && t < 108 && tid == 0 && (k == 7 || k == 10 || k == 15 || k == 2)) {
         const int slot = k == 7 ? 0 : k == 10 ? 1 : k == 15 ? 2 : 3;
+        // B staged (k == 2) belongs to step t - 1's records
         const int ts = k == 2 ? t - 1 : t;
         if (ts >= 100) gevt[(ts - 100) * 32 + slot] = wall_clock64();
       }
@@ -307,10 +326,6 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
 #endif
     };
     ev(0);
-    // statistics of step t-1 (wave-uniform: readlane results) and the lane's contexts c_{t-1}
-    float M1 = 0.f, Z1 = 1.f, A1 = 1.f, M2 = 0.f, Z2 = 1.f;
-    float4 cv = make_float4(0.f, 0.f, 0.f, 0.f);
-    float c2v = 0.f;
     // ============ 1. records B_{t-1}: wave jj stages record jj (wave 0 lanes 16..26 the halos)
     if (t > 0) {
       const int rb0 = ((s & 1) * B + b) * kW;
@@ -328,16 +343,27 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
       const int hw = (rb0 + (hleft ? j - 1 : j + 1)) * kRB +
                      (hq < kPadL ? kRBet + hq : hq < kPadL + kPadR ? kRBeh + hq - kPadL
                                                                    : kRBal + hq - kPadL - kPadR);
-      // first attempt branch-free (every lane issues its loads; an absent neighbour's halo
-      // words stay 0), the retry loop only on a miss
-      float4 x1 = ldc4(rRB, (rec + kRBctx) / 4 + lane);
-      float4 x2 = ldc4(rRB, i2);               // (lanes >= 10: in-record words, unused)
-      const float h0 = ldc(rRB, hsrc ? hw : 0);
-      float hv = hsrc ? h0 : 0.f;
-      bool ok1 = tag_ok4(x1, want);
-      bool ok2 = !two || tag_ok4(x2, want);
-      bool ok3 = !hsrc || tag_ok(hv, want);
-      if (any_lane(!(ok1 && ok2 && ok3)) && !gave_up) {
+      float4 x1 = make_float4(0.f, 0.f, 0.f, 0.f), x2 = x1;
+      float hv = 0.f;
+      bool ok1 = false, ok2 = !two, ok3 = !hsrc;
+#if SAT_FWD8_TRACE
+      // trace build: drain the wave's own earlier stores first, then time the poll alone
+      const long long tq0 = wall_clock64();
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const long long tq1 = wall_clock64();
+#endif
+      bool retry = true;
+      if (SAT_FWD8_POLL1) {
+        x1 = ldc4(rRB, (rec + kRBctx) / 4 + lane);
+        x2 = ldc4(rRB, i2);                    // (lanes >= 10: in-record words, unused)
+        const float h0 = ldc(rRB, hsrc ? hw : 0);
+        hv = hsrc ? h0 : 0.f;                  // an absent neighbour's halo words stay 0
+        ok1 = tag_ok4(x1, want);
+        ok2 = ok2 || tag_ok4(x2, want);
+        ok3 = ok3 || tag_ok(hv, want);
+        retry = any_lane(!(ok1 && ok2 && ok3)) && !gave_up;
+      }
+      if (retry) {
         for (unsigned spins = 0;; ++spins) {
           if (!ok1) x1 = ldc4(rRB, (rec + kRBctx) / 4 + lane);
           if (!ok2) x2 = ldc4(rRB, i2);
@@ -350,107 +376,150 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
           __builtin_amdgcn_s_sleep(1);
         }
       }
+#if SAT_FWD8_TRACE
+      {
+        const long long tq2 = wall_clock64();
+        if (evt && t >= 100 && t < 108 && lane == 0) {
+          evt[8 * 8 * 16 + ((t - 100) * 8 + wave) * 4 + 0] = tq1 - tq0;
+          evt[8 * 8 * 16 + ((t - 100) * 8 + wave) * 4 + 1] = tq2 - tq1;
+        }
+      }
+#endif
       recs[wave][2 + lane] = x1;
       if (lane < kM2 / 4) recs[wave][2 + kM1 / 4 + lane] = x2;
       else if (two) recs[wave][lane - kM2 / 4] = x2;
       if (hl) halo[hq] = hv;
       tick(0);
-      ev(1);
+    ev(1);
       lds_barrier();
       tick(1);
-      ev(2);
-      // ============ 2. combine, in the lanes that use it: the record scales from lanes 0..7
-      //      (DPP, identical arithmetic in every wave and every workgroup of the group), then
-      //      each lane its own four c1 dims 4 lane .. 4 lane + 3 and c2 dim lane & 31 -- the
-      //      dot below reads them from registers, so no context buffer and no barrier sit
-      //      between the records and the LSTM step
-      const int jj = lane & 7;
-      const float4 st = recs[jj][0];
-      const float z2 = recs[jj][1].x;
-      M1 = lanes8_max(st.x);
-      M2 = lanes8_max(st.w);
-      const float sc1 = __expf(st.x - M1), sc2 = __expf(st.w - M2);
-      Z1 = lanes8_sum(st.y * sc1);
-      A1 = lanes8_sum(st.z * sc1);
-      Z2 = lanes8_sum(z2 * sc2);
-      const float* rf = reinterpret_cast<const float*>(&recs[0][0]);
-      const int r2 = lane & 31;
+    ev(2);
+      // combine: thread d < 288 one context dim; the record scales from lanes 0..7 of each
+      // wave (DPP, identical arithmetic in every workgroup of the group), broadcast by readlane.
+      // Waves 5 and 6 normalise step t-1 on the own positions meanwhile (the statistics
+      // formed the same way): s_{t-1} on the convolution window (the next energies' location
+      // term reads it) and alpha_{t-1} (tagged for record B_t) -- off the step's critical
+      // path, which used to run them after publishing A_t.
+      {
+        const int jj = lane & 7;
+        const float4 st = recs[jj][0];
+        const float z2 = recs[jj][1].x;
+        const float M1 = lanes8_max(st.x), M2 = lanes8_max(st.w);
+        const float sc1 = __expf(st.x - M1), sc2 = __expf(st.w - M2);
+        const float Z1 = lanes8_sum(st.y * sc1), A1 = lanes8_sum(st.z * sc1);
+        const float Z2 = lanes8_sum(z2 * sc2);
+        if (wave < (kC + 63) / 64) {
+          if (tid < kC) {
+            const bool first = wave < kM1 / 64;    // wave-uniform: c1 dims (waves 0..3) or c2
+            const float sc = first ? sc1 : sc2;
+            const float* rf = reinterpret_cast<const float*>(&recs[0][2]) + tid;
+            float a = 0.f;
 #pragma unroll
-      for (int k = 0; k < kW; ++k) {
-        const float4 r = recs[k][2 + lane];
-        const float s1 = rdl(sc1, k);
-        cv.x = fmaf(r.x, s1, cv.x); cv.y = fmaf(r.y, s1, cv.y);
-        cv.z = fmaf(r.z, s1, cv.z); cv.w = fmaf(r.w, s1, cv.w);
-        c2v = fmaf(rf[k * kR4 * 4 + 4 * (2 + kM1 / 4) + r2], rdl(sc2, k), c2v);
-      }
-      const float ia = __builtin_amdgcn_rcpf(A1);
-      cv.x *= ia; cv.y *= ia; cv.z *= ia; cv.w *= ia;
-      c2v *= __builtin_amdgcn_rcpf(Z2);
-      // the REC0 context row: each workgroup stores its own 36 dims (chunks 9j .. 9j + 8)
-      if (wave == kW - 1) {
-        float* row = p.REC0 + ((int64_t)t * B + b) * kK0;
-        if (lane >= 9 * j && lane < 9 * j + 9) reinterpret_cast<float4*>(row)[lane] = cv;
-        if (j == kW - 1 && lane < kM2) row[kM1 + lane] = c2v;
+            for (int k = 0; k < kW; ++k) a = fmaf(rf[k * kR4 * 4], rdl(sc, k), a);
+            a *= __builtin_amdgcn_rcpf(first ? A1 : Z2);
+            cbuf[tid] = a;
+            // the REC0 context row: every workgroup forms all 288 dims, each stores its own 36
+            // (the whole row from workgroup 0 alone put it a step-long offset behind its group)
+            if (tid / (kC / kW) == j) p.REC0[((int64_t)t * B + b) * kK0 + tid] = a;
+          }
+        } else {
+          const unsigned bit = lsb_tag(t);
+          auto e_at = [&](int n) -> float {       // e_{t-1}(n) on the window, -inf where masked
+            if (n < 0 || n >= len) return -INFINITY;
+            if (n < n0) return halo[n - n0 + kPadL];
+            if (n < n0 + nt) return eown[n - n0];
+            return halo[kPadL + (n - n0 - nt)];
+          };
+          if (wave == 5) {
+            // s_{t-1} = softmax on n0-4 .. n0+nt+4, then (same wave, no barrier) the location
+            // features f_t of the own positions for the LOC history of the BPTT
+            if (lane < nt + kKW - 1) {
+              const float e = e_at(n0 - kPadL + lane);
+              const float sv = e == -INFINITY ? 0.f : __expf(e - M1) * __builtin_amdgcn_rcpf(Z1);
+              sp[lane] = sv;
+              if (!SAT_FWD8_NORM3 && lane >= kPadL && lane < nt + kPadL)
+                p.S1[((int64_t)t * B + b) * N + n0 + lane - kPadL] = sv;
+            }
+            if (t < T && 4 * 7 < nt) {         // no idle energy wave (N > 224): here
+              asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+              store_loc(t, lane);
+            }
+          } else if (wave == 6) {
+            const float* ap = alf[(t - 1) & 1];      // alpha_{t-2} at n0-1+k
+            if (lane <= nt) {
+              const int k = lane, n = n0 - 1 + k;
+              float av = 0.f;
+              if (n >= 0) {
+                // alpha_{t-2} at n and n-1: own from ap, n0-1 / n0-2 from the left halo
+                const float a_n = k >= 1 ? ap[k] : halo[kPadL + kPadR + 1];
+                const float a_m = k >= 2 ? ap[k - 1] : halo[kPadL + kPadR + k];
+                const float e = e_at(n);
+                const float pe = e == -INFINITY ? 0.f : __expf(e - M1);
+                av = ((1.f - u) * a_n + u * a_m + 1e-7f) * pe * __builtin_amdgcn_rcpf(A1);
+              }
+              const float at = tagf(av, bit);
+              alf[t & 1][k] = at;
+              if (k >= 1) p.AL1[((int64_t)t * B + b) * N + n] = at;
+            }
+          }
+          // wave 7 (idle in this window): the S1 / S2 / ST history stores (S1 recomputed with
+          // wave 5's arithmetic: the same bits), off waves 5 and 6 whose LDS results the next
+          // phases wait for
+          if (SAT_FWD8_NORM3 ? wave == 7 : wave == 6) {
+            if (SAT_FWD8_NORM3 && lane >= kPadL && lane < nt + kPadL) {
+              const float e = e_at(n0 - kPadL + lane);
+              p.S1[((int64_t)t * B + b) * N + n0 + lane - kPadL] =
+                  e == -INFINITY ? 0.f : __expf(e - M1) * __builtin_amdgcn_rcpf(Z1);
+            }
+            if (lane < nt) {
+              const float e2 = e2own[lane];
+              p.S2[((int64_t)s * B + b) * N + n0 + lane] =
+                  e2 == -INFINITY ? 0.f : __expf(e2 - M2) * __builtin_amdgcn_rcpf(Z2);
+            }
+            if (j == 0 && lane == 0) {
+              float* stp = p.ST + ((int64_t)s * B + b) * 4;
+              stp[0] = M1; stp[1] = Z1; stp[2] = A1 / Z1; stp[3] = Z2;
+            }
+          }
+        }
       }
     }
     tick(2);
     ev(3);
+    lds_barrier();
+    tick(3);
+    ev(4);
 
-    if (t == T) {
-      // the histories of the last attention step: alpha_{T-1} (wave 6), s_{T-1}, s2, the
-      // statistics (wave 7) -- the normalise roles of section 4 below
-      if (wave == 6 && lane <= nt) {
-        const float* ap = alf[(t - 1) & 1];
-        const int k = lane, n = n0 - 1 + k;
-        if (n >= 0) {
-          const float a_n = k >= 1 ? ap[k] : halo[kPadL + kPadR + 1];
-          const float a_m = k >= 2 ? ap[k - 1] : halo[kPadL + kPadR + k];
-          const float e = e_at(n);
-          const float pe = e == -INFINITY ? 0.f : __expf(e - M1);
-          const float av = ((1.f - u) * a_n + u * a_m + 1e-7f) * pe * __builtin_amdgcn_rcpf(A1);
-          if (k >= 1) p.AL1[((int64_t)t * B + b) * N + n] = tagf(av, lsb_tag(t));
-        }
-      }
-      if (wave == 7) {
-        if (lane >= kPadL && lane < nt + kPadL) {
-          const float e = e_at(n0 - kPadL + lane);
-          p.S1[((int64_t)t * B + b) * N + n0 + lane - kPadL] =
-              e == -INFINITY ? 0.f : __expf(e - M1) * __builtin_amdgcn_rcpf(Z1);
-        }
-        if (lane < nt) {
-          const float e2 = e2own[lane];
-          p.S2[((int64_t)s * B + b) * N + n0 + lane] =
-              e2 == -INFINITY ? 0.f : __expf(e2 - M2) * __builtin_amdgcn_rcpf(Z2);
-        }
-        if (j == 0 && lane == 0) {
-          float* stp = p.ST + ((int64_t)s * B + b) * 4;
-          stp[0] = M1; stp[1] = Z1; stp[2] = A1 / Z1; stp[3] = Z2;
-        }
-      }
-      break;
-    }
-
-    // ============ 3. LSTM step t: [h_{t-1} | c_{t-1}] dot (h staged with records A_{t-1}, c
-    //                 from the registers above), gates (one activation per lane), cell;
+    // ============ 2. LSTM step t: c part of the dot, gates (one activation per lane), cell;
     //                 publish record A_t
-    {
+    if (t < T) {
       f2 acc[8];
 #pragma unroll
       for (int q = 0; q < 8; ++q) acc[q] = f2{0.f, 0.f};
       if (t > 0) {
-        const float4 h4 = *reinterpret_cast<const float4*>(&hbuf[4 * lane]);
-        const float xs[8] = {h4.x, h4.y, h4.z, h4.w, cv.x, cv.y, cv.z, cv.w};
+#if SAT_FWD8_HMERGE
+        // h_{t-1} (staged with records A_{t-1}) and c_{t-1} in ONE dot and ONE transpose-reduce
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const f2 xx = {xs[i], xs[i]};
+        for (int i = 0; i < 4; ++i) {
+          const float xv = hbuf[64 * i + lane];
+          const f2 xx = {xv, xv};
+#pragma unroll
+          for (int q = 0; q < 8; ++q) acc[q] = __builtin_elementwise_fma(xx, w0[i][q], acc[q]);
+        }
+#endif
+#pragma unroll
+        for (int i = 4; i < 8; ++i) {
+          const float xv = cbuf[64 * (i - 4) + lane];
+          const f2 xx = {xv, xv};
 #pragma unroll
           for (int q = 0; q < 8; ++q) acc[q] = __builtin_elementwise_fma(xx, w0[i][q], acc[q]);
         }
         // c2 rows from LDS: lane l takes row l & 31 and columns 8 (l >> 5) .. + 7
-        const int hsel = lane >> 5;
-        const f2 xx = {c2v, c2v};
-        const float4 wa = *reinterpret_cast<const float4*>(&wc2[lane & 31][16 * wave + 8 * hsel]);
-        const float4 wb = *reinterpret_cast<const float4*>(&wc2[lane & 31][16 * wave + 8 * hsel + 4]);
+        const int r2 = lane & 31, hsel = lane >> 5;
+        const float xv = cbuf[kM1 + r2];
+        const f2 xx = {xv, xv};
+        const float4 wa = *reinterpret_cast<const float4*>(&wc2[r2][16 * wave + 8 * hsel]);
+        const float4 wb = *reinterpret_cast<const float4*>(&wc2[r2][16 * wave + 8 * hsel + 4]);
         const f2 c0 = __builtin_elementwise_fma(xx, f2{wa.x, wa.y}, f2{0.f, 0.f});
         const f2 c1 = __builtin_elementwise_fma(xx, f2{wa.z, wa.w}, f2{0.f, 0.f});
         const f2 c2 = __builtin_elementwise_fma(xx, f2{wb.x, wb.y}, f2{0.f, 0.f});
@@ -465,7 +534,11 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
       // lane holds column m = lane >> 2: activation of its gate (i, f, o sigmoid; j tanh via
       // 2 sigm(2x) - 1; forget_bias 1.0), then the cell lane (16q) gathers its unit's 4 gates
       const int gate = (lane >> 2) & 3;
+#if SAT_FWD8_HMERGE
       const float pre = v[0] + xgn;
+#else
+      const float pre = v[0] + gsum[wave][lane] + xgn;
+#endif
       const float sg = sigm_fast(gate == 1 ? 2.f * pre : pre + (gate == 2 ? 1.0f : 0.f));
       const float act = gate == 1 ? fmaf(2.f, sg, -1.f) : sg;
       const float gj = dpp_mov<0x104>(act);        // row_shl:4, 8, 12
@@ -497,10 +570,10 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
       }
       load_ops(t + 1, lane, wave, xgn, mcn, mhn);
       tick(4);
-      ev(5);
+    ev(5);
       lds_barrier();
       tick(5);
-      ev(6);
+    ev(6);
       // query partial over the own 32 units: wave w owns query columns 32w .. 32w+31; lane l
       // column 32w + (l & 31), units 16 (l >> 5) .. + 15; halves folded, quads gathered
       {
@@ -521,68 +594,20 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
           stc4x(xl, rRA, (ra + kQ) / 4 + lane, *reinterpret_cast<const float4*>(&hst[4 * lane]));
       }
       tick(6);
-      ev(7);
+    ev(7);
     }
+
+    if (t == T) break;
     tick(7);
     ev(8);
 
-    // ============ 4. in the shadow of record A_t's round trip: normalise step t-1 where it is
-    //      used (each energy wave s_{t-1} on its own location window, wave 6 alpha_{t-1},
-    //      wave 7 the whole window and the histories), then the query-independent energy part
-    //      a = K + b1 + convb W_loc + sum_k s_{t-1}[n-4+k] (W_conv[k] W_loc) -- the location
-    //      convolution and layer folded into one 10-tap product (modules/forward_attention.py:98-101)
+    // ============ 4. the query-independent energy part of step t (s_{t-1} came from wave 5
+    //                 before the last barrier): a = K + b1 + convb W_loc + sum_k s_{t-1}[n-4+k]
+    //                 (W_conv[k] W_loc) -- the location convolution and layer folded into one
+    //                 10-tap product (modules/forward_attention.py:98-101)
     // energy role: lane = dim chunk c (4 dims of [D1 | D2]), wave = positions 4w .. 4w+3
-    const bool epos = 4 * wave < nt;
-    if (t > 0) {
-      const float iz1 = __builtin_amdgcn_rcpf(Z1);
-      if (wave == 7) {
-        // the whole window (the LOC history reads it), then the S1 / S2 / ST histories
-        if (lane < nt + kKW - 1) {
-          const float e = e_at(n0 - kPadL + lane);
-          const float sv = e == -INFINITY ? 0.f : __expf(e - M1) * iz1;
-          sp[lane] = sv;
-          if (lane >= kPadL && lane < nt + kPadL)
-            p.S1[((int64_t)t * B + b) * N + n0 + lane - kPadL] = sv;
-        }
-        if (lane < nt) {
-          const float e2 = e2own[lane];
-          p.S2[((int64_t)s * B + b) * N + n0 + lane] =
-              e2 == -INFINITY ? 0.f : __expf(e2 - M2) * __builtin_amdgcn_rcpf(Z2);
-        }
-        if (j == 0 && lane == 0) {
-          float* stp = p.ST + ((int64_t)s * B + b) * 4;
-          stp[0] = M1; stp[1] = Z1; stp[2] = A1 / Z1; stp[3] = Z2;
-        }
-      } else if (epos && lane < 4 + kKW - 1) {
-        // the 13 window entries this wave's location term reads (identical bits to wave 7's)
-        const int w = 4 * wave + lane;
-        if (w < nt + kKW - 1) {
-          const float e = e_at(n0 - kPadL + w);
-          sp[w] = e == -INFINITY ? 0.f : __expf(e - M1) * iz1;
-        }
-      }
-      if (wave == 6 && lane <= nt) {
-        // alpha_{t-1} on the own positions (tagged: record B_t's halo and the statistics'
-        // weights read it), from alpha_{t-2} (own, and the left neighbour's last two)
-        const float* ap = alf[(t - 1) & 1];
-        const int k = lane, n = n0 - 1 + k;
-        float av = 0.f;
-        if (n >= 0) {
-          const float a_n = k >= 1 ? ap[k] : halo[kPadL + kPadR + 1];
-          const float a_m = k >= 2 ? ap[k - 1] : halo[kPadL + kPadR + k];
-          const float e = e_at(n);
-          const float pe = e == -INFINITY ? 0.f : __expf(e - M1);
-          av = ((1.f - u) * a_n + u * a_m + 1e-7f) * pe * __builtin_amdgcn_rcpf(A1);
-        }
-        const float at = tagf(av, lsb_tag(t));
-        alf[t & 1][k] = at;
-        if (k >= 1) p.AL1[((int64_t)t * B + b) * N + n] = at;
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the wave's own sp writes
-      if (wave == 7 && t < T) store_loc(t, lane);
-    }
     float4 Lr[4];
-    if (epos) {
+    if (4 * wave < nt) {
       const int c = lane;
 #pragma unroll
       for (int i = 0; i < 4; ++i) Lr[i] = *reinterpret_cast<const float4*>(&kc[4 * wave + i][4 * c]);
@@ -605,11 +630,22 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
       const unsigned want = lsb_tag(t);
       const int ra = (((t & 1) * B + b) * kW + wave) * kRA;
       const bool two = lane < kUW / 4;
-      float4 x1 = ldc4(rRA, ra / 4 + lane);
-      float4 x2 = ldc4(rRA, (ra + kQ) / 4 + (two ? lane : 0));
-      bool ok1 = tag_ok4(x1, want);
-      bool ok2 = !two || tag_ok4(x2, want);
-      if (any_lane(!(ok1 && ok2)) && !gave_up) {
+      float4 x1 = make_float4(0.f, 0.f, 0.f, 0.f), x2 = x1;
+      bool ok1 = false, ok2 = !two;
+#if SAT_FWD8_TRACE
+      const long long tq0 = wall_clock64();
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const long long tq1 = wall_clock64();
+#endif
+      bool retry = true;
+      if (SAT_FWD8_POLL1) {
+        x1 = ldc4(rRA, ra / 4 + lane);
+        x2 = ldc4(rRA, (ra + kQ) / 4 + (two ? lane : 0));
+        ok1 = tag_ok4(x1, want);
+        ok2 = ok2 || tag_ok4(x2, want);
+        retry = any_lane(!(ok1 && ok2)) && !gave_up;
+      }
+      if (retry) {
         for (unsigned spins = 0;; ++spins) {
           if (!ok1) x1 = ldc4(rRA, ra / 4 + lane);
           if (!ok2) x2 = ldc4(rRA, (ra + kQ) / 4 + lane);
@@ -620,6 +656,15 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
           __builtin_amdgcn_s_sleep(1);
         }
       }
+#if SAT_FWD8_TRACE
+      {
+        const long long tq2 = wall_clock64();
+        if (evt && t >= 100 && t < 108 && lane == 0) {
+          evt[8 * 8 * 16 + ((t - 100) * 8 + wave) * 4 + 2] = tq1 - tq0;
+          evt[8 * 8 * 16 + ((t - 100) * 8 + wave) * 4 + 3] = tq2 - tq1;
+        }
+      }
+#endif
       qst[wave][lane] = x1;
       if (two) reinterpret_cast<float4*>(hbuf)[(kUW / 4) * wave + lane] = x2;   // units 32 jj + 4 lane
     }
@@ -630,7 +675,7 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
     ev(11);
 
     // ============ 6. energies: q chunk summed per lane (record order), tanh, dots with v
-    if (epos) {
+    if (4 * wave < nt) {
       const unsigned bit = lsb_tag(t);
       const int c = lane;
       float4 q = qst[0][c];
@@ -644,12 +689,16 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int r = 4 * wave + i;
-        // tanh(a + q) from a' = 2 log2(e) a: 1 - 2 / (1 + exp2(fma(q, 2 log2 e, a')))
-        auto tz = [](float a2, float qv) {
+#if SAT_FWD8_ESCALE
+        auto tz = [](float a2, float qv) {        // tanh(a + q) from a' = 2 log2(e) a
           return fmaf(-2.f, __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(fmaf(qv, kTwoLog2e, a2))), 1.f);
         };
         const float4 z = make_float4(tz(Lr[i].x, q.x), tz(Lr[i].y, q.y), tz(Lr[i].z, q.z),
                                      tz(Lr[i].w, q.w));
+#else
+        const float4 z = make_float4(tanh_fast(Lr[i].x + q.x), tanh_fast(Lr[i].y + q.y),
+                                     tanh_fast(Lr[i].z + q.z), tanh_fast(Lr[i].w + q.w));
+#endif
         float a = v4.x * z.x;
         a = fmaf(v4.y, z.y, a); a = fmaf(v4.z, z.z, a); a = fmaf(v4.w, z.w, a);
         e[i] = d1 ? a : 0.f;
@@ -676,16 +725,19 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
         for (int k = 1; k < kW; ++k) q = add4(q, qst[k][lane]);
         reinterpret_cast<float4*>(p.Q + ((int64_t)t * B + b) * kQ)[lane] = q;
       }
-      if (wave == 7 && w7_stores && lane < kUW) {
-        // the cell's histories of step t for the own 32 units (in LDS since the cell
-        // barrier; rewritten only by step t+1's cell): one coalesced store each instead of
-        // four scattered ones per cell lane of every wave
-        const int cunit = kUW * j + lane;
-        const int64_t tbu = ((int64_t)t * B + b) * kU + cunit;
-        p.C0[((int64_t)(t + 1) * B + b) * kU + cunit] = cown[lane];
-        p.REC0[((int64_t)(t + 1) * B + b) * kK0 + kC + cunit] = hst[lane];
-        p.H0RAW[tbu] = hraw[lane];
-        reinterpret_cast<float4*>(p.G0)[tbu] = gown[lane];
+      if (wave == 7) {
+        store_loc(t, lane);                    // the LOC history, off the critical path
+        if (w7_stores && lane < kUW) {
+          // the cell's histories of step t for the own 32 units (in LDS since the cell
+          // barrier; rewritten only by step t+1's cell): one coalesced store each instead of
+          // four scattered ones per cell lane of every wave
+          const int cunit = kUW * j + lane;
+          const int64_t tbu = ((int64_t)t * B + b) * kU + cunit;
+          p.C0[((int64_t)(t + 1) * B + b) * kU + cunit] = cown[lane];
+          p.REC0[((int64_t)(t + 1) * B + b) * kK0 + kC + cunit] = hst[lane];
+          p.H0RAW[tbu] = hraw[lane];
+          reinterpret_cast<float4*>(p.G0)[tbu] = gown[lane];
+        }
       }
     }
     tick(11);
@@ -758,8 +810,27 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
     }
     tick(14);
     ev(15);
+    // ============ 7. h part of step t+1's gate sums (h_t arrived with records A_t)
+    if (!SAT_FWD8_HMERGE && t + 1 < T) {
+      f2 acc[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) acc[q] = f2{0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float xv = hbuf[64 * i + lane];
+        const f2 xx = {xv, xv};
+#pragma unroll
+        for (int q = 0; q < 8; ++q) acc[q] = __builtin_elementwise_fma(xx, w0[i][q], acc[q]);
+      }
+      float v[16];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) { v[2 * q] = acc[q].x; v[2 * q + 1] = acc[q].y; }
+      transpose_reduce16(v, lane);
+      gsum[wave][lane] = v[0];                    // own wave's slot: no barrier needed
+    }
+    tick(15);
   }
-#if SAT_FWD8_TRACE
+#if SAT_FWD8_TRACE || SAT_SEGMENT_CLOCKS
   if (p.prof && tid0 == 0)
     for (int i = 0; i < 16; ++i) p.prof[blockIdx.x * 16 + i] = tp[i];
 #endif

@@ -17,6 +17,12 @@ constexpr int kWave = 64;
 // thread-local last error (sat_last_error_string)
 void set_error(const char* fmt, ...);
 
+// Segment clocks of the persistent kernels (the `prof` descriptors' buffers): compiled in only
+// for instrumented builds (make EXTRA=-DSAT_SEGMENT_CLOCKS=1 BUILD=build_clk OUT=...); the
+// production build carries neither the clock reads nor the per-phase flag tests
+#ifndef SAT_SEGMENT_CLOCKS
+#define SAT_SEGMENT_CLOCKS 0
+#endif
 #define SAT_CHECK_ARG(cond, ...)                                                            \
   do {                                                                                      \
     if (!(cond)) {                                                                          \

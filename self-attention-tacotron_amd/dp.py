@@ -44,8 +44,23 @@ def allreduce_grads(flat: torch.Tensor, group=None) -> None:
         tdist.all_reduce(flat, op=tdist.ReduceOp.SUM, group=group)
 
 
+def _active(group, force: bool) -> bool:
+    return world_size(group) > 1 or (force and is_distributed(group))
+
+
+def exchange_bucket(arena: torch.Tensor, lo: int, hi: int, group=None,
+                    force: bool = False) -> None:
+    """The bucketed exchange's first collective: SUM all-reduce of ``arena[lo:hi]`` -- the
+    decoder's gradient rows, final once the decoder backward is done, reduced (on a stream of
+    the caller's) while the encoder backward runs.  Plain gradients: no pack / unpack; the
+    rest of the arena follows in ``exchange(..., done=(lo, hi))``."""
+    if not _active(group, force):
+        return
+    tdist.all_reduce(arena[lo:hi], op=tdist.ReduceOp.SUM, group=group)
+
+
 def exchange(arena: torch.Tensor, health: torch.Tensor, bn: torch.Tensor, tail: torch.Tensor,
-             group=None, force: bool = False) -> None:
+             group=None, force: bool = False, done=None) -> None:
     """A replica's whole per-step exchange as ONE SUM all-reduce over the contiguous arena
     ``[gradients | bn | tail]`` (``bn`` and ``tail`` are views of it):
 
@@ -59,10 +74,25 @@ def exchange(arena: torch.Tensor, health: torch.Tensor, bn: torch.Tensor, tail: 
     launches; the host arithmetic below is the same restatement for the ``gloo`` CPU tests.
 
     ``force`` runs the whole exchange (pack, collective, unpack) even in a one-rank group, where
-    it is the identity: the GPU tests drive the RCCL path that way on a one-GPU box."""
+    it is the identity: the GPU tests drive the RCCL path that way on a one-GPU box.
+
+    ``done = (lo, hi)``: that gradient range was reduced already (``exchange_bucket``); the
+    rest -- ``arena[:lo]`` and ``arena[hi:]`` (BN statistics and health tail included) -- is
+    reduced here as two collectives.  Every element is the same rank-ordered SUM either way
+    (bitwise equal to the single collective at world 2; at larger worlds the ring's per-chunk
+    summation order may differ in the last bit)."""
     w = world_size(group)
-    if w == 1 and not (force and is_distributed(group)):
+    if not _active(group, force):
         return
+
+    def reduce_all():
+        if done is None:
+            tdist.all_reduce(arena, op=tdist.ReduceOp.SUM, group=group)
+            return
+        lo, hi = done
+        if lo > 0:
+            tdist.all_reduce(arena[:lo], op=tdist.ReduceOp.SUM, group=group)
+        tdist.all_reduce(arena[hi:], op=tdist.ReduceOp.SUM, group=group)
     if arena.is_cuda:
         from . import _lib
         from . import kernels as K
@@ -70,13 +100,13 @@ def exchange(arena: torch.Tensor, health: torch.Tensor, bn: torch.Tensor, tail: 
         _lib.check(lib.sat_exchange_pack(health.data_ptr(), health.numel(), bn.data_ptr(),
                                          bn.numel(), tail.data_ptr(), 1.0 / w, K._stream()),
                    "sat_exchange_pack")
-        tdist.all_reduce(arena, op=tdist.ReduceOp.SUM, group=group)
+        reduce_all()
         _lib.check(lib.sat_exchange_unpack(tail.data_ptr(), health.numel(), health.data_ptr(),
                                            K._stream()), "sat_exchange_unpack")
         return
     tail[:health.numel()].copy_(health.abs().float())
     bn.mul_(1.0 / w)
-    tdist.all_reduce(arena, op=tdist.ReduceOp.SUM, group=group)
+    reduce_all()
     health.copy_(tail[:health.numel()].to(torch.int32))
 
 

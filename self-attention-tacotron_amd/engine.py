@@ -86,11 +86,20 @@ class Tacotron:
             from ._lib import SatLibraryError
             raise SatLibraryError("training step unhealthy: " + "; ".join(bad))
 
-    def backward(self, saved, zero: bool = True):
+    def backward(self, saved, zero: bool = True, on_decoder_grads=None):
         if zero:
             K.fill_(self.grads)
         model_backward(self.P, self.G, self.hp, self.d, saved, self.ws, attn_tile=self.attn_tile,
-                       pipe=self.pipe)
+                       pipe=self.pipe, on_decoder_grads=on_decoder_grads)
+
+    def decoder_grad_span(self):
+        """(lo, hi) of the gradient arena rows the decoder's backward writes: every parameter
+        after the encoder's (params.param_specs order: embedding, encoder/..., then
+        [speaker_embedding,] decoder/...), a contiguous 256-byte-aligned tail of the gradients.
+        The first bucket of the bucketed data-parallel exchange (train.Trainer)."""
+        first = next(p.name for p in self.layout.specs
+                     if p.name != "embedding" and not p.name.startswith("encoder/"))
+        return self.layout.offsets[first], self.params.numel()
 
     # ------------------------------------------------------------------ host views
     def params_dict(self) -> Dict[str, np.ndarray]:

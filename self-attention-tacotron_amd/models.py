@@ -25,6 +25,7 @@ LJSpeech/VCTK), as device tensors or numpy arrays.
 
 from __future__ import annotations
 
+import os
 from collections import namedtuple
 from typing import Dict, Optional
 
@@ -34,7 +35,7 @@ import torch
 from . import dp
 from . import params as PR
 from .engine import Tacotron
-from .train import Trainer
+from .train import StepGraphCache, Trainer
 
 
 class ModeKeys:
@@ -120,12 +121,63 @@ def _to_device(x, dev, dtype):
     return torch.as_tensor(np.asarray(x), dtype=dtype, device=dev)
 
 
+class _PinnedStager:
+    """Host -> device upload of a batch without a host-side wait.  A pageable ``as_tensor(...,
+    device=)`` blocks the host until the stream has drained (a synchronous copy), so the next
+    step's launches only start once the GPU is idle.  Here each array is packed into a pinned
+    buffer and copied with ``non_blocking=True`` in stream order; buffers rotate over a small
+    ring and a slot is rewritten only after the copy that last read it has finished (its event),
+    so the host runs ahead of the device by up to ``depth`` batches."""
+
+    def __init__(self, depth: int = 3):
+        self.depth = depth
+        self.slots = [dict() for _ in range(depth)]     # name -> pinned uint8 buffer
+        self.events = [None] * depth
+        self.i = 0
+
+    def upload(self, arrays, dev, dtypes):
+        """arrays: name -> numpy / tensor; dtypes: name -> torch dtype.  Returns device tensors."""
+        if not torch.cuda.is_available() or torch.device(dev).type != "cuda":
+            return {k: _to_device(v, dev, dtypes[k]) for k, v in arrays.items()}
+        slot, ev = self.slots[self.i], self.events[self.i]
+        if ev is not None:
+            ev.synchronize()                             # that slot's last copy is done
+        out = {}
+        for k, v in arrays.items():
+            if isinstance(v, torch.Tensor) and v.is_cuda:
+                out[k] = v.to(dtype=dtypes[k])
+                continue
+            h = torch.as_tensor(np.ascontiguousarray(np.asarray(v))).to(dtypes[k])
+            nb = h.numel() * h.element_size()
+            buf = slot.get(k)
+            if buf is None or buf.numel() < nb:
+                buf = torch.empty(max(nb, 1), dtype=torch.uint8, pin_memory=True)
+                slot[k] = buf
+            pin = buf[:nb].view(h.dtype).view(h.shape)
+            pin.copy_(h)
+            out[k] = torch.empty(h.shape, dtype=h.dtype, device=dev)
+            out[k].copy_(pin, non_blocking=True)
+        e = torch.cuda.Event()
+        e.record()
+        self.events[self.i] = e
+        self.i = (self.i + 1) % self.depth
+        return out
+
+
 class DualSourceSelfAttentionTacotronModel:
     """Estimator-shaped model (models/models.py:20-320) over the libsat_hip engine."""
 
     def __init__(self, params, model_dir=None, config=None, warm_start_from=None,
                  device="cuda", seed: int = 1234,
-                 init_values: Optional[Dict[str, np.ndarray]] = None):
+                 init_values: Optional[Dict[str, np.ndarray]] = None,
+                 graph_cache: Optional[int] = None, graph_t_quantum: Optional[int] = None):
+        """``graph_cache``: captured training steps kept per padded batch shape (LRU; 0 = every
+        TRAIN step eager; default SAT_GRAPH_CACHE or 0); ``graph_t_quantum``: pad T' to a
+        multiple of it before the lookup (default SAT_GRAPH_T_QUANTUM or 0 = exact shapes;
+        train.StepGraphCache).  Default eager: with the pinned asynchronous upload the eager
+        drop-in path keeps the GPU busy (its host issue runs ahead of the device), and it
+        measured as fast as the cache's steady state over ragged LJSpeech-like batches (bench
+        ``drop_in_ragged_ljs``), without the cache's first-sighting capture cost."""
         encoder_factory(params, True)                        # name checks, as the reference
         if params.decoder not in ("DualSourceDecoder", "DualSourceTransformerDecoder"):
             raise AssertionError(f"decoder must be a dual-source decoder: {params.decoder}")
@@ -143,6 +195,12 @@ class DualSourceSelfAttentionTacotronModel:
         dp.broadcast_params(self.engine.params)
         dp.broadcast_params(self.engine.bn.buf)
         self._trainer: Optional[Trainer] = None
+        self._graphs: Optional[StepGraphCache] = None
+        self._stager = _PinnedStager()
+        env = os.environ.get
+        self.graph_cache = int(env("SAT_GRAPH_CACHE", "0") if graph_cache is None else graph_cache)
+        self.graph_t_quantum = int(env("SAT_GRAPH_T_QUANTUM", "0") if graph_t_quantum is None
+                                   else graph_t_quantum)
         # dropout / zoneout masks differ per replica (each rank's shard is its own batch)
         self._seed = seed + 1000003 * dp.rank()
         self._eval_decoder = None
@@ -159,18 +217,16 @@ class DualSourceSelfAttentionTacotronModel:
         codes = labels.codes if hasattr(labels, "codes") else labels.mel
         cmask = (labels.code_loss_mask if hasattr(labels, "code_loss_mask")
                  else labels.spec_loss_mask)
-        b = {"source": _to_device(features.source, dev, torch.int64),
-             "source_length": _to_device(features.source_length, dev, torch.int64),
-             "mel": _to_device(codes, dev, torch.float32),
-             "mel_mask": _to_device(cmask, dev, torch.float32),
-             "done": _to_device(labels.done, dev, torch.float32),
-             "done_mask": _to_device(labels.binary_loss_mask, dev, torch.float32),
-             "target_length": _to_device(labels.target_length, dev, torch.int64)}
+        arrays = {"source": features.source, "source_length": features.source_length,
+                  "mel": codes, "mel_mask": cmask, "done": labels.done,
+                  "done_mask": labels.binary_loss_mask, "target_length": labels.target_length}
         if self.params.use_speaker_embedding:                 # models/models.py:69-70
             if getattr(features, "speaker_id", None) is None:
                 raise ValueError("use_speaker_embedding=True needs features.speaker_id")
-            b["speaker_id"] = _to_device(features.speaker_id, dev, torch.int64)
-        return b
+            arrays["speaker_id"] = features.speaker_id
+        i64 = ("source", "source_length", "target_length", "speaker_id")
+        dtypes = {k: torch.int64 if k in i64 else torch.float32 for k in arrays}
+        return self._stager.upload(arrays, dev, dtypes)
 
     def _get_trainer(self, batch) -> Trainer:
         """ONE trainer (one optimiser state) for every batch shape: its mask views are re-pointed
@@ -294,8 +350,12 @@ class DualSourceSelfAttentionTacotronModel:
             return self._predict(features)
         batch = self._batch(features, labels)
         if mode == ModeKeys.TRAIN:
+            # one captured step per padded batch shape, replayed when the shape comes back
+            # (train.StepGraphCache; eager on a first sighting or with graph_cache=0)
             tr = self._get_trainer(batch)
-            out = tr.step(batch)
+            if self._graphs is None:
+                self._graphs = StepGraphCache(tr, self.graph_cache, self.graph_t_quantum)
+            out = self._graphs.step(batch)
             return EstimatorSpec(mode, loss=out["loss"], train_op=tr.global_step,
                                  predictions=None, eval_metric_ops=None)
         if mode == ModeKeys.EVAL:

@@ -31,7 +31,8 @@ from .masks import mask_specs
 
 class Trainer:
     def __init__(self, model, B: int, N: int, Tp: int, seed: int = 1234,
-                 process_group=None, force_exchange: bool = False):
+                 process_group=None, force_exchange: bool = False,
+                 bucketed: Optional[bool] = None):
         self.m = model
         hp = model.hp
         dev = model.device
@@ -67,6 +68,17 @@ class Trainer:
         self.force_exchange = force_exchange
         self.cfg.grad_scale = dp.grad_scale(process_group)
         self.last_loss = None
+        # bucketed exchange (SAT_DP_BUCKETS=1 / bucketed=True): the decoder's gradient rows are
+        # all-reduced on a comm stream as soon as the decoder backward has issued them, beside
+        # the encoder backward (inside the captured forward/backward graph in split replay);
+        # the rest of the arena (encoder rows, BN statistics, health words) at the step's end.
+        # Off by default: measured on one rank only (tests/test_dp_gpu.py), not on 8 GPUs.
+        import os
+        self.bucketed = (os.environ.get("SAT_DP_BUCKETS", "0") == "1" if bucketed is None
+                         else bool(bucketed))
+        self._comm = (torch.cuda.Stream(device=dev) if torch.device(dev).type == "cuda"
+                      and self.bucketed else None)
+        self._bucket_done = None
 
     def reshape(self, B: int, N: int, Tp: int) -> None:
         """Point the mask views at a (B, N, T') batch shape."""
@@ -101,10 +113,30 @@ class Trainer:
         the seed advances on the device every step."""
         K.rng_fill_segments(self._mask_arena, self._mask_segs, self.seed)
 
+    def _bucketing(self) -> bool:
+        return self.bucketed and (self.world > 1 or
+                                  (self.force_exchange and dp.is_distributed(self.pg)))
+
+    def _decoder_bucket(self, streams):
+        """model_backward's on_decoder_grads hook: the first bucket's collective, on the comm
+        stream once every stream that carried decoder-gradient work has reached this point."""
+        lo, hi = self.m.decoder_grad_span()
+        if self._comm is not None:
+            for st in streams:
+                self._comm.wait_stream(st)
+            with torch.cuda.stream(self._comm):
+                dp.exchange_bucket(self.m.exchange, lo, hi, self.pg, force=self.force_exchange)
+        else:
+            dp.exchange_bucket(self.m.exchange, lo, hi, self.pg, force=self.force_exchange)
+        self._bucket_done = (lo, hi)
+
     def forward_backward(self, batch):
         self.draw_masks()
         out, sv = self.m.forward(batch, self.masks, training=True)
-        self.m.backward(sv)
+        self._bucket_done = None
+        self.m.backward(sv, on_decoder_grads=self._decoder_bucket if self._bucketing() else None)
+        if self._bucket_done is not None and self._comm is not None:
+            torch.cuda.current_stream().wait_stream(self._comm)   # joined (graph capture too)
         self.last_loss = out["loss"]
         self.last_saved = sv
         return out
@@ -115,7 +147,7 @@ class Trainer:
         (averaged, so replicas never drift apart) and the health words (non-zero everywhere iff
         on some rank, so the guarded update is skipped on every rank or on none)."""
         dp.exchange(self.m.exchange, self.m.health, self.m.bn.buf, self.m.health_tail, self.pg,
-                    force=self.force_exchange)
+                    force=self.force_exchange, done=self._bucket_done)
 
     def apply(self):
         """Guarded clip + Adam: skipped on the device when any health word of the step is set."""
@@ -174,9 +206,10 @@ class GraphedStep:
         self.batch = batch
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
+        self.warm_out = None                    # the last warm-up step's output (a real step)
         with torch.cuda.stream(s):
             for _ in range(warmup):
-                trainer.step(batch)
+                self.warm_out = trainer.step(batch)
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
         self.split = trainer.world > 1 if split is None else bool(split)
@@ -190,6 +223,14 @@ class GraphedStep:
             with torch.cuda.graph(self.g_apply):
                 trainer.apply()
         torch.cuda.synchronize()
+        # the graph holds raw pointers into the grow-only buffers the step used (the mask
+        # arena, the persistent kernels' scratch, the column-reduce / split-K / loss scratch):
+        # keep those exact buffers alive for the graph's lifetime, so a later, larger shape
+        # that replaces one of them (eager or another graph) never leaves this graph pointing
+        # at freed memory
+        m = trainer.m
+        self._keep = [trainer._mask_arena, *m._scratch.values(), *m.ws.bufs.values(),
+                      *K._SCRATCH.values(), *K._GEMM_WS.values()]
 
     def replay(self):
         self.t.check_health()
@@ -199,3 +240,82 @@ class GraphedStep:
             self.g_apply.replay()
         self.t.publish_health()
         return self.out
+
+
+class StepGraphCache:
+    """The drop-in training path's graph cache (``model_fn`` TRAIN over the reference's
+    bucketed, per-batch padded batches: datasets/ljspeech/dataset.py:235-286, train.py:39-65):
+    one captured step (``GraphedStep``) per padded batch shape, bounded LRU.
+
+    A shape seen for the first time runs its step eagerly -- the warm-up of its capture, a
+    real training step on that batch -- and is then captured; every later batch of that shape
+    is copied into the graph's static input buffers and replayed (one launch instead of ~225
+    from Python).  The least recently used graph is dropped beyond ``size`` entries (its
+    private memory pool goes with it); ``size = 0`` is the eager path.  Replays are bit-identical
+    to eager steps on the same batches (``tests/test_train_gpu.py``).
+
+    ``t_quantum`` > 0 pads T' (decoder steps) up to a multiple of it before the lookup, so
+    batches whose longest utterance differs by a few frames share a graph: the padding is the
+    reference's own batch padding (mel -3.0 -- masked, done 1 -- masked, both loss masks 0;
+    datasets/ljspeech/dataset.py:264-281), so the loss and every gradient are unchanged in exact
+    arithmetic (the padded steps carry zero loss seeds and the decoder head is causal); only the
+    dropout / zoneout draws of batch-major masks shift.  Default 0: exact shapes, bitwise ==
+    eager."""
+
+    def __init__(self, trainer: Trainer, size: int = 8, t_quantum: int = 0):
+        from collections import OrderedDict
+        self.t = trainer
+        self.size = int(size)
+        self.t_quantum = int(t_quantum)
+        self.entries: "OrderedDict[tuple, tuple]" = OrderedDict()
+        self.hits = self.misses = self.evictions = 0
+
+    def _pad_t(self, batch):
+        q = self.t_quantum
+        r = self.t.hp.outputs_per_step
+        Tp = batch["mel"].shape[1] // r
+        Tq = -(-Tp // q) * q if q > 0 else Tp
+        if Tq == Tp:
+            return batch
+        pad = (Tq - Tp)
+        out = dict(batch)
+        B = batch["mel"].shape[0]
+        dev = batch["mel"].device
+        out["mel"] = torch.cat([batch["mel"], torch.full((B, pad * r, batch["mel"].shape[2]), -3.0,
+                                                         device=dev)], 1)
+        out["mel_mask"] = torch.cat([batch["mel_mask"], torch.zeros(B, pad * r, device=dev)], 1)
+        out["done"] = torch.cat([batch["done"], torch.ones(B, pad, device=dev)], 1)
+        out["done_mask"] = torch.cat([batch["done_mask"], torch.zeros(B, pad, device=dev)], 1)
+        return out
+
+    @staticmethod
+    def key(batch):
+        return tuple(sorted((k, tuple(v.shape), v.dtype) for k, v in batch.items()))
+
+    def step(self, batch):
+        """One training step on ``batch`` (device tensors); returns {"loss": a tensor that this
+        cache does not overwrite later}."""
+        if self.size <= 0:
+            return {"loss": self.t.step(batch)["loss"]}
+        batch = self._pad_t(batch)
+        k = self.key(batch)
+        e = self.entries.get(k)
+        if e is None:
+            self.misses += 1
+            static = {n: v.clone() for n, v in batch.items()}
+            g = GraphedStep(self.t, static, warmup=1)     # this batch's step = the warm-up
+            self.entries[k] = (static, g)
+            while len(self.entries) > self.size:
+                self.entries.popitem(last=False)
+                self.evictions += 1
+            return {"loss": g.warm_out["loss"]}
+        self.hits += 1
+        self.entries.move_to_end(k)
+        static, g = e
+        for n, v in batch.items():
+            static[n].copy_(v, non_blocking=True)
+        # GraphedStep.replay() leaves Trainer.shape alone: the next eager step re-views the
+        # masks for its own shape (Trainer.reshape), the captured graph keeps its own views
+        out = g.replay()
+        return {"loss": out["loss"].clone()}
+

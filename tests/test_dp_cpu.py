@@ -65,7 +65,7 @@ def _worker(rank, world, port, q):
         tdist.all_reduce = counting
         tr.reduce_grads()
         tdist.all_reduce = real
-        res["collectives"] = calls
+        res["collectives"] = list(calls)
         gsum = sum(local_grad(r) for r in range(world))
         res["sum"] = bool(torch.equal(model.grads, gsum))
         res["scale"] = tr.cfg.grad_scale
@@ -97,6 +97,34 @@ def _worker(rank, world, port, q):
         gathered = [torch.empty_like(p_dp) for _ in range(world)]
         tdist.all_gather(gathered, p_dp)
         res["replicas_equal"] = all(torch.equal(gathered[0], x) for x in gathered[1:])
+        # the bucketed exchange: the decoder rows [lo, hi) reduced first (the
+        # hook model_backward calls once the decoder backward is issued), the rest at the end
+        # -- bitwise the single exchange's result, in three collectives
+        lo = 1024
+
+        def fresh_model():
+            a = torch.cat([local_grad(rank), local_bn(rank), torch.zeros(16)])
+            mm = types.SimpleNamespace(
+                hp=hp, device=torch.device("cpu"), params=torch.zeros(n), exchange=a,
+                grads=a[:n], health_tail=a[n + 64:], health=torch.zeros(16, dtype=torch.int32),
+                bn=types.SimpleNamespace(buf=a[n:n + 64]),
+                decoder_grad_span=lambda: (lo, n))
+            if rank == 1:
+                mm.health[5] = 3
+            return mm
+        m1, m2 = fresh_model(), fresh_model()
+        t1 = train.Trainer(m1, B=2, N=8, Tp=4, bucketed=False)
+        t2 = train.Trainer(m2, B=2, N=8, Tp=4, bucketed=True)
+        t1.reduce_grads()
+        assert t2._bucketing()
+        calls.clear()
+        tdist.all_reduce = counting
+        t2._decoder_bucket([])
+        t2.reduce_grads()
+        tdist.all_reduce = real
+        res["bucket_collectives"] = list(calls)
+        res["bucket_equal"] = bool(torch.equal(m1.exchange, m2.exchange)) and \
+            bool(torch.equal(m1.health, m2.health))
         # masks are drawn per replica: the model_fn seed offset differs by rank
         res["seed_offset"] = 1000003 * dp.rank()
         # max-over-ranks step time
@@ -125,6 +153,8 @@ def test_dp_world2_gloo():
         assert res["matches_single"]
         assert res["health"][3] == 7 and sum(res["health"]) == 7
         assert res["collectives"] == [4096 + 64 + 16]     # ONE collective per step
+        assert res["bucket_equal"]
+        assert res["bucket_collectives"] == [4096 - 1024, 1024, 64 + 16]
         assert res["seed_offset"] == 1000003 * r
         assert res["scale"] == pytest.approx(0.5) and res["world"] == 2
         assert res["max"] == pytest.approx(1.5)

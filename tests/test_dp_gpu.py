@@ -127,5 +127,31 @@ def test_split_step_with_rccl_exchange_equals_unsplit(cuda):
         # the health tail went through pack -> RCCL -> unpack: |code| floats of a healthy step
         assert torch.equal(m2.health_tail[:m2.health.numel()],
                            torch.zeros(m2.health.numel(), device=cuda))
+        # the bucketed exchange: the decoder's gradient rows all-reduced on a
+        # comm stream once the decoder backward is issued -- captured INSIDE the forward /
+        # backward graph, beside the encoder backward -- the rest between the two graphs;
+        # bitwise the single-exchange step
+        m3 = engine.Tacotron(hp, cuda, seed=42)
+        t3 = train.Trainer(m3, 2, N, Tp, seed=7, process_group=tdist.group.WORLD,
+                           force_exchange=True, bucketed=True)
+        lo, hi = m3.decoder_grad_span()
+        assert 0 < lo < hi == m3.params.numel() and lo % 64 == 0
+        calls.clear()
+        dp.tdist.all_reduce = counted
+        try:
+            g3 = train.GraphedStep(t3, batch, warmup=1, split=True)
+            for _ in range(3):
+                g3.replay()
+            torch.cuda.synchronize()
+        finally:
+            dp.tdist.all_reduce = real
+        rest = m3.exchange.numel() - hi
+        # warm-up step (3 collectives), the captured bucket, then 2 eager ones per replay
+        assert calls == [hi - lo, lo, rest, hi - lo] + [lo, rest] * 3
+        t3.check_health(wait=True)
+        assert torch.equal(m1.params, m3.params)
+        assert torch.equal(t1.exp_avg, t3.exp_avg)
+        assert torch.equal(t1.exp_avg_sq, t3.exp_avg_sq)
+        assert torch.equal(m1.bn.buf, m3.bn.buf)
     finally:
         tdist.destroy_process_group()

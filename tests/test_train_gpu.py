@@ -106,7 +106,9 @@ def test_model_fn_memory_flat_over_shapes(cuda):
     import gc
     from sat_amd import hparams, models as MD
     hp = hparams.ljspeech_hparams()
-    model = MD.DualSourceSelfAttentionTacotronModel(hp, device=cuda, seed=1)
+    # the eager drop-in path (graph_cache=0); the captured path keeps one graph pool per cached
+    # shape, bounded by its LRU (test_model_fn_graph_cache_*)
+    model = MD.DualSourceSelfAttentionTacotronModel(hp, device=cuda, seed=1, graph_cache=0)
     it = iter(MD.synthetic_input_fn(hp, 4, N=60, T=120, shape="ljs", seed=3)())
     feats, labels = next(it)
     big = MD.synthetic_input_fn(hp, 4, N=60, T=120, shape="max", seed=0)
@@ -142,3 +144,78 @@ def test_odd_rows_fused_attention_with_dropout(cuda):
     assert fused, "no multi-head attention took the fused path"
     assert np.isfinite(float(tr.last_loss.item()))
     assert torch.isfinite(m.grads).all()
+
+
+def _shape_batches(hp, shapes, seed=0):
+    from sat_amd import models as MD
+    out = []
+    for i, (B, N, T) in enumerate(shapes):
+        it = iter(MD.synthetic_input_fn(hp, B, N=N, T=T, shape="max", seed=seed + 17 * i)())
+        out.append(next(it))
+    return out
+
+
+def test_model_fn_graph_cache_equals_eager(cuda):
+    """model_fn TRAIN replays one captured step per padded batch shape (LRU),
+    eager only on a shape's first sighting; over two interleaved shapes the cached path's
+    losses and parameters equal the eager drop-in path's bit for bit."""
+    from sat_amd import hparams, models as MD
+    hp = hparams.ljspeech_hparams()
+    ma = MD.DualSourceSelfAttentionTacotronModel(hp, device=cuda, seed=3, graph_cache=4)
+    mb = MD.DualSourceSelfAttentionTacotronModel(hp, device=cuda, seed=3, graph_cache=0)
+    shapes = [(2, 13, 24), (2, 9, 32), (2, 13, 24), (2, 9, 32), (2, 13, 24), (2, 13, 24)]
+    for f, l in _shape_batches(hp, shapes, seed=5):
+        la = ma.model_fn(f, l, MD.ModeKeys.TRAIN, hp).loss
+        lb = mb.model_fn(f, l, MD.ModeKeys.TRAIN, hp).loss
+        torch.cuda.synchronize()
+        assert torch.equal(la, lb)
+        assert torch.equal(ma.engine.params, mb.engine.params)
+    c = ma._graphs
+    assert (c.misses, c.hits, c.evictions) == (2, 4, 0)
+    assert int(ma._trainer.global_step.item()) == len(shapes)
+
+
+def test_model_fn_graph_cache_lru_bound(cuda):
+    """A cache of two graphs over three cycling shapes evicts the least recently used one each
+    time; results stay equal to the eager path and the live graph count stays at the bound."""
+    from sat_amd import hparams, models as MD
+    hp = hparams.ljspeech_hparams()
+    ma = MD.DualSourceSelfAttentionTacotronModel(hp, device=cuda, seed=4, graph_cache=2)
+    mb = MD.DualSourceSelfAttentionTacotronModel(hp, device=cuda, seed=4, graph_cache=0)
+    shapes = [(2, 11, 16), (2, 7, 24), (2, 11, 16), (2, 5, 20), (2, 7, 24), (2, 5, 20)]
+    for f, l in _shape_batches(hp, shapes, seed=9):
+        la = ma.model_fn(f, l, MD.ModeKeys.TRAIN, hp).loss
+        lb = mb.model_fn(f, l, MD.ModeKeys.TRAIN, hp).loss
+        torch.cuda.synchronize()
+        assert torch.equal(la, lb)
+    assert torch.equal(ma.engine.params, mb.engine.params)
+    c = ma._graphs
+    assert len(c.entries) == 2 and c.evictions == 2 and c.hits == 2
+
+
+def test_graph_t_quantum_padding_keeps_the_step(cuda):
+    """graph_t_quantum pads T' with the reference's own batch padding (mel -3.0, done 1, loss
+    masks 0): with every dropout / zoneout rate 0 (so the masks are all ones and no draw can
+    differ), the padded step's loss and gradients equal the unpadded step's to fp32 rounding."""
+    from sat_amd import engine, hparams, train
+    hp = hparams.ljspeech_hparams()
+    for k in ("encoder_prenet_drop_rate", "decoder_prenet_drop_rate", "self_attention_drop_rate",
+              "decoder_self_attention_drop_rate", "zoneout_factor_cell", "zoneout_factor_output"):
+        hp.set_hparam(k, 0.0)
+    (f, l), = _shape_batches(hp, [(2, 10, 22)], seed=2)
+    from sat_amd import models as MD
+    batch = MD.DualSourceSelfAttentionTacotronModel(hp, device=cuda, seed=1)._batch(f, l)
+    res = []
+    for q in (0, 8):
+        m = engine.Tacotron(hp, cuda, seed=42)
+        tr = train.Trainer(m, 2, batch["source"].shape[1], 16, seed=7)
+        b = train.StepGraphCache(tr, 1, q)._pad_t(batch)
+        assert b["mel"].shape[1] // 2 == (11 if q == 0 else 16)
+        tr.reshape(2, b["source"].shape[1], b["mel"].shape[1] // 2)
+        out = tr.forward_backward(b)
+        torch.cuda.synchronize()
+        res.append((float(out["loss"].item()), m.grads.clone()))
+    (l0, g0), (l1, g1) = res
+    assert abs(l0 - l1) <= 1e-6 * abs(l0)
+    scale = float(g0.abs().max())
+    assert float((g0 - g1).abs().max()) <= 2e-5 * scale

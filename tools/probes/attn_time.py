@@ -1,5 +1,6 @@
-"""HIP-event time of the two attention-chain launches (sat_decoder_attention_fwd / _bwd) and the
-attention parameter-gradient pass (sat_attn_param_grads) on the
+"""HIP-event time of the two attention-chain launches (sat_decoder_attention_fwd / _bwd), the
+attention parameter-gradient pass (sat_attn_param_grads) and the decoder LSTM stack
+(sat_decoder_lstms_fwd / _bwd) on the
 training step's own buffers (B=32, N=200, T'=500, train mode) with whichever library is loaded
 (tools only; A/B two builds by running this twice, once with SAT_LIB_OVERRIDE=<other .so>).
 Also prints a checksum of the forward's histories and the BPTT outputs so two builds' results
@@ -20,7 +21,9 @@ from sat_amd import _lib, data, engine, hparams  # noqa: E402
 from sat_amd import kernels as K  # noqa: E402
 
 KW = {}
-for nm in ("decoder_attention_fwd", "decoder_attention_bwd", "attn_param_grads"):
+NAMES = ("decoder_attention_fwd", "decoder_attention_bwd", "attn_param_grads",
+         "decoder_lstms_fwd", "decoder_lstms_bwd")
+for nm in NAMES:
     orig = getattr(K, nm)
 
     def rec(_o=orig, _n=nm, **kw):
@@ -47,7 +50,7 @@ def timed(nm, reps):
     kw, fn = KW[nm], KW[nm + "_orig"]
     ts = []
     for i in range(reps + 1):
-        if nm.endswith("bwd"):
+        if nm == "decoder_attention_bwd":
             kw["RD"].copy_(RD0)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
@@ -61,7 +64,7 @@ def timed(nm, reps):
     return sorted(ts)
 
 
-for nm in ("decoder_attention_fwd", "decoder_attention_bwd", "attn_param_grads"):
+for nm in NAMES:
     ts = timed(nm, reps)
     med = ts[len(ts) // 2]
     print(f"{os.path.basename(_lib.LIB_PATH)} {nm}: median {med:.1f} us/launch = {med / Tp:.3f} "

@@ -29,16 +29,6 @@
 #include "sat_common.h"
 #include "persistent.h"
 
-#ifndef SAT_LSTM_POLL1
-#define SAT_LSTM_POLL1 1
-#endif
-#ifndef SAT_LSTM_LSB
-// forward hand-off payloads LSB-tagged (persistent.h lsb_tag: the step parity in each float's
-// mantissa LSB, as the attention chain's records) instead of 8-byte {value, tag} granules: half
-// the bytes every consumer wave pulls per step
-#define SAT_LSTM_LSB 1
-#endif
-
 namespace sat {
 namespace {
 
@@ -67,12 +57,6 @@ struct DecLstmFwdP {
 };
 
 __device__ __forceinline__ unsigned tag_of(float x) { return __float_as_uint(x); }
-// an 8-byte hand-off store of two tagged floats at 8-byte index i2 (store policy as stc4x)
-__device__ __forceinline__ void st2x(bool xl, __amdgpu_buffer_rsrc_t r, int i2, float a, float b) {
-  const v2u w = {__float_as_uint(a), __float_as_uint(b)};
-  if (xl) __builtin_amdgcn_raw_buffer_store_b64(w, r, i2 * 8, 0, 0);
-  else __builtin_amdgcn_raw_buffer_store_b64(w, r, i2 * 8, 0, 16);
-}
 
 // Forward.  Dot role: wave w owns units 2w, 2w+1 of the workgroup in both layers (8 gate
 // columns each), lane = k-slice ks: LSTM1's recurrent rows 4ks..4ks+3 and LSTM2's [input |
@@ -183,62 +167,11 @@ __global__ void __launch_bounds__(kThreads) dec_lstm_fwd_kernel(DecLstmFwdP p) {
     // ---- consume: h1_{i-1}, h1'_{i-1} (XA) and h2_{i-2} (XB) of the group's utterances
     if (i == 0) {
       xs[aub][au] = a_on ? p.H1S[(int64_t)ab * kU + au] : 0.f;
-    } else if (SAT_LSTM_LSB) {
-      // XA [2][B][U][2] = {h1, h1'} per unit, XB [2][B][U] = h2, every float tagged with
-      // lsb_tag(i - 1) (published at iteration i - 1 into slot (i - 1) & 1).  Threads 0..255:
-      // one float4 of XA (two units of one utterance), 256..383: one float4 of XB (4 units)
-      const int s1 = i - 1, slot = s1 & 1;
-      const unsigned want = lsb_tag(s1);
-      const bool isa = tid < kUBmax * (kU / 2);
-      const int ti = isa ? tid : tid - kUBmax * (kU / 2);
-      const int sub = isa ? ti / (kU / 2) : ti / (kU / 4);
-      const int sq = isa ? ti % (kU / 2) : ti % (kU / 4);
-      const int sb = g + kG * sub;
-      const bool on = sb < B && tid < kUBmax * (kU / 2 + kU / 4);
-      const auto rr = isa ? rXA : rXB;
-      const int idx = on ? (isa ? (slot * B + sb) * (kU / 2) + sq : (slot * B + sb) * (kU / 4) + sq) : 0;
-      float4 x = ldc4(rr, idx);
-      bool ok = !on || tag_ok4(x, want);
-      if (__builtin_amdgcn_ballot_w64(!ok) != 0) {
-        for (unsigned spins = 0;; ++spins) {
-          if (!ok) x = ldc4(rr, idx);
-          ok = ok || tag_ok4(x, want);
-          if (__builtin_amdgcn_ballot_w64(!ok) == 0) break;
-          if ((spins & 255u) == 255u) {
-            if (__hip_atomic_load(p.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) break;
-            if (spins > (1u << 20)) {   // a producer never published (not co-resident?)
-              __hip_atomic_store(p.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              break;
-            }
-          }
-          __builtin_amdgcn_s_sleep(1);
-        }
-      }
-      tick(0);
-      if (on && isa) {
-        xs[sub][2 * sq] = x.x;
-        xs[sub][2 * sq + 1] = x.z;
-        xs[sub][kU + 2 * sq] = x.y;
-        xs[sub][kU + 2 * sq + 1] = x.w;
-      } else if (on) {
-        *reinterpret_cast<float4*>(&xs[sub][2 * kU + 4 * sq]) = x;
-      }
     } else {
       const unsigned ep = (unsigned)i;
       const int par = i & 1;
       float4 ga = make_float4(0.f, 0.f, 0.f, 0.f), gb = ga;
       bool oka = !a_on, okb = !b_on;
-#if SAT_LSTM_POLL1
-      // first attempt branch-free: every thread issues both loads (clamped in-range addresses
-      // where it has no granule), the tags are checked, and only a miss enters the retry loop
-      {
-        const float4 fa = ldc4(rXA, a_on ? (par * B + ab) * kU + au : 0);
-        const float4 fb = ldc4(rXB, b_on ? (par * B + bb) * (kU / 2) + bu2 : 0);
-        if (!oka) { ga = fa; oka = tag_of(ga.y) == ep && tag_of(ga.w) == ep; }
-        if (!okb) { gb = fb; okb = tag_of(gb.y) == ep && tag_of(gb.w) == ep; }
-      }
-      if (__builtin_amdgcn_ballot_w64(!(oka && okb)) != 0)
-#endif
       for (unsigned spins = 0;; ++spins) {
         if (!oka) {
           ga = ldc4(rXA, (par * B + ab) * kU + au);
@@ -324,14 +257,7 @@ __global__ void __launch_bounds__(kThreads) dec_lstm_fwd_kernel(DecLstmFwdP p) {
       const float cn = gf * cst + gi * gj;
       const float hn = go * tanh_lstm(cn);
       const float c2 = mc * cn + (1.f - mc) * cst;
-      float h2 = mh * hn + (1.f - mh) * hst;
-      float hnp = hn;              // the raw output as every reader (and the history) sees it
-      if (SAT_LSTM_LSB && i < T) {
-        // handed-off values are tagged where they are made; the maker keeps the tagged bits
-        const unsigned bit = lsb_tag(i);
-        h2 = tagf(h2, bit);
-        if (layer == 0) hnp = tagf(hn, bit);
-      }
+      const float h2 = mh * hn + (1.f - mh) * hst;
       cst = c2;
       hst = h2;
       hpub = h2;
@@ -339,14 +265,10 @@ __global__ void __launch_bounds__(kThreads) dec_lstm_fwd_kernel(DecLstmFwdP p) {
       const int64_t bn = bu + (int64_t)B * kU;       // [t + 1]
       if (layer == 0) {
         if (i < T) {
-          if (SAT_LSTM_LSB) {
-            st2x(xl, rXA, ((i & 1) * B + pb) * kU + pu, h2, hnp);
-          } else {
-            const float tg = __uint_as_float((unsigned)(i + 1));
-            stc4x(xl, rXA, ((((i + 1) & 1) * B + pb) * kU + pu), make_float4(h2, tg, hn, tg));
-          }
+          const float tg = __uint_as_float((unsigned)(i + 1));
+          stc4x(xl, rXA, ((((i + 1) & 1) * B + pb) * kU + pu), make_float4(h2, tg, hn, tg));
         }
-        p.H1RAW[bu] = hnp;
+        p.H1RAW[bu] = hn;
         p.H1S[bn] = h2;
         p.C1S[bn] = c2;
         reinterpret_cast<float4*>(p.G1)[bu] = make_float4(gi, gj, gf, go);
@@ -359,14 +281,8 @@ __global__ void __launch_bounds__(kThreads) dec_lstm_fwd_kernel(DecLstmFwdP p) {
     }
     // LSTM2 lanes publish h2 (at i == 0: the initial state) in unit pairs: the uu = 1 partner
     // sits 8 lanes up
-    if (SAT_LSTM_LSB && i == 0 && cell && layer == 1) {
-      hst = tagf(hst, lsb_tag(0));      // the initial state, handed off at iteration 0
-      hpub = hst;
-    }
     const float hpart = dpp_mov<0x108>(hpub);
-    if (SAT_LSTM_LSB && cell && layer == 1 && puu == 0 && i < T) {
-      st2x(xl, rXB, (((i & 1) * B + pb) * kU + pu) / 2, hpub, hpart);
-    } else if (!SAT_LSTM_LSB && cell && layer == 1 && puu == 0 && i < T) {
+    if (cell && layer == 1 && puu == 0 && i < T) {
       const float tg = __uint_as_float((unsigned)(i + 1));
       stc4x(xl, rXB, ((((i + 1) & 1) * B + pb) * (kU / 2) + (pu >> 1)), make_float4(hpub, tg, hpart, tg));
     }
@@ -521,16 +437,16 @@ __global__ void __launch_bounds__(kThreads) dec_lstm_bwd_kernel(DecLstmBwdP p) {
       const unsigned w2 = lsb_tag(q2), w1 = lsb_tag(q1);
       float4 v2 = make_float4(0.f, 0.f, 0.f, 0.f), v1 = v2;
       bool ok2 = !(stage2 && bo), ok1 = !(stage1 && bo);
-#if SAT_LSTM_POLL1
       // first attempt branch-free (every thread issues both loads; slots of steps not yet
-      // staged are in-range addresses whose values are discarded), retry loop only on a miss
+      // staged are in-range addresses whose values are discarded), the retry loop only on a
+      // miss: 2.55 -> 2.50-2.52 us/step (round 6, two A/B rounds; the same change in the
+      // forward's granule poll measured 2.61 -> 2.72, not made there)
       {
         const float4 f2 = ldc4(rXG, i2), f1 = ldc4(rXG, i1);
         if (!ok2) { v2 = f2; ok2 = tag_ok4(v2, w2); }
         if (!ok1) { v1 = f1; ok1 = tag_ok4(v1, w1); }
       }
       if (__builtin_amdgcn_ballot_w64(!(ok1 && ok2)) != 0 && !gave_up)
-#endif
       for (unsigned spins = 0;; ++spins) {
         if (!ok2) v2 = ldc4(rXG, i2);
         if (!ok1) v1 = ldc4(rXG, i1);
@@ -600,348 +516,6 @@ __global__ void __launch_bounds__(kThreads) dec_lstm_bwd_kernel(DecLstmBwdP p) {
     for (int i = 0; i < 4; ++i) p.prof[blockIdx.x * 4 + i] = tp[i];
 }
 
-// ------------------------------------------------------------------------------------------
-// One utterance per 8 workgroups (the attention chain's layout): group g =
-// utterance g owns workgroups {g, g + 32, ...} (one XCD under the observed round-robin
-// placement), workgroup j units [32j, 32j + 32) of both layers, wave w of it units 32j + 4w ..
-// + 3 (16 gate columns per layer).  A step's hand-off then has 8 producers of ONE utterance
-// (3 KB of LSB-tagged floats per workgroup and step) where the 16 x 2-utterance layout above
-// gathers from 16 producers (12 KB of granules).  The weights per workgroup double (393 KB):
-// the LSTM1 recurrent rows and LSTM2's input rows live in registers (128 per lane), LSTM2's
-// recurrent rows in LDS (128 KB, laid out so every ds_read_b128 of a wave reads 1 KB
-// contiguous).  Same arithmetic per cell as the kernels above; the dot's summation order
-// differs.
-constexpr int kG8 = 32;            // groups = utterances
-constexpr int kW8 = 8;             // workgroups per utterance
-constexpr int kUW8 = kU / kW8;     // 32 units per workgroup per layer
-__device__ __forceinline__ int lds8_idx(int w, int a, int q, int lane) {
-  return ((w * 4 + a) * 4 + q) * 64 + lane;
-}
-
-__global__ void __launch_bounds__(kThreads) dec_lstm8_fwd_kernel(DecLstmFwdP p) {
-  __shared__ __attribute__((aligned(16))) float4 w2r[kW8 * 4 * 4 * 64];   // 128 KB
-  // h1_{i-1} | h1'_{i-1} | h2_{i-2}, double-buffered by iteration parity: a wave can only stage
-  // iteration i + 2 after its workgroup's barrier of iteration i + 1, i.e. after every wave of
-  // every workgroup published iteration i -- which each does after its iteration-i dot
-  __shared__ __attribute__((aligned(16))) float xsb[2][3][kU];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int g = blockIdx.x % kG8, j = blockIdx.x / kG8;
-  const int B = p.B, T = p.T;
-  if (g >= B) return;                  // no utterance: no partner outside this group
-  const int b = g;
-  const int u0 = j * kUW8, ucol = u0 + 4 * w;
-
-  // ---- weights: lane holds rows 4 lane + q of W1r and of W2's input half for the wave's 16
-  //      columns (units ucol .. ucol + 3, gates i j f o: 16 contiguous floats per row)
-  float w1[4][16], w2a[4][16];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const float4* s1 = reinterpret_cast<const float4*>(p.W1r + ((int64_t)(4 * lane + q) * kU + ucol) * 4);
-    const float4* s2 = reinterpret_cast<const float4*>(p.W2 + ((int64_t)(4 * lane + q) * kU + ucol) * 4);
-#pragma unroll
-    for (int c4 = 0; c4 < 4; ++c4) {
-      const float4 a = s1[c4], c = s2[c4];
-      w1[q][4 * c4] = a.x; w1[q][4 * c4 + 1] = a.y; w1[q][4 * c4 + 2] = a.z; w1[q][4 * c4 + 3] = a.w;
-      w2a[q][4 * c4] = c.x; w2a[q][4 * c4 + 1] = c.y; w2a[q][4 * c4 + 2] = c.z; w2a[q][4 * c4 + 3] = c.w;
-    }
-  }
-  for (int i = tid; i < kW8 * 4 * 4 * 64; i += kThreads) {   // W2 recurrent rows kU + 4 l + q
-    const int l = i & 63, c4 = (i >> 6) & 3, q = (i >> 8) & 3, ww = i >> 10;
-    w2r[i] = reinterpret_cast<const float4*>(
-        p.W2 + ((int64_t)(kU + 4 * l + q) * kU + u0 + 4 * ww) * 4)[c4];
-  }
-  // ---- cell role: output m = lane >> 1 = layer * 16 + uu * 4 + gate; lanes with gate 0
-  const int layer = lane >> 5, puu = (lane >> 3) & 3, pu = ucol + puu;
-  const bool cell = (lane & 7) == 0;
-  float cst = 0.f, hst = 0.f;
-  float4 bias2 = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (cell) {
-    const int64_t i0 = (int64_t)b * kU + pu;
-    cst = layer == 0 ? p.C1S[i0] : p.C2S[i0];
-    hst = layer == 0 ? p.H1S[i0] : p.H2S[i0];
-    if (layer == 1) bias2 = reinterpret_cast<const float4*>(p.b2)[pu];
-  }
-  const bool masked = p.m1c != nullptr;
-  // hand-off slots (LSB-tagged floats): XA [2][B][2][U] = {h1 | h1'} of LSTM1 step s,
-  // XB [2][B][U] = h2 of LSTM2 step s - 1, slot s & 1, published at iteration s
-  float* XA = p.xch;
-  float* XBb = p.xch + (size_t)4 * B * kU;
-  const auto rXA = rsrc(XA), rXB = rsrc(XBb);
-  auto ops_on = [&](int ii) {
-    const int tt = layer == 0 ? ii : ii - 1;
-    return cell && tt >= 0 && tt < T;
-  };
-  auto load_ops = [&](int ii, float4& xp_, float& mc_, float& mh_) {
-    const int tt = layer == 0 ? ii : ii - 1;
-    const int64_t bu = ops_on(ii) ? ((int64_t)tt * B + b) * kU + pu : 0;
-    const float* Mc = masked ? (layer == 0 ? p.m1c : p.m2c) : p.X1;
-    const float* Mh = masked ? (layer == 0 ? p.m1h : p.m2h) : p.X1;
-    xp_ = reinterpret_cast<const float4*>(p.X1)[bu];
-    mc_ = Mc[bu];
-    mh_ = Mh[bu];
-  };
-  float4 xpn;
-  float mcn, mhn;
-  load_ops(0, xpn, mcn, mhn);
-  __syncthreads();
-  const bool xl = (p.flags & 1) ? xcd_local_group(reinterpret_cast<unsigned*>(p.xch + (size_t)12 * B * kU), g, kG8, kW8, p.err) : false;
-  bool gave_up = false;
-
-  for (int i = 0; i <= T; ++i) {
-    const bool do1 = i < T, do2 = i >= 1;
-    const int t = layer == 0 ? i : i - 1;
-    const bool cell_step = cell && (layer == 0 ? do1 : do2);
-    float (*xs)[kU] = xsb[i & 1];
-    // ---- consume h1_{i-1}, h1'_{i-1} (XA) and h2_{i-2} (XB): 192 float4 chunks, 24 per wave
-    if (i == 0) {
-      if (tid < kU) xs[0][tid] = p.H1S[(int64_t)b * kU + tid];
-    } else if (lane < 24) {
-      const int s1 = i - 1, slot = s1 & 1;
-      const unsigned want = lsb_tag(s1);
-      const int id = 24 * w + lane, part = id >> 6, c = id & 63;
-      const bool isa = part < 2;
-      const auto rr = isa ? rXA : rXB;
-      const int idx = isa ? ((slot * B + b) * 2 + part) * (kU / 4) + c : (slot * B + b) * (kU / 4) + c;
-      float4 x = ldc4(rr, idx);
-      bool ok = tag_ok4(x, want);
-      if (__builtin_amdgcn_ballot_w64(!ok) != 0 && !gave_up) {
-        for (unsigned spins = 0;; ++spins) {
-          if (!ok) x = ldc4(rr, idx);
-          ok = ok || tag_ok4(x, want);
-          if (__builtin_amdgcn_ballot_w64(!ok) == 0) break;
-          if (poll_give_up(spins, p.err)) { gave_up = true; break; }
-          __builtin_amdgcn_s_sleep(1);
-        }
-      }
-      *reinterpret_cast<float4*>(&xs[part][4 * c]) = x;
-    }
-    const bool on_i = ops_on(i);
-    const float4 xp = (layer == 0 && on_i) ? xpn : bias2;
-    const float mc = (masked && on_i) ? mcn : 1.f - p.zc;
-    const float mh = (masked && on_i) ? mhn : 1.f - p.zh;
-    if (i < T) load_ops(i + 1, xpn, mcn, mhn);
-    lds_barrier();   // LDS staging only: a __syncthreads would drain the prefetch just issued
-    // ---- dots: v[layer * 16 + column]
-    float v[32];
-#pragma unroll
-    for (int c = 0; c < 32; ++c) v[c] = 0.f;
-    if (do1) {
-      const float4 x = reinterpret_cast<const float4*>(xs[0])[lane];
-      const float xv[4] = {x.x, x.y, x.z, x.w};
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int c = 0; c < 16; ++c) v[c] = fmaf(xv[q], w1[q][c], v[c]);
-    }
-    if (do2) {
-      const float4 x = reinterpret_cast<const float4*>(xs[1])[lane];
-      const float xv[4] = {x.x, x.y, x.z, x.w};
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int c = 0; c < 16; ++c) v[16 + c] = fmaf(xv[q], w2a[q][c], v[16 + c]);
-      const float4 y = reinterpret_cast<const float4*>(xs[2])[lane];
-      const float yv[4] = {y.x, y.y, y.z, y.w};
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int c4 = 0; c4 < 4; ++c4) {
-          const float4 wv = w2r[lds8_idx(w, q, c4, lane)];
-          v[16 + 4 * c4] = fmaf(yv[q], wv.x, v[16 + 4 * c4]);
-          v[16 + 4 * c4 + 1] = fmaf(yv[q], wv.y, v[16 + 4 * c4 + 1]);
-          v[16 + 4 * c4 + 2] = fmaf(yv[q], wv.z, v[16 + 4 * c4 + 2]);
-          v[16 + 4 * c4 + 3] = fmaf(yv[q], wv.w, v[16 + 4 * c4 + 3]);
-        }
-    }
-    transpose_reduce32(v, lane);
-    // gates of (layer, unit): i at lane l, j at l+2, f at l+4, o at l+6 (l % 8 == 0)
-    const float gj_ = dpp_mov<0x102>(v[0]);
-    const float gf_ = dpp_mov<0x104>(v[0]);
-    const float go_ = dpp_mov<0x106>(v[0]);
-    if (cell_step) {
-      const float gi = sigmoid_fast(v[0] + xp.x);
-      const float gj = tanh_lstm(gj_ + xp.y);
-      const float gf = sigmoid_fast(gf_ + xp.z + 1.0f);   // forget_bias = 1.0
-      const float go = sigmoid_fast(go_ + xp.w);
-      const float cn = gf * cst + gi * gj;
-      const float hn = go * tanh_lstm(cn);
-      const float c2 = mc * cn + (1.f - mc) * cst;
-      float h2 = mh * hn + (1.f - mh) * hst;
-      float hnp = hn;
-      if (i < T) {
-        // handed-off values are tagged where they are made; the maker keeps the tagged bits
-        const unsigned bit = lsb_tag(i);
-        h2 = tagf(h2, bit);
-        if (layer == 0) hnp = tagf(hn, bit);
-      }
-      cst = c2;
-      hst = h2;
-      const int64_t bu = ((int64_t)t * B + b) * kU + pu;
-      const int64_t bn = bu + (int64_t)B * kU;       // [t + 1]
-      if (layer == 0) {
-        if (i < T) {
-          const int base = ((i & 1) * B + b) * 2 * kU + pu;
-          stcx(xl, rXA, base, h2);
-          stcx(xl, rXA, base + kU, hnp);
-        }
-        p.H1RAW[bu] = hnp;
-        p.H1S[bn] = h2;
-        p.C1S[bn] = c2;
-        reinterpret_cast<float4*>(p.G1)[bu] = make_float4(gi, gj, gf, go);
-      } else {
-        if (i < T) stcx(xl, rXB, ((i & 1) * B + b) * kU + pu, h2);
-        p.H2RAW[bu] = hn;
-        p.H2S[bn] = h2;
-        p.C2S[bn] = c2;
-        reinterpret_cast<float4*>(p.G2)[bu] = make_float4(gi, gj, gf, go);
-      }
-    } else if (i == 0 && cell && layer == 1) {
-      hst = tagf(hst, lsb_tag(0));        // the initial state, handed off at iteration 0
-      stcx(xl, rXB, b * kU + pu, hst);
-    }
-  }
-}
-
-__global__ void __launch_bounds__(kThreads) dec_lstm8_bwd_kernel(DecLstmBwdP p) {
-  __shared__ __attribute__((aligned(16))) float4 w1l[kW8 * 4 * 4 * 64];   // 128 KB
-  // staged gate-gradient rows, double-buffered by iteration parity (as dec_lstm8_fwd_kernel's)
-  __shared__ __attribute__((aligned(16))) float dgb[2][2][4 * kU];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int g = blockIdx.x % kG8, j = blockIdx.x / kG8;
-  const int B = p.B, T = p.T;
-  if (g >= B) return;
-  const int b = g;
-  const int u0 = j * kUW8;
-  float* XG = reinterpret_cast<float*>(p.ctr);          // [2][2][B][4U]
-  unsigned* XID = p.ctr + (size_t)16 * B * kU;
-
-  // lane = k-slice 16 lane .. 16 lane + 15 of the 4U-long gate-gradient rows; the wave's units
-  // u = u0 + 4w + a (a < 4): LSTM2's recurrent row W2[U+u] and input row W2[u] in registers,
-  // LSTM1's recurrent row W1r[u] in LDS
-  float4 wa[4][4], wb[4][4];
-#pragma unroll
-  for (int a = 0; a < 4; ++a) {
-    const int u = u0 + 4 * w + a;
-    const float4* ra = reinterpret_cast<const float4*>(p.W2 + (int64_t)(kU + u) * 4 * kU) + 4 * lane;
-    const float4* rb = reinterpret_cast<const float4*>(p.W2 + (int64_t)u * 4 * kU) + 4 * lane;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      wa[a][q] = ra[q];
-      wb[a][q] = rb[q];
-    }
-  }
-  for (int i = tid; i < kW8 * 4 * 4 * 64; i += kThreads) {
-    const int l = i & 63, q = (i >> 6) & 3, a = (i >> 8) & 3, ww = i >> 10;
-    w1l[i] = reinterpret_cast<const float4*>(p.W1r + (int64_t)(u0 + 4 * ww + a) * 4 * kU)[4 * l + q];
-  }
-  // cell role: output m = lane >> 2 = a * 4 + prod (prod 0: r2 -> LSTM2, 2: r1 -> LSTM1)
-  const int m = lane >> 2, prod = m & 3, pa = m >> 2;
-  const int pu = u0 + 4 * w + pa;
-  const bool cell = (lane & 3) == 0 && (prod == 0 || prod == 2);
-  const int layer = prod == 0 ? 2 : 1;
-  float dhc = 0.f, dcc = 0.f;
-  const bool masked = p.m1c != nullptr;
-  const auto rXG = rsrc(XG);
-  auto load_ops = [&](int jj, float4& g4, float& cp, float& dyv, float& mc, float& mh) {
-    const int t = layer == 2 ? T - 1 - jj : T - jj;
-    const bool on = cell && t >= 0 && t < T;
-    const int64_t bu = on ? ((int64_t)t * B + b) * kU + pu : 0;
-    const float* Gp = layer == 2 ? p.G2 : p.G1;
-    const float* Cs = layer == 2 ? p.C2S : p.C1S;
-    const float* Mc = masked ? (layer == 2 ? p.m2c : p.m1c) : Cs;
-    const float* Mh = masked ? (layer == 2 ? p.m2h : p.m1h) : Cs;
-    g4 = reinterpret_cast<const float4*>(Gp)[bu];
-    cp = Cs[bu];
-    dyv = p.DH2[bu];
-    mc = Mc[bu];
-    mh = Mh[bu];
-  };
-  float4 g4n;
-  float cpn, dyn, mcn, mhn;
-  load_ops(0, g4n, cpn, dyn, mcn, mhn);
-  __syncthreads();
-  const bool xl = (p.flags & 1) ? xcd_local_group(XID, g, kG8, kW8, p.err) : false;
-  bool gave_up = false;
-
-  for (int jj = 0; jj <= T; ++jj) {
-    const int t2 = T - 1 - jj, t1 = T - jj;
-    const bool has2 = t2 >= 0, has1 = jj >= 1;
-    const bool stage2 = jj >= 1, stage1 = jj >= 2;   // DG2[t2+1] and DG1[t1+1] exist
-    const int t = layer == 2 ? t2 : t1;
-    const bool cell_step = cell && (layer == 2 ? has2 : has1);
-    const float4 g4 = g4n;
-    const float cp = cpn, dyv = dyn;
-    const float mc = masked ? mcn : 1.f - p.zc, mh = masked ? mhn : 1.f - p.zh;
-    float* dg2s = dgb[jj & 1][0];
-    float* dg1s = dgb[jj & 1][1];
-    // stage dgates2_{t2+1} (stream 0, q = jj - 1) and dgates1_{t1+1} (stream 1, q = jj - 2) of
-    // the utterance: thread = (stream tid / U, float4 column tid % U), one sc1 float4 each
-    {
-      const int st = tid / kU, q = tid - st * kU;
-      const int qs = st == 0 ? jj - 1 : jj - 2;
-      const bool need = st == 0 ? stage2 : stage1;
-      const int idx = ((((qs & 1) * 2 + st) * B + b) * kU) + q;
-      const unsigned want = lsb_tag(qs);
-      float4 v = ldc4(rXG, idx);
-      bool ok = !need || tag_ok4(v, want);
-      if (__builtin_amdgcn_ballot_w64(!ok) != 0 && !gave_up) {
-        for (unsigned spins = 0;; ++spins) {
-          if (!ok) v = ldc4(rXG, idx);
-          ok = ok || tag_ok4(v, want);
-          if (__builtin_amdgcn_ballot_w64(!ok) == 0) break;
-          if (poll_give_up(spins, p.err)) { gave_up = true; break; }
-          __builtin_amdgcn_s_sleep(1);
-        }
-      }
-      *reinterpret_cast<float4*>(&(st == 0 ? dg2s : dg1s)[4 * q]) = v;
-    }
-    if (jj < T) load_ops(jj + 1, g4n, cpn, dyn, mcn, mhn);   // in flight across the barrier
-    lds_barrier();   // (a __syncthreads would drain them: its release fence waits on vmcnt)
-    float v[16];
-#pragma unroll
-    for (int a = 0; a < 4; ++a) {
-      float r2 = 0.f, y1 = 0.f, r1 = 0.f;
-      if (stage2) {
-        const float4* d2 = reinterpret_cast<const float4*>(dg2s) + 4 * lane;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const float4 x = d2[q];
-          r2 = dot4(x, wa[a][q], r2);
-          y1 = dot4(x, wb[a][q], y1);
-        }
-      }
-      if (stage1) {
-        const float4* d1 = reinterpret_cast<const float4*>(dg1s) + 4 * lane;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) r1 = dot4(d1[q], w1l[lds8_idx(w, a, q, lane)], r1);
-      }
-      v[a * 4 + 0] = r2;
-      v[a * 4 + 1] = y1;
-      v[a * 4 + 2] = r1;
-      v[a * 4 + 3] = 0.f;
-    }
-    transpose_reduce16(v, lane);
-    const float y1v = dpp_mov<0x114>(v[0]);     // row_shr:4: y1 sits one output (4 lanes) below
-    if (cell_step) {
-      const float rec = layer == 2 ? (stage2 ? v[0] : 0.f) : (stage1 ? v[0] : 0.f);
-      const float dy = layer == 2 ? dyv : y1v;
-      const int qs = layer == 2 ? jj : jj - 1;            // the stream's sequence number
-      const float4 dg = tagf4(lstm_cell_bwd(g4, cp, dy, rec, mc, mh, dhc, dcc), lsb_tag(qs));
-      const int64_t bu = ((int64_t)t * B + b) * kU + pu;
-      reinterpret_cast<float4*>(layer == 2 ? p.DG2 : p.DG1)[bu] = dg;   // history (GEMMs)
-      stc4x(xl, rXG, ((((qs & 1) * 2 + (layer == 2 ? 0 : 1)) * B + b) * kU) + pu, dg);
-    }
-  }
-}
-
-// the 8-workgroups-per-utterance kernels only with SAT_LSTM8=1: measured slower (fwd 2.94 vs
-// 2.63, BPTT 3.32 vs 2.50 us/step; the LDS-resident third of the weights costs more per step than
-// the 8-producer hand-off saves)
-static bool lstm8_enabled() {
-  const char* e = getenv("SAT_LSTM8");
-  return e && e[0] == '1';
-}
-
 int check_coresident(const void* kernel, const char* name) {
   int dev = 0, cus = 0, per_cu = 0;
   if (hipGetDevice(&dev) != hipSuccess ||
@@ -983,9 +557,7 @@ extern "C" int sat_decoder_lstms_fwd(const SatDecLstmFwd* a, void* stream) {
                 aligned16(a->W1r) && aligned16(a->W2) && aligned16(a->xch),
                 "%s: 16-byte aligned operands", nm);
   SAT_CHECK_ARG((int64_t)(a->T + 1) * a->B * 4 * kU < (1ll << 29), "%s: histories too long", nm);
-  const bool l8 = lstm8_enabled();
-  int rc = check_coresident(l8 ? reinterpret_cast<const void*>(dec_lstm8_fwd_kernel)
-                               : reinterpret_cast<const void*>(dec_lstm_fwd_kernel), nm);
+  int rc = check_coresident(reinterpret_cast<const void*>(dec_lstm_fwd_kernel), nm);
   if (rc != SAT_OK) return rc;
   DecLstmFwdP p;
   p.B = a->B; p.T = a->T; p.zc = a->zc; p.zh = a->zh;
@@ -1000,8 +572,7 @@ extern "C" int sat_decoder_lstms_fwd(const SatDecLstmFwd* a, void* stream) {
     set_error("%s: memset failed", nm);
     return SAT_ERR_HIP;
   }
-  if (l8) hipLaunchKernelGGL(dec_lstm8_fwd_kernel, dim3(kG8 * kW8), dim3(kThreads), 0, s, p);
-  else hipLaunchKernelGGL(dec_lstm_fwd_kernel, dim3(kG * kGW), dim3(kThreads), 0, s, p);
+  hipLaunchKernelGGL(dec_lstm_fwd_kernel, dim3(kG * kGW), dim3(kThreads), 0, s, p);
   SAT_LAUNCH_CHECK(nm);
   return SAT_OK;
 }
@@ -1020,9 +591,7 @@ extern "C" int sat_decoder_lstms_bwd(const SatDecLstmBwd* a, void* stream) {
   SAT_CHECK_ARG(aligned16(a->W1r) && aligned16(a->W2) && aligned16(a->G1) && aligned16(a->G2) &&
                 aligned16(a->DG1) && aligned16(a->DG2), "%s: 16-byte aligned operands", nm);
   SAT_CHECK_ARG((int64_t)a->T * a->B * 4 * kU < (1ll << 29), "%s: histories too long", nm);
-  const bool l8 = lstm8_enabled();
-  int rc = check_coresident(l8 ? reinterpret_cast<const void*>(dec_lstm8_bwd_kernel)
-                               : reinterpret_cast<const void*>(dec_lstm_bwd_kernel), nm);
+  int rc = check_coresident(reinterpret_cast<const void*>(dec_lstm_bwd_kernel), nm);
   if (rc != SAT_OK) return rc;
   DecLstmBwdP p;
   p.B = a->B; p.T = a->T; p.zc = a->zc; p.zh = a->zh;
@@ -1037,8 +606,7 @@ extern "C" int sat_decoder_lstms_bwd(const SatDecLstmBwd* a, void* stream) {
     set_error("%s: memset failed", nm);
     return SAT_ERR_HIP;
   }
-  if (l8) hipLaunchKernelGGL(dec_lstm8_bwd_kernel, dim3(kG8 * kW8), dim3(kThreads), 0, s, p);
-  else hipLaunchKernelGGL(dec_lstm_bwd_kernel, dim3(kG * kGW), dim3(kThreads), 0, s, p);
+  hipLaunchKernelGGL(dec_lstm_bwd_kernel, dim3(kG * kGW), dim3(kThreads), 0, s, p);
   SAT_LAUNCH_CHECK(nm);
   return SAT_OK;
 }

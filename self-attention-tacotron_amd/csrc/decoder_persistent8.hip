@@ -63,6 +63,26 @@
 #define SAT_FWD8_HMERGE 1
 #endif
 
+#ifndef SAT_FWD8_R1
+// the S1 / S2 / ST history stores of step t-1 on wave 7 in the location-term window (where it
+// holds no positions and idles until record A_t arrives) instead of the combine window, where
+// the trace showed wave 7 finishing last (1.51 vs <= 1.39 us into the step): with R2,
+// 5.16 -> 5.10 us/step (two A/B rounds on one box, profiles/r06i_fwd8_rebalance_ab.txt)
+#define SAT_FWD8_R1 1
+#endif
+#ifndef SAT_FWD8_R2
+// record B's halo words published by wave 7 at the start of the statistics phase (the energies
+// and alpha_{t-1} are final there) instead of by wave 1 after its contexts: wave 1, which also
+// publishes the statistics, was the group's last B publisher in the trace: with R1,
+// 5.21 -> 5.10 us/step
+#define SAT_FWD8_R2 1
+#endif
+#ifndef SAT_FWD8_C2W
+// the wave that forms the 32 c2 partial contexts besides its own c1 columns (A/B: wave 3, the
+// trace's earliest B publisher, measured 5.10 -> 5.14 us/step against wave 0)
+#define SAT_FWD8_C2W 0
+#endif
+
 namespace sat {
 namespace {
 
@@ -303,8 +323,36 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
   long long* gevt = (p.prof && g == 0) ? p.prof + 256 * 16 + 8 * 8 * 20 + j * 4 : nullptr;
 #endif
 
+  // e_{t-1}(n) on the window around the own positions, -inf where masked (the own energies of
+  // step t-1 in eown until the energies phase of step t rewrites them; the neighbours' in halo)
+  auto e_at = [&](int n) -> float {
+    if (n < 0 || n >= len) return -INFINITY;
+    if (n < n0) return halo[n - n0 + kPadL];
+    if (n < n0 + nt) return eown[n - n0];
+    return halo[kPadL + (n - n0 - nt)];
+  };
+  // step t-1's histories S1 / S2 / ST (normalised alignments of both sources, statistics)
+  auto store_hist = [&](int tt, int lane_, float M1, float Z1, float A1, float M2, float Z2) {
+    const int ss = tt - 1;
+    if (lane_ >= kPadL && lane_ < nt + kPadL) {
+      const float e = e_at(n0 - kPadL + lane_);
+      p.S1[((int64_t)tt * B + b) * N + n0 + lane_ - kPadL] =
+          e == -INFINITY ? 0.f : __expf(e - M1) * __builtin_amdgcn_rcpf(Z1);
+    }
+    if (lane_ < nt) {
+      const float e2 = e2own[lane_];
+      p.S2[((int64_t)ss * B + b) * N + n0 + lane_] =
+          e2 == -INFINITY ? 0.f : __expf(e2 - M2) * __builtin_amdgcn_rcpf(Z2);
+    }
+    if (j == 0 && lane_ == 0) {
+      float* stp = p.ST + ((int64_t)ss * B + b) * 4;
+      stp[0] = M1; stp[1] = Z1; stp[2] = A1 / Z1; stp[3] = Z2;
+    }
+  };
+
   for (int t = 0; t <= T; ++t) {
     const int s = t - 1;
+    float M1 = 0.f, Z1 = 1.f, A1 = 1.f, M2 = 0.f, Z2 = 1.f;   // statistics of step t-1
     // lane-dependent indices re-derived from an opaque copy of the thread id every step: the
     // compiler cannot hoist per-lane addresses out of the loop (which kept ~150 of them live
     // and spilled the register-resident weights)
@@ -404,10 +452,12 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
         const int jj = lane & 7;
         const float4 st = recs[jj][0];
         const float z2 = recs[jj][1].x;
-        const float M1 = lanes8_max(st.x), M2 = lanes8_max(st.w);
+        M1 = lanes8_max(st.x);
+        M2 = lanes8_max(st.w);
         const float sc1 = __expf(st.x - M1), sc2 = __expf(st.w - M2);
-        const float Z1 = lanes8_sum(st.y * sc1), A1 = lanes8_sum(st.z * sc1);
-        const float Z2 = lanes8_sum(z2 * sc2);
+        Z1 = lanes8_sum(st.y * sc1);
+        A1 = lanes8_sum(st.z * sc1);
+        Z2 = lanes8_sum(z2 * sc2);
         if (wave < (kC + 63) / 64) {
           if (tid < kC) {
             const bool first = wave < kM1 / 64;    // wave-uniform: c1 dims (waves 0..3) or c2
@@ -424,12 +474,6 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
           }
         } else {
           const unsigned bit = lsb_tag(t);
-          auto e_at = [&](int n) -> float {       // e_{t-1}(n) on the window, -inf where masked
-            if (n < 0 || n >= len) return -INFINITY;
-            if (n < n0) return halo[n - n0 + kPadL];
-            if (n < n0 + nt) return eown[n - n0];
-            return halo[kPadL + (n - n0 - nt)];
-          };
           if (wave == 5) {
             // s_{t-1} = softmax on n0-4 .. n0+nt+4, then (same wave, no barrier) the location
             // features f_t of the own positions for the LOC history of the BPTT
@@ -465,20 +509,22 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
           // wave 7 (idle in this window): the S1 / S2 / ST history stores (S1 recomputed with
           // wave 5's arithmetic: the same bits), off waves 5 and 6 whose LDS results the next
           // phases wait for
-          if (SAT_FWD8_NORM3 ? wave == 7 : wave == 6) {
-            if (SAT_FWD8_NORM3 && lane >= kPadL && lane < nt + kPadL) {
-              const float e = e_at(n0 - kPadL + lane);
-              p.S1[((int64_t)t * B + b) * N + n0 + lane - kPadL] =
-                  e == -INFINITY ? 0.f : __expf(e - M1) * __builtin_amdgcn_rcpf(Z1);
-            }
-            if (lane < nt) {
-              const float e2 = e2own[lane];
-              p.S2[((int64_t)s * B + b) * N + n0 + lane] =
-                  e2 == -INFINITY ? 0.f : __expf(e2 - M2) * __builtin_amdgcn_rcpf(Z2);
-            }
-            if (j == 0 && lane == 0) {
-              float* stp = p.ST + ((int64_t)s * B + b) * 4;
-              stp[0] = M1; stp[1] = Z1; stp[2] = A1 / Z1; stp[3] = Z2;
+          // (deferred to wave 7's location-term window when it idles there, SAT_FWD8_R1; the
+          // last step's here)
+          const bool defer = SAT_FWD8_R1 && w7_stores && t < T;
+          if (SAT_FWD8_NORM3 ? (wave == 7 && !defer) : wave == 6) {
+            if (SAT_FWD8_NORM3) {
+              store_hist(t, lane, M1, Z1, A1, M2, Z2);
+            } else {
+              if (lane < nt) {
+                const float e2 = e2own[lane];
+                p.S2[((int64_t)s * B + b) * N + n0 + lane] =
+                    e2 == -INFINITY ? 0.f : __expf(e2 - M2) * __builtin_amdgcn_rcpf(Z2);
+              }
+              if (j == 0 && lane == 0) {
+                float* stp = p.ST + ((int64_t)s * B + b) * 4;
+                stp[0] = M1; stp[1] = Z1; stp[2] = A1 / Z1; stp[3] = Z2;
+              }
             }
           }
         }
@@ -607,6 +653,8 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
     //                 10-tap product (modules/forward_attention.py:98-101)
     // energy role: lane = dim chunk c (4 dims of [D1 | D2]), wave = positions 4w .. 4w+3
     float4 Lr[4];
+    if (SAT_FWD8_R1 && SAT_FWD8_NORM3 && w7_stores && wave == 7 && t > 0)
+      store_hist(t, lane, M1, Z1, A1, M2, Z2);   // wave 7 holds no positions: idle here
     if (4 * wave < nt) {
       const int c = lane;
 #pragma unroll
@@ -750,6 +798,17 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
     {
       const unsigned bit = lsb_tag(t);
       const float* al = alf[t & 1];            // alpha_{t-1} at n0-1+k
+      if (SAT_FWD8_R2 && wave == 7 && lane < kPadR + kPadL + 2) {
+        // record B's halo words (first 5 / last 4 energies, last 2 alpha_{t-1}): final since the
+        // energies barrier
+        const int rb = (((t & 1) * B + b) * kW + j) * kRB;
+        const int q = lane;
+        float v;
+        if (q < kPadR) v = q < nt ? eown[q] : -INFINITY;
+        else if (q < kPadR + kPadL) { const int i = nt - kPadL + (q - kPadR); v = i >= 0 ? eown[i] : -INFINITY; }
+        else { const int k = nt - 1 + (q - kPadR - kPadL); v = k >= 0 ? al[k] : 0.f; }
+        stcx(xl, rRB, rb + kRBeh + q, tagf(v == -INFINITY ? 0.f : v, bit));
+      }
       const float e1v = lane < kPmax ? eown[lane] : -INFINITY;
       const float e2v = lane < kPmax ? e2own[lane] : -INFINITY;
       const float m1 = tagf(fmaxf(wave_max_dpp(e1v), -3.402823466e38f), bit);
@@ -772,8 +831,8 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
     tick(13);
     ev(14);
     // partial contexts, published per wave: wave w owns c1 columns 32w .. 32w+31 (lane l:
-    // column 32w + (l & 31), positions 16 (l >> 5) .. + 15); wave 0 also the 32 c2 columns;
-    // wave 1 the halo words (first 5 / last 4 energies, last 2 alpha_{t-1})
+    // column 32w + (l & 31), positions 16 (l >> 5) .. + 15); wave SAT_FWD8_C2W also the 32 c2
+    // columns; wave 1 the halo words unless SAT_FWD8_R2 (then wave 7 in the statistics phase)
     {
       const unsigned bit = lsb_tag(t);
       const int rb = (((t & 1) * B + b) * kW + j) * kRB;
@@ -791,15 +850,15 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
       const float4 c4 = quad_gather(fold32(c));
       if (lane < 32 && (lane & 3) == 0)
         stc4x(xl, rRB, (rb + kRBctx) / 4 + 8 * wave + (lane >> 2), tagf4(c4, bit));
-      if (wave == 0) {
-        const float* ws2 = &wsc[0][1][r0];
+      if (wave == SAT_FWD8_C2W) {
+        const float* ws2 = &wsc[SAT_FWD8_C2W][1][r0];
         float c2 = 0.f;
 #pragma unroll
         for (int k = 0; k < 16; ++k) c2 = fmaf(ws2[k], v2s[r0 + k][col], c2);
         const float4 q4 = quad_gather(fold32(c2));
         if (lane < 32 && (lane & 3) == 0)
           stc4x(xl, rRB, (rb + kRBctx + kM1) / 4 + (lane >> 2), tagf4(q4, bit));
-      } else if (wave == 1 && lane < kPadR + kPadL + 2) {
+      } else if (!SAT_FWD8_R2 && wave == 1 && lane < kPadR + kPadL + 2) {
         const int q = lane;
         float v;
         if (q < kPadR) v = q < nt ? eown[q] : -INFINITY;

@@ -77,6 +77,12 @@
 // 5.21 -> 5.10 us/step
 #define SAT_FWD8_R2 1
 #endif
+#ifndef SAT_FWD8_STW
+#define SAT_FWD8_STW 1   // the wave that sums and publishes record B's statistics words
+#endif
+#ifndef SAT_FWD8_R4
+#define SAT_FWD8_R4 0    // A/B: the AL1 history store on wave 7 in the location window
+#endif
 #ifndef SAT_FWD8_C2W
 // the wave that forms the 32 c2 partial contexts besides its own c1 columns (A/B: wave 3, the
 // trace's earliest B publisher, measured 5.10 -> 5.14 us/step against wave 0)
@@ -503,7 +509,8 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
               }
               const float at = tagf(av, bit);
               alf[t & 1][k] = at;
-              if (k >= 1) p.AL1[((int64_t)t * B + b) * N + n] = at;
+              if (k >= 1 && !(SAT_FWD8_R4 && w7_stores && t < T))
+                p.AL1[((int64_t)t * B + b) * N + n] = at;
             }
           }
           // wave 7 (idle in this window): the S1 / S2 / ST history stores (S1 recomputed with
@@ -655,6 +662,9 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
     float4 Lr[4];
     if (SAT_FWD8_R1 && SAT_FWD8_NORM3 && w7_stores && wave == 7 && t > 0)
       store_hist(t, lane, M1, Z1, A1, M2, Z2);   // wave 7 holds no positions: idle here
+    if (SAT_FWD8_R4 && w7_stores && wave == 7 && t > 0 && lane >= 1 && lane <= nt &&
+        n0 - 1 + lane >= 0)
+      p.AL1[((int64_t)t * B + b) * N + n0 - 1 + lane] = alf[t & 1][lane];   // alpha_{t-1}
     if (4 * wave < nt) {
       const int c = lane;
 #pragma unroll
@@ -817,7 +827,7 @@ __global__ void __launch_bounds__(kTh) dec_attn_fwd8_kernel(Fwd8P p) {
       const float pe2 = e2v == -INFINITY ? 0.f : __expf(e2v - m2);
       const float w = lane < nt ? ((1.f - u) * al[lane + 1] + u * al[lane] + 1e-7f) * pe : 0.f;
       if (lane < kPmax) { wsc[wave][0][lane] = w; wsc[wave][1][lane] = lane < nt ? pe2 : 0.f; }
-      if (wave == 1) {
+      if (wave == SAT_FWD8_STW) {
         const float z1 = tagf(wave_sum_dpp(pe), bit), a1 = tagf(wave_sum_dpp(w), bit);
         const float z2 = tagf(wave_sum_dpp(pe2), bit);
         if (lane == 0) {

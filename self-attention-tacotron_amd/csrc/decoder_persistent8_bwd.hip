@@ -28,6 +28,18 @@
 #include "sat_common.h"
 #include "persistent.h"
 
+#ifndef SAT_BWD8_ZSUM
+// every wave forms dq_t itself from the 8 staged Q partials (no wave-0 sum + second barrier),
+// bitwise the same dq: 5.80-5.82 -> 5.74-5.77 us/step (two A/B rounds on one box, round 6)
+#define SAT_BWD8_ZSUM 1
+#endif
+#ifndef SAT_BWD8_MERGE3
+// A/B: the per-position scalar chain (3b) on the lanes of the wave that owns the position,
+// right after its DA / DS2 reduction (3a), instead of on wave 0 alone between two extra
+// barriers -- correct (tests green) but 5.77-5.79 vs 5.74-5.77 us/step with ZSUM: not kept
+#define SAT_BWD8_MERGE3 0
+#endif
+
 namespace sat {
 namespace {
 
@@ -188,8 +200,14 @@ __global__ void __launch_bounds__(kTh) dec_attn_bwd8_kernel(Bwd8P p) {
     const int64_t tb1 = (int64_t)(t + 1) * B + b, tb0 = (int64_t)t * B + b;
     y.cv = tid < kC ? p.REC0[tb1 * kK0 + tid] : 0.f;
     y.dv = tid < kC ? p.RD[tb0 * kK0 + tid] : 0.f;
+#if SAT_BWD8_MERGE3
+    const int pr = 4 * wave + (lane >> 3);
+    const bool pos = (lane & 7) == 0 && lane < 32 && pr < nt;
+    const int n = n0 + pr;
+#else
     const bool pos = tid < nt;
     const int n = n0 + tid;
+#endif
     y.st = pos ? p.S1[tb1 * N + n] : 0.f;
     y.s2 = pos ? p.S2[tb0 * N + n] : 0.f;
     y.apn = pos ? p.AL1[tb0 * N + n] : 0.f;
@@ -342,6 +360,48 @@ __global__ void __launch_bounds__(kTh) dec_attn_bwd8_kernel(Bwd8P p) {
         e[4 + i] = c;
       }
       transpose_reduce8(e, lane);              // lanes 8m: m < 4 DA(4w+m), m >= 4 DS2(4w+m-4)
+#if SAT_BWD8_MERGE3
+      // ---- 3b on the owning wave: lane 8m (m < 4) runs position r = 4w + m's scalar chain
+      //      with DS2 brought over from lane 8m + 32 (v_permlane32_swap) and the position's
+      //      history operands prefetched into that lane (prefetch_y)
+      {
+        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(e[0]), __float_as_uint(e[0]),
+                                                         false, false);
+        const float ds2v = __uint_as_float(sw[1]);       // lane l < 32: lane l + 32's value
+        const float s1 = (red[0] + red[1]) + (red[2] + red[3]), s3 = red[4];
+        float P1n = 0.f, P2n = 0.f;
+#pragma unroll
+        for (int k = 0; k < kW; ++k) { P1n += pst[k][0]; P2n += pst[k][1]; }
+        const int r = 4 * wave + (lane >> 3);
+        float p1 = 0.f;
+        if ((lane & 7) == 0 && lane < 32 && r < nt) {
+          const float* yn = ysh[yb];
+          const float dan = (1.f - u) * yn[r] + u * yn[r + 1];
+          const float da = (e[0] + dan - (s1 + P1n)) * __builtin_amdgcn_rcpf(y.sa);
+          const float prior = (1.f - u) * y.apn + u * y.apm;
+          const float ds = dsn[r] + da * (prior + 1e-7f);
+          const float yv = tagf(y.st * da, bit);
+          const float e1v = y.st * (ds - P2n);
+          const float e2v = y.s2 * (ds2v - s3);
+          const int64_t o = ((int64_t)t * B + b) * N + n0 + r;
+          p.DE1[o] = e1v;
+          p.DE2[o] = e2v;
+          ysh[1 - yb][r] = yv;
+          e1S[r] = e1v;
+          e2S[r] = e2v;
+          p1 = yv * prior;
+#pragma unroll
+          for (int f = 0; f < kF; ++f) lfS[r][f] = y.lf[f] - cw[kJF + f];
+        }
+        p1 = wave_sum_dpp(p1);
+        if (lane == 0) pw[wave][0] = p1;
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // own e1S / e2S / lfS for phase 4
+    } else if (lane == 0) {
+      pw[wave][0] = 0.f;                       // no own positions: no P1 partial
+    }
+    tick(4);
+#else
       if ((lane & 7) == 0) {
         const int m = lane >> 3;
         if (m < 4) daS[4 * wave + m] = e[0]; else ds2S[4 * wave + m - 4] = e[0];
@@ -384,6 +444,7 @@ __global__ void __launch_bounds__(kTh) dec_attn_bwd8_kernel(Bwd8P p) {
     tick(5);
     lds_barrier();
     tick(6);
+#endif
     // ---- 4. back through the kept energy tanh: dp = DE v (1 - z^2) (lane = chunk, wave =
     //         positions 4w..4w+3); the dq partial (sum over positions) and dL/df_t
     {
@@ -459,7 +520,14 @@ __global__ void __launch_bounds__(kTh) dec_attn_bwd8_kernel(Bwd8P p) {
       float P2 = 0.f;
 #pragma unroll
       for (int w = 0; w < kW; ++w) P2 += pw[w][1];
-      const float4 pword = tagf4(make_float4(pw[0][0], P2, ysh[1 - yb][0], 0.f), bit);
+#if SAT_BWD8_MERGE3
+      float P1 = 0.f;                          // per-wave partials of the position owners
+#pragma unroll
+      for (int w = 0; w < kW; ++w) P1 += pw[w][0];
+#else
+      const float P1 = pw[0][0];
+#endif
+      const float4 pword = tagf4(make_float4(P1, P2, ysh[1 - yb][0], 0.f), bit);
       const bool head = lane >= 1 && lane <= kHR * kF;                   // n0 .. n0+3
       const bool tail = lane > kHR * kF && lane <= kHR * kF + kHL * kF;  // n0+nt-5 .. n0+nt-1
       const int kh = lane - 1, kt = lane - 1 - kHR * kF;
@@ -489,6 +557,14 @@ __global__ void __launch_bounds__(kTh) dec_attn_bwd8_kernel(Bwd8P p) {
     }
     tick(10);
     lds_barrier();
+#if SAT_BWD8_ZSUM
+    // every wave sums the 8 staged partials of its lane's chunk itself (record order: the same
+    // bits wave 0 formed into qb) -- no wave-0-only phase and no second barrier
+    float4 dqz = qz[0][lane];
+#pragma unroll
+    for (int w = 1; w < kW; ++w) dqz = add4(dqz, qz[w][lane]);
+    if (wave == 0 && j == 0) reinterpret_cast<float4*>(p.DQP + ((int64_t)t * B + b) * kQ)[lane] = dqz;
+#else
     if (wave == 0) {
       float4 a = qz[0][lane];
 #pragma unroll
@@ -497,13 +573,18 @@ __global__ void __launch_bounds__(kTh) dec_attn_bwd8_kernel(Bwd8P p) {
       if (j == 0) reinterpret_cast<float4*>(p.DQP + ((int64_t)t * B + b) * kQ)[lane] = a;
     }
     lds_barrier();
+#endif
     tick(11);
     // ---- 2. the own units' reverse step: query term dq_t . Wq[unit] (wave w, units 4w..4w+3:
     //         row q of the wave holds unit q's sum), recurrent product from the R_{t+1} h rows,
     //         then the cell lane's pointwise reverse step (lstm.hip lstm_bwd_block)
     f2 dgp[8];
     {
+#if SAT_BWD8_ZSUM
+      const float4 dq4 = dqz;
+#else
       const float4 dq4 = *reinterpret_cast<const float4*>(&qb[4 * lane]);
+#endif
       float v[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k) {

@@ -33,6 +33,14 @@
 // bitwise the same dq: 5.80-5.82 -> 5.74-5.77 us/step (two A/B rounds on one box, round 6)
 #define SAT_BWD8_ZSUM 1
 #endif
+// trace builds only: the wave whose lane 0 keeps the segment clocks, and a split of segment 2
+// at the history prefetch (slot 15)
+#ifndef SAT_BWD8_TICKW
+#define SAT_BWD8_TICKW 0
+#endif
+#ifndef SAT_BWD8_TICK15
+#define SAT_BWD8_TICK15 0
+#endif
 #ifndef SAT_BWD8_MERGE3
 // A/B: the per-position scalar chain (3b) on the lanes of the wave that owns the position,
 // right after its DA / DS2 reduction (3a), instead of on wave 0 alone between two extra
@@ -117,7 +125,9 @@ __global__ void __launch_bounds__(kTh) dec_attn_bwd8_kernel(Bwd8P p) {
   __shared__ __attribute__((aligned(16))) float rst[kW][kC + kUW];   // staged R: c part + own h rows
   __shared__ __attribute__((aligned(16))) float4 qst[kW][64];        // staged dq partials / dq reduce
   __shared__ __attribute__((aligned(16))) float dcb[kC];             // dL/dctx_t
+#if !SAT_BWD8_ZSUM
   __shared__ __attribute__((aligned(16))) float qb[kQ];              // dq_t
+#endif
   __shared__ __attribute__((aligned(16))) float wred[kW][kK0];       // row-dot partials per wave
   __shared__ float ysh[2][kPmax + 1];       // Y_{t+1} at n0..n0+nt (last = right neighbour's)
   __shared__ float dfh[2][(kPmax + kHL + kHR) * kF];   // dL/df_{t+1} on n0-5 .. n0+nt+3
@@ -242,7 +252,7 @@ __global__ void __launch_bounds__(kTh) dec_attn_bwd8_kernel(Bwd8P p) {
   const bool xl = (p.flags & 1) ? xcd_local_group(p.XID, g, kGmax, kW, p.err) : false;
   long long t0 = p.prof ? wall_clock64() : 0;
   auto tick = [&](int seg) {
-    if (p.prof && tid0 == 0) {
+    if (p.prof && tid0 == 64 * SAT_BWD8_TICKW) {
       const long long t1 = wall_clock64();
       tp[seg] += t1 - t0;
       t0 = t1;
@@ -333,6 +343,9 @@ __global__ void __launch_bounds__(kTh) dec_attn_bwd8_kernel(Bwd8P p) {
       a = group16_sum(a);
       if (tap == 0) dsn[pos] = a;
     }
+#if SAT_BWD8_TICK15
+    tick(15);
+#endif
     if (t > 0) prefetch_y(t - 1, tid, lane, wave, ypre);
     tick(2);
     lds_barrier();

@@ -83,4 +83,7 @@ rows = [g + 32 * j for g in range(B) for j in range(8)]
 for i, n in enumerate(names):
     col = pr[rows, i]
     print(f"  {n:24s} {float(col.mean()) / Tp:6.3f} us/step (max {float(col.max()) / Tp:6.3f})")
+if float(pr[rows, 15].sum()) > 0:
+    print(f"  {'  of which before prefetch':24s} {float(pr[rows, 15].mean()) / Tp:6.3f} us/step "
+          "(slot 15; segment 2 is then the prefetch issue alone)")
 print(f"  total {float(pr[rows].sum(1).mean()) / Tp:.3f} us/step")

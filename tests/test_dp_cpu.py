@@ -1,5 +1,5 @@
-"""N>1 data-parallel path under ``gloo`` (world_size 2, CPU): the same dp.py functions and
-Trainer.reduce_grads the bench runs over RCCL on the GPUs."""
+"""N>1 data-parallel path under ``gloo`` (world_size 2, and 8 = C3's rank count, CPU): the same
+dp.py functions and Trainer.reduce_grads the bench runs over RCCL on the GPUs."""
 import os
 import socket
 import types
@@ -67,7 +67,11 @@ def _worker(rank, world, port, q):
         tdist.all_reduce = real
         res["collectives"] = list(calls)
         gsum = sum(local_grad(r) for r in range(world))
-        res["sum"] = bool(torch.equal(model.grads, gsum))
+        # world 2: a two-term sum is the same in any order (bitwise); at world 8 the backend's
+        # reduction order differs from rank order in the last bits
+        res["sum_err"] = float((model.grads - gsum).abs().max())
+        res["sum"] = bool(torch.equal(model.grads, gsum)) if world == 2 else \
+            bool(torch.allclose(model.grads, gsum, rtol=1e-6, atol=1e-9))
         res["scale"] = tr.cfg.grad_scale
         res["world"] = tr.world
         # BatchNorm moving statistics: the mean of the replicas' buffers
@@ -93,7 +97,9 @@ def _worker(rank, world, port, q):
 
         p_dp = adam_steps(lambda: model.grads.double() * tr.cfg.grad_scale)
         p_one = adam_steps(lambda: sum(local_grad(r).double() for r in range(world)) / world)
-        res["matches_single"] = bool(torch.allclose(p_dp, p_one, rtol=0, atol=1e-12))
+        # (world 8: the fp32 collective's summation order shows in the last bits of the update)
+        res["matches_single"] = bool(torch.allclose(p_dp, p_one, rtol=0,
+                                                    atol=1e-12 if world == 2 else 1e-9))
         gathered = [torch.empty_like(p_dp) for _ in range(world)]
         tdist.all_gather(gathered, p_dp)
         res["replicas_equal"] = all(torch.equal(gathered[0], x) for x in gathered[1:])
@@ -123,7 +129,12 @@ def _worker(rank, world, port, q):
         t2.reduce_grads()
         tdist.all_reduce = real
         res["bucket_collectives"] = list(calls)
-        res["bucket_equal"] = bool(torch.equal(m1.exchange, m2.exchange)) and \
+        # bitwise at world 2; at world 8 the ring's per-chunk summation order depends on the
+        # collective's length, so the bucketed ranges may differ from the single one in the
+        # last bits (dp.exchange); health words are exact either way
+        same = torch.equal if world == 2 else \
+            (lambda a, b: torch.allclose(a, b, rtol=1e-6, atol=1e-9))
+        res["bucket_equal"] = bool(same(m1.exchange, m2.exchange)) and \
             bool(torch.equal(m1.health, m2.health))
         # masks are drawn per replica: the model_fn seed offset differs by rank
         res["seed_offset"] = 1000003 * dp.rank()
@@ -136,28 +147,30 @@ def _worker(rank, world, port, q):
         q.put((rank, repr(e)))
 
 
-def test_dp_world2_gloo():
+@pytest.mark.parametrize("world", [2, 8])
+def test_dp_world_gloo(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    out = dict(q.get(timeout=240) for _ in procs)
+    out = dict(q.get(timeout=300) for _ in procs)
     for p in procs:
         p.join(timeout=60)
-    for r in range(2):
+    for r in range(world):
         res = out[r]
         assert isinstance(res, dict), res
-        assert res["bcast"] and res["sum"] and res["bn"] and res["replicas_equal"]
+        assert res["sum"], res["sum_err"]
+        assert res["bcast"] and res["sum"] and res["bn"] and res["replicas_equal"], res
         assert res["matches_single"]
         assert res["health"][3] == 7 and sum(res["health"]) == 7
         assert res["collectives"] == [4096 + 64 + 16]     # ONE collective per step
         assert res["bucket_equal"]
         assert res["bucket_collectives"] == [4096 - 1024, 1024, 64 + 16]
         assert res["seed_offset"] == 1000003 * r
-        assert res["scale"] == pytest.approx(0.5) and res["world"] == 2
-        assert res["max"] == pytest.approx(1.5)
+        assert res["scale"] == pytest.approx(1.0 / world) and res["world"] == world
+        assert res["max"] == pytest.approx(0.5 + world - 1)
 
 
 def test_single_process_is_identity():

@@ -1300,6 +1300,62 @@ static LdsPlan plan_lds(int M, int N, int K, int nb, bool can_split, int64_t ws_
   return pl;
 }
 
+// Measured plans for the training step's own products (tools/gemm_census.py --sweep on one
+// MI355X, profiles/r06q_gemm_census_sweep.txt: every forced tile / split-K plan of the LDS kernel
+// timed on the step's descriptors): used where the best measured plan beat the cycle model's
+// choice by >= 4 %.  Keyed on the descriptor's (M, N, K, batches, operand modes); any other
+// product, a forced plan (sat_gemm_force_plan) or SAT_GEMM_PLAN_TABLE=0 takes the model.
+struct PlanEntry { int M, N, K, nb, am, bm, tbm, tbn, splits; };
+static const PlanEntry kMeasuredPlans[] = {
+    // decoder: LSTM-stack input projection / its input gradient, the attention-LSTM weight
+    // gradient over [prenet | contexts | h] rows
+    {16000, 1024, 544, 1, A_K, B_N, 128, 128, 1},    // 173.9 -> 160.3 us
+    {16000, 544, 1024, 1, A_K, B_K, 64, 64, 2},      // 187.4 -> 176.9
+    {544, 1024, 16000, 1, A_M, B_N, 64, 64, 12},     // 204.1 -> 194.5
+    // weight gradients of the 128- / 256-wide dense layers (x^T dy over B T' or B N rows)
+    {128, 128, 6400, 1, A_M, B_N, 64, 64, 32},       // 18.3 -> 15.6 (x 8 per step)
+    {256, 256, 6400, 1, A_M, B_N, 64, 64, 12},       // 26.6 -> 23.4
+    {256, 32, 6400, 1, A_M, B_N, 64, 64, 32},        // 18.5 -> 15.4
+    {32, 32, 6400, 1, A_M, B_N, 64, 64, 32},         // 18.0 -> 15.1 (x 2)
+    {256, 128, 16000, 1, A_M, B_N, 64, 64, 24},      // 32.0 -> 27.3
+    {256, 256, 16000, 1, A_M, B_N, 64, 64, 24},      // 42.1 -> 39.8
+    {256, 224, 16000, 1, A_M, B_N, 64, 64, 24},      // 41.7 -> 39.8
+    {200, 256, 500, 32, A_M, B_N, 64, 64, 1},        // 33.1 -> 29.0 (memory values, batched)
+    // encoder / head forward and input gradients at 6400 / 16000 rows
+    {6400, 128, 128, 2, A_K, B_N, 64, 64, 1},        // 11.4 -> 10.2 (x 4)
+    {6400, 256, 256, 1, A_K, B_N, 64, 64, 1},        // 25.8 -> 20.7
+    {6400, 224, 256, 1, A_K, B_N, 64, 64, 1},        // 22.5 -> 18.7
+    {6400, 256, 224, 1, A_K, B_K, 64, 64, 1},        // 22.9 -> 18.4
+    {16000, 128, 256, 1, A_K, B_N, 64, 64, 1},       // 28.1 -> 23.0
+    // CBHG projections (Conv1D K = 3 as im2col products)
+    {6400, 128, 6144, 1, A_IM2COL, B_N, 64, 64, 6},  // 125.2 -> 116.5
+    {6400, 2048, 384, 1, A_IM2COL, B_FLIP, 64, 128, 1},   // 116.3 -> 111.5
+    {6144, 128, 6400, 1, A_IM2COLT, B_N, 64, 128, 8},     // 115.7 -> 111.1
+};
+static bool gemm_plan_table_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("SAT_GEMM_PLAN_TABLE");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+// the measured plan of a product, or {0} (then the cycle model plans it)
+static LdsPlan measured_plan(int M, int N, int K, int nb, int am, int bm, bool can_split,
+                             int64_t ws_bytes, int Mp, int c_div) {
+  if (!gemm_plan_table_enabled() || t_force_bm > 0) return LdsPlan{0, 0, 1, K};
+  for (const PlanEntry& e : kMeasuredPlans) {
+    if (e.M != M || e.N != N || e.K != K || e.nb != nb || e.am != am || e.bm != bm) continue;
+    if (c_div && c_div % e.tbm != 0) break;
+    if (e.splits == 1) return LdsPlan{e.tbm, e.tbn, 1, K};
+    if (!can_split) break;
+    const int kc = (ceil_div(K, e.splits) + BK - 1) / BK * BK;
+    const int se = ceil_div(K, kc);
+    if (se > 1 && (int64_t)se * nb * Mp * N * 4 > ws_bytes) break;
+    return LdsPlan{e.tbm, e.tbn, se, se > 1 ? kc : K};
+  }
+  return LdsPlan{0, 0, 1, K};
+}
+
 template <int BM, int BN, int GRP>
 static hipError_t launch_lds_grp(int am, int bm, dim3 grid, hipStream_t s, const GemmP& p) {
   if constexpr (GRP == 0) return launch_lds_tiles<BM, BN>(am, bm, grid, s, p);
@@ -1371,8 +1427,10 @@ static int launch_lds(const SatGemmDesc* d, GemmP& p, int nb, hipStream_t s) {
   // (a batched split-K: the reduce's epilogue has no per-batch bias / mul / add)
   const bool split_ok = (nb == 1 || (!p.bias && !p.mul && !p.add)) && d->ws != nullptr &&
                         !p.C2 && p.tri == 0;
-  const LdsPlan pl = plan_lds(p.M, d->N, d->K, nb, split_ok, d->ws_bytes,
-                              am == A_IM2COLT ? d->a_C : 0, 0);
+  LdsPlan pl = measured_plan(d->M, d->N, d->K, nb, am, bm, split_ok, d->ws_bytes, p.M,
+                             am == A_IM2COLT ? d->a_C : 0);
+  if (pl.bm == 0)
+    pl = plan_lds(p.M, d->N, d->K, nb, split_ok, d->ws_bytes, am == A_IM2COLT ? d->a_C : 0, 0);
   if (pl.bm == 0) return 1;
   return launch_lds_plan<0>(pl, am, bm, nb, p, s, "sat_gemm");
 }

@@ -44,15 +44,39 @@ struct EncBwdP {
   float* DG[2];
 };
 
-// Forward.  Dot role: thread t owns gate column c = t >> 1 and recurrent rows
-// k = 64 (t & 1) .. +64 of it (64 weights in registers); the pair's partial sums meet by DPP.
+// Forward.  Dot role (SAT_ENC_FWD_T, default): thread t owns gate columns 4cb .. 4cb+3
+// (cb = t >> 3) over recurrent rows 16rg .. 16rg+15 (rg = t & 7): 64 weights in registers, 16
+// state values read from LDS per step (4 ds_read_b128; the former layout -- one column, 64
+// rows per thread -- read 64, and 1024 threads x 256 B of LDS reads per step bound the step at
+// the LDS data path); the 8 row groups' partial sums of the 4 columns meet by a DPP
+// transpose-reduce, after which lanes 2m of each 8-lane group hold column 4cb + m.
 // Cell role: threads u < 128 own unit u's (c, h) state in registers.
+#ifndef SAT_ENC_FWD_T
+#define SAT_ENC_FWD_T 1
+#endif
 __global__ void __launch_bounds__(kTh) enc_lstm_fwd_kernel(EncFwdP p) {
   __shared__ __attribute__((aligned(16))) float hs[kU];
   __shared__ __attribute__((aligned(16))) float gp[kG4];
   const int tid = threadIdx.x;
   const int d = blockIdx.x & 1, b = blockIdx.x >> 1;
   const int N = p.N, B = p.B;
+#if SAT_ENC_FWD_T
+  const int lane = tid & 63;
+  const int cb = tid >> 3, rg = tid & 7;
+  const int c = 4 * cb + 2 * ((lane >> 2) & 1) + ((lane >> 1) & 1);   // column after the reduce
+  const bool hf = (lane & 1) != 0;                                    // false: the writer lane
+  f2 w[16][2];
+  {
+    const float* W = p.W[d];
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+#pragma unroll
+      for (int cp = 0; cp < 2; ++cp) {
+        const float* src = W + (int64_t)(16 * rg + r) * kG4 + 4 * cb + 2 * cp;
+        w[r][cp] = f2{src[0], src[1]};
+      }
+  }
+#else
   const int c = tid >> 1, hf = tid & 1;
   f2 w[32];
   {
@@ -61,6 +85,7 @@ __global__ void __launch_bounds__(kTh) enc_lstm_fwd_kernel(EncFwdP p) {
     for (int i = 0; i < 32; ++i)
       w[i] = f2{W[(int64_t)(64 * hf + 2 * i) * kG4 + c], W[(int64_t)(64 * hf + 2 * i + 1) * kG4 + c]};
   }
+#endif
   const int len = (int)p.lengths[b];
   const bool cell = tid < kU;
   const int u = tid;
@@ -96,6 +121,30 @@ __global__ void __launch_bounds__(kTh) enc_lstm_fwd_kernel(EncFwdP p) {
     const float xv = xn, mc = mcn, mh = mhn;
     xn = load_x(i + 1);
     load_m(i + 1, mcn, mhn);
+#if SAT_ENC_FWD_T
+    {
+      const float4* h4 = reinterpret_cast<const float4*>(&hs[16 * rg]);
+      f2 a0 = {0.f, 0.f}, a1 = {0.f, 0.f}, b0 = {0.f, 0.f}, b1 = {0.f, 0.f};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 h = h4[q];
+        a0 = __builtin_elementwise_fma(f2{h.x, h.x}, w[4 * q][0], a0);
+        a1 = __builtin_elementwise_fma(f2{h.x, h.x}, w[4 * q][1], a1);
+        b0 = __builtin_elementwise_fma(f2{h.y, h.y}, w[4 * q + 1][0], b0);
+        b1 = __builtin_elementwise_fma(f2{h.y, h.y}, w[4 * q + 1][1], b1);
+        a0 = __builtin_elementwise_fma(f2{h.z, h.z}, w[4 * q + 2][0], a0);
+        a1 = __builtin_elementwise_fma(f2{h.z, h.z}, w[4 * q + 2][1], a1);
+        b0 = __builtin_elementwise_fma(f2{h.w, h.w}, w[4 * q + 3][0], b0);
+        b1 = __builtin_elementwise_fma(f2{h.w, h.w}, w[4 * q + 3][1], b1);
+      }
+      const f2 s0 = a0 + b0, s1 = a1 + b1;
+      float v[4] = {s0.x, s0.y, s1.x, s1.y};
+      tr_dpp<4, 2>(v, lane);               // lane bit 2: columns {0, 1} | {2, 3}
+      tr_dpp<2, 1>(v, lane);               // lane bit 1: the column within the pair
+      v[0] += dpp_mov<0xB1>(v[0]);         // lane bit 0: the last pair of row groups
+      if (!hf) gp[c] = v[0] + xv;
+    }
+#else
     // ---- gate pre-activations: column c, rows 64 hf .. 64 hf + 63
     {
       const float4* h4 = reinterpret_cast<const float4*>(&hs[64 * hf]);
@@ -110,6 +159,7 @@ __global__ void __launch_bounds__(kTh) enc_lstm_fwd_kernel(EncFwdP p) {
       acc += dpp<0xB1>(acc);                // the pair (lanes t, t ^ 1) of column c
       if (hf == 0) gp[c] = acc + xv;
     }
+#endif
     // LDS-only barriers: a __syncthreads would also drain the prefetch and the history stores
     lds_barrier();
     // ---- cell

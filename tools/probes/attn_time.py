@@ -1,6 +1,6 @@
 """HIP-event time of the two attention-chain launches (sat_decoder_attention_fwd / _bwd), the
 attention parameter-gradient pass (sat_attn_param_grads) and the decoder LSTM stack
-(sat_decoder_lstms_fwd / _bwd) on the
+(sat_decoder_lstms_fwd / _bwd) and the encoder BiLSTM (sat_encoder_lstm_fwd / _bwd) on the
 training step's own buffers (B=32, N=200, T'=500, train mode) with whichever library is loaded
 (tools only; A/B two builds by running this twice, once with SAT_LIB_OVERRIDE=<other .so>).
 Also prints a checksum of the forward's histories and the BPTT outputs so two builds' results
@@ -22,7 +22,7 @@ from sat_amd import kernels as K  # noqa: E402
 
 KW = {}
 NAMES = ("decoder_attention_fwd", "decoder_attention_bwd", "attn_param_grads",
-         "decoder_lstms_fwd", "decoder_lstms_bwd")
+         "decoder_lstms_fwd", "decoder_lstms_bwd", "encoder_lstm_fwd", "encoder_lstm_bwd")
 for nm in NAMES:
     orig = getattr(K, nm)
 
@@ -74,4 +74,7 @@ sums = {k: float(f[k].double().sum()) for k in ("REC0", "Q", "AL1", "S2", "ZH")}
 sums.update({k: float(bw[k].double().sum()) for k in ("DG0", "DE1", "RD")})
 pg = KW["attn_param_grads"]
 sums.update({k: float(pg[k].double().sum()) for k in ("dK1", "dK2", "pg")})
+ef, eb = KW["encoder_lstm_fwd"], KW["encoder_lstm_bwd"]
+sums.update({"encH": float(ef["H"].double().sum()), "encG": float(ef["G_fw"].double().sum()),
+             "encDG": float(eb["DG_fw"].double().sum())})
 print("  checksums " + " ".join(f"{k}={v:.9e}" for k, v in sums.items()), flush=True)

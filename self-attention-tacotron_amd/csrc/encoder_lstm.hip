@@ -51,6 +51,12 @@ struct EncBwdP {
 // the LDS data path); the 8 row groups' partial sums of the 4 columns meet by a DPP
 // transpose-reduce, after which lanes 2m of each 8-lane group hold column 4cb + m.
 // Cell role: threads u < 128 own unit u's (c, h) state in registers.
+// SAT_ENC_DRAIN_CELL: wait for the step's operand prefetch right before the cell (whose stores
+// then stay in flight into the next step) instead of at the loop's back edge, where the
+// compiler's vmcnt(0) also waits for the cell's stores
+#ifndef SAT_ENC_DRAIN_CELL
+#define SAT_ENC_DRAIN_CELL 1
+#endif
 #ifndef SAT_ENC_FWD_T
 #define SAT_ENC_FWD_T 1
 #endif
@@ -114,6 +120,11 @@ __global__ void __launch_bounds__(kTh) enc_lstm_fwd_kernel(EncFwdP p) {
   };
   float xn = load_x(0), mcn, mhn;
   load_m(0, mcn, mhn);
+  // the register-resident weights (and the first operands) land before the step loop, in the
+  // compiler-visible form: left pending at the loop header, the waits for them are placed at
+  // their first use INSIDE the loop, where every later iteration's counts then also wait for
+  // that step's just-issued operand prefetch (and the previous step's history stores)
+  vm_drain();
   __syncthreads();
   for (int i = 0; i < N; ++i) {
     const int n = d ? N - 1 - i : i;
@@ -162,6 +173,9 @@ __global__ void __launch_bounds__(kTh) enc_lstm_fwd_kernel(EncFwdP p) {
 #endif
     // LDS-only barriers: a __syncthreads would also drain the prefetch and the history stores
     lds_barrier();
+#if SAT_ENC_DRAIN_CELL
+    vm_drain();   // this step's operand prefetch landed; the cell's stores then stay in flight
+#endif
     // ---- cell
     if (cell) {
       const float4 g = *reinterpret_cast<const float4*>(&gp[4 * u]);
@@ -236,6 +250,7 @@ __global__ void __launch_bounds__(kTh) enc_lstm_bwd_kernel(EncBwdP p) {
   };
   Ops nxt = load_ops(0);
   float dh_c = 0.f, dc_c = 0.f;
+  vm_drain();                              // (see the forward: weights landed before the loop)
   __syncthreads();
   for (int i = 0; i < N; ++i) {
     const int n = d ? i : N - 1 - i;
@@ -257,6 +272,9 @@ __global__ void __launch_bounds__(kTh) enc_lstm_bwd_kernel(EncBwdP p) {
       }
     }
     transpose_reduce8(v, lane);
+#if SAT_ENC_DRAIN_CELL
+    vm_drain();   // (see the forward)
+#endif
     if (lead) {
       const float dh_t = v[0] + dh_c;
       const float dc_t = dc_c;

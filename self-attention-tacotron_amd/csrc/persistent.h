@@ -171,6 +171,12 @@ __device__ __forceinline__ bool poll_give_up(unsigned spins, int* err) {
   return false;
 }
 
+// s_waitcnt vmcnt(0) in the compiler-visible form (gfx9 simm16: vmcnt 0, expcnt 7, lgkmcnt 15):
+// the waitcnt pass sees it and drops the loads it covers from its pending state.  Inline asm
+// is opaque to that pass, so an asm drain before a step loop still leaves the prologue's loads
+// "pending" at the loop header and their waits land inside the loop.
+__device__ __forceinline__ void vm_drain() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+
 // ---- wave-level dot helpers shared by the persistent kernels
 __device__ __forceinline__ float dot4(float4 a, float4 b, float acc) {
   acc = fmaf(a.x, b.x, acc);

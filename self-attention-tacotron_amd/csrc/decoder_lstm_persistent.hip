@@ -134,11 +134,21 @@ __global__ void __launch_bounds__(kThreads) dec_lstm_fwd_kernel(DecLstmFwdP p) {
     const int tt = layer == 0 ? ii : ii - 1;
     return cell && tt >= 0 && tt < T;
   };
+  // this lane's mask pointers, selected once and kept opaque: selected inside the step loop,
+  // the per-lane choice between two adjacent kernel-argument fields compiled to a per-lane
+  // global load of the pointer from the argument block -- a dependent load, and a vmcnt wait
+  // for it (behind every older memory operation of the wave), in every step
+  uint64_t mc_addr = (uint64_t)(masked ? (layer == 0 ? p.m1c : p.m2c) : p.X1);
+  uint64_t mh_addr = (uint64_t)(masked ? (layer == 0 ? p.m1h : p.m2h) : p.X1);
+  asm volatile("" : "+v"(mc_addr), "+v"(mh_addr));
   auto load_ops = [&](int ii, float4& xp_, float& mc_, float& mh_) {
     const int tt = layer == 0 ? ii : ii - 1;
     const int64_t bu = ops_on(ii) ? ((int64_t)tt * B + pb) * kU + pu : 0;
-    const float* Mc = masked ? (layer == 0 ? p.m1c : p.m2c) : p.X1;
-    const float* Mh = masked ? (layer == 0 ? p.m1h : p.m2h) : p.X1;
+    // (global address space: a generic pointer would compile to flat loads, which the waitcnt
+    // pass must treat as out of order)
+    typedef const __attribute__((address_space(1))) float* gptr;
+    const gptr Mc = reinterpret_cast<gptr>(mc_addr);
+    const gptr Mh = reinterpret_cast<gptr>(mh_addr);
     xp_ = reinterpret_cast<const float4*>(p.X1)[bu];
     mc_ = Mc[bu];
     mh_ = Mh[bu];

@@ -21,6 +21,22 @@ namespace {
 constexpr int kU = 128;            // units per direction
 constexpr int kG4 = 4 * kU;        // gate columns (512)
 constexpr int kTh = 1024;
+// BPTT workgroup: SAT_ENC_BWD8 (default) 8 waves, each 16 units x 8 gate columns per lane (128
+// weights); otherwise 16 waves of 8 units x 8 columns.  The step is issue-bound: the 16-wave
+// form spent ~3/4 of its instructions on per-wave overhead (the cell on 8 of 64 lanes, the
+// 64-lane reduce, addresses) that every wave repeats.
+#ifndef SAT_ENC_BWD8
+#define SAT_ENC_BWD8 1
+#endif
+// SAT_ENC_BWD_DMA: the cell operands (G, c_{t-1}, dL/dh, zoneout masks: 4 KB per step) stream
+// into LDS by asm LDS-DMA a chunk of 8 steps ahead (wave w loads step w of the next chunk,
+// double-buffered), waited for once per chunk; the per-step register prefetch exposed its
+// load latency (no operand loads at all: 229 -> 148 us, profiles/r06z_enc_bwd_dma_ab.txt)
+#ifndef SAT_ENC_BWD_DMA
+#define SAT_ENC_BWD_DMA 1
+#endif
+constexpr int kRowsB = SAT_ENC_BWD8 ? 16 : 8;      // units per wave
+constexpr int kThB = 64 * (kU / kRowsB);
 typedef float f2 __attribute__((ext_vector_type(2)));
 
 struct EncFwdP {
@@ -205,34 +221,45 @@ __global__ void __launch_bounds__(kTh) enc_lstm_fwd_kernel(EncFwdP p) {
   }
 }
 
-// Backward.  Recurrent product, wave-transposed: wave w owns rows 8w .. 8w+7 (units), lane l
-// gate columns 8l .. 8l+7 of them (64 weights in registers), so a step reads 8 floats of the
-// previous step's gate gradients per lane; the 8 partial row sums are transpose-reduced across
-// the wave and lane 8m runs unit 8w+m's reverse step with its carries in registers.  The gate
-// gradients of the previously processed step sit in LDS (double buffer: one barrier per step).
-__global__ void __launch_bounds__(kTh) enc_lstm_bwd_kernel(EncBwdP p) {
+// Backward.  Recurrent product, wave-transposed: wave w owns rows R w .. R w + R-1 (units; R =
+// kRowsB, 16 in the 8-wave form), lane l gate columns 8l .. 8l+7 of them (8R weights in
+// registers), so a step reads 8 floats of the previous step's gate gradients per lane; the R
+// partial row sums are transpose-reduced across the wave and lane (64/R) m runs unit R w + m's
+// reverse step with its carries in registers.  The gate gradients of the previously processed
+// step sit in LDS (double buffer: one barrier per step).
+__global__ void __launch_bounds__(kThB) enc_lstm_bwd_kernel(EncBwdP p) {
   __shared__ __attribute__((aligned(16))) float dgn[2][kG4];
+#if SAT_ENC_BWD_DMA
+  static_assert(kThB == 512, "one wave per step of an 8-step chunk");
+  // [buffer][step of the chunk][G 4U | c_{t-1} U | dL/dh U | mask c U | mask h U]
+  __shared__ __attribute__((aligned(16))) float opsb[2][8][8 * kU];
+#endif
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int d = blockIdx.x & 1, b = blockIdx.x >> 1;
   const int N = p.N, B = p.B;
-  f2 w[8][4];                              // row 8w + r, column pairs 8l + 2cp, +1
+  f2 w[kRowsB][4];                         // row kRowsB w + r, column pairs 8l + 2cp, +1
   {
 #pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      const float4* src = reinterpret_cast<const float4*>(p.W[d] + (int64_t)(8 * wave + r) * kG4 + 8 * lane);
+    for (int r = 0; r < kRowsB; ++r) {
+      const float4* src = reinterpret_cast<const float4*>(p.W[d] + (int64_t)(kRowsB * wave + r) * kG4 + 8 * lane);
       const float4 a0 = src[0], a1 = src[1];
       w[r][0] = f2{a0.x, a0.y}; w[r][1] = f2{a0.z, a0.w};
       w[r][2] = f2{a1.x, a1.y}; w[r][3] = f2{a1.z, a1.w};
     }
   }
-  for (int i = tid; i < kG4; i += kTh) dgn[0][i] = 0.f;
+  for (int i = tid; i < kG4; i += kThB) dgn[0][i] = 0.f;
   const int len = (int)p.lengths[b];
-  const bool lead = (lane & 7) == 0;
-  const int u = 8 * wave + (lane >> 3);
+  // after the transpose-reduce, lanes (64 / kRowsB) m .. hold unit kRowsB w + m
+  constexpr int kLPU = 64 / kRowsB;
+  const bool lead = (lane & (kLPU - 1)) == 0;
+  const int u = kRowsB * wave + lane / kLPU;
   const bool masked = p.mc[0] != nullptr;
   struct Ops { float4 g; float cp, dy, mc, mh; };
   auto load_ops = [&](int i) {
     Ops o{make_float4(0.f, 0.f, 0.f, 0.f), 0.f, 0.f, 1.f - p.zc, 1.f - p.zh};
+#if SAT_ENC_PROBE_NOLOAD
+    if (i >= 0) return o;   // timing probe only: no operand loads (wrong results)
+#endif
     if (lead && i < N) {
       const int n = d ? i : N - 1 - i;
       const int cprow = d ? n + 1 : n;      // c_{t-1} in processing order of the direction
@@ -248,22 +275,69 @@ __global__ void __launch_bounds__(kTh) enc_lstm_bwd_kernel(EncBwdP p) {
     }
     return o;
   };
+#if SAT_ENC_BWD_DMA
+  // step ii's operands (clamped to a valid step past N: loaded, never used) into opsb[buf][w]
+  auto dma_step = [&](int ii, int buf) {
+    const int ic = min(ii, N - 1);
+    const int n = d ? ic : N - 1 - ic;
+    const int cprow = d ? n + 1 : n;
+    const uint32_t base = lds_addr_of(&opsb[buf][wave][0]);
+    const float* g = p.G[d] + ((int64_t)n * B + b) * kU * 4;
+    lds_dma16(g + 4 * lane, base);
+    lds_dma16(g + 4 * kU / 2 + 4 * lane, base + 1024);
+    if (lane < kU / 4) {
+      lds_dma16(p.CS[d] + ((int64_t)cprow * B + b) * kU + 4 * lane, base + 2048);
+      lds_dma16(p.DY + (int64_t)b * p.dy_sb + (int64_t)n * p.dy_sn + d * kU + 4 * lane, base + 2560);
+      if (masked) {
+        const int64_t r = ((int64_t)n * B + b) * kU + 4 * lane;
+        lds_dma16(p.mc[d] + r, base + 3072);
+        lds_dma16(p.mh[d] + r, base + 3584);
+      }
+    }
+  };
+  dma_step(wave, 0);                       // chunk 0
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#elif SAT_ENC_BWD_PF2
+  // operands prefetched two steps ahead (one step ahead, their load latency showed in the step)
+  Ops nxt = load_ops(0), nxt2 = load_ops(1);
+#else
   Ops nxt = load_ops(0);
+#endif
   float dh_c = 0.f, dc_c = 0.f;
   vm_drain();                              // (see the forward: weights landed before the loop)
   __syncthreads();
   for (int i = 0; i < N; ++i) {
     const int n = d ? i : N - 1 - i;
+#if SAT_ENC_BWD_DMA
+    if ((i & 7) == 0) dma_step(i + 8 + wave, ((i >> 3) + 1) & 1);   // the next chunk
+    Ops o{make_float4(0.f, 0.f, 0.f, 0.f), 0.f, 0.f, 1.f - p.zc, 1.f - p.zh};
+    if (lead) {
+      const float* ob = &opsb[(i >> 3) & 1][i & 7][0];
+      o.g = *reinterpret_cast<const float4*>(&ob[4 * u]);
+      o.cp = ob[4 * kU + u];
+      o.dy = ob[5 * kU + u];
+      if (masked) {
+        o.mc = ob[6 * kU + u];
+        o.mh = ob[7 * kU + u];
+      }
+    }
+#else
     const Ops o = nxt;
+#if SAT_ENC_BWD_PF2
+    nxt = nxt2;
+    nxt2 = load_ops(i + 2);
+#else
     nxt = load_ops(i + 1);
+#endif
+#endif
     // ---- recurrent product of the previously processed step's gate gradients
-    float v[8];
+    float v[kRowsB];
     {
       const float4* g4 = reinterpret_cast<const float4*>(&dgn[i & 1][8 * lane]);
       const float4 ga = g4[0], gb = g4[1];
       const f2 g[4] = {f2{ga.x, ga.y}, f2{ga.z, ga.w}, f2{gb.x, gb.y}, f2{gb.z, gb.w}};
 #pragma unroll
-      for (int r = 0; r < 8; ++r) {
+      for (int r = 0; r < kRowsB; ++r) {
         f2 a = g[0] * w[r][0];
         a = __builtin_elementwise_fma(g[1], w[r][1], a);
         a = __builtin_elementwise_fma(g[2], w[r][2], a);
@@ -271,8 +345,12 @@ __global__ void __launch_bounds__(kTh) enc_lstm_bwd_kernel(EncBwdP p) {
         v[r] = a.x + a.y;
       }
     }
+#if SAT_ENC_BWD8
+    transpose_reduce16(v, lane);
+#else
     transpose_reduce8(v, lane);
-#if SAT_ENC_DRAIN_CELL
+#endif
+#if SAT_ENC_DRAIN_CELL && !SAT_ENC_BWD_DMA
     vm_drain();   // (see the forward)
 #endif
     if (lead) {
@@ -297,6 +375,10 @@ __global__ void __launch_bounds__(kTh) enc_lstm_bwd_kernel(EncBwdP p) {
       reinterpret_cast<float4*>(p.DG[d])[(int64_t)n * B * kU + bu] = dg;
       *reinterpret_cast<float4*>(&dgn[(i + 1) & 1][4 * u]) = dg;
     }
+#if SAT_ENC_BWD_DMA
+    // the chunk's last step: this wave's DMA of the next chunk has landed before the barrier
+    if ((i & 7) == 7) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
     lds_barrier();   // LDS only: a __syncthreads would drain the DG store and the prefetch
   }
 }
@@ -351,7 +433,7 @@ extern "C" int sat_encoder_lstm_bwd(const SatEncLstmBwd* a, void* stream) {
   p.lengths = a->lengths;
   p.DY = a->DY; p.dy_sb = a->dy_sb; p.dy_sn = a->dy_sn;
   p.DG[0] = a->DG_fw; p.DG[1] = a->DG_bw;
-  hipLaunchKernelGGL(enc_lstm_bwd_kernel, dim3(2 * a->B), dim3(kTh), 0, as_stream(stream), p);
+  hipLaunchKernelGGL(enc_lstm_bwd_kernel, dim3(2 * a->B), dim3(kThB), 0, as_stream(stream), p);
   SAT_LAUNCH_CHECK("sat_encoder_lstm_bwd");
   return SAT_OK;
 }

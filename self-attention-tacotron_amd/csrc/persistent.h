@@ -177,6 +177,23 @@ __device__ __forceinline__ bool poll_give_up(unsigned spins, int* err) {
 // "pending" at the loop header and their waits land inside the loop.
 __device__ __forceinline__ void vm_drain() { __builtin_amdgcn_s_waitcnt(0x0F70); }
 
+// One global_load_lds_dwordx4: 16 bytes per active lane from src into LDS at lds_addr + 16 *
+// lane (lds_addr wave-uniform).  Issued from inline asm, so the waitcnt pass does not track it:
+// the caller orders it with its own s_waitcnt vmcnt (the counter retires in issue order) and a
+// barrier before other waves read the bytes.
+__device__ __forceinline__ void lds_dma16(const void* src, uint32_t lds_addr) {
+  int keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(src), "s"(__builtin_amdgcn_readfirstlane(lds_addr))
+      : "memory");
+}
+__device__ __forceinline__ uint32_t lds_addr_of(const void* p) {
+  return (uint32_t)(uintptr_t)((__attribute__((address_space(3))) const char*)p);
+}
+
 // ---- wave-level dot helpers shared by the persistent kernels
 __device__ __forceinline__ float dot4(float4 a, float4 b, float acc) {
   acc = fmaf(a.x, b.x, acc);

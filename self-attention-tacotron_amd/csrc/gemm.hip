@@ -701,14 +701,21 @@ __device__ __forceinline__ void dma16(const float* src, uint32_t lds_off) {
 //   3 dW       : ONE product over M = sum_g (g+1)*C, rows (g, tap, ci) read dY's column block g.
 // waves per workgroup: 4 (2 x 2) for every tile but 128 x 128, which runs 8 (2 x 4, each wave
 // 64 x 32 as on the 128 x 64 tile) so its one workgroup per CU still has two waves per SIMD
+// The large tiles 256 x 128 / 128 x 256 run 8 waves of 64 x 64 (4 x 2 / 2 x 4) over a 2-stage
+// ring (96 KB, one workgroup per CU): half the tiles -- half the per-tile prologues and
+// epilogues -- of 128 x 128 on the 16000-row products, and 4 MFMAs per 4 fragment values.
 template <int BM, int BN>
-constexpr int lds_waves() { return (BM == 128 && BN == 128) ? 8 : 4; }
+constexpr int lds_waves() { return (BM * BN >= 128 * 128) ? 8 : 4; }
+template <int BM, int BN>
+constexpr int lds_wgm() { return BM == 256 ? 4 : 2; }       // waves along M
+template <int BM, int BN>
+constexpr int lds_stages() { return BM * BN > 128 * 128 ? 2 : 3; }
 
 template <int BM, int BN, int AM, int BMD, int GRP = 0>
 __global__ void __launch_bounds__((64 * lds_waves<BM, BN>())) gemm_lds_kernel(GemmP p) {
-  constexpr int ST = 3;
-  constexpr int NWV = lds_waves<BM, BN>(), WGN = NWV / 2;
-  constexpr int WM = BM / 2, WN = BN / WGN;           // 2 x WGN waves
+  constexpr int ST = lds_stages<BM, BN>();
+  constexpr int NWV = lds_waves<BM, BN>(), WGM = lds_wgm<BM, BN>(), WGN = NWV / WGM;
+  constexpr int WM = BM / WGM, WN = BN / WGN;         // WGM x WGN waves
   constexpr int SM = WM / 32, SN = WN / 32;           // 32x32 MFMA sub-tiles per wave
   constexpr bool AKM = (AM == A_K || AM == A_IM2COL); // A image K-major
   constexpr bool BKM = (BMD == B_K || BMD == B_FLIP); // B image K-major
@@ -1005,9 +1012,14 @@ __global__ void __launch_bounds__((64 * lds_waves<BM, BN>())) gemm_lds_kernel(Ge
     raw_barrier();
     read_frags(0, fa0, fb0);
   }
+  // Two stages (the large tiles): the DMA of kt+2 goes into kt's own stage right after the
+  // barrier that follows every wave's last read of it; it has the rest of kt and the first half
+  // of kt+1 -- one K-tile of 64 MFMAs per wave -- to land.
   auto tile = [&](int kt, int stage, const FA& ca, const FB& cb, FA& na, FB& nb) {
     const bool more2 = kt + 2 < nk;
-    if (more2) issue(stage == 0 ? 2 : stage - 1, kbeg + (kt + 2) * BK);
+    if constexpr (ST == 3) {
+      if (more2) issue(stage == 0 ? 2 : stage - 1, kbeg + (kt + 2) * BK);
+    }
     mfma_steps(0, 8, ca, cb);
     // every fragment read of this K-tile has landed by now (issued a half K-tile ago); saying so
     // with the compiler-visible form of s_waitcnt lgkmcnt(0), on both paths, stops it from
@@ -1015,18 +1027,26 @@ __global__ void __launch_bounds__((64 * lds_waves<BM, BN>())) gemm_lds_kernel(Ge
     // single out the older reads those steps use)
     __builtin_amdgcn_s_waitcnt(kLgkm0);
     if (kt + 1 < nk) {
-      if (more2) wait_vmcnt<LPT>(); else wait_vmcnt<0>();
-      raw_barrier();
-      read_frags(stage == 2 ? 0 : stage + 1, na, nb);
+      if constexpr (ST == 3) {
+        if (more2) wait_vmcnt<LPT>(); else wait_vmcnt<0>();
+        raw_barrier();
+        read_frags(stage == 2 ? 0 : stage + 1, na, nb);
+      } else {
+        wait_vmcnt<0>();
+        raw_barrier();
+        if (more2) issue(stage, kbeg + (kt + 2) * BK);
+        read_frags(stage ^ 1, na, nb);
+      }
     }
     mfma_steps(8, 16, ca, cb);
   };
+  constexpr int STL = ST - 1;
   int stage = 0, kt = 0;
   for (; kt + 1 < nk; kt += 2) {
     tile(kt, stage, fa0, fb0, fa1, fb1);
-    stage = stage == 2 ? 0 : stage + 1;
+    stage = stage == STL ? 0 : stage + 1;
     tile(kt + 1, stage, fa1, fb1, fa0, fb0);
-    stage = stage == 2 ? 0 : stage + 1;
+    stage = stage == STL ? 0 : stage + 1;
   }
   if (kt < nk) tile(kt, stage, fa0, fb0, fa1, fb1);
 
@@ -1202,7 +1222,8 @@ extern "C" int sat_gemm_probe_mode(int32_t m) {
   return SAT_OK;
 }
 extern "C" int sat_gemm_force_plan(int32_t bm, int32_t bn, int32_t splits) {
-  SAT_CHECK_ARG(bm == 0 || ((bm == 64 || bm == 128) && (bn == 64 || bn == 128) && splits >= 1),
+  SAT_CHECK_ARG(bm == 0 || ((((bm == 64 || bm == 128) && (bn == 64 || bn == 128)) ||
+                              (bm == 256 && bn == 128) || (bm == 128 && bn == 256)) && splits >= 1),
                 "sat_gemm_force_plan: bad plan");
   t_force_bm = bm; t_force_bn = bn; t_force_s = splits;
   return SAT_OK;
@@ -1303,12 +1324,14 @@ static LdsPlan plan_lds(int M, int N, int K, int nb, bool can_split, int64_t ws_
 // Measured plans for the training step's own products (tools/gemm_census.py --sweep on one
 // MI355X, profiles/r06q_gemm_census_sweep.txt: every forced tile / split-K plan of the LDS kernel
 // timed on the step's descriptors): used where the best measured plan beat the cycle model's
-// choice by >= 4 %.  Keyed on the descriptor's (M, N, K, batches, operand modes); any other
+// choice by >= 4 % (the first matching entry; a large-tile entry is followed by the plan it
+// replaced, taken under SAT_GEMM_BIG=0).  Keyed on the descriptor's (M, N, K, batches, operand modes); any other
 // product, a forced plan (sat_gemm_force_plan) or SAT_GEMM_PLAN_TABLE=0 takes the model.
 struct PlanEntry { int M, N, K, nb, am, bm, tbm, tbn, splits; };
 static const PlanEntry kMeasuredPlans[] = {
     // decoder: LSTM-stack input projection / its input gradient, the attention-LSTM weight
     // gradient over [prenet | contexts | h] rows
+    {16000, 1024, 544, 1, A_K, B_N, 128, 256, 1},    // 160.3 -> 150.4 (profiles/r06ze_*)
     {16000, 1024, 544, 1, A_K, B_N, 128, 128, 1},    // 173.9 -> 160.3 us
     {16000, 544, 1024, 1, A_K, B_K, 64, 64, 2},      // 187.4 -> 176.9
     {544, 1024, 16000, 1, A_M, B_N, 64, 64, 12},     // 204.1 -> 194.5
@@ -1327,11 +1350,21 @@ static const PlanEntry kMeasuredPlans[] = {
     {6400, 224, 256, 1, A_K, B_N, 64, 64, 1},        // 22.5 -> 18.7
     {6400, 256, 224, 1, A_K, B_K, 64, 64, 1},        // 22.9 -> 18.4
     {16000, 128, 256, 1, A_K, B_N, 64, 64, 1},       // 28.1 -> 23.0
+    {16000, 1024, 128, 1, A_K, B_N, 128, 256, 1},    // 52.3 -> 48.2
     // CBHG projections (Conv1D K = 3 as im2col products)
     {6400, 128, 6144, 1, A_IM2COL, B_N, 64, 64, 6},  // 125.2 -> 116.5
+    {6400, 2048, 384, 1, A_IM2COL, B_FLIP, 128, 256, 1},  // 111.5 -> 108.0
     {6400, 2048, 384, 1, A_IM2COL, B_FLIP, 64, 128, 1},   // 116.3 -> 111.5
     {6144, 128, 6400, 1, A_IM2COLT, B_N, 64, 128, 8},     // 115.7 -> 111.1
 };
+// SAT_GEMM_BIG=0: no 256 x 128 / 128 x 256 tile from the table or the conv bank (A/B switch)
+static bool gemm_big_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("SAT_GEMM_BIG");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
 static bool gemm_plan_table_enabled() {
   static const bool on = [] {
     const char* e = std::getenv("SAT_GEMM_PLAN_TABLE");
@@ -1346,6 +1379,7 @@ static LdsPlan measured_plan(int M, int N, int K, int nb, int am, int bm, bool c
   for (const PlanEntry& e : kMeasuredPlans) {
     if (e.M != M || e.N != N || e.K != K || e.nb != nb || e.am != am || e.bm != bm) continue;
     if (c_div && c_div % e.tbm != 0) break;
+    if ((e.tbm > 128 || e.tbn > 128) && !gemm_big_enabled()) continue;   // the next entry
     if (e.splits == 1) return LdsPlan{e.tbm, e.tbn, 1, K};
     if (!can_split) break;
     const int kc = (ceil_div(K, e.splits) + BK - 1) / BK * BK;
@@ -1382,10 +1416,27 @@ static int launch_lds_plan(const LdsPlan& pl, int am, int bm, int nb, GemmP& p, 
   p.nb = nb;
   const dim3 grid(gx, gy, pl.splits > 1 ? pl.splits * nb : nb);
   hipError_t e;
+  if constexpr (GRP == 0 || GRP == 2) {
+    if (pl.bm == 256 && pl.bn == 128) {
+      e = launch_lds_grp<256, 128, GRP>(am, bm, grid, s, p);
+      goto launched;
+    }
+  }
+  if constexpr (GRP == 0) {
+    if (pl.bm == 128 && pl.bn == 256) {
+      e = launch_lds_grp<128, 256, GRP>(am, bm, grid, s, p);
+      goto launched;
+    }
+  }
+  if (pl.bm > 128 || pl.bn > 128) {
+    set_error("%s: no %d x %d tile for this product", what, pl.bm, pl.bn);
+    return SAT_ERR_ARGUMENT;
+  }
   if (pl.bm == 128 && pl.bn == 128) e = launch_lds_grp<128, 128, GRP>(am, bm, grid, s, p);
   else if (pl.bm == 128) e = launch_lds_grp<128, 64, GRP>(am, bm, grid, s, p);
   else if (pl.bn == 128) e = launch_lds_grp<64, 128, GRP>(am, bm, grid, s, p);
   else e = launch_lds_grp<64, 64, GRP>(am, bm, grid, s, p);
+launched:
   if (e != hipSuccess) {
     set_error("%s: launch failed: %s", what, hipGetErrorString(e));
     return SAT_ERR_HIP;
@@ -1739,7 +1790,8 @@ extern "C" int sat_cbhg_convbank_fwd(const SatConvBank* d, void* stream) {
   LdsPlan pl = plan_lds(p.M, p.N, (d->max_k + 1) * d->C / 2, 1, false, 0, 0, d->Co);
   // measured at the C2 shape (tools/probes/conv_sol.py): 64x128 352 us, 64x64 384, 128x* 405
   // (row-major dispatch; longest-first dispatch, gemm_lds_kernel, takes 64x128 to 282 us)
-  if (t_force_bm == 0 && d->Co % 128 == 0) pl = {64, 128, 1, p.K};
+  if ((t_force_bm == 0 || pl.bm > 128 || pl.bn > 128) && d->Co % 128 == 0) pl = {64, 128, 1, p.K};
+  else if (pl.bm > 128 || pl.bn > 128) pl = {64, 64, 1, p.K};   // no large tile for this launch
   LdsPlan fixed = pl;
   fixed.splits = 1;
   fixed.kchunk = p.K;
@@ -1787,11 +1839,16 @@ extern "C" int sat_cbhg_convbank_bwd(const SatConvBank* d, void* stream) {
     p.beta = d->beta_dx;
     LdsPlan pl = plan_lds(p.M, p.N, p.K, 1, d->ws != nullptr, d->ws_bytes, 0, 0);
     // measured at the C2 shape (tools/probes/convbank_bwd_probe.py): 128 x 128 tiles split 4
-    // ways 373 us, the cost model's choice 414 (odd splits 490+: their chunks straddle banks)
-    const int kc4 = (ceil_div(p.K, 4) + BK - 1) / BK * BK;
+    // ways 373 us, the cost model's choice 414 (odd splits 490+: their chunks straddle banks);
+    // 256 x 128 tiles split 8 ways (200 workgroups, 56 CUs left to the weight gradient beside
+    // it): 366 -> 315 us alone, 642 -> 590 us with the weight gradient on a second stream
+    // (tools/probes/big_tile_probe.py, profiles/r06ze_big_tile_probe.txt)
+    const bool big = gemm_big_enabled() && d->C % 128 == 0;
+    const int ns = big ? 8 : 4;
+    const int kcs = (ceil_div(p.K, ns) + BK - 1) / BK * BK;
     if (t_force_bm == 0 && d->C % 128 == 0 && p.M >= 4096 && d->ws != nullptr &&
-        (int64_t)ceil_div(p.K, kc4) * p.M * p.N * 4 <= d->ws_bytes)
-      pl = {128, 128, ceil_div(p.K, kc4), kc4};
+        (int64_t)ceil_div(p.K, kcs) * p.M * p.N * 4 <= d->ws_bytes)
+      pl = {big ? 256 : 128, 128, ceil_div(p.K, kcs), kcs};
     const int e = launch_lds_plan<2>(pl, A_IM2COL, B_FLIP, 1, p, s, "sat_cbhg_convbank_bwd(dX)");
     if (e != SAT_OK) return e;
   }

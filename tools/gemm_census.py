@@ -85,7 +85,7 @@ def sweep(lib, descs, keys):
     for key in keys:
         d = descs[key]
         res = []
-        for bm, bn in ((128, 128), (128, 64), (64, 128), (64, 64)):
+        for bm, bn in ((256, 128), (128, 256), (128, 128), (128, 64), (64, 128), (64, 64)):
             for sp in (1, 2, 3, 4, 6, 8, 12, 16, 24, 32):
                 if sp > 1 and d.K < 512:
                     continue

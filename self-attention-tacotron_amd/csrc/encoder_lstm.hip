@@ -276,6 +276,7 @@ __global__ void __launch_bounds__(kThB) enc_lstm_bwd_kernel(EncBwdP p) {
     return o;
   };
 #if SAT_ENC_BWD_DMA
+  (void)load_ops;   // the register path of SAT_ENC_BWD_DMA=0
   // step ii's operands (clamped to a valid step past N: loaded, never used) into opsb[buf][w]
   auto dma_step = [&](int ii, int buf) {
     const int ic = min(ii, N - 1);
